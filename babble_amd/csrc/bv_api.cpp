@@ -1,0 +1,369 @@
+// bv_api.cpp — host side of libbabbleverify.so: the C ABI declared in
+// include/babbleverify.h.
+//
+// One bv_ctx owns a HIP stream, the precomputed G table (built on the device
+// at bv_create, kept resident in HBM) and growable device work buffers.
+// bv_verify_batch stages host buffers to HBM and runs the same device
+// pipeline as bv_verify_batch_device.  There is no CPU fallback: a missing or
+// non-gfx950 device is BV_E_NODEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/babbleverify.h"
+
+namespace bvk {
+hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
+hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
+hipError_t build_tables(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *);
+hipError_t scalar_prep(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint32_t *, const uint8_t *,
+                       const uint32_t *, const uint32_t *, uint32_t *, uint32_t *);
+hipError_t verify(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
+                  const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
+hipError_t verify_generic(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
+                          const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
+                          uint8_t *, uint64_t *);
+}  // namespace bvk
+
+namespace {
+
+constexpr uint64_t kTableEntries = 32ull * 256ull;             // per base point
+constexpr uint64_t kTableBytes = kTableEntries * 64ull;         // 512 KiB
+constexpr uint32_t kMaxTableKeys = 8192;                        // 4 GiB of key tables
+constexpr uint32_t kPrepM = 16;                                 // items per s^-1 batch
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      hipError_t e = hipFree(p);
+      if (e != hipSuccess) return e;
+      p = nullptr;
+      cap = 0;
+    }
+    size_t want = std::max(bytes, cap * 3 / 2);
+    want = (want + 255) & ~(size_t)255;
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T *as() const {
+    return (T *)p;
+  }
+};
+
+}  // namespace
+
+struct bv_ctx {
+  int device = 0;
+  uint32_t flags = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  DevBuf g_table, g_xy, g_bases;
+  // staging for the host entry point
+  DevBuf h_msg_bytes, h_msg_off, h_key_bytes, h_key_off, h_item_msg, h_item_key, h_r, h_s, h_pre;
+  // work buffers
+  DevBuf digests, kstatus, kxy, bases_jac, key_table, scratch, u12, status, bits;
+  hipEvent_t ev[8] = {};
+  bv_timing timing = {};
+};
+
+static int fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess) {
+  if (c) {
+    char buf[256];
+    if (e != hipSuccess)
+      snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    else
+      snprintf(buf, sizeof buf, "%s", what);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIPCHK(expr, code, what)                  \
+  do {                                            \
+    hipError_t _e = (expr);                       \
+    if (_e != hipSuccess) return fail(ctx, code, what, _e); \
+  } while (0)
+
+static const uint8_t kGenerator[64] = {
+    0x79, 0xBE, 0x66, 0x7E, 0xF9, 0xDC, 0xBB, 0xAC, 0x55, 0xA0, 0x62, 0x95, 0xCE, 0x87, 0x0B, 0x07,
+    0x02, 0x9B, 0xFC, 0xDB, 0x2D, 0xCE, 0x28, 0xD9, 0x59, 0xF2, 0x81, 0x5B, 0x16, 0xF8, 0x17, 0x98,
+    0x48, 0x3A, 0xDA, 0x77, 0x26, 0xA3, 0xC4, 0x65, 0x5D, 0xA4, 0xFB, 0xFC, 0x0E, 0x11, 0x08, 0xA8,
+    0xFD, 0x17, 0xB4, 0x48, 0xA6, 0x85, 0x54, 0x19, 0x9C, 0x47, 0xD0, 0x8F, 0xFB, 0x10, 0xD4, 0xB8};
+
+extern "C" int bv_abi_version(void) { return BV_ABI_VERSION; }
+
+extern "C" const char *bv_last_error(const bv_ctx *ctx) { return ctx ? ctx->err.c_str() : "null ctx"; }
+
+extern "C" int bv_create(bv_ctx **out, int device, uint32_t flags) {
+  if (!out) return BV_E_ARGS;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return BV_E_NODEVICE;
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess) return BV_E_NODEVICE;
+  }
+  if (device >= ndev) return BV_E_NODEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return BV_E_NODEVICE;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return BV_E_NODEVICE;
+  bv_ctx *ctx = new bv_ctx();
+  ctx->device = device;
+  ctx->flags = flags;
+  HIPCHK(hipSetDevice(device), BV_E_NODEVICE, "hipSetDevice");
+  HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
+  for (auto &e : ctx->ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
+  // G table: T[j][d] = d * 2^(8j) * G, built once on the device.
+  HIPCHK(ctx->g_table.ensure(kTableBytes), BV_E_OOM, "alloc G table");
+  HIPCHK(ctx->g_xy.ensure(64), BV_E_OOM, "alloc G");
+  HIPCHK(ctx->g_bases.ensure(32 * 24 * 4), BV_E_OOM, "alloc G bases");
+  uint32_t gxy[16];
+  for (int half = 0; half < 2; half++)
+    for (int i = 0; i < 8; i++) {
+      const uint8_t *q = kGenerator + 32 * half + 4 * (7 - i);
+      gxy[8 * half + i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    }
+  HIPCHK(hipMemcpyAsync(ctx->g_xy.p, gxy, sizeof gxy, hipMemcpyHostToDevice, ctx->stream), BV_E_LAUNCH, "copy G");
+  HIPCHK(bvk::build_tables(ctx->stream, 1, ctx->g_xy.as<uint32_t>(), nullptr, ctx->g_bases.as<uint32_t>(),
+                           ctx->g_table.as<uint32_t>()),
+         BV_E_LAUNCH, "G table");
+  HIPCHK(hipStreamSynchronize(ctx->stream), BV_E_LAUNCH, "G table sync");
+  *out = ctx;
+  return BV_OK;
+}
+
+extern "C" void bv_destroy(bv_ctx *ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  DevBuf *bufs[] = {&ctx->g_table, &ctx->g_xy, &ctx->g_bases, &ctx->h_msg_bytes, &ctx->h_msg_off,
+                    &ctx->h_key_bytes, &ctx->h_key_off, &ctx->h_item_msg, &ctx->h_item_key, &ctx->h_r,
+                    &ctx->h_s, &ctx->h_pre, &ctx->digests, &ctx->kstatus, &ctx->kxy, &ctx->bases_jac,
+                    &ctx->key_table, &ctx->scratch, &ctx->u12, &ctx->status, &ctx->bits};
+  for (auto *b : bufs) b->release();
+  for (auto &e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+extern "C" int bv_get_timing(const bv_ctx *ctx, bv_timing *out) {
+  if (!ctx || !out) return BV_E_ARGS;
+  *out = ctx->timing;
+  return BV_OK;
+}
+
+// Device pipeline over device-resident inputs.  msg_hash/status/bits may be
+// null (ctx buffers are used).  Caller holds ctx->mu and has set the device.
+static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
+                      hipStream_t st) {
+  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
+  const uint32_t n_keys = b->n_keys;
+  if (n_items > 0 && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be)) return fail(ctx, BV_E_ARGS, "null item arrays");
+  if (n_msgs > 0 && (!b->msg_bytes || !b->msg_off)) return fail(ctx, BV_E_ARGS, "null msg arrays");
+  if (n_items > 0 && n_keys == 0) return fail(ctx, BV_E_ARGS, "items without keys");
+  if (n_keys > 0 && (!b->key_off)) return fail(ctx, BV_E_ARGS, "null key_off");
+  if (((uintptr_t)b->r_be | (uintptr_t)b->s_be) & 3) return fail(ctx, BV_E_ARGS, "r_be/s_be must be 4-byte aligned");
+
+  uint32_t *dig = (uint32_t *)d_msg_hash;
+  if (!dig || ((uintptr_t)dig & 15)) {
+    HIPCHK(ctx->digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
+    dig = ctx->digests.as<uint32_t>();
+  }
+  uint8_t *status = d_status;
+  if (!status) {
+    HIPCHK(ctx->status.ensure(std::max<uint64_t>(n_items, 1)), BV_E_OOM, "alloc status");
+    status = ctx->status.as<uint8_t>();
+  }
+  uint64_t *bits = d_bits;
+  if (!bits) {
+    HIPCHK(ctx->bits.ensure(std::max<uint64_t>((n_items + 63) / 64, 1) * 8), BV_E_OOM, "alloc bits");
+    bits = ctx->bits.as<uint64_t>();
+  }
+  HIPCHK(ctx->kstatus.ensure(std::max<uint32_t>(n_keys, 1)), BV_E_OOM, "alloc kstatus");
+  HIPCHK(ctx->kxy.ensure(std::max<uint32_t>(n_keys, 1) * 64ull), BV_E_OOM, "alloc kxy");
+  HIPCHK(ctx->scratch.ensure(std::max<uint64_t>(n_items, 1) * 32), BV_E_OOM, "alloc scratch");
+  HIPCHK(ctx->u12.ensure(std::max<uint64_t>(n_items, 1) * 64), BV_E_OOM, "alloc u12");
+
+  // Per-key fixed-base tables pay off once a key signs enough items; with
+  // few items per key the generic per-lane path is cheaper.
+  const bool table_mode = n_keys <= kMaxTableKeys && n_items >= 16ull * n_keys;
+  if (table_mode) {
+    HIPCHK(ctx->bases_jac.ensure(std::max<uint32_t>(n_keys, 1) * 32ull * 96ull), BV_E_OOM, "alloc bases");
+    HIPCHK(ctx->key_table.ensure(std::max<uint32_t>(n_keys, 1) * kTableBytes), BV_E_OOM, "alloc key tables");
+  }
+
+  hipEvent_t *ev = ctx->ev;
+  HIPCHK(hipEventRecord(ev[0], st), BV_E_LAUNCH, "event");
+  HIPCHK(bvk::sha256(st, n_msgs, b->msg_bytes, b->msg_off, dig), BV_E_LAUNCH, "k_sha256");
+  HIPCHK(hipEventRecord(ev[1], st), BV_E_LAUNCH, "event");
+  HIPCHK(bvk::key_decode(st, n_keys, b->key_bytes, b->key_off, ctx->kstatus.as<uint8_t>(), ctx->kxy.as<uint32_t>()),
+         BV_E_LAUNCH, "k_key_decode");
+  if (table_mode)
+    HIPCHK(bvk::build_tables(st, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
+                             ctx->bases_jac.as<uint32_t>(), ctx->key_table.as<uint32_t>()),
+           BV_E_LAUNCH, "key tables");
+  HIPCHK(hipEventRecord(ev[2], st), BV_E_LAUNCH, "event");
+  HIPCHK(bvk::scalar_prep(st, n_items, kPrepM, (const uint32_t *)b->r_be, (const uint32_t *)b->s_be, b->pre,
+                          b->item_msg, dig, ctx->scratch.as<uint32_t>(), ctx->u12.as<uint32_t>()),
+         BV_E_LAUNCH, "k_scalar_prep");
+  HIPCHK(hipEventRecord(ev[3], st), BV_E_LAUNCH, "event");
+  if (table_mode)
+    HIPCHK(bvk::verify(st, n_items, b->item_key, (const uint32_t *)b->r_be, (const uint32_t *)b->s_be, b->pre,
+                       ctx->kstatus.as<uint8_t>(), ctx->u12.as<uint32_t>(), ctx->g_table.as<uint32_t>(),
+                       ctx->key_table.as<uint32_t>(), status, bits),
+           BV_E_LAUNCH, "k_verify");
+  else
+    HIPCHK(bvk::verify_generic(st, n_items, b->item_key, (const uint32_t *)b->r_be, (const uint32_t *)b->s_be,
+                               b->pre, ctx->kstatus.as<uint8_t>(), ctx->kxy.as<uint32_t>(), ctx->u12.as<uint32_t>(),
+                               ctx->g_table.as<uint32_t>(), status, bits),
+           BV_E_LAUNCH, "k_verify_generic");
+  HIPCHK(hipEventRecord(ev[4], st), BV_E_LAUNCH, "event");
+  if (d_msg_hash && (uint8_t *)dig != d_msg_hash)
+    HIPCHK(hipMemcpyAsync(d_msg_hash, dig, n_msgs * 32, hipMemcpyDeviceToDevice, st), BV_E_LAUNCH, "copy digests");
+  return BV_OK;
+}
+
+static void read_timing(bv_ctx *ctx) {
+  float t;
+  hipEvent_t *ev = ctx->ev;
+  ctx->timing.ms_sha256 = hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess ? t : -1.f;
+  ctx->timing.ms_keyprep = hipEventElapsedTime(&t, ev[1], ev[2]) == hipSuccess ? t : -1.f;
+  float prep = hipEventElapsedTime(&t, ev[2], ev[3]) == hipSuccess ? t : 0.f;
+  float ver = hipEventElapsedTime(&t, ev[3], ev[4]) == hipSuccess ? t : 0.f;
+  ctx->timing.ms_verify = prep + ver;
+  ctx->timing.ms_total = hipEventElapsedTime(&t, ev[0], ev[4]) == hipSuccess ? t : -1.f;
+}
+
+extern "C" int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresult, void *stream,
+                                      int async) {
+  if (!ctx || !dbatch || !dresult) return BV_E_ARGS;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+  int rc = run_device(ctx, dbatch, dresult->msg_hash, dresult->status, dresult->accept_bits, st);
+  if (rc != BV_OK) return rc;
+  if (!async) {
+    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "verify sync");
+    read_timing(ctx);
+  }
+  return BV_OK;
+}
+
+extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
+  if (!ctx || !b || !res) return BV_E_ARGS;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  hipStream_t st = ctx->stream;
+  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
+  const uint32_t n_keys = b->n_keys;
+  const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
+  const uint64_t key_len = n_keys ? b->key_off[n_keys] : 0;
+  // validate host offsets (a bad offset must not become an OOB device read)
+  for (uint64_t m = 0; m < n_msgs; m++)
+    if (b->msg_off[m] > b->msg_off[m + 1]) return fail(ctx, BV_E_ARGS, "msg_off not monotone");
+  for (uint32_t k = 0; k < n_keys; k++)
+    if (b->key_off[k] > b->key_off[k + 1]) return fail(ctx, BV_E_ARGS, "key_off not monotone");
+  for (uint64_t i = 0; i < n_items; i++)
+    if (b->item_msg[i] >= n_msgs || b->item_key[i] >= n_keys) return fail(ctx, BV_E_ARGS, "item index out of range");
+
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventCreate(&e1), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(e0, st), BV_E_LAUNCH, "event");
+  HIPCHK(ctx->h_msg_bytes.ensure(msg_len + 64), BV_E_OOM, "alloc msg bytes");
+  HIPCHK(ctx->h_msg_off.ensure((n_msgs + 1) * 8), BV_E_OOM, "alloc msg off");
+  HIPCHK(ctx->h_key_bytes.ensure(key_len + 64), BV_E_OOM, "alloc key bytes");
+  HIPCHK(ctx->h_key_off.ensure((uint64_t)(n_keys + 1) * 8), BV_E_OOM, "alloc key off");
+  HIPCHK(ctx->h_item_msg.ensure(std::max<uint64_t>(n_items, 1) * 4), BV_E_OOM, "alloc item msg");
+  HIPCHK(ctx->h_item_key.ensure(std::max<uint64_t>(n_items, 1) * 4), BV_E_OOM, "alloc item key");
+  HIPCHK(ctx->h_r.ensure(std::max<uint64_t>(n_items, 1) * 32), BV_E_OOM, "alloc r");
+  HIPCHK(ctx->h_s.ensure(std::max<uint64_t>(n_items, 1) * 32), BV_E_OOM, "alloc s");
+  HIPCHK(ctx->h_pre.ensure(std::max<uint64_t>(n_items, 1)), BV_E_OOM, "alloc pre");
+  auto h2d = [&](DevBuf &d, const void *src, size_t n) -> hipError_t {
+    if (n == 0) return hipSuccess;
+    return hipMemcpyAsync(d.p, src, n, hipMemcpyHostToDevice, st);
+  };
+  HIPCHK(h2d(ctx->h_msg_bytes, b->msg_bytes, msg_len), BV_E_LAUNCH, "h2d msg");
+  if (n_msgs) HIPCHK(h2d(ctx->h_msg_off, b->msg_off, (n_msgs + 1) * 8), BV_E_LAUNCH, "h2d msg off");
+  HIPCHK(h2d(ctx->h_key_bytes, b->key_bytes, key_len), BV_E_LAUNCH, "h2d keys");
+  if (n_keys) HIPCHK(h2d(ctx->h_key_off, b->key_off, (uint64_t)(n_keys + 1) * 8), BV_E_LAUNCH, "h2d key off");
+  HIPCHK(h2d(ctx->h_item_msg, b->item_msg, n_items * 4), BV_E_LAUNCH, "h2d item msg");
+  HIPCHK(h2d(ctx->h_item_key, b->item_key, n_items * 4), BV_E_LAUNCH, "h2d item key");
+  HIPCHK(h2d(ctx->h_r, b->r_be, n_items * 32), BV_E_LAUNCH, "h2d r");
+  HIPCHK(h2d(ctx->h_s, b->s_be, n_items * 32), BV_E_LAUNCH, "h2d s");
+  if (b->pre) HIPCHK(h2d(ctx->h_pre, b->pre, n_items), BV_E_LAUNCH, "h2d pre");
+  bv_batch d = {};
+  d.n_msgs = n_msgs;
+  d.msg_bytes = ctx->h_msg_bytes.as<uint8_t>();
+  d.msg_off = ctx->h_msg_off.as<uint64_t>();
+  d.n_keys = n_keys;
+  d.key_bytes = ctx->h_key_bytes.as<uint8_t>();
+  d.key_off = ctx->h_key_off.as<uint64_t>();
+  d.n_items = n_items;
+  d.item_msg = ctx->h_item_msg.as<uint32_t>();
+  d.item_key = ctx->h_item_key.as<uint32_t>();
+  d.r_be = ctx->h_r.as<uint8_t>();
+  d.s_be = ctx->h_s.as<uint8_t>();
+  d.pre = b->pre ? ctx->h_pre.as<uint8_t>() : nullptr;
+  int rc = run_device(ctx, &d, nullptr, nullptr, nullptr, st);
+  if (rc != BV_OK) return rc;
+  HIPCHK(hipEventRecord(e1, st), BV_E_LAUNCH, "event");
+  if (res->msg_hash && n_msgs)
+    HIPCHK(hipMemcpyAsync(res->msg_hash, ctx->digests.p, n_msgs * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
+           "d2h digests");
+  if (res->status && n_items)
+    HIPCHK(hipMemcpyAsync(res->status, ctx->status.p, n_items, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
+  if (res->accept_bits && n_items)
+    HIPCHK(hipMemcpyAsync(res->accept_bits, ctx->bits.p, (n_items + 63) / 64 * 8, hipMemcpyDeviceToHost, st),
+           BV_E_LAUNCH, "d2h bits");
+  HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "verify sync");
+  read_timing(ctx);
+  float t;
+  if (hipEventElapsedTime(&t, e0, ctx->ev[0]) == hipSuccess) ctx->timing.ms_h2d = t;
+  if (hipEventElapsedTime(&t, ctx->ev[4], e1) == hipSuccess) ctx->timing.ms_d2h = t;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return BV_OK;
+}
+
+extern "C" int bv_sha256_batch(bv_ctx *ctx, uint64_t n_msgs, const uint8_t *msg_bytes, const uint64_t *msg_off,
+                               uint8_t *out_hash) {
+  if (!ctx || (n_msgs && (!msg_bytes || !msg_off || !out_hash))) return BV_E_ARGS;
+  if (n_msgs == 0) return BV_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  for (uint64_t m = 0; m < n_msgs; m++)
+    if (msg_off[m] > msg_off[m + 1]) return fail(ctx, BV_E_ARGS, "msg_off not monotone");
+  hipStream_t st = ctx->stream;
+  const uint64_t len = msg_off[n_msgs];
+  HIPCHK(ctx->h_msg_bytes.ensure(len + 64), BV_E_OOM, "alloc msg bytes");
+  HIPCHK(ctx->h_msg_off.ensure((n_msgs + 1) * 8), BV_E_OOM, "alloc msg off");
+  HIPCHK(ctx->digests.ensure(n_msgs * 32), BV_E_OOM, "alloc digests");
+  if (len) HIPCHK(hipMemcpyAsync(ctx->h_msg_bytes.p, msg_bytes, len, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
+  HIPCHK(hipMemcpyAsync(ctx->h_msg_off.p, msg_off, (n_msgs + 1) * 8, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
+  HIPCHK(bvk::sha256(st, n_msgs, ctx->h_msg_bytes.as<uint8_t>(), ctx->h_msg_off.as<uint64_t>(),
+                     ctx->digests.as<uint32_t>()),
+         BV_E_LAUNCH, "k_sha256");
+  HIPCHK(hipMemcpyAsync(out_hash, ctx->digests.p, n_msgs * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h");
+  HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+  return BV_OK;
+}

@@ -1,0 +1,143 @@
+// point.h — secp256k1 group law on gfx950 (Jacobian coordinates, a = 0).
+//
+// Semantics follow btcec's KoblitzCurve (src/crypto/keys/curve.go:21):
+// the identity is tracked as an explicit flag (btcec's (0,0) / Z = 0), and
+// addJacobian's exceptional cases are honoured: P + P doubles, P + (-P) is
+// the identity.  These cases are data-dependent and rare, so they are
+// branches; an adversarial key or signature that hits them still gets the
+// exact group-law answer.
+#pragma once
+#include "field.h"
+
+struct gej {
+  fe X, Y, Z;
+};
+
+// dbl-2009-l (a = 0): 2M + 5S.  Caller guarantees the input is not the
+// identity; Y == 0 cannot occur on secp256k1 (no 2-torsion, b = 7).
+DEV void gej_double(gej &r, const gej &a) {
+  fe A, B, C, D, E, F, t;
+  fe_sqr(A, a.X);
+  fe_sqr(B, a.Y);
+  fe_sqr(C, B);
+  fe_add(t, a.X, B);
+  fe_sqr(t, t);
+  fe_sub(t, t, A);
+  fe_sub(t, t, C);
+  fe_dbl(D, t);
+  fe_dbl(E, A);
+  fe_add(E, E, A);
+  fe_sqr(F, E);
+  fe Z3;
+  fe_mul(Z3, a.Y, a.Z);
+  fe_dbl(r.Z, Z3);
+  fe_dbl(t, D);
+  fe_sub(r.X, F, t);
+  fe_sub(t, D, r.X);
+  fe_mul(r.Y, E, t);
+  fe_dbl(t, C);
+  fe_dbl(t, t);
+  fe_dbl(t, t);
+  fe_sub(r.Y, r.Y, t);
+}
+
+// r += (x2, y2) (affine), madd-2007-bl: 7M + 4S.  `inf` is r's identity flag.
+DEV void gej_add_ge(gej &r, bool &inf, const fe &x2, const fe &y2) {
+  if (inf) {
+    r.X = x2;
+    r.Y = y2;
+    fe_set(r.Z, 1);
+    inf = false;
+    return;
+  }
+  fe Z1Z1, U2, S2, H, HH, I, J, rr, V, t;
+  fe_sqr(Z1Z1, r.Z);
+  fe_mul(U2, x2, Z1Z1);
+  fe_mul(t, r.Z, Z1Z1);
+  fe_mul(S2, y2, t);
+  fe_sub(H, U2, r.X);
+  fe_sub(rr, S2, r.Y);
+  if (fe_is_zero(H)) {
+    if (fe_is_zero(rr)) {
+      gej d;
+      gej_double(d, r);
+      r = d;
+    } else {
+      inf = true;
+    }
+    return;
+  }
+  fe_sqr(HH, H);
+  fe_dbl(I, HH);
+  fe_dbl(I, I);
+  fe_mul(J, H, I);
+  fe_dbl(rr, rr);
+  fe_mul(V, r.X, I);
+  // Z3 = (Z1 + H)^2 - Z1Z1 - HH
+  fe_add(t, r.Z, H);
+  fe_sqr(t, t);
+  fe_sub(t, t, Z1Z1);
+  fe_sub(r.Z, t, HH);
+  // X3 = rr^2 - J - 2V
+  fe_sqr(t, rr);
+  fe_sub(t, t, J);
+  fe_sub(t, t, V);
+  fe_sub(r.X, t, V);
+  // Y3 = rr (V - X3) - 2 Y1 J
+  fe_sub(t, V, r.X);
+  fe_mul(t, rr, t);
+  fe_mul(J, r.Y, J);
+  fe_dbl(J, J);
+  fe_sub(r.Y, t, J);
+}
+
+// r += b (both Jacobian), add-2007-bl with exceptional cases: 11M + 5S.
+DEV void gej_add(gej &r, bool &rinf, const gej &b, bool binf) {
+  if (binf) return;
+  if (rinf) {
+    r = b;
+    rinf = false;
+    return;
+  }
+  fe Z1Z1, Z2Z2, U1, U2, S1, S2, H, I, J, rr, V, t;
+  fe_sqr(Z1Z1, r.Z);
+  fe_sqr(Z2Z2, b.Z);
+  fe_mul(U1, r.X, Z2Z2);
+  fe_mul(U2, b.X, Z1Z1);
+  fe_mul(t, b.Z, Z2Z2);
+  fe_mul(S1, r.Y, t);
+  fe_mul(t, r.Z, Z1Z1);
+  fe_mul(S2, b.Y, t);
+  fe_sub(H, U2, U1);
+  fe_sub(rr, S2, S1);
+  if (fe_is_zero(H)) {
+    if (fe_is_zero(rr)) {
+      gej d;
+      gej_double(d, r);
+      r = d;
+    } else {
+      rinf = true;
+    }
+    return;
+  }
+  fe_dbl(I, H);
+  fe_sqr(I, I);
+  fe_mul(J, H, I);
+  fe_dbl(rr, rr);
+  fe_mul(V, U1, I);
+  // Z3 = ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H
+  fe_add(t, r.Z, b.Z);
+  fe_sqr(t, t);
+  fe_sub(t, t, Z1Z1);
+  fe_sub(t, t, Z2Z2);
+  fe_mul(r.Z, t, H);
+  fe_sqr(t, rr);
+  fe_sub(t, t, J);
+  fe_sub(t, t, V);
+  fe_sub(r.X, t, V);
+  fe_sub(t, V, r.X);
+  fe_mul(t, rr, t);
+  fe_mul(J, S1, J);
+  fe_dbl(J, J);
+  fe_sub(r.Y, t, J);
+}

@@ -1,0 +1,409 @@
+// verify_core.h — the per-unit work of every kernel, as __host__ __device__
+// functions.  kernels.hip maps them onto the grid; tests/emu compiles the
+// same source for the host so index logic and arithmetic are exercised on
+// the CPU (with sanitizers) before a GPU run.  Nothing here is a CPU path of
+// the product: libbabbleverify.so only ever runs these on gfx950.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/babbleverify.h"
+#include "point.h"
+#include "sha256.h"
+
+#define BV_NWIN 32       // 8-bit windows over a 256-bit scalar
+#define BV_WSIZE 256     // entries per window (entry 0 unused)
+#define BV_ENTRY_U32 16  // affine x, y = 16 words (64 bytes)
+#define BV_TABLE_U32 ((uint64_t)BV_NWIN * BV_WSIZE * BV_ENTRY_U32)
+
+// key status (k_key_decode output)
+#define KS_OK 0
+#define KS_EMPTY 1
+#define KS_BAD 2
+
+// p - N: r + N < p  <=>  r < p - N
+static constexpr uint32_t P_MINUS_N[8] = {0x2FC9BAEEu, 0x402DA172u, 0x50B75FC4u, 0x45512319u,
+                                          0x00000001u, 0u, 0u, 0u};
+
+// ---------------------------------------------------------------------------
+// loads / stores
+// ---------------------------------------------------------------------------
+DEV void fe_load_be(fe &r, const uint8_t *b) {  // 32 big-endian bytes, any alignment
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint8_t *q = b + 4 * (7 - i);
+    r.v[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+DEV void fe_load_be_words(fe &r, const uint32_t *w) {  // 8 dwords holding 32 BE bytes
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = bswap32(w[7 - i]);
+}
+DEV void sc_load_be_words(sc &r, const uint32_t *w) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = bswap32(w[7 - i]);
+}
+DEV void fe_store(uint32_t *p, const fe &a) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) p[i] = a.v[i];
+}
+DEV void fe_load(fe &a, const uint32_t *p) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) a.v[i] = p[i];
+}
+DEV void fe_load4(fe &a, const uint32_t *p) {  // 16-byte aligned: 2 x dwordx4
+  const uint4 *q = (const uint4 *)p;
+  uint4 l = q[0], h = q[1];
+  a.v[0] = l.x; a.v[1] = l.y; a.v[2] = l.z; a.v[3] = l.w;
+  a.v[4] = h.x; a.v[5] = h.y; a.v[6] = h.z; a.v[7] = h.w;
+}
+DEV void store16(uint32_t *p, const uint32_t *v) {  // 64 bytes, 16-byte aligned
+  uint4 *q = (uint4 *)p;
+#pragma unroll
+  for (int c = 0; c < 4; c++) q[c] = make_uint4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+}
+DEV bool u256_lt(const uint32_t *a, const uint32_t *b) {
+#pragma unroll
+  for (int i = 7; i >= 0; i--) {
+    if (a[i] != b[i]) return a[i] < b[i];
+  }
+  return false;
+}
+DEV bool u256_is_zero(const uint32_t *a) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x |= a[i];
+  return x == 0;
+}
+
+// ---------------------------------------------------------------------------
+// SHA-256 of message m -> 8 dwords holding the 32 big-endian digest bytes
+// (crypto.SHA256, src/crypto/hash.go:8)
+// ---------------------------------------------------------------------------
+DEV void sha256_one(uint64_t m, const uint8_t *bytes, const uint64_t *off, uint32_t *digest_words) {
+  const uint64_t o = off[m];
+  const uint64_t len = off[m + 1] - o;
+  uint32_t h[8];
+  sha256_msg(h, bytes, o, len);
+  uint32_t be[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) be[i] = bswap32(h[i]);
+  uint4 *dst = (uint4 *)(digest_words + 8 * m);
+  dst[0] = make_uint4(be[0], be[1], be[2], be[3]);
+  dst[1] = make_uint4(be[4], be[5], be[6], be[7]);
+}
+
+// ---------------------------------------------------------------------------
+// elliptic.Unmarshal(btcec.S256(), b) (src/crypto/keys/public_key.go:14-20):
+// len 65, prefix 0x04, x < p, y < p, y^2 == x^3 + 7.  len 0 -> ToPublicKey
+// returns nil (KS_EMPTY: ecdsa.Verify panics at pub.Curve).
+// ---------------------------------------------------------------------------
+DEV void key_decode_one(uint32_t k, const uint8_t *kbytes, const uint64_t *koff, uint8_t *kstatus, uint32_t *kxy) {
+  const uint64_t o = koff[k];
+  const uint64_t len = koff[k + 1] - o;
+  uint8_t st = KS_BAD;
+  fe x, y;
+  fe_set(x, 0);
+  fe_set(y, 0);
+  if (len == 0) {
+    st = KS_EMPTY;
+  } else if (len == 65 && kbytes[o] == 4) {
+    fe_load_be(x, kbytes + o + 1);
+    fe_load_be(y, kbytes + o + 33);
+    if (!fe_ge_p(x) && !fe_ge_p(y)) {
+      fe y2, x3, seven;
+      fe_sqr(y2, y);
+      fe_sqr(x3, x);
+      fe_mul(x3, x3, x);
+      fe_set(seven, 7);
+      fe_add(x3, x3, seven);
+      if (fe_eq(y2, x3)) st = KS_OK;
+    }
+  }
+  kstatus[k] = st;
+  fe_store(kxy + 16 * k, x);
+  fe_store(kxy + 16 * k + 8, y);
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-base tables.  T[b][j][d] = d * 2^(8j) * P_b (affine), d in 1..255.
+// ---------------------------------------------------------------------------
+// B_j = 2^(8j) P_b (Jacobian), j = 0..31: a serial doubling chain per base.
+DEV void table_bases_one(uint32_t b, const uint32_t *bxy, uint32_t *bases_jac) {
+  gej P;
+  fe_load(P.X, bxy + 16 * b);
+  fe_load(P.Y, bxy + 16 * b + 8);
+  fe_set(P.Z, 1);
+  uint32_t *out = bases_jac + (uint64_t)b * BV_NWIN * 24;
+  for (int j = 0; j < BV_NWIN; j++) {
+    fe_store(out + 24 * j, P.X);
+    fe_store(out + 24 * j + 8, P.Y);
+    fe_store(out + 24 * j + 16, P.Z);
+    if (j + 1 < BV_NWIN) {
+      for (int k = 0; k < 8; k++) gej_double(P, P);
+    }
+  }
+}
+
+DEV void jac_to_affine(fe &x, fe &y, const uint32_t *jac) {
+  fe X, Y, Z, zi, zi2, zi3;
+  fe_load(X, jac);
+  fe_load(Y, jac + 8);
+  fe_load(Z, jac + 16);
+  fe_inv(zi, Z);
+  fe_sqr(zi2, zi);
+  fe_mul(zi3, zi2, zi);
+  fe_mul(x, X, zi2);
+  fe_mul(y, Y, zi3);
+}
+
+// d * B (B affine), MSB-first double-and-add over the 8 bits of d.  The
+// returned Z is 1 for d == 0 so it can join a batch inversion.
+DEV void table_point(gej &R, bool &inf, fe &Z, const fe &bx, const fe &by, uint32_t d) {
+  inf = true;
+  fe_set(R.X, 0);
+  fe_set(R.Y, 0);
+  fe_set(R.Z, 0);
+  for (int bit = 7; bit >= 0; bit--) {
+    if (!inf) gej_double(R, R);
+    if ((d >> bit) & 1) gej_add_ge(R, inf, bx, by);
+  }
+  if (inf) fe_set(Z, 1);
+  else Z = R.Z;
+}
+
+// Store entry d given Z^-1 (canonical affine; d == 0 stored as zeros).
+DEV void table_store(uint32_t *table, uint32_t b, uint32_t j, uint32_t d, const gej &R, bool inf, const fe &zi) {
+  fe zi2, zi3, x, y;
+  fe_sqr(zi2, zi);
+  fe_mul(zi3, zi2, zi);
+  fe_mul(x, R.X, zi2);
+  fe_mul(y, R.Y, zi3);
+  fe_canon(x);
+  fe_canon(y);
+  if (d == 0 || inf) {
+    fe_set(x, 0);
+    fe_set(y, 0);
+  }
+  uint32_t v[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    v[i] = x.v[i];
+    v[8 + i] = y.v[i];
+  }
+  store16(table + (((uint64_t)b * BV_NWIN + j) * BV_WSIZE + d) * BV_ENTRY_U32, v);
+}
+
+// ---------------------------------------------------------------------------
+// Scalars: u1 = e * s^-1, u2 = r * s^-1 (mod N)  (ecdsa.Verify steps 4-6)
+// ---------------------------------------------------------------------------
+DEV void sc_sqrn(sc &a, int n) {
+  for (int i = 0; i < n; i++) sc_mont(a, a, a);
+}
+
+// x^(N-2) in the Montgomery domain (xR -> x^-1 R): 255 S + 45 M.
+// The top 128 bits of N-2 are 2^128 - 2 (runs of ones, built from
+// x^(2^k - 1)); the low 128 bits use a 4-bit sliding window (chain generated
+// offline; tests/test_emu.py checks inverses against Python ints).
+__host__ __device__ __noinline__ inline void sc_inverse(sc &r, const sc &x) {
+  sc x2, x3, x5, x7, x9, x11, x13, x15;
+  sc_mont(x2, x, x);
+  sc_mont(x3, x2, x);
+  sc_mont(x5, x3, x2);
+  sc_mont(x7, x5, x2);
+  sc_mont(x9, x7, x2);
+  sc_mont(x11, x9, x2);
+  sc_mont(x13, x11, x2);
+  sc_mont(x15, x13, x2);
+  sc a2 = x3, a4, a8, a16, a32, a64, t;
+  a4 = a2; sc_sqrn(a4, 2); sc_mont(a4, a4, a2);
+  a8 = a4; sc_sqrn(a8, 4); sc_mont(a8, a8, a4);
+  a16 = a8; sc_sqrn(a16, 8); sc_mont(a16, a16, a8);
+  a32 = a16; sc_sqrn(a32, 16); sc_mont(a32, a32, a16);
+  a64 = a32; sc_sqrn(a64, 32); sc_mont(a64, a64, a32);
+  t = a64;
+  sc_sqrn(t, 32); sc_mont(t, t, a32);
+  sc_sqrn(t, 16); sc_mont(t, t, a16);
+  sc_sqrn(t, 8); sc_mont(t, t, a8);
+  sc_sqrn(t, 4); sc_mont(t, t, a4);
+  sc_sqrn(t, 2); sc_mont(t, t, a2);
+  sc_sqrn(t, 1); sc_mont(t, t, x);  // x^(2^127 - 1)
+  sc_sqrn(t, 1);                    // x^(2^128 - 2)
+#define SQM(n, m) sc_sqrn(t, n); sc_mont(t, t, m);
+  SQM(4, x11) SQM(3, x5) SQM(4, x5) SQM(4, x7) SQM(5, x13) SQM(2, x3) SQM(5, x7) SQM(6, x13)
+  SQM(5, x11) SQM(4, x13) SQM(3, x) SQM(6, x5) SQM(10, x7) SQM(4, x7) SQM(5, x15) SQM(4, x15)
+  SQM(5, x9) SQM(6, x11) SQM(4, x13) SQM(5, x3) SQM(6, x13) SQM(10, x13) SQM(4, x9) SQM(9, x9)
+  SQM(4, x15) SQM(1, x)
+#undef SQM
+  r = t;
+}
+
+DEV bool s_usable(const uint8_t *pre, uint64_t i, const sc &s) {
+  return (pre == nullptr || pre[i] == 0) && !u256_is_zero(s.v) && u256_lt(s.v, SC_N);
+}
+
+// Thread t of T owns items t, t+T, ..., t+(M-1)T; one Fermat inversion for
+// all of them (Montgomery's trick).  Unusable items contribute s = 1.
+DEV void scalar_prep_thread(uint64_t t, uint64_t T, uint64_t n_items, uint32_t M, const uint32_t *r_be,
+                            const uint32_t *s_be, const uint8_t *pre, const uint32_t *item_msg,
+                            const uint32_t *digest_words, uint32_t *scratch, uint32_t *u12) {
+  sc R2, R1;
+  sc_load_const(R2, SC_R2);
+  sc_load_const(R1, SC_R1);
+  sc acc = R1;
+  for (uint32_t m = 0; m < M; m++) {
+    const uint64_t i = t + (uint64_t)m * T;
+    if (i >= n_items) break;
+    sc s, sM;
+    sc_load_be_words(s, s_be + 8 * i);
+    if (s_usable(pre, i, s)) sc_mont(sM, s, R2);
+    else sM = R1;
+#pragma unroll
+    for (int k = 0; k < 8; k++) scratch[8 * i + k] = acc.v[k];
+    sc_mont(acc, acc, sM);
+  }
+  sc inv;
+  sc_inverse(inv, acc);
+  for (int m = (int)M - 1; m >= 0; m--) {
+    const uint64_t i = t + (uint64_t)m * T;
+    if (i >= n_items) continue;
+    sc s, sM, pfx, w, e, r, u1, u2;
+    sc_load_be_words(s, s_be + 8 * i);
+    const bool ok = s_usable(pre, i, s);
+    if (ok) sc_mont(sM, s, R2);
+    else sM = R1;
+#pragma unroll
+    for (int k = 0; k < 8; k++) pfx.v[k] = scratch[8 * i + k];
+    sc_mont(w, inv, pfx);  // s^-1 R
+    sc_mont(inv, inv, sM);
+    sc_load_be_words(e, digest_words + 8 * (uint64_t)item_msg[i]);  // hashToInt: 256 bits, unreduced
+    sc_load_be_words(r, r_be + 8 * i);
+    if (!ok || u256_is_zero(r.v) || !u256_lt(r.v, SC_N)) {
+      sc_load_const(u1, SC_R1);  // never used: the item does not reach the math
+      u2 = u1;
+    } else {
+      sc_mont(u1, e, w);  // e * s^-1 mod N  (e < 2^256 = R, w < N)
+      sc_mont(u2, r, w);
+    }
+    uint32_t v[16];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      v[k] = u1.v[k];
+      v[8 + k] = u2.v[k];
+    }
+    store16(u12 + 16 * i, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Item decision table.  Returns 0xFF when the item must run
+// the math, else its final status.  The host pre-class is re-checked against
+// the r/s bytes so an inconsistent pre byte cannot skip a range check.
+// ---------------------------------------------------------------------------
+DEV uint8_t classify(uint8_t pre, uint8_t ks, const fe &r, const fe &s) {
+  if (pre & BV_PRE_PARTS_BAD) return BV_REJECT_ERR;
+  if (ks == KS_EMPTY) return BV_REF_PANIC;
+  uint32_t rc = pre & 3u, scl = (pre >> 2) & 3u;
+  if (rc == BV_SC_OK) rc = u256_is_zero(r.v) ? BV_SC_NONPOS : (u256_lt(r.v, SC_N) ? BV_SC_OK : BV_SC_GE_N);
+  if (scl == BV_SC_OK) scl = u256_is_zero(s.v) ? BV_SC_NONPOS : (u256_lt(s.v, SC_N) ? BV_SC_OK : BV_SC_GE_N);
+  if (rc == BV_SC_NIL) return BV_REF_PANIC;
+  if (rc == BV_SC_NONPOS) return BV_REJECT;
+  if (scl == BV_SC_NIL) return BV_REF_PANIC;
+  if (scl == BV_SC_NONPOS) return BV_REJECT;
+  if (rc == BV_SC_GE_N || scl == BV_SC_GE_N) return BV_REJECT;
+  if (ks != KS_OK) return BV_REF_PANIC;
+  return 0xFF;
+}
+
+// x(R) mod N == r, projectively: X == r Z^2, or (r + N < p and X == (r+N) Z^2)
+DEV bool final_check(const gej &R, bool inf, const fe &r) {
+  if (inf) return false;
+  fe z2, t;
+  fe_sqr(z2, R.Z);
+  fe_mul(t, r, z2);
+  if (fe_eq(t, R.X)) return true;
+  if (u256_lt(r.v, P_MINUS_N)) {
+    fe rn;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) rn.v[i] = addc32(r.v[i], SC_N[i], c);
+    fe_mul(t, rn, z2);
+    if (fe_eq(t, R.X)) return true;
+  }
+  return false;
+}
+
+// R += sum_j T[j][digit_j(u)] over the 32 byte-digits of the 256-bit u.
+DEV void table_add(gej &R, bool &inf, const uint32_t *tab, const uint32_t *u) {
+  for (int j = 0; j < BV_NWIN; j++) {
+    const uint32_t d = (u[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+    if (d) {
+      const uint32_t *e = tab + ((uint64_t)j * BV_WSIZE + d) * BV_ENTRY_U32;
+      fe x, y;
+      fe_load4(x, e);
+      fe_load4(y, e + 8);
+      gej_add_ge(R, inf, x, y);
+    }
+  }
+}
+
+DEV void load_u12(uint32_t u[16], const uint32_t *u12, uint64_t i) {
+  const uint4 *q = (const uint4 *)(u12 + 16 * i);
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    uint4 v = q[c];
+    u[4 * c] = v.x;
+    u[4 * c + 1] = v.y;
+    u[4 * c + 2] = v.z;
+    u[4 * c + 3] = v.w;
+  }
+}
+
+// One signature item with per-key tables: R = u1 G + u2 Q as 64 mixed adds.
+DEV uint8_t verify_item_tables(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
+                               const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12,
+                               const uint32_t *g_table, const uint32_t *key_table) {
+  const uint32_t k = item_key[i];
+  fe r, s;
+  fe_load_be_words(r, r_be + 8 * i);
+  fe_load_be_words(s, s_be + 8 * i);
+  uint8_t st = classify(pre ? pre[i] : 0, kstatus[k], r, s);
+  if (st != 0xFF) return st;
+  uint32_t u[16];
+  load_u12(u, u12, i);
+  gej R;
+  bool inf = true;
+  fe_set(R.X, 0);
+  fe_set(R.Y, 0);
+  fe_set(R.Z, 0);
+  table_add(R, inf, g_table, u);
+  table_add(R, inf, key_table + (uint64_t)k * BV_TABLE_U32, u + 8);
+  return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
+}
+
+// One signature item without a key table: u2 Q by a per-lane double-and-add.
+DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
+                                const uint8_t *pre, const uint8_t *kstatus, const uint32_t *kxy,
+                                const uint32_t *u12, const uint32_t *g_table) {
+  const uint32_t k = item_key[i];
+  fe r, s;
+  fe_load_be_words(r, r_be + 8 * i);
+  fe_load_be_words(s, s_be + 8 * i);
+  uint8_t st = classify(pre ? pre[i] : 0, kstatus[k], r, s);
+  if (st != 0xFF) return st;
+  uint32_t u[16];
+  load_u12(u, u12, i);
+  fe qx, qy;
+  fe_load(qx, kxy + 16 * k);
+  fe_load(qy, kxy + 16 * k + 8);
+  gej R;
+  bool inf = true;
+  fe_set(R.X, 0);
+  fe_set(R.Y, 0);
+  fe_set(R.Z, 0);
+  for (int bit = 255; bit >= 0; bit--) {
+    if (!inf) gej_double(R, R);
+    if ((u[8 + (bit >> 5)] >> (bit & 31)) & 1u) gej_add_ge(R, inf, qx, qy);
+  }
+  table_add(R, inf, g_table, u);
+  return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
+}

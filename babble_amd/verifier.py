@@ -1,0 +1,164 @@
+"""Verifier: the Python handle on one bv_ctx (one gfx950 device).
+
+    v = Verifier(device=0)
+    res = v.verify(packed_batch)          # host buffers (bv_verify_batch)
+    res.status, res.accept_bits, res.msg_hash
+
+    dev = v.to_device(packed_batch)       # inputs resident in HBM (torch
+    v.verify_device(dev)                  # tensors as plumbing), then
+                                          # bv_verify_batch_device
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import native
+from .batch import PackedBatch
+
+
+@dataclass
+class VerifyResult:
+    msg_hash: np.ndarray     # [n_msgs, 32] u8
+    status: np.ndarray       # [n_items] u8
+    accept_bits: np.ndarray  # [ceil(n_items/64)] u64
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data if a is not None and a.size else 0
+
+
+class DeviceBatch:
+    """Device-resident copy of a PackedBatch plus its result buffers."""
+
+    def __init__(self, packed: PackedBatch, device: int):
+        import torch
+
+        dev = torch.device("cuda", device)
+
+        def t(a, dtype, pad=0):
+            a = np.ascontiguousarray(a)
+            out = torch.zeros(max(a.size + pad, 1), dtype=dtype, device=dev)
+            if a.size:
+                out[: a.size].copy_(torch.from_numpy(a.view(np.uint8) if dtype == torch.uint8 else a).to(dev))
+            return out
+
+        self.n_msgs, self.n_keys, self.n_items = packed.n_msgs, packed.n_keys, packed.n_items
+        self.msg_bytes = t(packed.msg_bytes, torch.uint8, pad=64)
+        self.msg_off = t(packed.msg_off.astype(np.int64), torch.int64)
+        self.key_bytes = t(packed.key_bytes, torch.uint8, pad=64)
+        self.key_off = t(packed.key_off.astype(np.int64), torch.int64)
+        self.item_msg = t(packed.item_msg.astype(np.int32), torch.int32)
+        self.item_key = t(packed.item_key.astype(np.int32), torch.int32)
+        self.r_be = t(packed.r_be.reshape(-1), torch.uint8)
+        self.s_be = t(packed.s_be.reshape(-1), torch.uint8)
+        self.pre = t(packed.pre, torch.uint8) if packed.pre is not None else None
+        self.msg_hash = torch.zeros(max(self.n_msgs, 1) * 32, dtype=torch.uint8, device=dev)
+        self.status = torch.zeros(max(self.n_items, 1), dtype=torch.uint8, device=dev)
+        self.accept_bits = torch.zeros(max((self.n_items + 63) // 64, 1), dtype=torch.int64, device=dev)
+        b = native.BvBatch()
+        b.n_msgs = self.n_msgs
+        b.msg_bytes = self.msg_bytes.data_ptr()
+        b.msg_off = self.msg_off.data_ptr()
+        b.n_keys = self.n_keys
+        b.key_bytes = self.key_bytes.data_ptr()
+        b.key_off = self.key_off.data_ptr()
+        b.n_items = self.n_items
+        b.item_msg = self.item_msg.data_ptr()
+        b.item_key = self.item_key.data_ptr()
+        b.r_be = self.r_be.data_ptr()
+        b.s_be = self.s_be.data_ptr()
+        b.pre = self.pre.data_ptr() if self.pre is not None else 0
+        self.cbatch = b
+        r = native.BvResult()
+        r.msg_hash = self.msg_hash.data_ptr()
+        r.status = self.status.data_ptr()
+        r.accept_bits = self.accept_bits.data_ptr()
+        self.cresult = r
+
+    def result(self) -> VerifyResult:
+        return VerifyResult(
+            self.msg_hash.cpu().numpy()[: self.n_msgs * 32].reshape(self.n_msgs, 32),
+            self.status.cpu().numpy()[: self.n_items],
+            self.accept_bits.cpu().numpy().view(np.uint64)[: (self.n_items + 63) // 64],
+        )
+
+
+class Verifier:
+    def __init__(self, device: int = 0, flags: int = native.F_DEFAULT):
+        self._L = native.lib()
+        self.device = device
+        ctx = ctypes.c_void_p()
+        rc = self._L.bv_create(ctypes.byref(ctx), device, flags)
+        if rc != native.BV_OK:
+            raise native.BvError(rc, "bv_create failed (no usable gfx950 device?)")
+        self._ctx = ctx
+
+    def close(self):
+        if self._ctx:
+            self._L.bv_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != native.BV_OK:
+            raise native.BvError(rc, self._L.bv_last_error(self._ctx).decode(errors="replace"))
+
+    def verify(self, b: PackedBatch) -> VerifyResult:
+        keep = []
+
+        def c(a, dt):
+            a = np.ascontiguousarray(a, dtype=dt)
+            keep.append(a)
+            return a
+
+        cb = native.BvBatch()
+        cb.n_msgs = b.n_msgs
+        cb.msg_bytes = _p(c(b.msg_bytes, np.uint8))
+        cb.msg_off = _p(c(b.msg_off, np.uint64))
+        cb.n_keys = b.n_keys
+        cb.key_bytes = _p(c(b.key_bytes, np.uint8))
+        cb.key_off = _p(c(b.key_off, np.uint64))
+        cb.n_items = b.n_items
+        cb.item_msg = _p(c(b.item_msg, np.uint32))
+        cb.item_key = _p(c(b.item_key, np.uint32))
+        cb.r_be = _p(c(b.r_be, np.uint8))
+        cb.s_be = _p(c(b.s_be, np.uint8))
+        cb.pre = _p(c(b.pre, np.uint8)) if b.pre is not None else 0
+        h = np.zeros((max(b.n_msgs, 1), 32), np.uint8)
+        st = np.zeros(max(b.n_items, 1), np.uint8)
+        bits = np.zeros(max((b.n_items + 63) // 64, 1), np.uint64)
+        res = native.BvResult(h.ctypes.data, st.ctypes.data, bits.ctypes.data)
+        self._check(self._L.bv_verify_batch(self._ctx, ctypes.byref(cb), ctypes.byref(res)))
+        return VerifyResult(h[: b.n_msgs], st[: b.n_items], bits[: (b.n_items + 63) // 64])
+
+    def to_device(self, b: PackedBatch) -> DeviceBatch:
+        return DeviceBatch(b, self.device)
+
+    def verify_device(self, d: DeviceBatch, stream: Optional[int] = None, sync: bool = True) -> None:
+        self._check(self._L.bv_verify_batch_device(self._ctx, ctypes.byref(d.cbatch), ctypes.byref(d.cresult),
+                                                   stream or 0, 0 if sync else 1))
+
+    def sha256(self, msgs: Sequence[bytes]) -> list:
+        msgs = [bytes(m) for m in msgs]
+        if not msgs:
+            return []
+        buf = np.frombuffer(b"".join(msgs) or b"\0", np.uint8).copy()
+        off = np.zeros(len(msgs) + 1, np.uint64)
+        off[1:] = np.cumsum([len(m) for m in msgs], dtype=np.uint64)
+        out = np.zeros((len(msgs), 32), np.uint8)
+        self._check(self._L.bv_sha256_batch(self._ctx, len(msgs), buf.ctypes.data, off.ctypes.data, out.ctypes.data))
+        return [out[i].tobytes() for i in range(len(msgs))]
+
+    def timing(self) -> dict:
+        t = native.BvTiming()
+        self._check(self._L.bv_get_timing(self._ctx, ctypes.byref(t)))
+        return {k: getattr(t, k) for k, _ in native.BvTiming._fields_}

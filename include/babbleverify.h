@@ -1,0 +1,140 @@
+/*
+ * babbleverify.h — C ABI of libbabbleverify.so, the MI355X batch verifier for
+ * Babble's event-ingestion hot path (SHA-256 of canonical bodies + ECDSA over
+ * secp256k1).  Plain C types only: this is what a Go cgo shim (see
+ * INTEGRATION.md) or any other FFI binds.
+ *
+ * Reference interfaces each entry point replaces (paths under the reference
+ * tree, sikoba/babble v0.8.4):
+ *   bv_verify_batch   N x { crypto.SHA256(body)              src/crypto/hash.go:8
+ *                           keys.ToPublicKey(pub)             src/crypto/keys/public_key.go:14
+ *                           keys.Verify(pub, hash, r, s) }    src/crypto/keys/signature.go:20
+ *                     as composed by Event.Verify             src/hashgraph/event.go:219-247
+ *                     InternalTransaction.Verify              src/hashgraph/internal_transaction.go:139-154
+ *                     Block.Verify                            src/hashgraph/block.go:343-357
+ *   bv_sha256_batch   N x crypto.SHA256                       src/crypto/hash.go:8-13
+ *   bv_decode_signature  keys.DecodeSignature + the sign/range
+ *                     pre-checks of ecdsa.Verify              src/crypto/keys/signature.go:31-39
+ *   bv_hex_decode     common.DecodeFromString                 src/common/hex.go:15-17
+ *
+ * Threading: every entry point is re-entrant.  A bv_ctx serialises its own
+ * calls with an internal mutex (processJoinRequest, node_rpc.go:250-260, calls
+ * the verifier outside Node.coreLock); use one ctx per thread for concurrency.
+ * Ownership: all pointers are caller-owned and only read/written during the
+ * call; nothing is retained.  There is no CPU fallback: if no gfx950 device is
+ * usable the calls fail with BV_E_NODEVICE.
+ */
+#ifndef BABBLEVERIFY_H
+#define BABBLEVERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BV_ABI_VERSION 1
+
+/* Return codes (per-item outcomes are never errors; they go to status[]). */
+#define BV_OK 0
+#define BV_E_ARGS (-1)
+#define BV_E_NODEVICE (-2)
+#define BV_E_OOM (-3)
+#define BV_E_LAUNCH (-4)
+#define BV_E_COMM (-5)
+
+/* Item status (SURVEY §8a-9 decision table). */
+#define BV_REJECT 0     /* keys.Verify returned false                          */
+#define BV_ACCEPT 1     /* keys.Verify returned true                           */
+#define BV_REJECT_ERR 2 /* DecodeSignature returned an error (parts != 2)      */
+#define BV_REF_PANIC 3  /* the Go reference would panic on this input          */
+
+/* Pre-class byte per item, decided on the host from the signature text.
+ * bits 0-1: class of r, bits 2-3: class of s, bit 7: parts != 2.
+ * pre == 0 means "r and s parsed and both in [1, N-1]": run the math.       */
+#define BV_SC_OK 0     /* 0 < v < N                                          */
+#define BV_SC_NIL 1    /* big.Int SetString failed -> nil (Go would panic)   */
+#define BV_SC_NONPOS 2 /* v <= 0                                             */
+#define BV_SC_GE_N 3   /* v >= N (possibly wider than 256 bits)              */
+#define BV_PRE_PARTS_BAD 0x80
+#define BV_PRE(rc, sc) ((uint8_t)((rc) | ((sc) << 2)))
+
+/* Flags for bv_create. */
+#define BV_F_DEFAULT 0u
+#define BV_F_KEY_CACHE 1u /* keep per-key tables across calls (validator sets
+                             are stable); off by default                       */
+
+typedef struct bv_ctx bv_ctx;
+
+/* One batch, struct-of-arrays.  Messages are hashed once each; items point
+ * at a message and a key, so one BlockBody serves its 100 signatures. */
+typedef struct {
+  uint64_t n_msgs;
+  const uint8_t *msg_bytes;  /* concatenated canonical JSON bodies            */
+  const uint64_t *msg_off;   /* n_msgs + 1 offsets into msg_bytes            */
+  uint32_t n_keys;
+  const uint8_t *key_bytes;  /* concatenated raw pubkey bytes (any length)   */
+  const uint64_t *key_off;   /* n_keys + 1 offsets into key_bytes            */
+  uint64_t n_items;
+  const uint32_t *item_msg;  /* message index per item                       */
+  const uint32_t *item_key;  /* key index per item                           */
+  const uint8_t *r_be;       /* 32 * n_items, big-endian r (valid if class OK) */
+  const uint8_t *s_be;       /* 32 * n_items, big-endian s                    */
+  const uint8_t *pre;        /* n_items pre-class bytes (NULL = all 0)       */
+} bv_batch;
+
+typedef struct {
+  uint8_t *msg_hash;     /* 32 * n_msgs digests (NULL: not returned)          */
+  uint8_t *status;       /* n_items BV_* statuses (NULL: not returned)        */
+  uint64_t *accept_bits; /* ceil(n_items/64) words, bit i = item i ACCEPT,
+                            LSB-first (NULL: not returned)                     */
+} bv_result;
+
+/* Timing of the last call, device-side (HIP events on the ctx stream). */
+typedef struct {
+  float ms_total;   /* first kernel start -> last kernel end                  */
+  float ms_sha256;  /* message hashing                                         */
+  float ms_keyprep; /* key decode + per-key table build                        */
+  float ms_verify;  /* ECDSA verify kernel(s)                                  */
+  float ms_h2d;     /* host -> device staging (host-buffer entry point only)   */
+  float ms_d2h;     /* device -> host results                                  */
+} bv_timing;
+
+int bv_abi_version(void);
+
+/* Create a context on `device` (HIP ordinal; -1 = current device). */
+int bv_create(bv_ctx **out, int device, uint32_t flags);
+void bv_destroy(bv_ctx *ctx);
+const char *bv_last_error(const bv_ctx *ctx);
+
+/* Synchronous batch verify from host buffers (the cgo entry point). */
+int bv_verify_batch(bv_ctx *ctx, const bv_batch *batch, bv_result *result);
+
+/* Same, with every bv_batch / bv_result pointer in device memory of the ctx's
+ * device (inputs already resident in HBM).  `stream` is a hipStream_t (NULL =
+ * the ctx stream); the call returns after the work is enqueued when
+ * `async` != 0, else after it completes. */
+int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresult,
+                           void *stream, int async);
+
+/* SHA-256 of n messages (host buffers) -> 32*n bytes. */
+int bv_sha256_batch(bv_ctx *ctx, uint64_t n_msgs, const uint8_t *msg_bytes,
+                    const uint64_t *msg_off, uint8_t *out_hash);
+
+/* Device-timing breakdown of the last verify call on this ctx. */
+int bv_get_timing(const bv_ctx *ctx, bv_timing *out);
+
+/* Host helpers mirroring the Go parsing semantics (no device needed). */
+/* keys.DecodeSignature + classification: writes 32-byte BE r,s (zero when the
+ * class is not OK) and returns the pre byte. */
+uint8_t bv_decode_signature(const char *sig, size_t len, uint8_t r_be[32], uint8_t s_be[32]);
+/* common.DecodeFromString: hex.DecodeString(s[2:]) keeping the prefix decoded
+ * before the first error.  Returns the decoded length, or -1 where Go panics
+ * (len < 2).  `out` must hold (len-2)/2 bytes. */
+int64_t bv_hex_decode(const char *s, size_t len, uint8_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BABBLEVERIFY_H */

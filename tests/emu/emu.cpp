@@ -1,0 +1,198 @@
+// Host emulation of the device pipeline — TEST INFRASTRUCTURE ONLY.
+//
+// Compiles babble_amd/csrc/verify_core.h (the exact per-unit source the
+// gfx950 kernels run) for the host and replays kernels.hip's grid mapping
+// serially, so tests can check index logic and arithmetic on the CPU (and
+// under AddressSanitizer, tests/emu/Makefile `asan`) before a GPU run.
+// Not linked into libbabbleverify.so; the product never runs this.
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../babble_amd/csrc/verify_core.h"
+
+namespace {
+
+void emu_build_tables(uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, uint32_t *table) {
+  std::vector<uint32_t> bases((size_t)n_bases * BV_NWIN * 24);
+  for (uint32_t b = 0; b < n_bases; b++) {
+    if (bstatus && bstatus[b] != KS_OK) continue;
+    table_bases_one(b, bxy, bases.data());
+  }
+  // k_table_fill, one (b, j) block at a time; the scans run serially.
+  for (uint32_t b = 0; b < n_bases; b++) {
+    if (bstatus && bstatus[b] != KS_OK) continue;
+    for (uint32_t j = 0; j < BV_NWIN; j++) {
+      fe bx, by;
+      jac_to_affine(bx, by, bases.data() + ((uint64_t)b * BV_NWIN + j) * 24);
+      std::vector<gej> R(256);
+      std::vector<fe> Z(256), pre(256), suf(256);
+      bool inf[256];
+      for (uint32_t d = 0; d < 256; d++) table_point(R[d], inf[d], Z[d], bx, by, d);
+      pre[0] = Z[0];
+      for (int d = 1; d < 256; d++) fe_mul(pre[d], pre[d - 1], Z[d]);
+      suf[255] = Z[255];
+      for (int d = 254; d >= 0; d--) fe_mul(suf[d], suf[d + 1], Z[d]);
+      fe inv;
+      fe_inv(inv, pre[255]);
+      for (uint32_t d = 0; d < 256; d++) {
+        fe zi = inv;
+        if (d > 0) fe_mul(zi, zi, pre[d - 1]);
+        if (d < 255) fe_mul(zi, zi, suf[d + 1]);
+        table_store(table, b, j, d, R[d], inf[d], zi);
+      }
+    }
+  }
+}
+
+template <class F>
+void parallel_for(uint64_t n, int nt, F f) {
+  if (nt < 1) nt = 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; t++)
+    th.emplace_back([=]() {
+      for (uint64_t i = t; i < n; i += nt) f(i);
+    });
+  for (auto &x : th) x.join();
+}
+
+template <class T>
+T *aligned(std::vector<uint8_t> &store, size_t bytes) {
+  store.assign(bytes + 64, 0);
+  uintptr_t p = ((uintptr_t)store.data() + 15) & ~(uintptr_t)15;
+  return (T *)p;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Same pipeline and mode choice as bv_api.cpp run_device, on the host.
+// force_mode: -1 = same rule as the library, 0 = generic, 1 = tables.
+int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint64_t *bits, int n_threads,
+                     int force_mode) {
+  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
+  const uint32_t n_keys = b->n_keys;
+  // device-style aligned + padded copies of the inputs
+  std::vector<uint8_t> s_msg, s_dig, s_kst, s_kxy, s_r, s_s, s_scr, s_u12, s_gt, s_kt, s_gxy;
+  const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
+  uint8_t *msg = aligned<uint8_t>(s_msg, msg_len + 64);
+  if (msg_len) memcpy(msg, b->msg_bytes, msg_len);
+  uint32_t *dig = aligned<uint32_t>(s_dig, (n_msgs + 1) * 32);
+  uint8_t *kst = aligned<uint8_t>(s_kst, n_keys + 1);
+  uint32_t *kxy = aligned<uint32_t>(s_kxy, (n_keys + 1) * 64ull);
+  uint32_t *r = aligned<uint32_t>(s_r, n_items * 32 + 32);
+  uint32_t *s = aligned<uint32_t>(s_s, n_items * 32 + 32);
+  if (n_items) {
+    memcpy(r, b->r_be, n_items * 32);
+    memcpy(s, b->s_be, n_items * 32);
+  }
+  uint32_t *scratch = aligned<uint32_t>(s_scr, n_items * 32 + 32);
+  uint32_t *u12 = aligned<uint32_t>(s_u12, n_items * 64 + 64);
+  parallel_for(n_msgs, n_threads, [&](uint64_t m) { sha256_one(m, msg, b->msg_off, dig); });
+  for (uint32_t k = 0; k < n_keys; k++) key_decode_one(k, b->key_bytes, b->key_off, kst, kxy);
+  const bool table_mode = force_mode >= 0 ? force_mode == 1 : (n_keys <= 8192 && n_items >= 16ull * n_keys);
+  // G table
+  uint32_t *gt = aligned<uint32_t>(s_gt, BV_TABLE_U32 * 4);
+  uint32_t *gxy = aligned<uint32_t>(s_gxy, 64);
+  static const uint32_t G[16] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu, 0xCE870B07u, 0x55A06295u,
+                                 0xF9DCBBACu, 0x79BE667Eu, 0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                                 0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+  memcpy(gxy, G, 64);
+  emu_build_tables(1, gxy, nullptr, gt);
+  uint32_t *kt = nullptr;
+  if (table_mode) {
+    kt = aligned<uint32_t>(s_kt, (uint64_t)(n_keys ? n_keys : 1) * BV_TABLE_U32 * 4);
+    emu_build_tables(n_keys, kxy, kst, kt);
+  }
+  const uint32_t M = 16;
+  const uint64_t T = ((n_items + M - 1) / M + 255) / 256 * 256;  // kernel grid size
+  parallel_for(T, n_threads, [&](uint64_t t) {
+    scalar_prep_thread(t, T, n_items, M, r, s, b->pre, b->item_msg, dig, scratch, u12);
+  });
+  std::vector<uint8_t> st(n_items + 1);
+  parallel_for(n_items, n_threads, [&](uint64_t i) {
+    st[i] = table_mode ? verify_item_tables(i, b->item_key, r, s, b->pre, kst, u12, gt, kt)
+                       : verify_item_generic(i, b->item_key, r, s, b->pre, kst, kxy, u12, gt);
+  });
+  if (msg_hash && n_msgs) memcpy(msg_hash, dig, n_msgs * 32);
+  if (status && n_items) memcpy(status, st.data(), n_items);
+  if (bits) {
+    const uint64_t nw = (n_items + 63) / 64;
+    memset(bits, 0, nw * 8);
+    for (uint64_t i = 0; i < n_items; i++)
+      if (st[i] == BV_ACCEPT) bits[i / 64] |= 1ull << (i % 64);
+  }
+  return table_mode ? 1 : 0;
+}
+
+// s^-1 mod N through the device chain (Montgomery in/out handled here).
+void emu_sc_inverse(const uint32_t s_le[8], uint32_t out_le[8]) {
+  sc s, sM, R2, inv, one, r;
+  for (int i = 0; i < 8; i++) s.v[i] = s_le[i];
+  sc_load_const(R2, SC_R2);
+  sc_mont(sM, s, R2);
+  sc_inverse(inv, sM);
+  for (int i = 0; i < 8; i++) one.v[i] = i == 0;
+  sc_mont(r, inv, one);
+  for (int i = 0; i < 8; i++) out_le[i] = r.v[i];
+}
+
+// a * b mod p, canonical (field arithmetic known-answer tests)
+void emu_fe_mul(const uint32_t a[8], const uint32_t b[8], uint32_t out[8]) {
+  fe x, y, z;
+  for (int i = 0; i < 8; i++) {
+    x.v[i] = a[i];
+    y.v[i] = b[i];
+  }
+  fe_mul(z, x, y);
+  fe_canon(z);
+  for (int i = 0; i < 8; i++) out[i] = z.v[i];
+}
+void emu_fe_sqr(const uint32_t a[8], uint32_t out[8]) {
+  fe x, z;
+  for (int i = 0; i < 8; i++) x.v[i] = a[i];
+  fe_sqr(z, x);
+  fe_canon(z);
+  for (int i = 0; i < 8; i++) out[i] = z.v[i];
+}
+void emu_fe_add(const uint32_t a[8], const uint32_t b[8], uint32_t out[8]) {
+  fe x, y, z;
+  for (int i = 0; i < 8; i++) {
+    x.v[i] = a[i];
+    y.v[i] = b[i];
+  }
+  fe_add(z, x, y);
+  fe_canon(z);
+  for (int i = 0; i < 8; i++) out[i] = z.v[i];
+}
+void emu_fe_sub(const uint32_t a[8], const uint32_t b[8], uint32_t out[8]) {
+  fe x, y, z;
+  for (int i = 0; i < 8; i++) {
+    x.v[i] = a[i];
+    y.v[i] = b[i];
+  }
+  fe_sub(z, x, y);
+  fe_canon(z);
+  for (int i = 0; i < 8; i++) out[i] = z.v[i];
+}
+void emu_fe_inv(const uint32_t a[8], uint32_t out[8]) {
+  fe x, z;
+  for (int i = 0; i < 8; i++) x.v[i] = a[i];
+  fe_inv(z, x);
+  fe_canon(z);
+  for (int i = 0; i < 8; i++) out[i] = z.v[i];
+}
+// a * b * R^-1 mod N
+void emu_sc_mont(const uint32_t a[8], const uint32_t b[8], uint32_t out[8]) {
+  sc x, y, z;
+  for (int i = 0; i < 8; i++) {
+    x.v[i] = a[i];
+    y.v[i] = b[i];
+  }
+  sc_mont(z, x, y);
+  for (int i = 0; i < 8; i++) out[i] = z.v[i];
+}
+
+}  // extern "C"
