@@ -247,9 +247,8 @@ static void read_timing(bv_ctx *ctx) {
   hipEvent_t *ev = ctx->ev;
   ctx->timing.ms_sha256 = hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess ? t : -1.f;
   ctx->timing.ms_keyprep = hipEventElapsedTime(&t, ev[1], ev[2]) == hipSuccess ? t : -1.f;
-  float prep = hipEventElapsedTime(&t, ev[2], ev[3]) == hipSuccess ? t : 0.f;
-  float ver = hipEventElapsedTime(&t, ev[3], ev[4]) == hipSuccess ? t : 0.f;
-  ctx->timing.ms_verify = prep + ver;
+  ctx->timing.ms_scalar = hipEventElapsedTime(&t, ev[2], ev[3]) == hipSuccess ? t : -1.f;
+  ctx->timing.ms_verify = hipEventElapsedTime(&t, ev[3], ev[4]) == hipSuccess ? t : -1.f;
   ctx->timing.ms_total = hipEventElapsedTime(&t, ev[0], ev[4]) == hipSuccess ? t : -1.f;
 }
 

@@ -96,7 +96,8 @@ typedef struct {
   float ms_total;   /* first kernel start -> last kernel end                  */
   float ms_sha256;  /* message hashing                                         */
   float ms_keyprep; /* key decode + per-key table build                        */
-  float ms_verify;  /* ECDSA verify kernel(s)                                  */
+  float ms_scalar;  /* k_scalar_prep: batched s^-1, u1, u2                     */
+  float ms_verify;  /* k_verify / k_verify_generic (point arithmetic)          */
   float ms_h2d;     /* host -> device staging (host-buffer entry point only)   */
   float ms_d2h;     /* device -> host results                                  */
 } bv_timing;

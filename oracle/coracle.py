@@ -35,6 +35,16 @@ class _Batch(ctypes.Structure):
     ]
 
 
+def default_threads() -> int:
+    """Host threads the oracle may use: this process's CPU affinity, capped at
+    16 (the GPU box's CPU share per GPU)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def build() -> str:
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
@@ -84,7 +94,7 @@ def verify_batch(arrs: dict, n_threads: int = 0):
     babble_amd.batch.pack layout).  Returns (msg_hash[n_msgs,32], status[n], bits)."""
     L = lib()
     if n_threads <= 0:
-        n_threads = os.cpu_count() or 1
+        n_threads = default_threads()
     b = _Batch()
     n_msgs = len(arrs["msg_off"]) - 1
     n_items = len(arrs["item_msg"])

@@ -448,6 +448,13 @@ int oracle_item_status(const uint8_t *pub, uint64_t publen, const uint8_t digest
   if (pre & BV_PRE_PARTS_BAD) return BV_REJECT_ERR;
   if (publen == 0) return BV_REF_PANIC;
   int rc = pre & 3, sc = (pre >> 2) & 3;
+  /* ABI rule (babbleverify.h): a class-OK value is re-checked against its
+   * bytes, so r = 0 reads as "<= 0" and r >= N as ">= N". */
+  uint64_t rv[4], sv[4];
+  u256_from_be(rv, r_be);
+  u256_from_be(sv, s_be);
+  if (rc == BV_SC_OK) rc = (rv[0] | rv[1] | rv[2] | rv[3]) == 0 ? BV_SC_NONPOS : (u256_ge(rv, SC_N) ? BV_SC_GE_N : BV_SC_OK);
+  if (sc == BV_SC_OK) sc = (sv[0] | sv[1] | sv[2] | sv[3]) == 0 ? BV_SC_NONPOS : (u256_ge(sv, SC_N) ? BV_SC_GE_N : BV_SC_OK);
   if (rc == BV_SC_NIL) return BV_REF_PANIC;
   if (rc == BV_SC_NONPOS) return BV_REJECT;
   if (sc == BV_SC_NIL) return BV_REF_PANIC;

@@ -62,7 +62,7 @@ def unop(name: str, a: int) -> int:
 
 def verify_batch(arrs: dict, n_threads: int = 0, force_mode: int = -1):
     L = lib()
-    n_threads = n_threads or (os.cpu_count() or 1)
+    n_threads = n_threads or min(16, len(os.sched_getaffinity(0)))
     keep = []
 
     def ptr(a, dt):

@@ -1,0 +1,93 @@
+"""Host build of the device per-unit source (tests/emu) against the oracle.
+
+The kernels' arithmetic (field.h, point.h, sha256.h, verify_core.h) is
+compiled for the CPU and replayed with kernels.hip's index mapping; these
+tests catch arithmetic and indexing bugs before any GPU run.  The GPU tests
+(test_gpu.py) then check the real kernels bit for bit.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from babble_amd import synth
+from oracle import coracle
+from oracle import gosemantics as gs
+from tests.emu import emu
+from tests.helpers import golden_items_batch
+
+P, N = gs.P, gs.N
+
+
+def test_field_arithmetic_known_answers():
+    rng = random.Random(3)
+    edge = [0, 1, 2, P - 1, P, P + 1, 2**256 - 1, 2**256 - 2, 2**256 - P, 977, 2**32, 2**255, 2**32 + 977]
+    vals = edge + [rng.getrandbits(256) for _ in range(200)]
+    for a in vals:
+        for b in rng.sample(vals, 6) + edge[:6]:
+            assert emu.binop("emu_fe_mul", a, b) == a * b % P
+            assert emu.binop("emu_fe_add", a, b) == (a + b) % P
+            assert emu.binop("emu_fe_sub", a, b) == (a - b) % P
+        assert emu.unop("emu_fe_sqr", a) == a * a % P
+    for a in vals[:30]:
+        if a % P:
+            assert emu.unop("emu_fe_inv", a) == pow(a, -1, P)
+
+
+def test_scalar_montgomery_and_inverse():
+    rng = random.Random(4)
+    R = 2**256
+    for _ in range(100):
+        a, b = rng.getrandbits(256), rng.randrange(N)  # a < R, b < N (the mont precondition)
+        assert emu.binop("emu_sc_mont", a, b) == a * b * pow(R, -1, N) % N
+    for s in [1, 2, N - 1, N - 2, (N + 1) // 2] + [rng.randrange(1, N) for _ in range(60)]:
+        assert emu.unop("emu_sc_inverse", s) == pow(s, -1, N)
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_golden_items(mode):
+    batch, expected, _ = golden_items_batch()
+    h, st, bits, m = emu.verify_batch(batch.as_dict(), force_mode=mode)
+    assert m == mode
+    assert np.array_equal(st, expected)
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_adversarial_mix(mode):
+    b = synth.adversarial(2500, seed=21, n_creators=4, scale_per_million=dict(
+        rflip=20000, sflip=20000, body=10000, highs=10000, range=8000, fmt=8000, key=12000))
+    h, st, bits = coracle.verify_batch(b.as_dict())
+    h2, st2, bits2, _ = emu.verify_batch(b.as_dict(), force_mode=mode)
+    assert np.array_equal(h, h2)
+    assert np.array_equal(st, st2)
+    assert np.array_equal(bits, bits2)
+    assert set(np.unique(st)) == {0, 1, 2, 3}
+
+
+def test_c1_hashgraph_10k_events():
+    """C1: 4 peers, 10k events in the InsertEvent play order; all ACCEPT."""
+    b = synth.events(10_000, n_creators=4, seed=1)
+    h2, st2, bits2, m = emu.verify_batch(b.as_dict())
+    assert m == 1 and np.all(st2 == 1)
+    for i in (0, 1, 5, 9999):
+        assert h2[i].tobytes() == gs.SHA256(b.message(i))
+
+
+def test_blocks_shared_messages():
+    wb = synth.blocks(6, n_validators=20, seed=5)
+    b = wb.batch
+    # invalidate 5 % of signatures
+    rng = np.random.default_rng(1)
+    bad = rng.choice(b.n_items, size=b.n_items // 20, replace=False)
+    b.s_be[bad, 31] ^= 1
+    h, st, bits = coracle.verify_batch(b.as_dict())
+    h2, st2, bits2, _ = emu.verify_batch(b.as_dict())
+    assert np.array_equal(st, st2) and np.array_equal(h, h2)
+    assert int((st2 == 0).sum()) == len(bad)
+
+
+def test_empty_and_ragged():
+    b = synth.events(67, n_creators=3, seed=8)
+    h, st, bits = coracle.verify_batch(b.as_dict())
+    h2, st2, bits2, _ = emu.verify_batch(b.as_dict())
+    assert np.array_equal(st, st2) and len(bits2) == 2 and np.array_equal(bits, bits2)

@@ -1,0 +1,225 @@
+"""Parity tests proper: the gfx950 kernels through the C ABI against the
+oracle (bit-exact statuses, digests and accept bits).  Run on the GPU box:
+    python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+"""
+import hashlib
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from babble_amd import native, synth
+from babble_amd.batch import BatchBuilder
+from oracle import coracle
+from oracle import gosemantics as gs
+from tests.helpers import bits_from_status, golden_items_batch, load
+
+pytestmark = pytest.mark.gpu
+
+MIX = dict(rflip=20000, sflip=20000, body=10000, highs=10000, range=8000, fmt=8000, key=12000)
+
+
+@pytest.fixture(scope="module")
+def verifier():
+    from babble_amd.verifier import Verifier
+
+    v = Verifier(device=0)
+    yield v
+    v.close()
+
+
+def check_against_oracle(v, b, device_api=False):
+    h, st, bits = coracle.verify_batch(b.as_dict())
+    if device_api:
+        d = v.to_device(b)
+        v.verify_device(d)
+        res = d.result()
+    else:
+        res = v.verify(b)
+    assert np.array_equal(res.msg_hash, h), "digests differ from oracle"
+    bad = np.flatnonzero(res.status != st)
+    assert bad.size == 0, f"{bad.size} statuses differ, first {bad[:8]}: gpu {res.status[bad[:8]]} oracle {st[bad[:8]]}"
+    assert np.array_equal(res.accept_bits, bits)
+    return res
+
+
+def test_golden_items(verifier):
+    batch, expected, _ = golden_items_batch()
+    res = verifier.verify(batch)
+    assert np.array_equal(res.status, expected)
+    assert np.array_equal(res.accept_bits, bits_from_status(expected))
+
+
+def test_golden_items_from_signature_text(verifier):
+    """Host path as the Go shim would drive it: signature text ->
+    bv_decode_signature -> device."""
+    items = load("golden_items.json")
+    bb = BatchBuilder()
+    for it in items:
+        m = bb.add_msg(bytes.fromhex(it["body"]))
+        k = bb.add_key(bytes.fromhex(it["pub"]))
+        bb.add_item(m, k, it["sig"].encode("utf-8"))
+    res = verifier.verify(bb.pack())
+    assert np.array_equal(res.status, np.array([it["status"] for it in items], np.uint8))
+
+
+def test_golden_sha256(verifier):
+    fx = load("golden_sha256.json")
+    msgs = [bytes.fromhex(e["msg"]) for e in fx]
+    got = verifier.sha256(msgs)
+    assert [g.hex() for g in got] == [e["digest"] for e in fx]
+
+
+def test_sha256_boundaries_and_alignment(verifier):
+    rng = np.random.default_rng(3)
+    msgs = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in
+            list(range(0, 300)) + [1 << 16, (1 << 20) + 3]]
+    got = verifier.sha256(msgs)
+    assert got == [hashlib.sha256(m).digest() for m in msgs]
+
+
+def test_golden_events_digests(verifier):
+    ev = load("golden_events.json")["events"]
+    got = verifier.sha256([e["json"].encode("latin-1") for e in ev])
+    assert [g.hex() for g in got] == [e["digest"] for e in ev]
+
+
+def test_c1_hashgraph(verifier):
+    b = synth.events(10_000, n_creators=4, seed=1)
+    res = check_against_oracle(verifier, b)
+    assert np.all(res.status == 1)
+
+
+@pytest.mark.parametrize("device_api", [False, True])
+def test_c4_adversarial_mix(verifier, device_api):
+    b = synth.adversarial(20_000, seed=4, scale_per_million=MIX)
+    res = check_against_oracle(verifier, b, device_api=device_api)
+    assert set(np.unique(res.status)) == {0, 1, 2, 3}
+
+
+def test_c4_adversarial_full_rate(verifier):
+    """C4 at 10^5 items with the exact per-million corruption mix."""
+    b = synth.adversarial(100_000, seed=44)
+    check_against_oracle(verifier, b)
+
+
+def test_generic_path_few_items_per_key(verifier):
+    """Keys with fewer than 16 items each take the per-lane path."""
+    b = synth.adversarial(640, seed=9, n_creators=64, scale_per_million=MIX)
+    assert b.n_items < 16 * b.n_keys
+    check_against_oracle(verifier, b)
+
+
+def test_c5_blocks_check_block(verifier):
+    wb = synth.blocks(200, n_validators=100, seed=5)
+    b = wb.batch
+    rng = np.random.default_rng(5)
+    bad = rng.choice(b.n_items, size=b.n_items // 20, replace=False)
+    b.s_be[bad, 7] ^= 0x40
+    res = check_against_oracle(verifier, b)
+    valid = res.status.reshape(wb.n_blocks, wb.n_validators).astype(bool).sum(axis=1)
+    tc = gs.trust_count(wb.n_validators)
+    assert np.all(valid > tc)
+    assert int(valid.sum()) == b.n_items - len(bad)
+
+
+def test_edge_sizes(verifier):
+    for n in (1, 63, 64, 65, 127, 129):
+        b = synth.events(n, n_creators=2, seed=n)
+        res = check_against_oracle(verifier, b)
+        assert len(res.accept_bits) == (n + 63) // 64
+
+
+def test_empty_batch(verifier):
+    b = BatchBuilder().pack()
+    res = verifier.verify(b)
+    assert res.status.size == 0 and res.msg_hash.size == 0
+
+
+def test_messages_without_items(verifier):
+    bb = BatchBuilder()
+    for n in (0, 5, 64, 200):
+        bb.add_msg(os.urandom(n))
+    res = verifier.verify(bb.pack())
+    assert [res.msg_hash[i].tobytes() for i in range(4)] == [hashlib.sha256(bb._msgs[i]).digest() for i in range(4)]
+
+
+def test_bad_index_rejected(verifier):
+    b = synth.events(10, n_creators=2, seed=3)
+    b.item_key[3] = 99
+    with pytest.raises(native.BvError):
+        verifier.verify(b)
+
+
+def test_full_size_properties(verifier):
+    """BASELINE size (1M events): every valid signature accepted, digests of a
+    sample equal hashlib, a seeded corrupted subset rejected exactly, and a
+    random sample agrees with the oracle."""
+    b = synth.events(1_000_000, n_creators=64, seed=2)
+    d = verifier.to_device(b)
+    verifier.verify_device(d)
+    res = d.result()
+    assert np.all(res.status == 1)
+    assert np.all(res.accept_bits == np.uint64(0xFFFFFFFFFFFFFFFF))
+    for i in np.random.default_rng(0).choice(b.n_items, 50, replace=False):
+        assert res.msg_hash[i].tobytes() == hashlib.sha256(b.message(int(i))).digest()
+    rng = np.random.default_rng(11)
+    bad = np.sort(rng.choice(b.n_items, 997, replace=False))
+    b.r_be[bad, 17] ^= 0x10
+    res2 = verifier.verify(b)
+    assert np.array_equal(np.flatnonzero(res2.status != 1), bad)
+    sample = np.sort(rng.choice(b.n_items, 3000, replace=False))
+    sub = dict(b.as_dict())
+    h, st, _ = coracle.verify_batch(dict(msg_bytes=sub["msg_bytes"], msg_off=sub["msg_off"],
+                                         key_bytes=sub["key_bytes"], key_off=sub["key_off"],
+                                         item_msg=sub["item_msg"][sample], item_key=sub["item_key"][sample],
+                                         r_be=sub["r_be"][sample], s_be=sub["s_be"][sample],
+                                         pre=sub["pre"][sample]))
+    assert np.array_equal(res2.status[sample], st)
+
+
+def test_reentrant_contexts():
+    from babble_amd.verifier import Verifier
+
+    b = synth.adversarial(3000, seed=31, n_creators=8, scale_per_million=MIX)
+    _, st, _ = coracle.verify_batch(b.as_dict())
+    out = {}
+
+    def run(k):
+        v = Verifier(0)
+        for _ in range(3):
+            out[k] = v.verify(b).status.copy()
+        v.close()
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for k in range(3):
+        assert np.array_equal(out[k], st)
+
+
+def test_shared_context_threads(verifier):
+    b = synth.events(5000, n_creators=8, seed=12)
+    errs = []
+
+    def run():
+        try:
+            for _ in range(3):
+                assert np.all(verifier.verify(b).status == 1)
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    th = [threading.Thread(target=run) for _ in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs
+
+
+def test_native_library_is_the_one_loaded():
+    maps = open("/proc/self/maps").read()
+    assert native.LIB_PATH in maps

@@ -1,0 +1,103 @@
+"""The oracle itself, pinned before it is trusted (CPU only).
+
+* SHA-256: FIPS 180-4 known answers + hashlib at every padding boundary.
+* secp256k1: generator/known multiples, C oracle == Python restatement ==
+  OpenSSL on well-formed items (OpenSSL is an independent implementation of
+  the verification equation ecdsa.Verify evaluates).
+* Every golden fixture re-derived by both oracles.
+"""
+import hashlib
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import coracle, openssl_xcheck
+from oracle import gosemantics as gs
+from tests.helpers import golden_items_batch, load
+
+N, P = gs.N, gs.P
+
+
+def test_sha256_golden_and_fips():
+    for e in load("golden_sha256.json"):
+        m = bytes.fromhex(e["msg"])
+        assert hashlib.sha256(m).hexdigest() == e["digest"]
+        assert gs.sha256_fips(m).hex() == e["digest"]
+        assert coracle.sha256(m).hex() == e["digest"]
+
+
+def test_sha256_random_lengths():
+    rng = random.Random(5)
+    for _ in range(200):
+        m = os.urandom(rng.randrange(0, 3000))
+        assert coracle.sha256(m) == hashlib.sha256(m).digest()
+
+
+def test_generator_known_multiples():
+    # 2G and 3G of secp256k1 (public known values)
+    g2 = (0xC6047F9441ED7D6D3045406E95C07CD85C778E4B8CEF3CA7ABAC09B95C709EE5,
+          0x1AE168FEA63DC339A3C58419466CEAEEF7F632653266D0E1236431A950CFE52A)
+    g3 = (0xF9308A019258C31049344F85F89D5229B531C845836F99B08601F113BCE036F9,
+          0x388F7B0F632DE8140FE337E62A37F3566500A99934C2231B6CB9FD7584B8E672)
+    assert gs.scalar_mult(1, gs.G) == gs.G
+    assert gs.scalar_mult(2, gs.G) == g2 == coracle.scalar_base_mult(2)
+    assert gs.scalar_mult(3, gs.G) == g3 == coracle.scalar_base_mult(3)
+    assert gs.scalar_mult(N - 1, gs.G) == (gs.GX, P - gs.GY) == coracle.scalar_base_mult(N - 1)
+    assert gs.scalar_mult(N, gs.G) is None
+    assert coracle.scalar_base_mult(0) is None
+    # no point with x = 0: 7 is not a square mod p (so (0,0) can be the identity)
+    assert pow(7, (P - 1) // 2, P) == P - 1
+
+
+def test_reference_demo_keys_decode():
+    """The four pubkeys of the reference's demo peers.json (data shipped with
+    the reference) decode as valid uncompressed secp256k1 points."""
+    for pk in load("reference_demo_peers.json"):
+        b = gs.DecodeFromString(pk["PubKeyHex"])
+        assert len(b) == 65 and gs.Unmarshal(b) is not None
+        assert coracle.lib().oracle_unmarshal(b, 65, None) == 1
+
+
+def _sign(d, digest, k):
+    R = gs.scalar_mult(k, gs.G)
+    r = R[0] % N
+    return r, pow(k, -1, N) * (int.from_bytes(digest, "big") + r * d) % N
+
+
+@pytest.mark.skipif(not openssl_xcheck.available(), reason="libcrypto not present")
+def test_c_oracle_python_oracle_openssl_agree():
+    rng = random.Random(9)
+    for i in range(40):
+        d = rng.randrange(1, N)
+        pub = gs.Marshal(gs.scalar_mult(d, gs.G))
+        dig = os.urandom(32)
+        r, s = _sign(d, dig, rng.randrange(1, N))
+        for rr, ss, dd in [(r, s, dig), (r, N - s, dig), (r ^ 4, s, dig), (r, s, bytes([dig[0] ^ 1]) + dig[1:])]:
+            if not (0 < rr < N):
+                continue
+            py = gs.item_status(pub, dd, rr, ss)
+            c = coracle.item_status(pub, dd, 0, rr.to_bytes(32, "big"), ss.to_bytes(32, "big"))
+            o = openssl_xcheck.verify(pub, dd, rr, ss)
+            assert py == c == (gs.ACCEPT if o else gs.REJECT)
+
+
+def test_golden_items_both_oracles():
+    batch, expected, items = golden_items_batch()
+    _, st, bits = coracle.verify_batch(batch.as_dict(), n_threads=4)
+    assert np.array_equal(st, expected)
+    for it in items[:: 7]:
+        pub = bytes.fromhex(it["pub"])
+        assert gs.item_status_from_sigstr(pub, gs.SHA256(bytes.fromhex(it["body"])), it["sig"]) == it["status"]
+
+
+def test_golden_events_and_blocks():
+    ev = load("golden_events.json")
+    for e in ev["events"]:
+        raw = e["json"].encode("latin-1")
+        assert hashlib.sha256(raw).hexdigest() == e["digest"]
+    bl = load("golden_blocks.json")
+    peers = [gs.Peer(PubKeyHex=gs.EncodeToString(bytes.fromhex(v))) for v in bl["validators"]]
+    assert gs.peer_set_hash(peers).hex() == bl["blocks"][0]["peers_hash"]
+    assert gs.trust_count(len(peers)) == bl["blocks"][0]["trust_count"] == 4
