@@ -1,10 +1,11 @@
 // bv_api.cpp — host side of libbabbleverify.so: the C ABI declared in
 // include/babbleverify.h.
 //
-// One bv_ctx owns a HIP stream, the precomputed G table (built on the device
-// at bv_create, kept resident in HBM) and growable device work buffers.
-// bv_verify_batch stages host buffers to HBM and runs the same device
-// pipeline as bv_verify_batch_device.  There is no CPU fallback: a missing or
+// One bv_ctx owns two HIP streams (main + keys), the generator table (16-bit
+// windows, 64 MiB, built on the device at bv_create and kept resident in
+// HBM) and growable device work buffers.  bv_verify_batch stages host
+// buffers to HBM and runs the same device pipeline as
+// bv_verify_batch_device.  There is no CPU fallback: a missing or
 // non-gfx950 device is BV_E_NODEVICE.
 #include <hip/hip_runtime.h>
 
@@ -19,11 +20,13 @@
 namespace bvk {
 hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
 hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
-hipError_t build_tables(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *);
+hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *);
 hipError_t scalar_prep(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint32_t *, const uint8_t *,
                        const uint32_t *, const uint32_t *, uint32_t *, uint32_t *);
-hipError_t verify(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
-                  const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
+hipError_t verify_g(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
+                    const uint8_t *, const uint32_t *, const uint32_t *, uint32_t *);
+hipError_t verify_q(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
+                    const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
 hipError_t verify_generic(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
                           const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
                           uint8_t *, uint64_t *);
@@ -31,10 +34,13 @@ hipError_t verify_generic(hipStream_t, uint64_t, const uint32_t *, const uint32_
 
 namespace {
 
-constexpr uint64_t kTableEntries = 32ull * 256ull;             // per base point
-constexpr uint64_t kTableBytes = kTableEntries * 64ull;         // 512 KiB
-constexpr uint32_t kMaxTableKeys = 8192;                        // 4 GiB of key tables
-constexpr uint32_t kPrepM = 16;                                 // items per s^-1 batch
+constexpr int kGW = 16;                                                 // generator window bits
+constexpr int kKW = 8;                                                  // key window bits
+constexpr uint64_t kGTableBytes = (256 / kGW) * (1ull << kGW) * 64ull;  // 64 MiB
+constexpr uint64_t kKTableBytes = (256 / kKW) * (1ull << kKW) * 64ull;  // 512 KiB per key
+constexpr uint32_t kMaxTableKeys = 8192;                                // 4 GiB of key tables
+constexpr uint32_t kPrepM = 16;                                         // items per s^-1 batch
+constexpr uint32_t kRgWords = 25;                                       // R_G words per item
 
 struct DevBuf {
   void *p = nullptr;
@@ -68,20 +74,25 @@ struct DevBuf {
   }
 };
 
+// timing events (see read_timing)
+enum { E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_COUNT };
+
 }  // namespace
 
 struct bv_ctx {
   int device = 0;
   uint32_t flags = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // main
+  hipStream_t kstream = nullptr;  // key tables
   std::mutex mu;
   std::string err;
   DevBuf g_table, g_xy, g_bases;
   // staging for the host entry point
   DevBuf h_msg_bytes, h_msg_off, h_key_bytes, h_key_off, h_item_msg, h_item_key, h_r, h_s, h_pre;
   // work buffers
-  DevBuf digests, kstatus, kxy, bases_jac, key_table, scratch, u12, status, bits;
-  hipEvent_t ev[8] = {};
+  DevBuf digests, kstatus, kxy, bases_jac, key_table, scratch, u12, rg, status, bits;
+  hipEvent_t ev[E_COUNT] = {};
+  bool table_mode = false;
   bv_timing timing = {};
 };
 
@@ -97,9 +108,9 @@ static int fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess
   return code;
 }
 
-#define HIPCHK(expr, code, what)                  \
-  do {                                            \
-    hipError_t _e = (expr);                       \
+#define HIPCHK(expr, code, what)                            \
+  do {                                                      \
+    hipError_t _e = (expr);                                 \
     if (_e != hipSuccess) return fail(ctx, code, what, _e); \
   } while (0)
 
@@ -112,6 +123,31 @@ static const uint8_t kGenerator[64] = {
 extern "C" int bv_abi_version(void) { return BV_ABI_VERSION; }
 
 extern "C" const char *bv_last_error(const bv_ctx *ctx) { return ctx ? ctx->err.c_str() : "null ctx"; }
+
+extern "C" void bv_destroy(bv_ctx *ctx);
+
+static int create_impl(bv_ctx *ctx) {
+  HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
+  HIPCHK(hipStreamCreateWithFlags(&ctx->kstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
+  for (auto &e : ctx->ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
+  // G table: T[j][d] = d * 2^(16j) * G, built once on the device.
+  HIPCHK(ctx->g_table.ensure(kGTableBytes), BV_E_OOM, "alloc G table");
+  HIPCHK(ctx->g_xy.ensure(64), BV_E_OOM, "alloc G");
+  HIPCHK(ctx->g_bases.ensure((256 / kGW) * 24 * 4), BV_E_OOM, "alloc G bases");
+  uint32_t gxy[16];
+  for (int half = 0; half < 2; half++)
+    for (int i = 0; i < 8; i++) {
+      const uint8_t *q = kGenerator + 32 * half + 4 * (7 - i);
+      gxy[8 * half + i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    }
+  HIPCHK(hipMemcpyAsync(ctx->g_xy.p, gxy, sizeof gxy, hipMemcpyHostToDevice, ctx->stream), BV_E_LAUNCH, "copy G");
+  HIPCHK(bvk::build_tables(ctx->stream, kGW, 1, ctx->g_xy.as<uint32_t>(), nullptr, ctx->g_bases.as<uint32_t>(),
+                           ctx->g_table.as<uint32_t>()),
+         BV_E_LAUNCH, "G table");
+  HIPCHK(hipStreamSynchronize(ctx->stream), BV_E_LAUNCH, "G table sync");
+  return BV_OK;
+}
 
 extern "C" int bv_create(bv_ctx **out, int device, uint32_t flags) {
   if (!out) return BV_E_ARGS;
@@ -128,24 +164,11 @@ extern "C" int bv_create(bv_ctx **out, int device, uint32_t flags) {
   bv_ctx *ctx = new bv_ctx();
   ctx->device = device;
   ctx->flags = flags;
-  HIPCHK(hipSetDevice(device), BV_E_NODEVICE, "hipSetDevice");
-  HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
-  for (auto &e : ctx->ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
-  // G table: T[j][d] = d * 2^(8j) * G, built once on the device.
-  HIPCHK(ctx->g_table.ensure(kTableBytes), BV_E_OOM, "alloc G table");
-  HIPCHK(ctx->g_xy.ensure(64), BV_E_OOM, "alloc G");
-  HIPCHK(ctx->g_bases.ensure(32 * 24 * 4), BV_E_OOM, "alloc G bases");
-  uint32_t gxy[16];
-  for (int half = 0; half < 2; half++)
-    for (int i = 0; i < 8; i++) {
-      const uint8_t *q = kGenerator + 32 * half + 4 * (7 - i);
-      gxy[8 * half + i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
-    }
-  HIPCHK(hipMemcpyAsync(ctx->g_xy.p, gxy, sizeof gxy, hipMemcpyHostToDevice, ctx->stream), BV_E_LAUNCH, "copy G");
-  HIPCHK(bvk::build_tables(ctx->stream, 1, ctx->g_xy.as<uint32_t>(), nullptr, ctx->g_bases.as<uint32_t>(),
-                           ctx->g_table.as<uint32_t>()),
-         BV_E_LAUNCH, "G table");
-  HIPCHK(hipStreamSynchronize(ctx->stream), BV_E_LAUNCH, "G table sync");
+  int rc = create_impl(ctx);
+  if (rc != BV_OK) {
+    bv_destroy(ctx);
+    return rc;
+  }
   *out = ctx;
   return BV_OK;
 }
@@ -154,13 +177,16 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  DevBuf *bufs[] = {&ctx->g_table, &ctx->g_xy, &ctx->g_bases, &ctx->h_msg_bytes, &ctx->h_msg_off,
-                    &ctx->h_key_bytes, &ctx->h_key_off, &ctx->h_item_msg, &ctx->h_item_key, &ctx->h_r,
-                    &ctx->h_s, &ctx->h_pre, &ctx->digests, &ctx->kstatus, &ctx->kxy, &ctx->bases_jac,
-                    &ctx->key_table, &ctx->scratch, &ctx->u12, &ctx->status, &ctx->bits};
+  if (ctx->kstream) (void)hipStreamSynchronize(ctx->kstream);
+  DevBuf *bufs[] = {&ctx->g_table,     &ctx->g_xy,      &ctx->g_bases,    &ctx->h_msg_bytes, &ctx->h_msg_off,
+                    &ctx->h_key_bytes, &ctx->h_key_off, &ctx->h_item_msg, &ctx->h_item_key,  &ctx->h_r,
+                    &ctx->h_s,         &ctx->h_pre,     &ctx->digests,    &ctx->kstatus,     &ctx->kxy,
+                    &ctx->bases_jac,   &ctx->key_table, &ctx->scratch,    &ctx->u12,         &ctx->rg,
+                    &ctx->status,      &ctx->bits};
   for (auto *b : bufs) b->release();
   for (auto &e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->kstream) (void)hipStreamDestroy(ctx->kstream);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -177,11 +203,13 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
                       hipStream_t st) {
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
-  if (n_items > 0 && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be)) return fail(ctx, BV_E_ARGS, "null item arrays");
+  if (n_items > 0 && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be))
+    return fail(ctx, BV_E_ARGS, "null item arrays");
   if (n_msgs > 0 && (!b->msg_bytes || !b->msg_off)) return fail(ctx, BV_E_ARGS, "null msg arrays");
   if (n_items > 0 && n_keys == 0) return fail(ctx, BV_E_ARGS, "items without keys");
-  if (n_keys > 0 && (!b->key_off)) return fail(ctx, BV_E_ARGS, "null key_off");
-  if (((uintptr_t)b->r_be | (uintptr_t)b->s_be) & 3) return fail(ctx, BV_E_ARGS, "r_be/s_be must be 4-byte aligned");
+  if (n_keys > 0 && !b->key_off) return fail(ctx, BV_E_ARGS, "null key_off");
+  if (((uintptr_t)b->r_be | (uintptr_t)b->s_be) & 15)
+    return fail(ctx, BV_E_ARGS, "r_be/s_be must be 16-byte aligned");
 
   uint32_t *dig = (uint32_t *)d_msg_hash;
   if (!dig || ((uintptr_t)dig & 15)) {
@@ -206,50 +234,71 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
   // Per-key fixed-base tables pay off once a key signs enough items; with
   // few items per key the generic per-lane path is cheaper.
   const bool table_mode = n_keys <= kMaxTableKeys && n_items >= 16ull * n_keys;
+  ctx->table_mode = table_mode;
   if (table_mode) {
-    HIPCHK(ctx->bases_jac.ensure(std::max<uint32_t>(n_keys, 1) * 32ull * 96ull), BV_E_OOM, "alloc bases");
-    HIPCHK(ctx->key_table.ensure(std::max<uint32_t>(n_keys, 1) * kTableBytes), BV_E_OOM, "alloc key tables");
+    HIPCHK(ctx->bases_jac.ensure(std::max<uint32_t>(n_keys, 1) * (256 / kKW) * 96ull), BV_E_OOM, "alloc bases");
+    HIPCHK(ctx->key_table.ensure(std::max<uint32_t>(n_keys, 1) * kKTableBytes), BV_E_OOM, "alloc key tables");
+    HIPCHK(ctx->rg.ensure(std::max<uint64_t>(n_items, 1) * kRgWords * 4), BV_E_OOM, "alloc R_G");
   }
 
   hipEvent_t *ev = ctx->ev;
-  HIPCHK(hipEventRecord(ev[0], st), BV_E_LAUNCH, "event");
-  HIPCHK(bvk::sha256(st, n_msgs, b->msg_bytes, b->msg_off, dig), BV_E_LAUNCH, "k_sha256");
-  HIPCHK(hipEventRecord(ev[1], st), BV_E_LAUNCH, "event");
+  const uint32_t *r32 = (const uint32_t *)b->r_be, *s32 = (const uint32_t *)b->s_be;
+  HIPCHK(hipEventRecord(ev[E_START], st), BV_E_LAUNCH, "event");
   HIPCHK(bvk::key_decode(st, n_keys, b->key_bytes, b->key_off, ctx->kstatus.as<uint8_t>(), ctx->kxy.as<uint32_t>()),
          BV_E_LAUNCH, "k_key_decode");
-  if (table_mode)
-    HIPCHK(bvk::build_tables(st, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
+  HIPCHK(hipEventRecord(ev[E_FORK], st), BV_E_LAUNCH, "event");
+  if (table_mode) {  // key tables on the keys stream, concurrent with the main stream below
+    HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_FORK], 0), BV_E_LAUNCH, "fork");
+    HIPCHK(bvk::build_tables(ctx->kstream, kKW, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
                              ctx->bases_jac.as<uint32_t>(), ctx->key_table.as<uint32_t>()),
            BV_E_LAUNCH, "key tables");
-  HIPCHK(hipEventRecord(ev[2], st), BV_E_LAUNCH, "event");
-  HIPCHK(bvk::scalar_prep(st, n_items, kPrepM, (const uint32_t *)b->r_be, (const uint32_t *)b->s_be, b->pre,
-                          b->item_msg, dig, ctx->scratch.as<uint32_t>(), ctx->u12.as<uint32_t>()),
+    HIPCHK(hipEventRecord(ev[E_KEYS], ctx->kstream), BV_E_LAUNCH, "event");
+  }
+  HIPCHK(bvk::sha256(st, n_msgs, b->msg_bytes, b->msg_off, dig), BV_E_LAUNCH, "k_sha256");
+  HIPCHK(hipEventRecord(ev[E_SHA], st), BV_E_LAUNCH, "event");
+  HIPCHK(bvk::scalar_prep(st, n_items, kPrepM, r32, s32, b->pre, b->item_msg, dig, ctx->scratch.as<uint32_t>(),
+                          ctx->u12.as<uint32_t>()),
          BV_E_LAUNCH, "k_scalar_prep");
-  HIPCHK(hipEventRecord(ev[3], st), BV_E_LAUNCH, "event");
-  if (table_mode)
-    HIPCHK(bvk::verify(st, n_items, b->item_key, (const uint32_t *)b->r_be, (const uint32_t *)b->s_be, b->pre,
-                       ctx->kstatus.as<uint8_t>(), ctx->u12.as<uint32_t>(), ctx->g_table.as<uint32_t>(),
-                       ctx->key_table.as<uint32_t>(), status, bits),
-           BV_E_LAUNCH, "k_verify");
-  else
-    HIPCHK(bvk::verify_generic(st, n_items, b->item_key, (const uint32_t *)b->r_be, (const uint32_t *)b->s_be,
-                               b->pre, ctx->kstatus.as<uint8_t>(), ctx->kxy.as<uint32_t>(), ctx->u12.as<uint32_t>(),
-                               ctx->g_table.as<uint32_t>(), status, bits),
+  HIPCHK(hipEventRecord(ev[E_SCALAR], st), BV_E_LAUNCH, "event");
+  if (table_mode) {
+    HIPCHK(bvk::verify_g(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(),
+                         ctx->u12.as<uint32_t>(), ctx->g_table.as<uint32_t>(), ctx->rg.as<uint32_t>()),
+           BV_E_LAUNCH, "k_verify_g");
+    HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
+    HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
+    HIPCHK(bvk::verify_q(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(),
+                         ctx->u12.as<uint32_t>(), ctx->key_table.as<uint32_t>(), ctx->rg.as<uint32_t>(), status,
+                         bits),
+           BV_E_LAUNCH, "k_verify_q");
+  } else {
+    HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
+    HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
+    HIPCHK(bvk::verify_generic(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(),
+                               ctx->kxy.as<uint32_t>(), ctx->u12.as<uint32_t>(), ctx->g_table.as<uint32_t>(), status,
+                               bits),
            BV_E_LAUNCH, "k_verify_generic");
-  HIPCHK(hipEventRecord(ev[4], st), BV_E_LAUNCH, "event");
+  }
+  HIPCHK(hipEventRecord(ev[E_END], st), BV_E_LAUNCH, "event");
   if (d_msg_hash && (uint8_t *)dig != d_msg_hash)
     HIPCHK(hipMemcpyAsync(d_msg_hash, dig, n_msgs * 32, hipMemcpyDeviceToDevice, st), BV_E_LAUNCH, "copy digests");
   return BV_OK;
 }
 
-static void read_timing(bv_ctx *ctx) {
+static float elapsed(hipEvent_t a, hipEvent_t b) {
   float t;
+  return hipEventElapsedTime(&t, a, b) == hipSuccess ? t : -1.f;
+}
+
+static void read_timing(bv_ctx *ctx) {
   hipEvent_t *ev = ctx->ev;
-  ctx->timing.ms_sha256 = hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess ? t : -1.f;
-  ctx->timing.ms_keyprep = hipEventElapsedTime(&t, ev[1], ev[2]) == hipSuccess ? t : -1.f;
-  ctx->timing.ms_scalar = hipEventElapsedTime(&t, ev[2], ev[3]) == hipSuccess ? t : -1.f;
-  ctx->timing.ms_verify = hipEventElapsedTime(&t, ev[3], ev[4]) == hipSuccess ? t : -1.f;
-  ctx->timing.ms_total = hipEventElapsedTime(&t, ev[0], ev[4]) == hipSuccess ? t : -1.f;
+  bv_timing &t = ctx->timing;
+  t.ms_sha256 = elapsed(ev[E_FORK], ev[E_SHA]);
+  t.ms_keyprep = ctx->table_mode ? elapsed(ev[E_START], ev[E_KEYS]) : elapsed(ev[E_START], ev[E_FORK]);
+  t.ms_scalar = elapsed(ev[E_SHA], ev[E_SCALAR]);
+  t.ms_verify_g = elapsed(ev[E_SCALAR], ev[E_G]);
+  t.ms_verify = elapsed(ev[E_JOINED], ev[E_END]);
+  t.ms_total = elapsed(ev[E_START], ev[E_END]);
 }
 
 extern "C" int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresult, void *stream,
@@ -274,9 +323,14 @@ extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   hipStream_t st = ctx->stream;
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
+  if ((n_msgs && (!b->msg_off || !b->msg_bytes)) || (n_keys && (!b->key_off || !b->key_bytes)) ||
+      (n_items && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be)))
+    return fail(ctx, BV_E_ARGS, "null input array");
   const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
   const uint64_t key_len = n_keys ? b->key_off[n_keys] : 0;
   // validate host offsets (a bad offset must not become an OOB device read)
+  if (n_msgs && b->msg_off[0] != 0) return fail(ctx, BV_E_ARGS, "msg_off[0] != 0");
+  if (n_keys && b->key_off[0] != 0) return fail(ctx, BV_E_ARGS, "key_off[0] != 0");
   for (uint64_t m = 0; m < n_msgs; m++)
     if (b->msg_off[m] > b->msg_off[m + 1]) return fail(ctx, BV_E_ARGS, "msg_off not monotone");
   for (uint32_t k = 0; k < n_keys; k++)
@@ -325,7 +379,6 @@ extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   d.pre = b->pre ? ctx->h_pre.as<uint8_t>() : nullptr;
   int rc = run_device(ctx, &d, nullptr, nullptr, nullptr, st);
   if (rc != BV_OK) return rc;
-  HIPCHK(hipEventRecord(e1, st), BV_E_LAUNCH, "event");
   if (res->msg_hash && n_msgs)
     HIPCHK(hipMemcpyAsync(res->msg_hash, ctx->digests.p, n_msgs * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
            "d2h digests");
@@ -334,11 +387,11 @@ extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   if (res->accept_bits && n_items)
     HIPCHK(hipMemcpyAsync(res->accept_bits, ctx->bits.p, (n_items + 63) / 64 * 8, hipMemcpyDeviceToHost, st),
            BV_E_LAUNCH, "d2h bits");
+  HIPCHK(hipEventRecord(e1, st), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "verify sync");
   read_timing(ctx);
-  float t;
-  if (hipEventElapsedTime(&t, e0, ctx->ev[0]) == hipSuccess) ctx->timing.ms_h2d = t;
-  if (hipEventElapsedTime(&t, ctx->ev[4], e1) == hipSuccess) ctx->timing.ms_d2h = t;
+  ctx->timing.ms_h2d = elapsed(e0, ctx->ev[E_START]);
+  ctx->timing.ms_d2h = elapsed(ctx->ev[E_END], e1);
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return BV_OK;
@@ -350,6 +403,7 @@ extern "C" int bv_sha256_batch(bv_ctx *ctx, uint64_t n_msgs, const uint8_t *msg_
   if (n_msgs == 0) return BV_OK;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  if (msg_off[0] != 0) return fail(ctx, BV_E_ARGS, "msg_off[0] != 0");
   for (uint64_t m = 0; m < n_msgs; m++)
     if (msg_off[m] > msg_off[m + 1]) return fail(ctx, BV_E_ARGS, "msg_off not monotone");
   hipStream_t st = ctx->stream;

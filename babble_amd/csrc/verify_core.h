@@ -10,10 +10,14 @@
 #include "point.h"
 #include "sha256.h"
 
-#define BV_NWIN 32       // 8-bit windows over a 256-bit scalar
-#define BV_WSIZE 256     // entries per window (entry 0 unused)
+// Fixed-base tables: T[j][d] = d * 2^(W j) * P (affine, 64 bytes), d < 2^W.
+// The generator table is built once per context with wide windows; key
+// tables are built per batch with 8-bit windows (cheap to build).
 #define BV_ENTRY_U32 16  // affine x, y = 16 words (64 bytes)
-#define BV_TABLE_U32 ((uint64_t)BV_NWIN * BV_WSIZE * BV_ENTRY_U32)
+#define BV_GW 16         // G window bits: 16 windows x 65536 entries (64 MiB)
+#define BV_KW 8          // key window bits: 32 windows x 256 entries (512 KiB)
+#define BV_NWIN(w) (256 / (w))
+#define BV_TABLE_U32(w) ((uint64_t)BV_NWIN(w) * (1ull << (w)) * BV_ENTRY_U32)
 
 // key status (k_key_decode output)
 #define KS_OK 0
@@ -125,21 +129,23 @@ DEV void key_decode_one(uint32_t k, const uint8_t *kbytes, const uint64_t *koff,
 }
 
 // ---------------------------------------------------------------------------
-// Fixed-base tables.  T[b][j][d] = d * 2^(8j) * P_b (affine), d in 1..255.
+// Fixed-base tables
 // ---------------------------------------------------------------------------
-// B_j = 2^(8j) P_b (Jacobian), j = 0..31: a serial doubling chain per base.
-DEV void table_bases_one(uint32_t b, const uint32_t *bxy, uint32_t *bases_jac) {
+// B_j = 2^(w j) P_b (Jacobian, 24 words each), j < 256/w: a serial doubling
+// chain per base.
+DEV void table_bases_one(uint32_t b, const uint32_t *bxy, uint32_t *bases_jac, int w) {
+  const int nwin = 256 / w;
   gej P;
   fe_load(P.X, bxy + 16 * b);
   fe_load(P.Y, bxy + 16 * b + 8);
   fe_set(P.Z, 1);
-  uint32_t *out = bases_jac + (uint64_t)b * BV_NWIN * 24;
-  for (int j = 0; j < BV_NWIN; j++) {
+  uint32_t *out = bases_jac + (uint64_t)b * nwin * 24;
+  for (int j = 0; j < nwin; j++) {
     fe_store(out + 24 * j, P.X);
     fe_store(out + 24 * j + 8, P.Y);
     fe_store(out + 24 * j + 16, P.Z);
-    if (j + 1 < BV_NWIN) {
-      for (int k = 0; k < 8; k++) gej_double(P, P);
+    if (j + 1 < nwin) {
+      for (int k = 0; k < w; k++) gej_double(P, P);
     }
   }
 }
@@ -156,14 +162,14 @@ DEV void jac_to_affine(fe &x, fe &y, const uint32_t *jac) {
   fe_mul(y, Y, zi3);
 }
 
-// d * B (B affine), MSB-first double-and-add over the 8 bits of d.  The
+// d * B (B affine), MSB-first double-and-add over `bits` bits of d.  The
 // returned Z is 1 for d == 0 so it can join a batch inversion.
-DEV void table_point(gej &R, bool &inf, fe &Z, const fe &bx, const fe &by, uint32_t d) {
+DEV void table_point(gej &R, bool &inf, fe &Z, const fe &bx, const fe &by, uint32_t d, int bits) {
   inf = true;
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
   fe_set(R.Z, 0);
-  for (int bit = 7; bit >= 0; bit--) {
+  for (int bit = bits - 1; bit >= 0; bit--) {
     if (!inf) gej_double(R, R);
     if ((d >> bit) & 1) gej_add_ge(R, inf, bx, by);
   }
@@ -171,8 +177,8 @@ DEV void table_point(gej &R, bool &inf, fe &Z, const fe &bx, const fe &by, uint3
   else Z = R.Z;
 }
 
-// Store entry d given Z^-1 (canonical affine; d == 0 stored as zeros).
-DEV void table_store(uint32_t *table, uint32_t b, uint32_t j, uint32_t d, const gej &R, bool inf, const fe &zi) {
+// Store one entry given Z^-1 (canonical affine; d == 0 stored as zeros).
+DEV void table_store(uint32_t *entry, uint32_t d, const gej &R, bool inf, const fe &zi) {
   fe zi2, zi3, x, y;
   fe_sqr(zi2, zi);
   fe_mul(zi3, zi2, zi);
@@ -190,7 +196,7 @@ DEV void table_store(uint32_t *table, uint32_t b, uint32_t j, uint32_t d, const 
     v[i] = x.v[i];
     v[8 + i] = y.v[i];
   }
-  store16(table + (((uint64_t)b * BV_NWIN + j) * BV_WSIZE + d) * BV_ENTRY_U32, v);
+  store16(entry, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -314,6 +320,14 @@ DEV uint8_t classify(uint8_t pre, uint8_t ks, const fe &r, const fe &s) {
   return 0xFF;
 }
 
+DEV uint8_t classify_item(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
+                          const uint8_t *pre, const uint8_t *kstatus, fe &r) {
+  fe s;
+  fe_load_be_words(r, r_be + 8 * i);
+  fe_load_be_words(s, s_be + 8 * i);
+  return classify(pre ? pre[i] : 0, kstatus[item_key[i]], r, s);
+}
+
 // x(R) mod N == r, projectively: X == r Z^2, or (r + N < p and X == (r+N) Z^2)
 DEV bool final_check(const gej &R, bool inf, const fe &r) {
   if (inf) return false;
@@ -332,12 +346,21 @@ DEV bool final_check(const gej &R, bool inf, const fe &r) {
   return false;
 }
 
-// R += sum_j T[j][digit_j(u)] over the 32 byte-digits of the 256-bit u.
+// W-bit digit j of the 256-bit little-endian limb array u (W divides 32 or
+// is 16/8).
+template <int W>
+DEV uint32_t digit(const uint32_t *u, int j) {
+  const int bit = j * W;
+  return (u[bit >> 5] >> (bit & 31)) & ((1u << W) - 1u);
+}
+
+// R += sum_j T[j][digit_j(u)] over the 256/W digits of u.
+template <int W>
 DEV void table_add(gej &R, bool &inf, const uint32_t *tab, const uint32_t *u) {
-  for (int j = 0; j < BV_NWIN; j++) {
-    const uint32_t d = (u[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+  for (int j = 0; j < BV_NWIN(W); j++) {
+    const uint32_t d = digit<W>(u, j);
     if (d) {
-      const uint32_t *e = tab + ((uint64_t)j * BV_WSIZE + d) * BV_ENTRY_U32;
+      const uint32_t *e = tab + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
       fe x, y;
       fe_load4(x, e);
       fe_load4(y, e + 8);
@@ -346,37 +369,66 @@ DEV void table_add(gej &R, bool &inf, const uint32_t *tab, const uint32_t *u) {
   }
 }
 
-DEV void load_u12(uint32_t u[16], const uint32_t *u12, uint64_t i) {
-  const uint4 *q = (const uint4 *)(u12 + 16 * i);
-#pragma unroll
-  for (int c = 0; c < 4; c++) {
-    uint4 v = q[c];
-    u[4 * c] = v.x;
-    u[4 * c + 1] = v.y;
-    u[4 * c + 2] = v.z;
-    u[4 * c + 3] = v.w;
-  }
+DEV void load_u(uint32_t u[8], const uint32_t *u12, uint64_t i, int half) {
+  const uint4 *q = (const uint4 *)(u12 + 16 * i + 8 * half);
+  uint4 a = q[0], b = q[1];
+  u[0] = a.x; u[1] = a.y; u[2] = a.z; u[3] = a.w;
+  u[4] = b.x; u[5] = b.y; u[6] = b.z; u[7] = b.w;
 }
 
-// One signature item with per-key tables: R = u1 G + u2 Q as 64 mixed adds.
-DEV uint8_t verify_item_tables(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
-                               const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12,
-                               const uint32_t *g_table, const uint32_t *key_table) {
-  const uint32_t k = item_key[i];
-  fe r, s;
-  fe_load_be_words(r, r_be + 8 * i);
-  fe_load_be_words(s, s_be + 8 * i);
-  uint8_t st = classify(pre ? pre[i] : 0, kstatus[k], r, s);
-  if (st != 0xFF) return st;
-  uint32_t u[16];
-  load_u12(u, u12, i);
+// Partial point R_G = u1 G, kept in HBM between k_verify_g and k_verify_q as
+// 25 SoA words per item (X, Y, Z limbs, inf flag) for coalesced access.
+#define RG_WORDS 25
+DEV void rg_store(uint32_t *rg, uint64_t n, uint64_t i, const gej &R, bool inf) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    rg[(uint64_t)k * n + i] = R.X.v[k];
+    rg[(uint64_t)(8 + k) * n + i] = R.Y.v[k];
+    rg[(uint64_t)(16 + k) * n + i] = R.Z.v[k];
+  }
+  rg[(uint64_t)24 * n + i] = inf ? 1u : 0u;
+}
+DEV void rg_load(const uint32_t *rg, uint64_t n, uint64_t i, gej &R, bool &inf) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    R.X.v[k] = rg[(uint64_t)k * n + i];
+    R.Y.v[k] = rg[(uint64_t)(8 + k) * n + i];
+    R.Z.v[k] = rg[(uint64_t)(16 + k) * n + i];
+  }
+  inf = rg[(uint64_t)24 * n + i] != 0;
+}
+
+// Phase 1 (overlaps the key-table build): R_G = u1 G for items that reach
+// the math.
+DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
+                       const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12, const uint32_t *g_table,
+                       uint32_t *rg) {
+  fe r;
+  if (classify_item(i, item_key, r_be, s_be, pre, kstatus, r) != 0xFF) return;
+  uint32_t u[8];
+  load_u(u, u12, i, 0);
   gej R;
   bool inf = true;
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
   fe_set(R.Z, 0);
-  table_add(R, inf, g_table, u);
-  table_add(R, inf, key_table + (uint64_t)k * BV_TABLE_U32, u + 8);
+  table_add<BV_GW>(R, inf, g_table, u);
+  rg_store(rg, n, i, R, inf);
+}
+
+// Phase 2: R = R_G + u2 Q with the key's table; final check -> status.
+DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
+                          const uint32_t *s_be, const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12,
+                          const uint32_t *key_table, const uint32_t *rg) {
+  fe r;
+  const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
+  if (st != 0xFF) return st;
+  uint32_t u[8];
+  load_u(u, u12, i, 1);
+  gej R;
+  bool inf;
+  rg_load(rg, n, i, R, inf);
+  table_add<BV_KW>(R, inf, key_table + (uint64_t)item_key[i] * BV_TABLE_U32(BV_KW), u);
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
 }
 
@@ -384,14 +436,13 @@ DEV uint8_t verify_item_tables(uint64_t i, const uint32_t *item_key, const uint3
 DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
                                 const uint8_t *pre, const uint8_t *kstatus, const uint32_t *kxy,
                                 const uint32_t *u12, const uint32_t *g_table) {
-  const uint32_t k = item_key[i];
-  fe r, s;
-  fe_load_be_words(r, r_be + 8 * i);
-  fe_load_be_words(s, s_be + 8 * i);
-  uint8_t st = classify(pre ? pre[i] : 0, kstatus[k], r, s);
+  fe r;
+  const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
   if (st != 0xFF) return st;
-  uint32_t u[16];
-  load_u12(u, u12, i);
+  const uint32_t k = item_key[i];
+  uint32_t u1[8], u2[8];
+  load_u(u1, u12, i, 0);
+  load_u(u2, u12, i, 1);
   fe qx, qy;
   fe_load(qx, kxy + 16 * k);
   fe_load(qy, kxy + 16 * k + 8);
@@ -402,8 +453,8 @@ DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint
   fe_set(R.Z, 0);
   for (int bit = 255; bit >= 0; bit--) {
     if (!inf) gej_double(R, R);
-    if ((u[8 + (bit >> 5)] >> (bit & 31)) & 1u) gej_add_ge(R, inf, qx, qy);
+    if ((u2[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge(R, inf, qx, qy);
   }
-  table_add(R, inf, g_table, u);
+  table_add<BV_GW>(R, inf, g_table, u1);
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
 }

@@ -64,6 +64,7 @@ class BvTiming(ctypes.Structure):
         ("ms_sha256", ctypes.c_float),
         ("ms_keyprep", ctypes.c_float),
         ("ms_scalar", ctypes.c_float),
+        ("ms_verify_g", ctypes.c_float),
         ("ms_verify", ctypes.c_float),
         ("ms_h2d", ctypes.c_float),
         ("ms_d2h", ctypes.c_float),

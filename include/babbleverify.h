@@ -93,13 +93,15 @@ typedef struct {
 
 /* Timing of the last call, device-side (HIP events on the ctx stream). */
 typedef struct {
-  float ms_total;   /* first kernel start -> last kernel end                  */
-  float ms_sha256;  /* message hashing                                         */
-  float ms_keyprep; /* key decode + per-key table build                        */
-  float ms_scalar;  /* k_scalar_prep: batched s^-1, u1, u2                     */
-  float ms_verify;  /* k_verify / k_verify_generic (point arithmetic)          */
-  float ms_h2d;     /* host -> device staging (host-buffer entry point only)   */
-  float ms_d2h;     /* device -> host results                                  */
+  float ms_total;    /* first kernel start -> last kernel end                  */
+  float ms_sha256;   /* k_sha256: message hashing                              */
+  float ms_keyprep;  /* key decode + per-key table build (own stream, overlaps
+                        hashing, s^-1 and the u1 G phase)                       */
+  float ms_scalar;   /* k_scalar_prep: batched s^-1, u1, u2                     */
+  float ms_verify_g; /* k_verify_g: u1 G from the generator table               */
+  float ms_verify;   /* k_verify_q (+ u2 Q, decision, bits) or k_verify_generic */
+  float ms_h2d;      /* host -> device staging (host-buffer entry point only)   */
+  float ms_d2h;      /* device -> host results                                  */
 } bv_timing;
 
 int bv_abi_version(void);

@@ -7,44 +7,13 @@
 // Not linked into libbabbleverify.so; the product never runs this.
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
 #include "../../babble_amd/csrc/verify_core.h"
 
 namespace {
-
-void emu_build_tables(uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, uint32_t *table) {
-  std::vector<uint32_t> bases((size_t)n_bases * BV_NWIN * 24);
-  for (uint32_t b = 0; b < n_bases; b++) {
-    if (bstatus && bstatus[b] != KS_OK) continue;
-    table_bases_one(b, bxy, bases.data());
-  }
-  // k_table_fill, one (b, j) block at a time; the scans run serially.
-  for (uint32_t b = 0; b < n_bases; b++) {
-    if (bstatus && bstatus[b] != KS_OK) continue;
-    for (uint32_t j = 0; j < BV_NWIN; j++) {
-      fe bx, by;
-      jac_to_affine(bx, by, bases.data() + ((uint64_t)b * BV_NWIN + j) * 24);
-      std::vector<gej> R(256);
-      std::vector<fe> Z(256), pre(256), suf(256);
-      bool inf[256];
-      for (uint32_t d = 0; d < 256; d++) table_point(R[d], inf[d], Z[d], bx, by, d);
-      pre[0] = Z[0];
-      for (int d = 1; d < 256; d++) fe_mul(pre[d], pre[d - 1], Z[d]);
-      suf[255] = Z[255];
-      for (int d = 254; d >= 0; d--) fe_mul(suf[d], suf[d + 1], Z[d]);
-      fe inv;
-      fe_inv(inv, pre[255]);
-      for (uint32_t d = 0; d < 256; d++) {
-        fe zi = inv;
-        if (d > 0) fe_mul(zi, zi, pre[d - 1]);
-        if (d < 255) fe_mul(zi, zi, suf[d + 1]);
-        table_store(table, b, j, d, R[d], inf[d], zi);
-      }
-    }
-  }
-}
 
 template <class F>
 void parallel_for(uint64_t n, int nt, F f) {
@@ -55,6 +24,61 @@ void parallel_for(uint64_t n, int nt, F f) {
       for (uint64_t i = t; i < n; i += nt) f(i);
     });
   for (auto &x : th) x.join();
+}
+
+// k_table_bases + k_table_fill<w>: one (b, window, chunk) block per task; the
+// block's prefix/suffix scans run serially.
+void emu_build_tables(int w, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, uint32_t *table,
+                      int nt) {
+  const uint32_t nwin = 256 / w, chunks = (1u << w) / 256u;
+  std::vector<uint32_t> bases((size_t)n_bases * nwin * 24);
+  parallel_for(n_bases, nt, [&](uint64_t b) {
+    if (bstatus && bstatus[b] != KS_OK) return;
+    table_bases_one((uint32_t)b, bxy, bases.data(), w);
+  });
+  parallel_for((uint64_t)n_bases * nwin * chunks, nt, [&](uint64_t task) {
+    const uint32_t b = (uint32_t)(task / ((uint64_t)nwin * chunks));
+    const uint32_t jc = (uint32_t)(task % ((uint64_t)nwin * chunks));
+    const uint32_t j = jc / chunks, c = jc % chunks;
+    if (bstatus && bstatus[b] != KS_OK) return;
+    fe bx, by;
+    jac_to_affine(bx, by, bases.data() + ((uint64_t)b * nwin + j) * 24);
+    std::vector<gej> R(256);
+    std::vector<fe> Z(256), pre(256), suf(256);
+    bool inf[256];
+    for (uint32_t t = 0; t < 256; t++) table_point(R[t], inf[t], Z[t], bx, by, c * 256 + t, w);
+    pre[0] = Z[0];
+    for (int t = 1; t < 256; t++) fe_mul(pre[t], pre[t - 1], Z[t]);
+    suf[255] = Z[255];
+    for (int t = 254; t >= 0; t--) fe_mul(suf[t], suf[t + 1], Z[t]);
+    fe inv;
+    fe_inv(inv, pre[255]);
+    for (uint32_t t = 0; t < 256; t++) {
+      fe zi = inv;
+      if (t > 0) fe_mul(zi, zi, pre[t - 1]);
+      if (t < 255) fe_mul(zi, zi, suf[t + 1]);
+      const uint32_t d = c * 256 + t;
+      uint32_t *entry = table + (uint64_t)b * BV_TABLE_U32(w) + (((uint64_t)j << w) + d) * BV_ENTRY_U32;
+      table_store(entry, d, R[t], inf[t], zi);
+    }
+  });
+}
+
+// The generator table is a constant: built once per process (like bv_create).
+const uint32_t *emu_g_table(int nt) {
+  static std::vector<uint8_t> store;
+  static uint32_t *gt = nullptr;
+  static std::once_flag once;
+  std::call_once(once, [&]() {
+    store.assign(BV_TABLE_U32(BV_GW) * 4 + 64, 0);
+    gt = (uint32_t *)(((uintptr_t)store.data() + 15) & ~(uintptr_t)15);
+    alignas(16) static const uint32_t G[16] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
+                                               0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu,
+                                               0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                                               0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+    emu_build_tables(BV_GW, 1, G, nullptr, gt, nt);
+  });
+  return gt;
 }
 
 template <class T>
@@ -75,7 +99,7 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
   // device-style aligned + padded copies of the inputs
-  std::vector<uint8_t> s_msg, s_dig, s_kst, s_kxy, s_r, s_s, s_scr, s_u12, s_gt, s_kt, s_gxy;
+  std::vector<uint8_t> s_msg, s_dig, s_kst, s_kxy, s_r, s_s, s_scr, s_u12, s_kt;
   const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
   uint8_t *msg = aligned<uint8_t>(s_msg, msg_len + 64);
   if (msg_len) memcpy(msg, b->msg_bytes, msg_len);
@@ -93,29 +117,31 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
   parallel_for(n_msgs, n_threads, [&](uint64_t m) { sha256_one(m, msg, b->msg_off, dig); });
   for (uint32_t k = 0; k < n_keys; k++) key_decode_one(k, b->key_bytes, b->key_off, kst, kxy);
   const bool table_mode = force_mode >= 0 ? force_mode == 1 : (n_keys <= 8192 && n_items >= 16ull * n_keys);
-  // G table
-  uint32_t *gt = aligned<uint32_t>(s_gt, BV_TABLE_U32 * 4);
-  uint32_t *gxy = aligned<uint32_t>(s_gxy, 64);
-  static const uint32_t G[16] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu, 0xCE870B07u, 0x55A06295u,
-                                 0xF9DCBBACu, 0x79BE667Eu, 0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
-                                 0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
-  memcpy(gxy, G, 64);
-  emu_build_tables(1, gxy, nullptr, gt);
+  const uint32_t *gt = emu_g_table(n_threads);
   uint32_t *kt = nullptr;
   if (table_mode) {
-    kt = aligned<uint32_t>(s_kt, (uint64_t)(n_keys ? n_keys : 1) * BV_TABLE_U32 * 4);
-    emu_build_tables(n_keys, kxy, kst, kt);
+    kt = aligned<uint32_t>(s_kt, (uint64_t)(n_keys ? n_keys : 1) * BV_TABLE_U32(BV_KW) * 4);
+    emu_build_tables(BV_KW, n_keys, kxy, kst, kt, n_threads);
   }
+  std::vector<uint8_t> s_rg;
+  uint32_t *rg = table_mode ? aligned<uint32_t>(s_rg, (n_items + 1) * RG_WORDS * 4) : nullptr;
   const uint32_t M = 16;
   const uint64_t T = ((n_items + M - 1) / M + 255) / 256 * 256;  // kernel grid size
   parallel_for(T, n_threads, [&](uint64_t t) {
     scalar_prep_thread(t, T, n_items, M, r, s, b->pre, b->item_msg, dig, scratch, u12);
   });
   std::vector<uint8_t> st(n_items + 1);
-  parallel_for(n_items, n_threads, [&](uint64_t i) {
-    st[i] = table_mode ? verify_item_tables(i, b->item_key, r, s, b->pre, kst, u12, gt, kt)
-                       : verify_item_generic(i, b->item_key, r, s, b->pre, kst, kxy, u12, gt);
-  });
+  if (table_mode) {
+    parallel_for(n_items, n_threads,
+                 [&](uint64_t i) { verify_item_g(i, n_items, b->item_key, r, s, b->pre, kst, u12, gt, rg); });
+    parallel_for(n_items, n_threads, [&](uint64_t i) {
+      st[i] = verify_item_q(i, n_items, b->item_key, r, s, b->pre, kst, u12, kt, rg);
+    });
+  } else {
+    parallel_for(n_items, n_threads, [&](uint64_t i) {
+      st[i] = verify_item_generic(i, b->item_key, r, s, b->pre, kst, kxy, u12, gt);
+    });
+  }
   if (msg_hash && n_msgs) memcpy(msg_hash, dig, n_msgs * 32);
   if (status && n_items) memcpy(status, st.data(), n_items);
   if (bits) {
