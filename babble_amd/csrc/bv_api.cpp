@@ -20,7 +20,7 @@
 namespace bvk {
 hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
 hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
-hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *);
+hipError_t build_tables(hipStream_t, bool, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *);
 hipError_t scalar_prep(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint32_t *, const uint8_t *,
                        const uint32_t *, const uint32_t *, uint32_t *, uint32_t *);
 hipError_t verify_g(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
@@ -34,10 +34,12 @@ hipError_t verify_generic(hipStream_t, uint64_t, const uint32_t *, const uint32_
 
 namespace {
 
-constexpr int kGW = 16;                                                 // generator window bits
-constexpr int kKW = 8;                                                  // key window bits
-constexpr uint64_t kGTableBytes = (256 / kGW) * (1ull << kGW) * 64ull;  // 64 MiB
-constexpr uint64_t kKTableBytes = (256 / kKW) * (1ull << kKW) * 64ull;  // 512 KiB per key
+// Table geometry (must match verify_core.h): generator 16-bit windows x 16
+// (64 MiB, once per ctx); GLV key tables 8-bit windows x 16 + phi (512 KiB).
+constexpr uint32_t kGNwin = 16, kKNwin = 16;
+constexpr uint64_t kGTableBytes = kGNwin * (1ull << 16) * 64ull;
+constexpr uint64_t kKTableBytes = 2ull * kKNwin * (1ull << 8) * 64ull;
+constexpr uint32_t kUStride = 20;  // per-item scalar words (u1, k1, k2, signs)
 constexpr uint32_t kMaxTableKeys = 8192;                                // 4 GiB of key tables
 constexpr uint32_t kPrepM = 16;                                         // items per s^-1 batch
 constexpr uint32_t kRgWords = 25;                                       // R_G words per item
@@ -134,7 +136,7 @@ static int create_impl(bv_ctx *ctx) {
   // G table: T[j][d] = d * 2^(16j) * G, built once on the device.
   HIPCHK(ctx->g_table.ensure(kGTableBytes), BV_E_OOM, "alloc G table");
   HIPCHK(ctx->g_xy.ensure(64), BV_E_OOM, "alloc G");
-  HIPCHK(ctx->g_bases.ensure((256 / kGW) * 24 * 4), BV_E_OOM, "alloc G bases");
+  HIPCHK(ctx->g_bases.ensure(kGNwin * 24 * 4), BV_E_OOM, "alloc G bases");
   uint32_t gxy[16];
   for (int half = 0; half < 2; half++)
     for (int i = 0; i < 8; i++) {
@@ -142,7 +144,7 @@ static int create_impl(bv_ctx *ctx) {
       gxy[8 * half + i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
     }
   HIPCHK(hipMemcpyAsync(ctx->g_xy.p, gxy, sizeof gxy, hipMemcpyHostToDevice, ctx->stream), BV_E_LAUNCH, "copy G");
-  HIPCHK(bvk::build_tables(ctx->stream, kGW, 1, ctx->g_xy.as<uint32_t>(), nullptr, ctx->g_bases.as<uint32_t>(),
+  HIPCHK(bvk::build_tables(ctx->stream, false, 1, ctx->g_xy.as<uint32_t>(), nullptr, ctx->g_bases.as<uint32_t>(),
                            ctx->g_table.as<uint32_t>()),
          BV_E_LAUNCH, "G table");
   HIPCHK(hipStreamSynchronize(ctx->stream), BV_E_LAUNCH, "G table sync");
@@ -205,7 +207,7 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
   const uint32_t n_keys = b->n_keys;
   if (n_items > 0 && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be))
     return fail(ctx, BV_E_ARGS, "null item arrays");
-  if (n_msgs > 0 && (!b->msg_bytes || !b->msg_off)) return fail(ctx, BV_E_ARGS, "null msg arrays");
+  if (n_msgs > 0 && !b->msg_off) return fail(ctx, BV_E_ARGS, "null msg_off");
   if (n_items > 0 && n_keys == 0) return fail(ctx, BV_E_ARGS, "items without keys");
   if (n_keys > 0 && !b->key_off) return fail(ctx, BV_E_ARGS, "null key_off");
   if (((uintptr_t)b->r_be | (uintptr_t)b->s_be) & 15)
@@ -229,14 +231,14 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
   HIPCHK(ctx->kstatus.ensure(std::max<uint32_t>(n_keys, 1)), BV_E_OOM, "alloc kstatus");
   HIPCHK(ctx->kxy.ensure(std::max<uint32_t>(n_keys, 1) * 64ull), BV_E_OOM, "alloc kxy");
   HIPCHK(ctx->scratch.ensure(std::max<uint64_t>(n_items, 1) * 32), BV_E_OOM, "alloc scratch");
-  HIPCHK(ctx->u12.ensure(std::max<uint64_t>(n_items, 1) * 64), BV_E_OOM, "alloc u12");
+  HIPCHK(ctx->u12.ensure(std::max<uint64_t>(n_items, 1) * kUStride * 4), BV_E_OOM, "alloc u12");
 
   // Per-key fixed-base tables pay off once a key signs enough items; with
   // few items per key the generic per-lane path is cheaper.
   const bool table_mode = n_keys <= kMaxTableKeys && n_items >= 16ull * n_keys;
   ctx->table_mode = table_mode;
   if (table_mode) {
-    HIPCHK(ctx->bases_jac.ensure(std::max<uint32_t>(n_keys, 1) * (256 / kKW) * 96ull), BV_E_OOM, "alloc bases");
+    HIPCHK(ctx->bases_jac.ensure(std::max<uint32_t>(n_keys, 1) * kKNwin * 96ull), BV_E_OOM, "alloc bases");
     HIPCHK(ctx->key_table.ensure(std::max<uint32_t>(n_keys, 1) * kKTableBytes), BV_E_OOM, "alloc key tables");
     HIPCHK(ctx->rg.ensure(std::max<uint64_t>(n_items, 1) * kRgWords * 4), BV_E_OOM, "alloc R_G");
   }
@@ -249,7 +251,7 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
   HIPCHK(hipEventRecord(ev[E_FORK], st), BV_E_LAUNCH, "event");
   if (table_mode) {  // key tables on the keys stream, concurrent with the main stream below
     HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_FORK], 0), BV_E_LAUNCH, "fork");
-    HIPCHK(bvk::build_tables(ctx->kstream, kKW, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
+    HIPCHK(bvk::build_tables(ctx->kstream, true, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
                              ctx->bases_jac.as<uint32_t>(), ctx->key_table.as<uint32_t>()),
            BV_E_LAUNCH, "key tables");
     HIPCHK(hipEventRecord(ev[E_KEYS], ctx->kstream), BV_E_LAUNCH, "event");
@@ -323,11 +325,13 @@ extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   hipStream_t st = ctx->stream;
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
-  if ((n_msgs && (!b->msg_off || !b->msg_bytes)) || (n_keys && (!b->key_off || !b->key_bytes)) ||
+  if ((n_msgs && !b->msg_off) || (n_keys && !b->key_off) ||
       (n_items && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be)))
     return fail(ctx, BV_E_ARGS, "null input array");
   const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
   const uint64_t key_len = n_keys ? b->key_off[n_keys] : 0;
+  // byte arrays may be null only when empty (all-empty messages or keys)
+  if ((msg_len && !b->msg_bytes) || (key_len && !b->key_bytes)) return fail(ctx, BV_E_ARGS, "null byte array");
   // validate host offsets (a bad offset must not become an OOB device read)
   if (n_msgs && b->msg_off[0] != 0) return fail(ctx, BV_E_ARGS, "msg_off[0] != 0");
   if (n_keys && b->key_off[0] != 0) return fail(ctx, BV_E_ARGS, "key_off[0] != 0");

@@ -355,30 +355,120 @@ DEV void sc_load_const(sc &r, const uint32_t *c) {
   for (int i = 0; i < 8; i++) r.v[i] = c[i];
 }
 
-// x^(N-2) in the Montgomery domain: input xR, output x^-1 R.
-// Fixed 4-bit window over the constant exponent.
-DEV void sc_inv_mont(sc &r, const sc &x) {
-  // N - 2 = FFFFFFFF FFFFFFFF FFFFFFFF FFFFFFFE BAAEDCE6 AF48A03B BFD25E8C D036413F
-  sc tab[16];
-  sc_load_const(tab[0], SC_R1);
-  tab[1] = x;
+// r = a + b mod N (a, b < N)
+DEV void sc_add(sc &r, const sc &a, const sc &b) {
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 2; i < 16; i++) sc_mont(tab[i], tab[i - 1], x);
-  const uint32_t e[8] = {0xD036413Fu, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
-                         0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  sc acc;
-  sc_load_const(acc, SC_R1);
+  for (int i = 0; i < 8; i++) r.v[i] = addc32(a.v[i], b.v[i], c);
+  if (c || sc_ge_n(r)) sc_sub_n(r);
+}
+// r = a - b mod N (a, b < N)
+DEV void sc_sub(sc &r, const sc &a, const sc &b) {
+  uint32_t br = 0;
 #pragma unroll
-  for (int i = 63; i >= 0; i--) {
-    if (i != 63) {
-      sc_mont(acc, acc, acc);
-      sc_mont(acc, acc, acc);
-      sc_mont(acc, acc, acc);
-      sc_mont(acc, acc, acc);
-    }
-    uint32_t nib = (e[i >> 3] >> (4 * (i & 7))) & 15u;
-    // nibble is a compile-time constant after unrolling
-    if (nib) sc_mont(acc, acc, tab[nib]);
+  for (int i = 0; i < 8; i++) r.v[i] = subb32(a.v[i], b.v[i], br);
+  if (br) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = addc32(r.v[i], SC_N[i], c);
   }
-  r = acc;
+}
+
+// ---------------------------------------------------------------------------
+// GLV endomorphism of secp256k1: lambda * (x, y) = (beta * x, y).
+// k = k1 + k2 * lambda (mod N) with |k1|, |k2| < 2^128 (the lattice split of
+// Gallant-Lambert-Vanstone; constants checked in tests/test_emu.py).
+// ---------------------------------------------------------------------------
+static constexpr uint32_t FE_BETA[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,
+                                        0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu};
+// round(2^384 * b2 / N), round(2^384 * (-b1) / N)
+static constexpr uint32_t GLV_G1[8] = {0x45DBB031u, 0xE893209Au, 0x71E8CA7Fu, 0x3DAA8A14u,
+                                       0x9284EB15u, 0xE86C90E4u, 0xA7D46BCDu, 0x3086D221u};
+static constexpr uint32_t GLV_G2[8] = {0x8AC47F71u, 0x1571B4AEu, 0x9DF506C6u, 0x221208ACu,
+                                       0x0ABFE4C4u, 0x6F547FA9u, 0x010E8828u, 0xE4437ED6u};
+// -b1 * R, -b2 * R, lambda * R (mod N): Montgomery forms for sc_mont
+static constexpr uint32_t GLV_MB1R[8] = {0x0AD9263Cu, 0xC50468D0u, 0xFAA6ED42u, 0x1B1C8205u,
+                                         0x8AC47F71u, 0x1571B4AEu, 0x9DF506C6u, 0x221208ACu};
+static constexpr uint32_t GLV_MB2R[8] = {0x6A144696u, 0x0CAC5E50u, 0xF3BA5939u, 0x1E8A8DC5u,
+                                         0xBA244FCEu, 0x176CDF65u, 0x8E173580u, 0xC25575EBu};
+static constexpr uint32_t GLV_LAMR[8] = {0xC9926C9Eu, 0xF07DEB3Du, 0x83C6944Cu, 0x2C93E7ADu,
+                                         0x52697D91u, 0x73A96606u, 0x8558D639u, 0x53284017u};
+// (N - 1) / 2
+static constexpr uint32_t SC_HALF_N[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u,
+                                          0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
+
+// round(k * g / 2^384) for 256-bit k, g (result < 2^129)
+DEV void glv_mulshift(sc &c, const sc &k, const uint32_t *g) {
+  fe a, b;
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.v[i] = k.v[i];
+    b.v[i] = g[i];
+  }
+  mul_512(w, a, b);
+  uint32_t cy = w[11] >> 31;  // rounding bit (bit 383)
+#pragma unroll
+  for (int i = 0; i < 4; i++) c.v[i] = addc32(w[12 + i], 0u, cy);
+  c.v[4] = cy;
+#pragma unroll
+  for (int i = 5; i < 8; i++) c.v[i] = 0;
+}
+
+// k -> (|k1|, |k2|) as 128-bit magnitudes (4 limbs each) and sign bits
+// (bit 0: k1 negative, bit 1: k2 negative), k = k1 + k2 lambda (mod N).
+DEV void glv_split(uint32_t mag1[4], uint32_t mag2[4], uint32_t &signs, const sc &k) {
+  sc c1, c2, t, r1, r2, mb;
+  glv_mulshift(c1, k, GLV_G1);
+  glv_mulshift(c2, k, GLV_G2);
+  sc_load_const(mb, GLV_MB1R);
+  sc_mont(c1, c1, mb);  // c1 * (-b1) mod N
+  sc_load_const(mb, GLV_MB2R);
+  sc_mont(c2, c2, mb);  // c2 * (-b2) mod N
+  sc_add(r2, c1, c2);
+  sc_load_const(mb, GLV_LAMR);
+  sc_mont(t, r2, mb);   // r2 * lambda mod N
+  sc_sub(r1, k, t);
+  signs = 0;
+  sc h;
+  sc_load_const(h, SC_HALF_N);
+  sc n;
+  sc_load_const(n, SC_N);
+  // r > (N-1)/2 -> negative: magnitude N - r
+  bool gt1 = false, gt2 = false;
+  {
+    bool decided = false;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) {
+      if (!decided && r1.v[i] != h.v[i]) {
+        gt1 = r1.v[i] > h.v[i];
+        decided = true;
+      }
+    }
+    decided = false;
+#pragma unroll
+    for (int i = 7; i >= 0; i--) {
+      if (!decided && r2.v[i] != h.v[i]) {
+        gt2 = r2.v[i] > h.v[i];
+        decided = true;
+      }
+    }
+  }
+  if (gt1) {
+    sc z;
+    sc_sub(z, n, r1);
+    r1 = z;
+    signs |= 1u;
+  }
+  if (gt2) {
+    sc z;
+    sc_sub(z, n, r2);
+    r2 = z;
+    signs |= 2u;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    mag1[i] = r1.v[i];
+    mag2[i] = r2.v[i];
+  }
 }

@@ -35,21 +35,23 @@ __global__ void __launch_bounds__(64) k_key_decode(uint32_t n_keys, const uint8_
 
 __global__ void __launch_bounds__(64) k_table_bases(uint32_t n_bases, const uint32_t *__restrict__ bxy,
                                                     const uint8_t *__restrict__ bstatus,
-                                                    uint32_t *__restrict__ bases_jac, int w) {
+                                                    uint32_t *__restrict__ bases_jac, int w, int nwin) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n_bases) return;
   if (bstatus && bstatus[b] != KS_OK) return;
-  table_bases_one(b, bxy, bases_jac, w);
+  table_bases_one(b, bxy, bases_jac, w, nwin);
 }
 
-// blockDim = 256, grid (nwin * 2^W/256, n_bases).  Block (j, c) computes
+// blockDim = 256, grid (NWIN * 2^W/256, n_bases).  Block (j, c) computes
 // entries d = 256c + t of window j and normalises them to affine with one
-// field inversion (prefix/suffix products in LDS).
-template <int W>
+// field inversion (prefix/suffix products in LDS).  PHI: also write the
+// phi(T) half of a GLV key table.
+template <int W, int NWIN, bool PHI>
 __global__ void __launch_bounds__(256) k_table_fill(const uint32_t *__restrict__ bases_jac,
                                                     const uint8_t *__restrict__ bstatus,
                                                     uint32_t *__restrict__ table) {
   constexpr uint32_t chunks = (1u << W) / 256u;
+  constexpr uint64_t half_u32 = (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
   const uint32_t b = blockIdx.y;
   const uint32_t j = blockIdx.x / chunks;
   const uint32_t d = (blockIdx.x % chunks) * 256u + threadIdx.x;
@@ -60,7 +62,7 @@ __global__ void __launch_bounds__(256) k_table_fill(const uint32_t *__restrict__
   __shared__ fe sBx, sBy, sInvTotal;
   if (t == 0) {
     fe x, y;
-    jac_to_affine(x, y, bases_jac + ((uint64_t)b * BV_NWIN(W) + j) * 24);
+    jac_to_affine(x, y, bases_jac + ((uint64_t)b * NWIN + j) * 24);
     sBx = x;
     sBy = y;
   }
@@ -91,8 +93,8 @@ __global__ void __launch_bounds__(256) k_table_fill(const uint32_t *__restrict__
   fe zi = sInvTotal;  // Z_t^-1 = prefix(t-1) * suffix(t+1) * (prod Z)^-1
   if (t > 0) fe_mul(zi, zi, sPre[t - 1]);
   if (t < 255) fe_mul(zi, zi, sSuf[t + 1]);
-  uint32_t *entry = table + (uint64_t)b * BV_TABLE_U32(W) + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
-  table_store(entry, d, R, inf, zi);
+  uint32_t *entry = table + (uint64_t)b * (PHI ? 2 : 1) * half_u32 + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
+  table_store(entry, PHI ? entry + half_u32 : nullptr, d, R, inf, zi);
 }
 
 __global__ void __launch_bounds__(256) k_scalar_prep(uint64_t n_items, uint32_t M, const uint32_t *__restrict__ r_be,
@@ -168,19 +170,21 @@ hipError_t key_decode(hipStream_t st, uint32_t n, const uint8_t *kb, const uint6
   return hipGetLastError();
 }
 
-// w = 8 (key tables) or 16 (generator table)
-hipError_t build_tables(hipStream_t st, int w, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
+// key = false: the generator table (16-bit windows over 256 bits, built once
+// per ctx); key = true: GLV key tables (8-bit windows over 128 bits + phi).
+hipError_t build_tables(hipStream_t st, bool key, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
                         uint32_t *bases_jac, uint32_t *table) {
   if (n_bases == 0) return hipSuccess;
-  if (w != 8 && w != 16) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_table_bases, grid1(n_bases, 64), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w);
+  const int w = key ? BV_KW : BV_GW, nwin = key ? BV_KNWIN : BV_GNWIN;
+  hipLaunchKernelGGL(k_table_bases, grid1(n_bases, 64), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w, nwin);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (w == 8)
-    hipLaunchKernelGGL(k_table_fill<8>, dim3(BV_NWIN(8), n_bases), dim3(256), 0, st, bases_jac, bstatus, table);
+  if (key)
+    hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
+                       dim3(256), 0, st, bases_jac, bstatus, table);
   else
-    hipLaunchKernelGGL(k_table_fill<16>, dim3(BV_NWIN(16) * 256, n_bases), dim3(256), 0, st, bases_jac, bstatus,
-                       table);
+    hipLaunchKernelGGL((k_table_fill<BV_GW, BV_GNWIN, false>), dim3(BV_GNWIN * ((1u << BV_GW) / 256u), n_bases),
+                       dim3(256), 0, st, bases_jac, bstatus, table);
   return hipGetLastError();
 }
 

@@ -11,13 +11,21 @@
 #include "sha256.h"
 
 // Fixed-base tables: T[j][d] = d * 2^(W j) * P (affine, 64 bytes), d < 2^W.
-// The generator table is built once per context with wide windows; key
-// tables are built per batch with 8-bit windows (cheap to build).
+// The generator table is built once per context with wide windows over the
+// full 256-bit u1.  Key tables are built per batch with 8-bit windows over
+// 128 bits only: u2 is split GLV-style (u2 = k1 + k2 lambda, |k1|,|k2| <
+// 2^128) and the second half of a key table holds phi(T) = (beta x, y), so
+// the serial doubling chain per key is 120 doublings instead of 248.
 #define BV_ENTRY_U32 16  // affine x, y = 16 words (64 bytes)
-#define BV_GW 16         // G window bits: 16 windows x 65536 entries (64 MiB)
-#define BV_KW 8          // key window bits: 32 windows x 256 entries (512 KiB)
-#define BV_NWIN(w) (256 / (w))
-#define BV_TABLE_U32(w) ((uint64_t)BV_NWIN(w) * (1ull << (w)) * BV_ENTRY_U32)
+#define BV_GW 16         // G window bits
+#define BV_GNWIN 16      //   x 16 windows x 65536 entries = 64 MiB
+#define BV_KW 8          // key window bits
+#define BV_KNWIN 16      //   x 16 windows (128 bits) x 256 entries, x 2 (T, phi T) = 512 KiB
+#define BV_GTABLE_U32 ((uint64_t)BV_GNWIN * (1ull << BV_GW) * BV_ENTRY_U32)
+#define BV_KHALF_U32 ((uint64_t)BV_KNWIN * (1ull << BV_KW) * BV_ENTRY_U32)
+#define BV_KTABLE_U32 (2 * BV_KHALF_U32)
+// per-item scalars (k_scalar_prep output): u1[8] | k1[4] | k2[4] | signs | pad
+#define BV_U_STRIDE 20
 
 // key status (k_key_decode output)
 #define KS_OK 0
@@ -131,10 +139,9 @@ DEV void key_decode_one(uint32_t k, const uint8_t *kbytes, const uint64_t *koff,
 // ---------------------------------------------------------------------------
 // Fixed-base tables
 // ---------------------------------------------------------------------------
-// B_j = 2^(w j) P_b (Jacobian, 24 words each), j < 256/w: a serial doubling
+// B_j = 2^(w j) P_b (Jacobian, 24 words each), j < nwin: a serial doubling
 // chain per base.
-DEV void table_bases_one(uint32_t b, const uint32_t *bxy, uint32_t *bases_jac, int w) {
-  const int nwin = 256 / w;
+DEV void table_bases_one(uint32_t b, const uint32_t *bxy, uint32_t *bases_jac, int w, int nwin) {
   gej P;
   fe_load(P.X, bxy + 16 * b);
   fe_load(P.Y, bxy + 16 * b + 8);
@@ -178,7 +185,8 @@ DEV void table_point(gej &R, bool &inf, fe &Z, const fe &bx, const fe &by, uint3
 }
 
 // Store one entry given Z^-1 (canonical affine; d == 0 stored as zeros).
-DEV void table_store(uint32_t *entry, uint32_t d, const gej &R, bool inf, const fe &zi) {
+// With `phi` != null also store phi(entry) = (beta x, y) there.
+DEV void table_store(uint32_t *entry, uint32_t *phi, uint32_t d, const gej &R, bool inf, const fe &zi) {
   fe zi2, zi3, x, y;
   fe_sqr(zi2, zi);
   fe_mul(zi3, zi2, zi);
@@ -197,6 +205,15 @@ DEV void table_store(uint32_t *entry, uint32_t d, const gej &R, bool inf, const 
     v[8 + i] = y.v[i];
   }
   store16(entry, v);
+  if (phi) {
+    fe beta, bx;
+    fe_load(beta, FE_BETA);
+    fe_mul(bx, x, beta);
+    fe_canon(bx);
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = bx.v[i];
+    store16(phi, v);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -283,20 +300,23 @@ DEV void scalar_prep_thread(uint64_t t, uint64_t T, uint64_t n_items, uint32_t M
     sc_mont(inv, inv, sM);
     sc_load_be_words(e, digest_words + 8 * (uint64_t)item_msg[i]);  // hashToInt: 256 bits, unreduced
     sc_load_be_words(r, r_be + 8 * i);
+    uint32_t v[20];
     if (!ok || u256_is_zero(r.v) || !u256_lt(r.v, SC_N)) {
-      sc_load_const(u1, SC_R1);  // never used: the item does not reach the math
-      u2 = u1;
+#pragma unroll
+      for (int k = 0; k < 20; k++) v[k] = 0;  // never used: the item does not reach the math
     } else {
       sc_mont(u1, e, w);  // e * s^-1 mod N  (e < 2^256 = R, w < N)
       sc_mont(u2, r, w);
-    }
-    uint32_t v[16];
+      uint32_t signs;
+      glv_split(v + 8, v + 12, signs, u2);
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      v[k] = u1.v[k];
-      v[8 + k] = u2.v[k];
+      for (int k = 0; k < 8; k++) v[k] = u1.v[k];
+      v[16] = signs;
+      v[17] = v[18] = v[19] = 0;
     }
-    store16(u12 + 16 * i, v);
+    uint4 *q = (uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i);
+#pragma unroll
+    for (int c = 0; c < 5; c++) q[c] = make_uint4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
   }
 }
 
@@ -354,26 +374,36 @@ DEV uint32_t digit(const uint32_t *u, int j) {
   return (u[bit >> 5] >> (bit & 31)) & ((1u << W) - 1u);
 }
 
-// R += sum_j T[j][digit_j(u)] over the 256/W digits of u.
-template <int W>
-DEV void table_add(gej &R, bool &inf, const uint32_t *tab, const uint32_t *u) {
-  for (int j = 0; j < BV_NWIN(W); j++) {
+// R += sum_{j < NWIN} T[j][digit_j(u)].  With `neg`, every entry is
+// negated ((x, y) -> (x, p - y)): the point of a negative GLV half.
+template <int W, int NWIN>
+DEV void table_add(gej &R, bool &inf, const uint32_t *tab, const uint32_t *u, bool neg = false) {
+  for (int j = 0; j < NWIN; j++) {
     const uint32_t d = digit<W>(u, j);
     if (d) {
       const uint32_t *e = tab + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
       fe x, y;
       fe_load4(x, e);
       fe_load4(y, e + 8);
+      if (neg) fe_neg(y, y);
       gej_add_ge(R, inf, x, y);
     }
   }
 }
 
-DEV void load_u(uint32_t u[8], const uint32_t *u12, uint64_t i, int half) {
-  const uint4 *q = (const uint4 *)(u12 + 16 * i + 8 * half);
+DEV void load_u1(uint32_t u[8], const uint32_t *u12, uint64_t i) {
+  const uint4 *q = (const uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i);
   uint4 a = q[0], b = q[1];
   u[0] = a.x; u[1] = a.y; u[2] = a.z; u[3] = a.w;
   u[4] = b.x; u[5] = b.y; u[6] = b.z; u[7] = b.w;
+}
+// k1 magnitude, k2 magnitude (4 limbs each) and the sign word
+DEV void load_k(uint32_t k1[4], uint32_t k2[4], uint32_t &signs, const uint32_t *u12, uint64_t i) {
+  const uint4 *q = (const uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i + 8);
+  uint4 a = q[0], b = q[1], c = q[2];
+  k1[0] = a.x; k1[1] = a.y; k1[2] = a.z; k1[3] = a.w;
+  k2[0] = b.x; k2[1] = b.y; k2[2] = b.z; k2[3] = b.w;
+  signs = c.x;
 }
 
 // Partial point R_G = u1 G, kept in HBM between k_verify_g and k_verify_q as
@@ -406,33 +436,37 @@ DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const u
   fe r;
   if (classify_item(i, item_key, r_be, s_be, pre, kstatus, r) != 0xFF) return;
   uint32_t u[8];
-  load_u(u, u12, i, 0);
+  load_u1(u, u12, i);
   gej R;
   bool inf = true;
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
   fe_set(R.Z, 0);
-  table_add<BV_GW>(R, inf, g_table, u);
+  table_add<BV_GW, BV_GNWIN>(R, inf, g_table, u);
   rg_store(rg, n, i, R, inf);
 }
 
-// Phase 2: R = R_G + u2 Q with the key's table; final check -> status.
+// Phase 2: R = R_G + k1 Q + k2 phi(Q) with the key's two half-tables;
+// final check -> status.
 DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
                           const uint32_t *s_be, const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12,
                           const uint32_t *key_table, const uint32_t *rg) {
   fe r;
   const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
   if (st != 0xFF) return st;
-  uint32_t u[8];
-  load_u(u, u12, i, 1);
+  uint32_t k1[4], k2[4], signs;
+  load_k(k1, k2, signs, u12, i);
   gej R;
   bool inf;
   rg_load(rg, n, i, R, inf);
-  table_add<BV_KW>(R, inf, key_table + (uint64_t)item_key[i] * BV_TABLE_U32(BV_KW), u);
+  const uint32_t *tab = key_table + (uint64_t)item_key[i] * BV_KTABLE_U32;
+  table_add<BV_KW, BV_KNWIN>(R, inf, tab, k1, signs & 1u);
+  table_add<BV_KW, BV_KNWIN>(R, inf, tab + BV_KHALF_U32, k2, (signs >> 1) & 1u);
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
 }
 
-// One signature item without a key table: u2 Q by a per-lane double-and-add.
+// One signature item without a key table: k1 Q + k2 phi(Q) by a joint
+// (Strauss-Shamir) per-lane double-and-add over the 128-bit GLV halves.
 DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
                                 const uint8_t *pre, const uint8_t *kstatus, const uint32_t *kxy,
                                 const uint32_t *u12, const uint32_t *g_table) {
@@ -440,21 +474,27 @@ DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint
   const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
   if (st != 0xFF) return st;
   const uint32_t k = item_key[i];
-  uint32_t u1[8], u2[8];
-  load_u(u1, u12, i, 0);
-  load_u(u2, u12, i, 1);
-  fe qx, qy;
-  fe_load(qx, kxy + 16 * k);
-  fe_load(qy, kxy + 16 * k + 8);
+  uint32_t u1[8], k1[4], k2[4], signs;
+  load_u1(u1, u12, i);
+  load_k(k1, k2, signs, u12, i);
+  fe q1x, q1y, q2x, q2y, beta;
+  fe_load(q1x, kxy + 16 * k);
+  fe_load(q1y, kxy + 16 * k + 8);
+  fe_load(beta, FE_BETA);
+  fe_mul(q2x, q1x, beta);  // phi(Q) = (beta x, y)
+  q2y = q1y;
+  if (signs & 1u) fe_neg(q1y, q1y);
+  if (signs & 2u) fe_neg(q2y, q2y);
   gej R;
   bool inf = true;
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
   fe_set(R.Z, 0);
-  for (int bit = 255; bit >= 0; bit--) {
+  for (int bit = 127; bit >= 0; bit--) {
     if (!inf) gej_double(R, R);
-    if ((u2[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge(R, inf, qx, qy);
+    if ((k1[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge(R, inf, q1x, q1y);
+    if ((k2[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge(R, inf, q2x, q2y);
   }
-  table_add<BV_GW>(R, inf, g_table, u1);
+  table_add<BV_GW, BV_GNWIN>(R, inf, g_table, u1);
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
 }

@@ -28,13 +28,15 @@ void parallel_for(uint64_t n, int nt, F f) {
 
 // k_table_bases + k_table_fill<w>: one (b, window, chunk) block per task; the
 // block's prefix/suffix scans run serially.
-void emu_build_tables(int w, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, uint32_t *table,
+void emu_build_tables(bool key, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, uint32_t *table,
                       int nt) {
-  const uint32_t nwin = 256 / w, chunks = (1u << w) / 256u;
+  const int w = key ? BV_KW : BV_GW;
+  const uint32_t nwin = key ? BV_KNWIN : BV_GNWIN, chunks = (1u << w) / 256u;
+  const uint64_t half_u32 = (uint64_t)nwin * (1ull << w) * BV_ENTRY_U32;
   std::vector<uint32_t> bases((size_t)n_bases * nwin * 24);
   parallel_for(n_bases, nt, [&](uint64_t b) {
     if (bstatus && bstatus[b] != KS_OK) return;
-    table_bases_one((uint32_t)b, bxy, bases.data(), w);
+    table_bases_one((uint32_t)b, bxy, bases.data(), w, nwin);
   });
   parallel_for((uint64_t)n_bases * nwin * chunks, nt, [&](uint64_t task) {
     const uint32_t b = (uint32_t)(task / ((uint64_t)nwin * chunks));
@@ -58,8 +60,8 @@ void emu_build_tables(int w, uint32_t n_bases, const uint32_t *bxy, const uint8_
       if (t > 0) fe_mul(zi, zi, pre[t - 1]);
       if (t < 255) fe_mul(zi, zi, suf[t + 1]);
       const uint32_t d = c * 256 + t;
-      uint32_t *entry = table + (uint64_t)b * BV_TABLE_U32(w) + (((uint64_t)j << w) + d) * BV_ENTRY_U32;
-      table_store(entry, d, R[t], inf[t], zi);
+      uint32_t *entry = table + (uint64_t)b * (key ? 2 : 1) * half_u32 + (((uint64_t)j << w) + d) * BV_ENTRY_U32;
+      table_store(entry, key ? entry + half_u32 : nullptr, d, R[t], inf[t], zi);
     }
   });
 }
@@ -70,13 +72,13 @@ const uint32_t *emu_g_table(int nt) {
   static uint32_t *gt = nullptr;
   static std::once_flag once;
   std::call_once(once, [&]() {
-    store.assign(BV_TABLE_U32(BV_GW) * 4 + 64, 0);
+    store.assign(BV_GTABLE_U32 * 4 + 64, 0);
     gt = (uint32_t *)(((uintptr_t)store.data() + 15) & ~(uintptr_t)15);
     alignas(16) static const uint32_t G[16] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
                                                0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu,
                                                0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
                                                0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
-    emu_build_tables(BV_GW, 1, G, nullptr, gt, nt);
+    emu_build_tables(false, 1, G, nullptr, gt, nt);
   });
   return gt;
 }
@@ -113,15 +115,15 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
     memcpy(s, b->s_be, n_items * 32);
   }
   uint32_t *scratch = aligned<uint32_t>(s_scr, n_items * 32 + 32);
-  uint32_t *u12 = aligned<uint32_t>(s_u12, n_items * 64 + 64);
+  uint32_t *u12 = aligned<uint32_t>(s_u12, n_items * BV_U_STRIDE * 4 + 64);
   parallel_for(n_msgs, n_threads, [&](uint64_t m) { sha256_one(m, msg, b->msg_off, dig); });
   for (uint32_t k = 0; k < n_keys; k++) key_decode_one(k, b->key_bytes, b->key_off, kst, kxy);
   const bool table_mode = force_mode >= 0 ? force_mode == 1 : (n_keys <= 8192 && n_items >= 16ull * n_keys);
   const uint32_t *gt = emu_g_table(n_threads);
   uint32_t *kt = nullptr;
   if (table_mode) {
-    kt = aligned<uint32_t>(s_kt, (uint64_t)(n_keys ? n_keys : 1) * BV_TABLE_U32(BV_KW) * 4);
-    emu_build_tables(BV_KW, n_keys, kxy, kst, kt, n_threads);
+    kt = aligned<uint32_t>(s_kt, (uint64_t)(n_keys ? n_keys : 1) * BV_KTABLE_U32 * 4);
+    emu_build_tables(true, n_keys, kxy, kst, kt, n_threads);
   }
   std::vector<uint8_t> s_rg;
   uint32_t *rg = table_mode ? aligned<uint32_t>(s_rg, (n_items + 1) * RG_WORDS * 4) : nullptr;
@@ -163,6 +165,15 @@ void emu_sc_inverse(const uint32_t s_le[8], uint32_t out_le[8]) {
   for (int i = 0; i < 8; i++) one.v[i] = i == 0;
   sc_mont(r, inv, one);
   for (int i = 0; i < 8; i++) out_le[i] = r.v[i];
+}
+
+// GLV split of k (< N): magnitudes |k1|, |k2| (4 limbs each) and signs
+void emu_glv_split(const uint32_t k_le[8], uint32_t out[9]) {
+  sc k;
+  for (int i = 0; i < 8; i++) k.v[i] = k_le[i];
+  uint32_t signs;
+  glv_split(out, out + 4, signs, k);
+  out[8] = signs;
 }
 
 // a * b mod p, canonical (field arithmetic known-answer tests)

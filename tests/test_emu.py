@@ -44,6 +44,34 @@ def test_scalar_montgomery_and_inverse():
         assert emu.unop("emu_sc_inverse", s) == pow(s, -1, N)
 
 
+LAMBDA = 0x5363AD4CC05C30E0A5261C028812645A122E22EA20816678DF02967C1B23BD72
+BETA = 0x7AE96A2B657C07106E64479EAC3434E99CF0497512F58995C1396C28719501EE
+
+
+def test_glv_constants_and_split():
+    """lambda (mod N) and beta (mod p) are cube roots of one with
+    lambda * G = (beta * Gx, Gy); the device split k = k1 + k2 lambda has
+    |k1|, |k2| < 2^128."""
+    import ctypes
+
+    assert pow(LAMBDA, 3, N) == 1 and pow(BETA, 3, P) == 1
+    assert gs.scalar_mult(LAMBDA, gs.G) == (BETA * gs.GX % P, gs.GY)
+    L = emu.lib()
+    L.emu_glv_split.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    rng = random.Random(8)
+    ks = [0, 1, 2, N - 1, N - 2, (N - 1) // 2, (N + 1) // 2, LAMBDA, N - LAMBDA, 2**128, 2**128 - 1, 2**255]
+    ks += [rng.randrange(N) for _ in range(3000)]
+    for k in ks:
+        kin = np.array([(k >> (32 * i)) & 0xFFFFFFFF for i in range(8)], np.uint32)
+        out = np.zeros(9, np.uint32)
+        L.emu_glv_split(kin.ctypes.data, out.ctypes.data)
+        m1 = sum(int(out[i]) << (32 * i) for i in range(4))
+        m2 = sum(int(out[4 + i]) << (32 * i) for i in range(4))
+        k1 = -m1 if out[8] & 1 else m1
+        k2 = -m2 if out[8] & 2 else m2
+        assert (k1 + k2 * LAMBDA - k) % N == 0, hex(k)
+
+
 @pytest.mark.parametrize("mode", [1, 0])
 def test_golden_items(mode):
     batch, expected, _ = golden_items_batch()

@@ -1,0 +1,88 @@
+// Microbenchmark: per-instruction VALU throughput on gfx950 for the integer
+// ops the field arithmetic can be built from.  Each kernel runs a loop of
+// 16 independent instances of one instruction (inline asm, so the exact
+// opcode is issued), full occupancy; reports wave-instructions per cycle per
+// SIMD relative to the measured clock-free rate (T lane-ops/s).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#define CHECK(x)                                                                           \
+  do {                                                                                     \
+    hipError_t e = (x);                                                                    \
+    if (e != hipSuccess) {                                                                 \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+      return 1;                                                                            \
+    }                                                                                      \
+  } while (0)
+
+#define REP16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
+
+template <int OP>
+__global__ void __launch_bounds__(256) kop(uint32_t *out, uint32_t seed, int iters) {
+  uint32_t a[16];
+  uint64_t w[16];
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    a[c] = seed + c * 77u + threadIdx.x;
+    w[c] = ((uint64_t)a[c] << 7) ^ c;
+  }
+  const uint32_t b = seed * 2654435761u;
+  for (int i = 0; i < iters; i++) {
+#define BODY(c)                                                                                      \
+  if constexpr (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[c]) : "v"(b));                 \
+  if constexpr (OP == 1) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(w[c]) : "v"(a[c]), "v"(b) : "vcc"); \
+  if constexpr (OP == 2) asm volatile("v_mad_u32_u24 %0, %0, %1, %0" : "+v"(a[c]) : "v"(b));         \
+  if constexpr (OP == 3) asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(a[c]) : "v"(b));          \
+  if constexpr (OP == 4) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(w[c]) : "v"(w[(c + 1) & 15])); \
+  if constexpr (OP == 5) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[c]) : "v"(b));              \
+  if constexpr (OP == 6) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[c]) : "v"(b));              \
+  if constexpr (OP == 7) asm volatile("v_fma_f64 %0, %0, %1, %0" : "+v"(w[c]) : "v"(w[(c + 3) & 15]));
+    REP16(BODY)
+#undef BODY
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int c = 0; c < 16; c++) s ^= a[c] ^ (uint32_t)w[c] ^ (uint32_t)(w[c] >> 32);
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <int OP>
+static int run(const char *name, uint32_t *out, int blocks) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  const int iters = 4096;
+  hipLaunchKernelGGL(kop<OP>, dim3(blocks), dim3(256), 0, 0, out, 1u, iters);
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL(kop<OP>, dim3(blocks), dim3(256), 0, 0, out, 2u, iters);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  const double ops = (double)blocks * 256 * iters * 16;
+  // wave-instructions per SIMD per ns, then cycles at 2.4 GHz
+  const double wave_instr = ops / 64.0;
+  const double per_simd_per_s = wave_instr / 1024.0 / (ms * 1e-3);
+  printf("%-20s %8.3f ms  %7.2f T lane-ops/s  %5.2f cycles/wave-instr @2.4GHz\n", name, ms, ops / (ms * 1e-3) / 1e12,
+         2.4e9 / per_simd_per_s);
+  return 0;
+}
+
+int main() {
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, 0));
+  uint32_t *out;
+  const int blocks = p.multiProcessorCount * 8;
+  CHECK(hipMalloc(&out, sizeof(uint32_t) * 256 * blocks));
+  run<0>("v_add_u32", out, blocks);
+  run<1>("v_mad_u64_u32", out, blocks);
+  run<2>("v_mad_u32_u24", out, blocks);
+  run<3>("v_mul_hi_u32_u24", out, blocks);
+  run<4>("v_lshl_add_u64", out, blocks);
+  run<5>("v_mul_lo_u32", out, blocks);
+  run<6>("v_mul_hi_u32", out, blocks);
+  run<7>("v_fma_f64", out, blocks);
+  return 0;
+}
