@@ -41,7 +41,9 @@ DEV void gej_double(gej &r, const gej &a) {
   fe_sub(r.Y, r.Y, t);
 }
 
-// r += (x2, y2) (affine), madd-2007-bl: 7M + 4S.  `inf` is r's identity flag.
+// r += (x2, y2) (affine): 8M + 3S + 7 add/sub (madd with Z3 = Z1 H; fewer
+// additions and live temporaries than madd-2007-bl's 7M + 4S + 11, and on
+// gfx950 a multiply costs the same as a square).  `inf` is r's identity flag.
 DEV void gej_add_ge(gej &r, bool &inf, const fe &x2, const fe &y2) {
   if (inf) {
     r.X = x2;
@@ -50,15 +52,15 @@ DEV void gej_add_ge(gej &r, bool &inf, const fe &x2, const fe &y2) {
     inf = false;
     return;
   }
-  fe Z1Z1, U2, S2, H, HH, I, J, rr, V, t;
+  fe Z1Z1, U2, S2, H, R, t;
   fe_sqr(Z1Z1, r.Z);
   fe_mul(U2, x2, Z1Z1);
   fe_mul(t, r.Z, Z1Z1);
   fe_mul(S2, y2, t);
   fe_sub(H, U2, r.X);
-  fe_sub(rr, S2, r.Y);
+  fe_sub(R, S2, r.Y);
   if (fe_is_zero(H)) {
-    if (fe_is_zero(rr)) {
+    if (fe_is_zero(R)) {
       gej d;
       gej_double(d, r);
       r = d;
@@ -67,28 +69,21 @@ DEV void gej_add_ge(gej &r, bool &inf, const fe &x2, const fe &y2) {
     }
     return;
   }
+  fe HH, HHH, V;
   fe_sqr(HH, H);
-  fe_dbl(I, HH);
-  fe_dbl(I, I);
-  fe_mul(J, H, I);
-  fe_dbl(rr, rr);
-  fe_mul(V, r.X, I);
-  // Z3 = (Z1 + H)^2 - Z1Z1 - HH
-  fe_add(t, r.Z, H);
-  fe_sqr(t, t);
-  fe_sub(t, t, Z1Z1);
-  fe_sub(r.Z, t, HH);
-  // X3 = rr^2 - J - 2V
-  fe_sqr(t, rr);
-  fe_sub(t, t, J);
+  fe_mul(HHH, H, HH);
+  fe_mul(V, r.X, HH);
+  fe_mul(r.Z, r.Z, H);
+  // X3 = R^2 - HHH - 2V
+  fe_sqr(t, R);
+  fe_sub(t, t, HHH);
   fe_sub(t, t, V);
   fe_sub(r.X, t, V);
-  // Y3 = rr (V - X3) - 2 Y1 J
+  // Y3 = R (V - X3) - Y1 HHH
   fe_sub(t, V, r.X);
-  fe_mul(t, rr, t);
-  fe_mul(J, r.Y, J);
-  fe_dbl(J, J);
-  fe_sub(r.Y, t, J);
+  fe_mul(t, R, t);
+  fe_mul(HHH, r.Y, HHH);
+  fe_sub(r.Y, t, HHH);
 }
 
 // r += b (both Jacobian), add-2007-bl with exceptional cases: 11M + 5S.

@@ -220,6 +220,7 @@ DEV void table_store(uint32_t *entry, uint32_t *phi, uint32_t d, const gej &R, b
 // Scalars: u1 = e * s^-1, u2 = r * s^-1 (mod N)  (ecdsa.Verify steps 4-6)
 // ---------------------------------------------------------------------------
 DEV void sc_sqrn(sc &a, int n) {
+#pragma unroll 1
   for (int i = 0; i < n; i++) sc_mont(a, a, a);
 }
 
@@ -227,7 +228,7 @@ DEV void sc_sqrn(sc &a, int n) {
 // The top 128 bits of N-2 are 2^128 - 2 (runs of ones, built from
 // x^(2^k - 1)); the low 128 bits use a 4-bit sliding window (chain generated
 // offline; tests/test_emu.py checks inverses against Python ints).
-__host__ __device__ __noinline__ inline void sc_inverse(sc &r, const sc &x) {
+DEV void sc_inverse(sc &r, const sc &x) {
   sc x2, x3, x5, x7, x9, x11, x13, x15;
   sc_mont(x2, x, x);
   sc_mont(x3, x2, x);
@@ -374,10 +375,12 @@ DEV uint32_t digit(const uint32_t *u, int j) {
   return (u[bit >> 5] >> (bit & 31)) & ((1u << W) - 1u);
 }
 
-// R += sum_{j < NWIN} T[j][digit_j(u)].  With `neg`, every entry is
-// negated ((x, y) -> (x, p - y)): the point of a negative GLV half.
+// R += sum_{j < NWIN} T[j][digit_j(u)].  With `neg` (a negative GLV half)
+// the sum is subtracted instead: R - T = -((-R) + T), so R is negated before
+// and after the additions rather than negating every entry.
 template <int W, int NWIN>
 DEV void table_add(gej &R, bool &inf, const uint32_t *tab, const uint32_t *u, bool neg = false) {
+  if (neg) fe_neg(R.Y, R.Y);
   for (int j = 0; j < NWIN; j++) {
     const uint32_t d = digit<W>(u, j);
     if (d) {
@@ -385,10 +388,10 @@ DEV void table_add(gej &R, bool &inf, const uint32_t *tab, const uint32_t *u, bo
       fe x, y;
       fe_load4(x, e);
       fe_load4(y, e + 8);
-      if (neg) fe_neg(y, y);
       gej_add_ge(R, inf, x, y);
     }
   }
+  if (neg) fe_neg(R.Y, R.Y);
 }
 
 DEV void load_u1(uint32_t u[8], const uint32_t *u12, uint64_t i) {
@@ -460,8 +463,16 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
   bool inf;
   rg_load(rg, n, i, R, inf);
   const uint32_t *tab = key_table + (uint64_t)item_key[i] * BV_KTABLE_U32;
-  table_add<BV_KW, BV_KNWIN>(R, inf, tab, k1, signs & 1u);
-  table_add<BV_KW, BV_KNWIN>(R, inf, tab + BV_KHALF_U32, k2, (signs >> 1) & 1u);
+  // One loop body for both GLV halves (one inlined copy of the point
+  // addition: smaller code, fewer live registers than two table_add calls).
+#pragma unroll 1
+  for (int h = 0; h < 2; h++) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) kk[c] = h ? k2[c] : k1[c];
+    table_add<BV_KW, BV_KNWIN>(R, inf, tab + (h ? BV_KHALF_U32 : 0), kk, (signs >> h) & 1u);
+  }
+  fe_load_be_words(r, r_be + 8 * i);  // reloaded: not kept live through the loop
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
 }
 

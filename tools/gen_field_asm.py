@@ -1,0 +1,664 @@
+"""Generator for babble_amd/csrc/field_asm.h — hand-scheduled gfx950 field
+arithmetic mod p = 2^256 - 2^32 - 977 (secp256k1, src/crypto/keys/curve.go:21).
+
+Why: the compiled C++ field multiply (field.h mul_512 + fe_reduce) lowers to
+347 VALU instructions on gfx950, 153 of them v_mov (64-bit operand pairs for
+v_mad_u64_u32) and 30 s_nop (VCC carry-chain hazards); fe_add/fe_sub are
+55/66 with 22 s_nop each.  rocprofv3 shows the verify kernels are VALU-issue
+bound (profiles/r01_pmc_summary.json), so instruction count is the roofline.
+
+Programs emitted:
+  fe_mul  product-scanning (Comba) 8x8 using v_mad_u64_u32's carry-out: each
+          column accumulates in a 64-bit pair P_k, carry-outs are counted in
+          the high word of the next column's pair, so a product costs one mad
+          + one addc and a column one v_mov; then the fold 2^256 = 2^32 + 977
+          as two interleaved carry chains and a short tail.
+  fe_add  s = a + b and t = s + (2^32 + 977) as two interleaved chains, then a
+          lane select (no s_nop on the main path).
+  fe_sub  same with borrows and t = s - (2^32 + 977).
+
+Each program is written in logical order over named registers, then list-
+scheduled: an instruction issues once its register dependences (RAW, WAR,
+WAW, pairs split into halves) are met and no SGPR it reads as a carry/mask
+was written by a VALU fewer than HAZARD_STATES wait states earlier; s_nop is
+inserted only when nothing else can issue.  The scheduled list is both
+(1) executed by the interpreter here against Python integers
+(tests/test_field_asm.py) and (2) printed as the inline-asm block.
+
+    python tools/gen_field_asm.py            # rewrite the header
+    python tools/gen_field_asm.py --check    # exit 1 if the header is stale
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "babble_amd", "csrc", "field_asm.h")
+
+M32 = (1 << 32) - 1
+M64 = (1 << 64) - 1
+P = 2**256 - 2**32 - 977
+K = 2**32 + 977  # 2^256 mod p
+HAZARD_STATES = 2  # VALU writes SGPR -> VALU reads it: 2 wait states (gfx950)
+MUL_BASE = 0       # physical VGPR temporaries of fe_mul: v[MUL_BASE, MUL_BASE+34)
+MUL_NREGS = 34
+
+# ops: name -> (dst-operand positions, src-operand positions, sgpr-src positions)
+#   every op: (op, d, ...); positions index into the tuple
+OPS = {
+    "mad": ((1, 2), (3, 4, 5), ()),        # d64, cy | a, b, c64
+    "addc": ((1, 2), (3, 4, 5), (5,)),     # d, cy | a, b, cin
+    "add_co": ((1, 2), (3, 4), ()),
+    "subb": ((1, 2), (3, 4, 5), (5,)),
+    "sub_co": ((1, 2), (3, 4), ()),
+    "add": ((1,), (2, 3), ()),
+    "mov": ((1,), (2,), ()),
+    "cnd": ((1,), (2, 3, 4), (4,)),        # d = mask ? s1 : s0
+    "mul24": ((1,), (2, 3), ()),           # d = a * b (24-bit operands)
+    "mul_lo": ((1,), (2, 3), ()),          # d = lo32(a * b)
+    "nop": ((), (), ()),
+}
+
+
+class Prog:
+    """A straight-line VALU program over named registers.
+
+    Names: physical VGPR 'v12'; even-aligned pair 'v[12:13]'; asm operands
+    '%[x]' (32-bit VGPR operands; '%[c*]' are 64-bit SGPR lane masks).
+    Python ints are inline constants or (977) 32-bit literals in v_mov.
+    """
+
+    def __init__(self, name: str):
+        self.name = name
+        self.ins: list[tuple] = []
+        self.slow: tuple[str, "Prog"] | None = None  # (mask, block run iff any lane's mask bit)
+
+    def emit(self, *ins):
+        assert ins[0] in OPS, ins
+        self.ins.append(tuple(ins))
+
+    def mad(self, d, cy, a, b, c):
+        self.emit("mad", d, cy, a, b, c)
+
+    def addc(self, d, cy, a, b, cin):
+        self.emit("addc", d, cy, a, b, cin)
+
+    def add_co(self, d, cy, a, b):
+        self.emit("add_co", d, cy, a, b)
+
+    def subb(self, d, cy, a, b, bin_):
+        self.emit("subb", d, cy, a, b, bin_)
+
+    def sub_co(self, d, cy, a, b):
+        self.emit("sub_co", d, cy, a, b)
+
+    def add(self, d, a, b):
+        self.emit("add", d, a, b)
+
+    def mov(self, d, s):
+        self.emit("mov", d, s)
+
+    def cnd(self, d, s0, s1, mask):
+        self.emit("cnd", d, s0, s1, mask)
+
+    def mul24(self, d, a, b):
+        self.emit("mul24", d, a, b)
+
+    def mul_lo(self, d, a, b):
+        self.emit("mul_lo", d, a, b)
+
+
+# ---------------------------------------------------------------------------
+# registers
+# ---------------------------------------------------------------------------
+def v(n: int) -> str:
+    return f"v{n}"
+
+
+def pair(lo: str) -> str:
+    n = int(lo[1:])
+    assert lo[0] == "v" and n % 2 == 0, lo
+    return f"v[{n}:{n + 1}]"
+
+
+def is_pair(x) -> bool:
+    return isinstance(x, str) and x.startswith("v[")
+
+
+def halves(x) -> list[str]:
+    if is_pair(x):
+        a, b = x[2:-1].split(":")
+        return [f"v{a}", f"v{b}"]
+    if isinstance(x, str):
+        return [x]
+    return []
+
+
+def is_sgpr(x) -> bool:
+    return isinstance(x, str) and x.startswith("%[c")
+
+
+def reads(ins) -> list[str]:
+    out = []
+    for p in OPS[ins[0]][1]:
+        out += halves(ins[p])
+    return out
+
+
+def writes(ins) -> list[str]:
+    out = []
+    for p in OPS[ins[0]][0]:
+        out += halves(ins[p])
+    return out
+
+
+def sgpr_reads(ins) -> list[str]:
+    return [ins[p] for p in OPS[ins[0]][2] if is_sgpr(ins[p])]
+
+
+# ---------------------------------------------------------------------------
+# list scheduler with the SGPR hazard
+# ---------------------------------------------------------------------------
+BRANCH_STATES = 2  # s_cmp_lg_u64 + s_cbranch_scc0 between the blocks
+
+
+def schedule(g: Prog, ages: dict[str, int] | None = None) -> Prog:
+    """List-schedule g.ins; `ages` = wait states already elapsed since each
+    SGPR's last VALU write at entry (for a slow block after a branch)."""
+    ins = g.ins
+    n = len(ins)
+    preds: list[set[int]] = [set() for _ in range(n)]
+    last_w: dict[str, int] = {}
+    last_r: dict[str, list[int]] = {}
+    for j, x in enumerate(ins):
+        for r in reads(x):
+            if r in last_w:
+                preds[j].add(last_w[r])
+        for w in writes(x):
+            if w in last_w:
+                preds[j].add(last_w[w])
+            for i in last_r.get(w, []):
+                if i != j:
+                    preds[j].add(i)
+        for r in reads(x):
+            last_r.setdefault(r, []).append(j)
+        for w in writes(x):
+            last_w[w] = j
+            last_r[w] = []
+    done = [False] * n
+    out = Prog(g.name)
+    t = 0                      # wait-state clock
+    sgpr_wtime: dict[str, int] = {k: -a for k, a in (ages or {}).items()}
+    remaining = n
+    while remaining:
+        pick = None
+        for j in range(n):
+            if done[j] or any(not done[i] for i in preds[j]):
+                continue
+            if all(t - sgpr_wtime.get(s, -99) >= HAZARD_STATES for s in sgpr_reads(ins[j])):
+                pick = j
+                break
+        if pick is None:
+            out.emit("nop")
+            t += 1
+            continue
+        x = ins[pick]
+        out.ins.append(x)
+        t += 1
+        for p in OPS[x[0]][0]:
+            if is_sgpr(x[p]):
+                sgpr_wtime[x[p]] = t
+        done[pick] = True
+        remaining -= 1
+    if g.slow is not None:
+        mask, blk = g.slow
+        exit_ages = {k: t - w + BRANCH_STATES for k, w in sgpr_wtime.items()}
+        out.slow = (mask, schedule(blk, exit_ages))
+    return out
+
+
+def check_hazards(g: Prog, wt: dict[str, int] | None = None, t: int = 0) -> None:
+    wt = dict(wt or {})
+    for x in g.ins:
+        t += 1
+        if x[0] == "nop":
+            continue
+        for s in sgpr_reads(x):
+            assert t - 1 - wt.get(s, -99) >= HAZARD_STATES, (g.name, x, t, wt.get(s))
+        for p in OPS[x[0]][0]:
+            if is_sgpr(x[p]):
+                wt[x[p]] = t
+    if g.slow is not None:
+        check_hazards(g.slow[1], wt, t + BRANCH_STATES)
+
+
+# ---------------------------------------------------------------------------
+# interpreter (one lane)
+# ---------------------------------------------------------------------------
+class Machine:
+    def __init__(self):
+        self.r: dict[str, int] = {}
+
+    def get(self, x) -> int:
+        if isinstance(x, int):
+            return x & M32  # inline constants -16..64 are 32-bit sign-extended
+        if is_pair(x):
+            lo, hi = halves(x)
+            return self.get(lo) | (self.get(hi) << 32)
+        if x not in self.r:
+            raise KeyError(f"read of undefined register {x}")
+        return self.r[x]
+
+    def put(self, x, val: int):
+        if is_pair(x):
+            lo, hi = halves(x)
+            self.r[lo] = val & M32
+            self.r[hi] = (val >> 32) & M32
+        else:
+            self.r[x] = val
+
+    def run(self, g: Prog, force_slow: bool = False):
+        self._run(g)
+        if g.slow is not None:
+            mask, blk = g.slow
+            if force_slow or self.get(mask):
+                self.run(blk, force_slow)
+
+    def _run(self, g: Prog):
+        for x in g.ins:
+            op = x[0]
+            if op == "nop":
+                continue
+            if op == "mad":
+                s = self.get(x[3]) * self.get(x[4]) + self.get(x[5])
+                self.put(x[1], s & M64)
+                self.put(x[2], s >> 64)
+            elif op in ("addc", "add_co"):
+                s = self.get(x[3]) + self.get(x[4]) + (self.get(x[5]) if op == "addc" else 0)
+                self.put(x[1], s & M32)
+                self.put(x[2], s >> 32)
+            elif op in ("subb", "sub_co"):
+                s = self.get(x[3]) - self.get(x[4]) - (self.get(x[5]) if op == "subb" else 0)
+                self.put(x[1], s & M32)
+                self.put(x[2], 1 if s < 0 else 0)
+            elif op == "add":
+                self.put(x[1], (self.get(x[2]) + self.get(x[3])) & M32)
+            elif op == "mov":
+                self.put(x[1], self.get(x[2]))
+            elif op == "cnd":
+                self.put(x[1], self.get(x[3]) if self.get(x[4]) else self.get(x[2]))
+            elif op == "mul_lo":
+                self.put(x[1], (self.get(x[2]) * self.get(x[3])) & M32)
+            elif op == "mul24":
+                a, b = self.get(x[2]), self.get(x[3])
+                assert a < 2**24 and b < 2**24
+                self.put(x[1], (a * b) & M32)
+            else:
+                raise ValueError(op)
+
+
+# ---------------------------------------------------------------------------
+# programs (logical order; schedule() interleaves)
+# ---------------------------------------------------------------------------
+CY = ["%[c0]", "%[c1]", "%[c2]", "%[c3]"]
+
+
+def gen_mul(base: int = MUL_BASE) -> Prog:
+    """r = a * b mod p, weakly reduced (< 2^256).
+    Operands %[a0..7], %[b0..7] -> %[r0..7]; physical temporaries
+    v[base, base+34); carries %[c0..3]."""
+    g = Prog("fe_mul")
+    A = [f"%[a{i}]" for i in range(8)]
+    B = [f"%[b{i}]" for i in range(8)]
+    R = [f"%[r{i}]" for i in range(8)]
+    Pl = [v(base + 2 * k) for k in range(15)]
+    Ph = [v(base + 2 * k + 1) for k in range(15)]
+    PP = [pair(x) for x in Pl]
+    K977 = v(base + 30)
+    T0, T1, T2, T3 = v(base + 30), v(base + 31), v(base + 32), v(base + 33)
+
+    # ---- 512-bit product ----
+    for k in range(15):
+        terms = [(i, k - i) for i in range(8) if 0 <= k - i < 8]
+        src = 0 if k == 0 else PP[k]
+        counted = 0 < k < 14  # col 0 (src 0) and col 14 (top) cannot carry
+        c2 = Ph[k + 1] if k < 14 else None
+        for j, (i, jj) in enumerate(terms):
+            cy = CY[j % 3]
+            g.mad(PP[k], cy, A[i], B[jj], src)
+            src = PP[k]
+            if counted:
+                g.addc(c2, cy, 0 if j == 0 else c2, 0, cy)
+        if k < 14:
+            g.mov(Pl[k + 1], Ph[k])
+            if not counted:
+                g.mov(c2, 0)
+            if k < 8:
+                g.mov(Ph[k], 0)  # {L_k, 0} pair for the fold
+    W = Pl + [Ph[14]]  # w_0 .. w_15
+    L, H = W[:8], W[8:]
+
+    # ---- fold: R = L + 977 H + 2^32 H ----
+    # Y_i = 977 H_i + L_i in place (< 2^43); S = Ylo + (Yhi << 32);
+    # R = S + (H << 32); R_0 = Y_0.lo stays in P_0.lo until the tail.
+    # R_8 goes to T1 with T0 = 0 so {T0, T1} = R_8 * 2^32.
+    g.mov(K977, 977)
+    cyD = CY[3]
+    for i in range(8):
+        g.mad(PP[i], cyD, H[i], K977, PP[i])
+    # K977 is needed again in the tail: keep a copy in T2
+    g.mov(T2, K977)
+    cS, cR = CY[0], CY[1]
+    Ylo = [Pl[i] for i in range(8)]
+    Yhi = [Ph[i] for i in range(8)]
+    g.add_co(Ylo[1], cS, Ylo[1], Yhi[0])
+    g.add_co(R[1], cR, Ylo[1], H[0])
+    for i in range(2, 8):
+        g.addc(Ylo[i], cS, Ylo[i], Yhi[i - 1], cS)
+        g.addc(R[i], cR, Ylo[i], H[i - 1], cR)
+    g.addc(Yhi[7], cS, Yhi[7], 0, cS)       # S_8
+    g.mov(T0, 0)
+    g.addc(T1, cR, Yhi[7], H[7], cR)        # R_8; cR = c9 (weight 2^288)
+
+    # ---- fold 1: add (R_8 + c9 2^32)(2^32 + 977) ----
+    TT = pair(T0)
+    cE = CY[2]
+    g.mad(TT, cE, T1, T2, TT)               # E = 977 R_8 + 2^32 R_8 (+ cE 2^64)
+    g.cnd(T3, 0, T2, cR)                    # 977 c9 -> limb 1
+    g.add(T1, T1, T3)
+    g.cnd(T3, 0, 1, cE)                     # limb 2: cE | c9 (exclusive)
+    g.cnd(T3, T3, 1, cR)
+    cF = CY[0]
+    g.add_co(R[0], cF, Ylo[0], T0)
+    g.addc(R[1], cF, R[1], T1, cF)
+    g.addc(R[2], cF, R[2], T3, cF)
+    # ---- rare tail (uniform branch, taken iff some lane carried out of
+    # limb 2): propagate into limbs 3..7; if that wraps past 2^256 (value is
+    # then < 2^66) add 2^32 + 977 once more.  A no-op for lanes without the
+    # carry, so the whole wave may run it.
+    s = Prog("fe_mul_tail")
+    for i in range(3, 8):
+        s.addc(R[i], cF, R[i], 0, cF)
+    s.cnd(T3, 0, T2, cF)
+    s.cnd(T1, 0, 1, cF)
+    cG = CY[1]
+    s.add_co(R[0], cG, R[0], T3)
+    s.addc(R[1], cG, R[1], T1, cG)
+    s.addc(R[2], cG, R[2], 0, cG)
+    g.slow = (cF, s)
+    return g
+
+
+def _addsub(name: str, sub: bool) -> Prog:
+    """r = a +/- b mod p, weakly reduced.  Chain s = a +/- b (carry c0) and
+    chain t = s +/- K (carry c1) interleave; r = c0 ? t : s.  When both
+    chains carried (only possible with a result within K of the wrap) K is
+    applied once more on limbs 0..2."""
+    g = Prog(name)
+    A = [f"%[a{i}]" for i in range(8)]
+    B = [f"%[b{i}]" for i in range(8)]
+    R = [f"%[r{i}]" for i in range(8)]
+    T = [f"%[t{i}]" for i in range(8)]
+    k977 = "%[k]"
+    c0, c1, c2 = CY[0], CY[1], CY[2]
+    first = g.sub_co if sub else g.add_co
+    nxt = g.subb if sub else g.addc
+    g.mov(k977, 977)
+    Kl = [k977, 1, 0, 0, 0, 0, 0, 0]
+    first(R[0], c0, A[0], B[0])
+    for i in range(1, 8):
+        nxt(R[i], c0, A[i], B[i], c0)
+    first(T[0], c1, R[0], Kl[0])
+    for i in range(1, 8):
+        nxt(T[i], c1, R[i], Kl[i], c1)
+    for i in range(8):
+        g.cnd(R[i], R[i], T[i], c0)
+    g.cnd(T[0], 0, 1, c1)
+    g.cnd(T[0], 0, T[0], c0)                # u = c0 & c1
+    g.mul24(T[1], T[0], k977)               # 977 u
+    first(R[0], c2, R[0], T[1])
+    nxt(R[1], c2, R[1], T[0], c2)
+    nxt(R[2], c2, R[2], 0, c2)
+    return g
+
+
+def gen_add() -> Prog:
+    return _addsub("fe_add", sub=False)
+
+
+def gen_sub() -> Prog:
+    return _addsub("fe_sub", sub=True)
+
+
+
+
+# secp256k1 group order N (curve.go:13) and Montgomery constants (R = 2^256)
+N_ORDER = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+N_LIMBS = [(N_ORDER >> (32 * i)) & M32 for i in range(8)]
+N_C = 2**256 - N_ORDER  # 129 bits
+N_C_LIMBS = [(N_C >> (32 * i)) & M32 for i in range(8)]
+NINV = (-pow(N_ORDER, -1, 2**32)) % 2**32
+MONT_BASE = 0
+MONT_NREGS = 32
+
+
+def _nlimb(j: int):
+    """N_j as an operand: the low four limbs come in VGPR operands, the high
+    four (0xFFFFFFFE, 0xFFFFFFFF x3) are the inline constants -2 / -1."""
+    return f"%[n{j}]" if j < 4 else (-2 if N_LIMBS[j] == 0xFFFFFFFE else -1)
+
+
+def gen_mont(base: int = MONT_BASE) -> Prog:
+    """r = a * b * 2^-256 mod N (Montgomery, product scanning / FIPS), for
+    a * b < N 2^256 (a < 2^256, b < N); output < N.  Operands %[a0..7],
+    %[b0..7], %[n0..3] (N's low limbs), %[nc0..3] (2^256 - N low limbs),
+    %[ninv] (-N^-1 mod 2^32) -> %[r0..7].  Temporaries v[base, base+32):
+    column pairs P_0..P_15; m_k lives in P_{k+8}.lo until column k+7 ends."""
+    g = Prog("sc_mont")
+    A = [f"%[a{i}]" for i in range(8)]
+    B = [f"%[b{i}]" for i in range(8)]
+    R = [f"%[r{i}]" for i in range(8)]
+    Pl = [v(base + 2 * k) for k in range(16)]
+    Ph = [v(base + 2 * k + 1) for k in range(16)]
+    PP = [pair(x) for x in Pl]
+    M = [Pl[k + 8] for k in range(8)]
+    for k in range(15):
+        ab = [(A[i], B[k - i]) for i in range(8) if 0 <= k - i < 8]
+        mn = [(M[i], _nlimb(k - i)) for i in range(8) if 0 <= k - i < 8 and i < k]
+        terms = ab + mn
+        src = 0 if k == 0 else PP[k]
+        c2 = Ph[k + 1]
+        nprod = 0
+        for j, (x, y) in enumerate(terms):
+            cy = CY[nprod % 3]
+            g.mad(PP[k], cy, x, y, src)
+            if src != 0:
+                g.addc(c2, cy, 0 if nprod == 0 or (nprod == 1 and k == 0) else c2, 0, cy)
+            elif k == 0:
+                pass
+            src = PP[k]
+            nprod += 1
+        if k < 8:
+            g.mul_lo(M[k], Pl[k], "%[ninv]")
+            cy = CY[nprod % 3]
+            g.mad(PP[k], cy, M[k], _nlimb(0), PP[k])   # low word becomes 0
+            g.addc(c2, cy, 0 if k == 0 else c2, 0, cy)
+        g.mov(Pl[k + 1], Ph[k])
+    # T = t_0..t_7 (+ t_8 = P_15.hi in {0,1}), T < 2N; t_j = P_{8+j}.lo, t_7 = P_15.lo
+    T = [Pl[8 + j] for j in range(8)]
+    t8 = Ph[15]
+    # D = T + (2^256 - N): carry-out | t_8  <=>  T >= N; then r = sel ? D : T
+    D = [Pl[j] for j in range(8)]
+    cD = CY[0]
+    NC = ["%[nc0]", "%[nc1]", "%[nc2]", "%[nc3]", 1, 0, 0, 0]
+    g.add_co(D[0], cD, T[0], NC[0])
+    for j in range(1, 8):
+        g.addc(D[j], cD, T[j], NC[j], cD)
+    g.addc(Ph[0], cD, t8, 0, cD)                 # t_8 + carry in {0, 1}
+    sel = CY[1]
+    g.sub_co(Ph[1], sel, 0, Ph[0])                # borrow <=> value != 0
+    for j in range(8):
+        g.cnd(R[j], T[j], D[j], sel)
+    return g
+
+
+PROGRAMS = {"fe_mul": gen_mul, "fe_add": gen_add, "fe_sub": gen_sub, "sc_mont": gen_mont}
+
+
+def build(name: str) -> Prog:
+    g = schedule(PROGRAMS[name]())
+    check_hazards(g)
+    return g
+
+
+# ---------------------------------------------------------------------------
+# printer
+# ---------------------------------------------------------------------------
+def fmt(x) -> str:
+    if isinstance(x, int):
+        return str(x)
+    return x
+
+
+def asm_line(x) -> str:
+    op = x[0]
+    if op == "nop":
+        return "s_nop 0"
+    if op == "mad":
+        return f"v_mad_u64_u32 {fmt(x[1])}, {fmt(x[2])}, {fmt(x[3])}, {fmt(x[4])}, {fmt(x[5])}"
+    if op == "addc":
+        return f"v_addc_co_u32_e64 {x[1]}, {x[2]}, {fmt(x[3])}, {fmt(x[4])}, {x[5]}"
+    if op == "add_co":
+        return f"v_add_co_u32_e64 {x[1]}, {x[2]}, {fmt(x[3])}, {fmt(x[4])}"
+    if op == "subb":
+        return f"v_subb_co_u32_e64 {x[1]}, {x[2]}, {fmt(x[3])}, {fmt(x[4])}, {x[5]}"
+    if op == "sub_co":
+        return f"v_sub_co_u32_e64 {x[1]}, {x[2]}, {fmt(x[3])}, {fmt(x[4])}"
+    if op == "add":
+        return f"v_add_u32_e64 {x[1]}, {fmt(x[2])}, {fmt(x[3])}"
+    if op == "mov":
+        return f"v_mov_b32_e32 {x[1]}, {fmt(x[2])}"
+    if op == "cnd":
+        return f"v_cndmask_b32_e64 {x[1]}, {fmt(x[2])}, {fmt(x[3])}, {x[4]}"
+    if op == "mul24":
+        return f"v_mul_u32_u24_e64 {x[1]}, {fmt(x[2])}, {fmt(x[3])}"
+    if op == "mul_lo":
+        return f"v_mul_lo_u32 {x[1]}, {fmt(x[2])}, {fmt(x[3])}"
+    raise ValueError(op)
+
+
+def asm_body(g: Prog) -> str:
+    lines = []
+    for x in g.ins:
+        lines.append(f'      "{asm_line(x)}\\n"')
+    if g.slow is not None:
+        mask, blk = g.slow
+        lines.append(f'      "s_cmp_lg_u64 {mask}, 0\\n"')
+        lines.append(f'      "s_cbranch_scc0 BV_{g.name.upper()}_SKIP_%=\\n"')
+        lines.append(asm_body(blk))
+        lines.append(f'      "BV_{g.name.upper()}_SKIP_%=:\\n"')
+    return "\n".join(lines)
+
+
+def stats(g: Prog) -> dict:
+    from collections import Counter
+
+    c = Counter(x[0] for x in g.ins)
+    out = dict(c)
+    if g.slow is not None:
+        out["rare_tail"] = len(g.slow[1].ins)
+    return out
+
+
+def header() -> str:
+    mul = build("fe_mul")
+    add = build("fe_add")
+    sub = build("fe_sub")
+    mont = build("sc_mont")
+    clob_m = ", ".join(f'"v{MONT_BASE + i}"' for i in range(MONT_NREGS))
+    n_in = ", ".join(f'[n{i}] "v"({hex(N_LIMBS[i])}u)' for i in range(4))
+    nc_in = ", ".join(f'[nc{i}] "v"({hex(N_C_LIMBS[i])}u)' for i in range(4))
+    st = {k: stats(build(k)) for k in PROGRAMS}
+    clob = ", ".join(f'"v{MUL_BASE + i}"' for i in range(MUL_NREGS))
+    a_in = ", ".join(f'[a{i}] "v"(a.v[{i}])' for i in range(8))
+    b_in = ", ".join(f'[b{i}] "v"(b.v[{i}])' for i in range(8))
+    r_out = ", ".join(f'[r{i}] "=&v"(r.v[{i}])' for i in range(8))
+    t_out = ", ".join(f'[t{i}] "=&v"(t[{i}])' for i in range(8))
+    c_out = ", ".join(f'[c{i}] "=&s"(c{i})' for i in range(4))
+    c3_out = ", ".join(f'[c{i}] "=&s"(c{i})' for i in range(3))
+    return f"""// field_asm.h — GENERATED by tools/gen_field_asm.py; do not edit.
+//
+// Hand-scheduled gfx950 field arithmetic mod p = 2^256 - 2^32 - 977 for the
+// device build of field.h.  Same contract as the C++ functions there:
+// inputs < 2^256, outputs weakly reduced (< 2^256, congruent mod p).
+// Instruction mix (after scheduling):
+//   fe_mul: {st['fe_mul']}
+//   fe_add: {st['fe_add']}
+//   fe_sub: {st['fe_sub']}
+//   sc_mont: {st['sc_mont']}
+// The program lists are verified against Python integers by
+// tests/test_field_asm.py (interpreter in the generator), and end to end on
+// the GPU by the bit-exact parity tests.
+#pragma once
+#include <stdint.h>
+
+// r = a * b mod p (weak).  Temporaries: v{MUL_BASE}..v{MUL_BASE + MUL_NREGS - 1} (clobbered).
+__device__ __forceinline__ void fe_mul_asm(fe &r, const fe &a, const fe &b) {{
+  uint64_t c0, c1, c2, c3;
+  asm volatile(
+{asm_body(mul)}
+      : {r_out}, {c_out}
+      : {a_in}, {b_in}
+      : {clob}, "scc");
+}}
+
+// r = a + b mod p (weak)
+__device__ __forceinline__ void fe_add_asm(fe &r, const fe &a, const fe &b) {{
+  uint64_t c0, c1, c2;
+  uint32_t t[8], k;
+  asm volatile(
+{asm_body(add)}
+      : {r_out}, {t_out}, [k] "=&v"(k), {c3_out}
+      : {a_in}, {b_in});
+}}
+
+// r = a - b mod p (weak)
+__device__ __forceinline__ void fe_sub_asm(fe &r, const fe &a, const fe &b) {{
+  uint64_t c0, c1, c2;
+  uint32_t t[8], k;
+  asm volatile(
+{asm_body(sub)}
+      : {r_out}, {t_out}, [k] "=&v"(k), {c3_out}
+      : {a_in}, {b_in});
+}}
+
+// r = a * b * 2^-256 mod N (Montgomery), a < 2^256, b < N; r < N.
+// Temporaries: v{MONT_BASE}..v{MONT_BASE + MONT_NREGS - 1} (clobbered).
+__device__ __forceinline__ void sc_mont_asm(sc &r, const sc &a, const sc &b) {{
+  uint64_t c0, c1, c2;
+  asm volatile(
+{asm_body(mont)}
+      : {r_out}, {c3_out}
+      : {a_in}, {b_in}, {n_in}, {nc_in}, [ninv] "v"({hex(NINV)}u)
+      : {clob_m});
+}}
+"""
+
+
+def main():
+    text = header()
+    if "--check" in sys.argv:
+        cur = open(OUT).read() if os.path.exists(OUT) else ""
+        if cur != text:
+            print(f"{OUT} is stale: run python tools/gen_field_asm.py", file=sys.stderr)
+            sys.exit(1)
+        return
+    with open(OUT, "w") as f:
+        f.write(text)
+    for k in PROGRAMS:
+        print(k, stats(build(k)))
+
+
+if __name__ == "__main__":
+    main()
