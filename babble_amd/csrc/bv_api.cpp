@@ -20,27 +20,35 @@
 namespace bvk {
 hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
 hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
-hipError_t build_tables(hipStream_t, bool, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *);
-hipError_t scalar_prep(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint32_t *, const uint8_t *,
-                       const uint32_t *, const uint32_t *, uint32_t *, uint32_t *);
+hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
+                        uint32_t *);
+hipError_t sinv(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *);
 hipError_t verify_g(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
-                    const uint8_t *, const uint32_t *, const uint32_t *, uint32_t *);
-hipError_t verify_q(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
+                    const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
+                    const uint32_t *, uint32_t *);
+hipError_t verify_q(hipStream_t, int, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
                     const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
 hipError_t verify_generic(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
                           const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
-                          uint8_t *, uint64_t *);
+                          const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
 }  // namespace bvk
 
 namespace {
 
 // Table geometry (must match verify_core.h): generator 16-bit windows x 16
-// (64 MiB, once per ctx); GLV key tables 8-bit windows x 16 + phi (512 KiB).
+// (64 MiB, once per ctx); GLV key tables K8 (8-bit windows x 16 + phi,
+// 512 KiB per key) or K12 (12-bit windows x 11 + phi, 5.5 MiB per key, from
+// 22 six-bit sub-tables).
 constexpr uint32_t kGNwin = 16, kKNwin = 16;
 constexpr uint64_t kGTableBytes = kGNwin * (1ull << 16) * 64ull;
 constexpr uint64_t kKTableBytes = 2ull * kKNwin * (1ull << 8) * 64ull;
-constexpr uint32_t kUStride = 20;  // per-item scalar words (u1, k1, k2, signs)
-constexpr uint32_t kMaxTableKeys = 8192;                                // 4 GiB of key tables
+constexpr uint64_t kK12TableBytes = 2ull * 11 * (1ull << 12) * 64ull;
+constexpr uint64_t kK12SubBytes = 22ull * 64 * 64;
+constexpr uint32_t kBasesPerKey = 22;       // max(K8 16 windows, K12 22 sub-tables)
+constexpr uint64_t kK12MinItemsPerKey = 2048;  // K12 pays for its 11x larger build above this
+constexpr uint32_t kUStride = 12;  // per-item GLV words (k1, k2, signs)
+constexpr uint32_t kMaxTableKeys = 8192;                                // K8: 4 GiB of key tables
+constexpr uint32_t kMaxK12Keys = 1024;                                  // K12: 5.6 GiB
 constexpr uint32_t kPrepM = 16;                                         // items per s^-1 batch
 constexpr uint32_t kRgWords = 25;                                       // R_G words per item
 
@@ -77,7 +85,7 @@ struct DevBuf {
 };
 
 // timing events (see read_timing)
-enum { E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_COUNT };
+enum { E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_SINV, E_COUNT };
 
 }  // namespace
 
@@ -86,15 +94,17 @@ struct bv_ctx {
   uint32_t flags = 0;
   hipStream_t stream = nullptr;   // main
   hipStream_t kstream = nullptr;  // key tables
+  hipStream_t sstream = nullptr;  // batched s^-1
   std::mutex mu;
   std::string err;
   DevBuf g_table, g_xy, g_bases;
   // staging for the host entry point
   DevBuf h_msg_bytes, h_msg_off, h_key_bytes, h_key_off, h_item_msg, h_item_key, h_r, h_s, h_pre;
   // work buffers
-  DevBuf digests, kstatus, kxy, bases_jac, key_table, scratch, u12, rg, status, bits;
+  DevBuf digests, kstatus, kxy, bases_jac, key_sub, key_table, scratch, u12, rg, status, bits;
   hipEvent_t ev[E_COUNT] = {};
   bool table_mode = false;
+  int key_w = 0;  // 8 or 12 in table mode
   bv_timing timing = {};
 };
 
@@ -132,6 +142,7 @@ static int create_impl(bv_ctx *ctx) {
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
   HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
   HIPCHK(hipStreamCreateWithFlags(&ctx->kstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
+  HIPCHK(hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
   for (auto &e : ctx->ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
   // G table: T[j][d] = d * 2^(16j) * G, built once on the device.
   HIPCHK(ctx->g_table.ensure(kGTableBytes), BV_E_OOM, "alloc G table");
@@ -144,7 +155,7 @@ static int create_impl(bv_ctx *ctx) {
       gxy[8 * half + i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
     }
   HIPCHK(hipMemcpyAsync(ctx->g_xy.p, gxy, sizeof gxy, hipMemcpyHostToDevice, ctx->stream), BV_E_LAUNCH, "copy G");
-  HIPCHK(bvk::build_tables(ctx->stream, false, 1, ctx->g_xy.as<uint32_t>(), nullptr, ctx->g_bases.as<uint32_t>(),
+  HIPCHK(bvk::build_tables(ctx->stream, 0, 1, ctx->g_xy.as<uint32_t>(), nullptr, ctx->g_bases.as<uint32_t>(), nullptr,
                            ctx->g_table.as<uint32_t>()),
          BV_E_LAUNCH, "G table");
   HIPCHK(hipStreamSynchronize(ctx->stream), BV_E_LAUNCH, "G table sync");
@@ -180,15 +191,17 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->kstream) (void)hipStreamSynchronize(ctx->kstream);
+  if (ctx->sstream) (void)hipStreamSynchronize(ctx->sstream);
   DevBuf *bufs[] = {&ctx->g_table,     &ctx->g_xy,      &ctx->g_bases,    &ctx->h_msg_bytes, &ctx->h_msg_off,
                     &ctx->h_key_bytes, &ctx->h_key_off, &ctx->h_item_msg, &ctx->h_item_key,  &ctx->h_r,
                     &ctx->h_s,         &ctx->h_pre,     &ctx->digests,    &ctx->kstatus,     &ctx->kxy,
-                    &ctx->bases_jac,   &ctx->key_table, &ctx->scratch,    &ctx->u12,         &ctx->rg,
+                    &ctx->bases_jac,   &ctx->key_sub,     &ctx->key_table, &ctx->scratch,    &ctx->u12,         &ctx->rg,
                     &ctx->status,      &ctx->bits};
   for (auto *b : bufs) b->release();
   for (auto &e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->kstream) (void)hipStreamDestroy(ctx->kstream);
+  if (ctx->sstream) (void)hipStreamDestroy(ctx->sstream);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -236,48 +249,59 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
   // Per-key fixed-base tables pay off once a key signs enough items; with
   // few items per key the generic per-lane path is cheaper.
   const bool table_mode = n_keys <= kMaxTableKeys && n_items >= 16ull * n_keys;
+  const int key_w = !table_mode ? 0
+                    : (n_keys <= kMaxK12Keys && n_items >= kK12MinItemsPerKey * n_keys && !(ctx->flags & BV_F_K8))
+                        ? 12
+                        : 8;
   ctx->table_mode = table_mode;
+  ctx->key_w = key_w;
   if (table_mode) {
-    HIPCHK(ctx->bases_jac.ensure(std::max<uint32_t>(n_keys, 1) * kKNwin * 96ull), BV_E_OOM, "alloc bases");
-    HIPCHK(ctx->key_table.ensure(std::max<uint32_t>(n_keys, 1) * kKTableBytes), BV_E_OOM, "alloc key tables");
+    const uint64_t nk = std::max<uint32_t>(n_keys, 1);
+    HIPCHK(ctx->bases_jac.ensure(nk * kBasesPerKey * 96ull), BV_E_OOM, "alloc bases");
+    if (key_w == 12) HIPCHK(ctx->key_sub.ensure(nk * kK12SubBytes), BV_E_OOM, "alloc key sub-tables");
+    HIPCHK(ctx->key_table.ensure(nk * (key_w == 12 ? kK12TableBytes : kKTableBytes)), BV_E_OOM,
+           "alloc key tables");
     HIPCHK(ctx->rg.ensure(std::max<uint64_t>(n_items, 1) * kRgWords * 4), BV_E_OOM, "alloc R_G");
   }
 
   hipEvent_t *ev = ctx->ev;
   const uint32_t *r32 = (const uint32_t *)b->r_be, *s32 = (const uint32_t *)b->s_be;
+  uint32_t *w = ctx->scratch.as<uint32_t>(), *u12 = ctx->u12.as<uint32_t>();
   HIPCHK(hipEventRecord(ev[E_START], st), BV_E_LAUNCH, "event");
+  // s^-1 needs only s: its own stream, concurrent with everything up to k_verify_g
+  HIPCHK(hipStreamWaitEvent(ctx->sstream, ev[E_START], 0), BV_E_LAUNCH, "fork");
+  HIPCHK(bvk::sinv(ctx->sstream, n_items, kPrepM, s32, b->pre, w), BV_E_LAUNCH, "k_sinv");
+  HIPCHK(hipEventRecord(ev[E_SINV], ctx->sstream), BV_E_LAUNCH, "event");
   HIPCHK(bvk::key_decode(st, n_keys, b->key_bytes, b->key_off, ctx->kstatus.as<uint8_t>(), ctx->kxy.as<uint32_t>()),
          BV_E_LAUNCH, "k_key_decode");
   HIPCHK(hipEventRecord(ev[E_FORK], st), BV_E_LAUNCH, "event");
   if (table_mode) {  // key tables on the keys stream, concurrent with the main stream below
     HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_FORK], 0), BV_E_LAUNCH, "fork");
-    HIPCHK(bvk::build_tables(ctx->kstream, true, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
-                             ctx->bases_jac.as<uint32_t>(), ctx->key_table.as<uint32_t>()),
+    HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
+                             ctx->bases_jac.as<uint32_t>(), ctx->key_sub.as<uint32_t>(),
+                             ctx->key_table.as<uint32_t>()),
            BV_E_LAUNCH, "key tables");
     HIPCHK(hipEventRecord(ev[E_KEYS], ctx->kstream), BV_E_LAUNCH, "event");
   }
   HIPCHK(bvk::sha256(st, n_msgs, b->msg_bytes, b->msg_off, dig), BV_E_LAUNCH, "k_sha256");
   HIPCHK(hipEventRecord(ev[E_SHA], st), BV_E_LAUNCH, "event");
-  HIPCHK(bvk::scalar_prep(st, n_items, kPrepM, r32, s32, b->pre, b->item_msg, dig, ctx->scratch.as<uint32_t>(),
-                          ctx->u12.as<uint32_t>()),
-         BV_E_LAUNCH, "k_scalar_prep");
+  HIPCHK(hipStreamWaitEvent(st, ev[E_SINV], 0), BV_E_LAUNCH, "join");
   HIPCHK(hipEventRecord(ev[E_SCALAR], st), BV_E_LAUNCH, "event");
   if (table_mode) {
-    HIPCHK(bvk::verify_g(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(),
-                         ctx->u12.as<uint32_t>(), ctx->g_table.as<uint32_t>(), ctx->rg.as<uint32_t>()),
+    HIPCHK(bvk::verify_g(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(), b->item_msg, dig, w,
+                         u12, ctx->g_table.as<uint32_t>(), ctx->rg.as<uint32_t>()),
            BV_E_LAUNCH, "k_verify_g");
     HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
     HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
-    HIPCHK(bvk::verify_q(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(),
-                         ctx->u12.as<uint32_t>(), ctx->key_table.as<uint32_t>(), ctx->rg.as<uint32_t>(), status,
-                         bits),
+    HIPCHK(bvk::verify_q(st, key_w, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(), u12,
+                         ctx->key_table.as<uint32_t>(), ctx->rg.as<uint32_t>(), status, bits),
            BV_E_LAUNCH, "k_verify_q");
   } else {
     HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
     HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
     HIPCHK(bvk::verify_generic(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(),
-                               ctx->kxy.as<uint32_t>(), ctx->u12.as<uint32_t>(), ctx->g_table.as<uint32_t>(), status,
+                               ctx->kxy.as<uint32_t>(), b->item_msg, dig, w, ctx->g_table.as<uint32_t>(), status,
                                bits),
            BV_E_LAUNCH, "k_verify_generic");
   }
@@ -296,8 +320,9 @@ static void read_timing(bv_ctx *ctx) {
   hipEvent_t *ev = ctx->ev;
   bv_timing &t = ctx->timing;
   t.ms_sha256 = elapsed(ev[E_FORK], ev[E_SHA]);
+  t.key_path = (uint32_t)ctx->key_w;
   t.ms_keyprep = ctx->table_mode ? elapsed(ev[E_START], ev[E_KEYS]) : elapsed(ev[E_START], ev[E_FORK]);
-  t.ms_scalar = elapsed(ev[E_SHA], ev[E_SCALAR]);
+  t.ms_scalar = elapsed(ev[E_START], ev[E_SINV]);
   t.ms_verify_g = elapsed(ev[E_SCALAR], ev[E_G]);
   t.ms_verify = elapsed(ev[E_JOINED], ev[E_END]);
   t.ms_total = elapsed(ev[E_START], ev[E_END]);

@@ -3,12 +3,13 @@
 //
 // Pipeline for one batch (bv_api.cpp drives it; two streams):
 //   main stream                               keys stream
-//   k_key_decode  (Unmarshal, public_key.go:14)
+//   k_key_decode  (Unmarshal, public_key.go:14)   sinv stream
 //        |--------- fork ------------------>  k_table_bases  B_j = 2^(8j) Q
 //   k_sha256      (crypto.SHA256, hash.go:8)  k_table_fill<8> d * B_j, affine
-//   k_scalar_prep (batched s^-1; u1, u2)            |
-//   k_verify_g    (R_G = u1 G, 16 adds from         |
-//                  the 64 MiB G table)              |
+//        |<-- join -- k_sinv (batched s^-1,         |
+//                     needs only s)                 |
+//   k_verify_g    (u1, u2, GLV split; R_G = u1 G,   |
+//                  16 adds from the G table)        |
 //        |<-------- join ------------------------- -+
 //   k_verify_q    (R = R_G + u2 Q, 32 adds from the key's table; decision
 //                  table; x(R) mod N == r; status + __ballot accept bits)
@@ -42,23 +43,23 @@ __global__ void __launch_bounds__(64) k_table_bases(uint32_t n_bases, const uint
   table_bases_one(b, bxy, bases_jac, w, nwin);
 }
 
-// blockDim = 256, grid (NWIN * 2^W/256, n_bases).  Block (j, c) computes
-// entries d = 256c + t of window j and normalises them to affine with one
-// field inversion (prefix/suffix products in LDS).  PHI: also write the
-// phi(T) half of a GLV key table.
-template <int W, int NWIN, bool PHI>
-__global__ void __launch_bounds__(256) k_table_fill(const uint32_t *__restrict__ bases_jac,
-                                                    const uint8_t *__restrict__ bstatus,
-                                                    uint32_t *__restrict__ table) {
-  constexpr uint32_t chunks = (1u << W) / 256u;
+// blockDim = BLOCK (<= 2^W), grid (NWIN * 2^W/BLOCK, n_bases).  Block (j, c)
+// computes entries d = BLOCK c + t of window j and normalises them to
+// affine with one field inversion (prefix/suffix products in LDS).  PHI:
+// also write the phi(T) half of a GLV key table.
+template <int W, int NWIN, bool PHI, int BLOCK = 256>
+__global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict__ bases_jac,
+                                                      const uint8_t *__restrict__ bstatus,
+                                                      uint32_t *__restrict__ table) {
+  constexpr uint32_t chunks = (1u << W) / BLOCK;
   constexpr uint64_t half_u32 = (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
   const uint32_t b = blockIdx.y;
   const uint32_t j = blockIdx.x / chunks;
-  const uint32_t d = (blockIdx.x % chunks) * 256u + threadIdx.x;
+  const uint32_t d = (blockIdx.x % chunks) * BLOCK + threadIdx.x;
   const uint32_t t = threadIdx.x;
   if (bstatus && bstatus[b] != KS_OK) return;  // uniform per block
-  __shared__ fe sPre[256];
-  __shared__ fe sSuf[256];
+  __shared__ fe sPre[BLOCK];
+  __shared__ fe sSuf[BLOCK];
   __shared__ fe sBx, sBy, sInvTotal;
   if (t == 0) {
     fe x, y;
@@ -75,6 +76,67 @@ __global__ void __launch_bounds__(256) k_table_fill(const uint32_t *__restrict__
   sPre[t] = Z;
   sSuf[t] = Z;
   __syncthreads();
+  for (uint32_t s = 1; s < BLOCK; s <<= 1) {
+    fe p = sPre[t], q = sSuf[t];
+    if (t >= s) fe_mul(p, p, sPre[t - s]);
+    if (t + s < BLOCK) fe_mul(q, q, sSuf[t + s]);
+    __syncthreads();
+    sPre[t] = p;
+    sSuf[t] = q;
+    __syncthreads();
+  }
+  if (t == 0) {
+    fe x;
+    fe_inv(x, sPre[BLOCK - 1]);
+    sInvTotal = x;
+  }
+  __syncthreads();
+  fe zi = sInvTotal;  // Z_t^-1 = prefix(t-1) * suffix(t+1) * (prod Z)^-1
+  if (t > 0) fe_mul(zi, zi, sPre[t - 1]);
+  if (t < BLOCK - 1) fe_mul(zi, zi, sSuf[t + 1]);
+  uint32_t *entry = table + (uint64_t)b * (PHI ? 2 : 1) * half_u32 + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
+  table_store(entry, PHI ? entry + half_u32 : nullptr, d, R, inf, zi);
+}
+
+// K12 key tables from the 6-bit sub-tables (verify_core.h: pair_*).
+// blockDim 256, E entries per thread, grid (NWIN * 2^W / (256 E), n_keys).
+// S_2j and S_2j+1 are staged in LDS; the block's chord denominators are
+// inverted with one field inversion (per-thread running products, then
+// block prefix/suffix products in LDS).  Blocks of the top window that hold
+// only digits >= 2^(128 - W j) (never read) exit at once.
+template <int W, int L, int NWIN, int E>
+__global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__ sub,
+                                                    const uint8_t *__restrict__ bstatus,
+                                                    uint32_t *__restrict__ table) {
+  constexpr uint32_t per_block = 256u * E, chunks = (1u << W) / per_block, NS = 1u << L;
+  constexpr uint64_t half_u32 = (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
+  const uint32_t b = blockIdx.y, j = blockIdx.x / chunks, c = blockIdx.x % chunks, t = threadIdx.x;
+  if (bstatus && bstatus[b] != KS_OK) return;
+  const int live_bits = 128 - W * (int)j;
+  if (live_bits < W && ((c * per_block) >> live_bits) != 0) return;
+  __shared__ uint32_t sLo[NS * BV_ENTRY_U32], sHi[NS * BV_ENTRY_U32];
+  __shared__ fe sPre[256], sSuf[256], sInv;
+  const uint32_t *sk = sub + ((uint64_t)b * 2 * NWIN + 2 * j) * NS * BV_ENTRY_U32;
+  for (uint32_t x = t; x < NS * BV_ENTRY_U32; x += 256) {
+    sLo[x] = sk[x];
+    sHi[x] = sk[NS * BV_ENTRY_U32 + x];
+  }
+  __syncthreads();
+  const uint32_t d0 = c * per_block + t * E;
+  fe pre[E], acc;
+  fe_set(acc, 1);
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    const uint32_t d = d0 + e, lo = d & (NS - 1), hi = d >> L;
+    fe x1, y1, x2, y2, H;
+    pair_load(sLo, sHi, lo, hi, x1, y1, x2, y2);
+    pair_denominator(H, pair_kind(lo, hi), x1, x2);
+    pre[e] = acc;
+    fe_mul(acc, acc, H);
+  }
+  sPre[t] = acc;
+  sSuf[t] = acc;
+  __syncthreads();
   for (uint32_t s = 1; s < 256; s <<= 1) {
     fe p = sPre[t], q = sSuf[t];
     if (t >= s) fe_mul(p, p, sPre[t - s]);
@@ -87,24 +149,32 @@ __global__ void __launch_bounds__(256) k_table_fill(const uint32_t *__restrict__
   if (t == 0) {
     fe x;
     fe_inv(x, sPre[255]);
-    sInvTotal = x;
+    sInv = x;
   }
   __syncthreads();
-  fe zi = sInvTotal;  // Z_t^-1 = prefix(t-1) * suffix(t+1) * (prod Z)^-1
-  if (t > 0) fe_mul(zi, zi, sPre[t - 1]);
-  if (t < 255) fe_mul(zi, zi, sSuf[t + 1]);
-  uint32_t *entry = table + (uint64_t)b * (PHI ? 2 : 1) * half_u32 + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
-  table_store(entry, PHI ? entry + half_u32 : nullptr, d, R, inf, zi);
+  fe q = sInv;  // (this thread's product)^-1 = prefix(t-1) * suffix(t+1) * total^-1
+  if (t > 0) fe_mul(q, q, sPre[t - 1]);
+  if (t < 255) fe_mul(q, q, sSuf[t + 1]);
+  uint32_t *base = table + (uint64_t)b * 2 * half_u32 + ((uint64_t)j << W) * BV_ENTRY_U32;
+#pragma unroll
+  for (int e = E - 1; e >= 0; e--) {
+    const uint32_t d = d0 + e, lo = d & (NS - 1), hi = d >> L;
+    const int kind = pair_kind(lo, hi);
+    fe x1, y1, x2, y2, H, Hinv;
+    pair_load(sLo, sHi, lo, hi, x1, y1, x2, y2);
+    pair_denominator(H, kind, x1, x2);
+    fe_mul(Hinv, q, pre[e]);
+    fe_mul(q, q, H);
+    uint32_t *entry = base + (uint64_t)d * BV_ENTRY_U32;
+    pair_store(entry, entry + half_u32, kind, x1, y1, x2, y2, Hinv);
+  }
 }
 
-__global__ void __launch_bounds__(256) k_scalar_prep(uint64_t n_items, uint32_t M, const uint32_t *__restrict__ r_be,
-                                                     const uint32_t *__restrict__ s_be, const uint8_t *__restrict__ pre,
-                                                     const uint32_t *__restrict__ item_msg,
-                                                     const uint32_t *__restrict__ digest_words,
-                                                     uint32_t *__restrict__ scratch, uint32_t *__restrict__ u12) {
+__global__ void __launch_bounds__(256) k_sinv(uint64_t n_items, uint32_t M, const uint32_t *__restrict__ s_be,
+                                              const uint8_t *__restrict__ pre, uint32_t *__restrict__ w_out) {
   const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  scalar_prep_thread(t, T, n_items, M, r_be, s_be, pre, item_msg, digest_words, scratch, u12);
+  sinv_thread(t, T, n_items, M, s_be, pre, w_out);
 }
 
 __device__ __forceinline__ void write_status(uint64_t i, uint64_t n_items, uint8_t st, uint8_t *status,
@@ -117,12 +187,16 @@ __device__ __forceinline__ void write_status(uint64_t i, uint64_t n_items, uint8
 __global__ void __launch_bounds__(256) k_verify_g(uint64_t n_items, const uint32_t *__restrict__ item_key,
                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
-                                                  const uint32_t *__restrict__ u12,
+                                                  const uint32_t *__restrict__ item_msg,
+                                                  const uint32_t *__restrict__ digest_words,
+                                                  const uint32_t *__restrict__ w_in, uint32_t *__restrict__ u12,
                                                   const uint32_t *__restrict__ g_table, uint32_t *__restrict__ rg) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_items) verify_item_g(i, n_items, item_key, r_be, s_be, pre, kstatus, u12, g_table, rg);
+  if (i < n_items)
+    verify_item_g(i, n_items, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, u12, g_table, rg);
 }
 
+template <int W, int NWIN>
 __global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, const uint32_t *__restrict__ item_key,
                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
@@ -132,7 +206,7 @@ __global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, const uint32
                                                   uint64_t *__restrict__ bits) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t st = BV_REJECT;
-  if (i < n_items) st = verify_item_q(i, n_items, item_key, r_be, s_be, pre, kstatus, u12, key_table, rg);
+  if (i < n_items) st = verify_item_q<W, NWIN>(i, n_items, item_key, r_be, s_be, pre, kstatus, u12, key_table, rg);
   write_status(i, n_items, st, status, bits);
 }
 
@@ -142,12 +216,15 @@ __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, const 
                                                         const uint8_t *__restrict__ pre,
                                                         const uint8_t *__restrict__ kstatus,
                                                         const uint32_t *__restrict__ kxy,
-                                                        const uint32_t *__restrict__ u12,
+                                                        const uint32_t *__restrict__ item_msg,
+                                                        const uint32_t *__restrict__ digest_words,
+                                                        const uint32_t *__restrict__ w_in,
                                                         const uint32_t *__restrict__ g_table,
                                                         uint8_t *__restrict__ status, uint64_t *__restrict__ bits) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t st = BV_REJECT;
-  if (i < n_items) st = verify_item_generic(i, item_key, r_be, s_be, pre, kstatus, kxy, u12, g_table);
+  if (i < n_items)
+    st = verify_item_generic(i, item_key, r_be, s_be, pre, kstatus, kxy, item_msg, digest_words, w_in, g_table);
   write_status(i, n_items, st, status, bits);
 }
 
@@ -170,57 +247,72 @@ hipError_t key_decode(hipStream_t st, uint32_t n, const uint8_t *kb, const uint6
   return hipGetLastError();
 }
 
-// key = false: the generator table (16-bit windows over 256 bits, built once
-// per ctx); key = true: GLV key tables (8-bit windows over 128 bits + phi).
-hipError_t build_tables(hipStream_t st, bool key, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
-                        uint32_t *bases_jac, uint32_t *table) {
+// kw = 0: the generator table (16-bit windows over 256 bits, built once per
+// ctx); kw = 8 / 12: the K8 / K12 GLV key tables (verify_core.h).  `sub`
+// is the K12 sub-table scratch (n_bases * BV_K12SUB_U32 words).
+hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
+                        uint32_t *bases_jac, uint32_t *sub, uint32_t *table) {
   if (n_bases == 0) return hipSuccess;
-  const int w = key ? BV_KW : BV_GW, nwin = key ? BV_KNWIN : BV_GNWIN;
+  const int w = kw == 0 ? BV_GW : kw == 8 ? BV_KW : BV_K12L;
+  const int nwin = kw == 0 ? BV_GNWIN : kw == 8 ? BV_KNWIN : BV_K12NSUB;
   hipLaunchKernelGGL(k_table_bases, grid1(n_bases, 64), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w, nwin);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (key)
-    hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
-                       dim3(256), 0, st, bases_jac, bstatus, table);
-  else
+  if (kw == 0) {
     hipLaunchKernelGGL((k_table_fill<BV_GW, BV_GNWIN, false>), dim3(BV_GNWIN * ((1u << BV_GW) / 256u), n_bases),
                        dim3(256), 0, st, bases_jac, bstatus, table);
+  } else if (kw == 8) {
+    hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
+                       dim3(256), 0, st, bases_jac, bstatus, table);
+  } else {
+    hipLaunchKernelGGL((k_table_fill<BV_K12L, BV_K12NSUB, false, 1 << BV_K12L>), dim3(BV_K12NSUB, n_bases),
+                       dim3(1 << BV_K12L), 0, st, bases_jac, bstatus, sub);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    constexpr int E = 4;
+    hipLaunchKernelGGL((k_table_pair<BV_K12W, BV_K12L, BV_K12NWIN, E>),
+                       dim3(BV_K12NWIN * ((1u << BV_K12W) / (256u * E)), n_bases), dim3(256), 0, st, sub, bstatus,
+                       table);
+  }
   return hipGetLastError();
 }
 
-hipError_t scalar_prep(hipStream_t st, uint64_t n, uint32_t M, const uint32_t *r_be, const uint32_t *s_be,
-                       const uint8_t *pre, const uint32_t *item_msg, const uint32_t *dig, uint32_t *scratch,
-                       uint32_t *u12) {
+hipError_t sinv(hipStream_t st, uint64_t n, uint32_t M, const uint32_t *s_be, const uint8_t *pre, uint32_t *w) {
   if (n == 0) return hipSuccess;
   const uint64_t threads = (n + M - 1) / M;
-  hipLaunchKernelGGL(k_scalar_prep, grid1(threads, 256), dim3(256), 0, st, n, M, r_be, s_be, pre, item_msg, dig,
-                     scratch, u12);
+  hipLaunchKernelGGL(k_sinv, grid1(threads, 256), dim3(256), 0, st, n, M, s_be, pre, w);
   return hipGetLastError();
 }
 
 hipError_t verify_g(hipStream_t st, uint64_t n, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
-                    const uint8_t *pre, const uint8_t *kst, const uint32_t *u12, const uint32_t *g_table,
-                    uint32_t *rg) {
+                    const uint8_t *pre, const uint8_t *kst, const uint32_t *item_msg, const uint32_t *dig,
+                    const uint32_t *w, uint32_t *u12, const uint32_t *g_table, uint32_t *rg) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_verify_g, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, u12, g_table, rg);
+  hipLaunchKernelGGL(k_verify_g, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, item_msg, dig, w,
+                     u12, g_table, rg);
   return hipGetLastError();
 }
 
-hipError_t verify_q(hipStream_t st, uint64_t n, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
-                    const uint8_t *pre, const uint8_t *kst, const uint32_t *u12, const uint32_t *key_table,
-                    const uint32_t *rg, uint8_t *status, uint64_t *bits) {
+hipError_t verify_q(hipStream_t st, int kw, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
+                    const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst, const uint32_t *u12,
+                    const uint32_t *key_table, const uint32_t *rg, uint8_t *status, uint64_t *bits) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_verify_q, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, u12, key_table,
-                     rg, status, bits);
+  if (kw == 8)
+    hipLaunchKernelGGL((k_verify_q<BV_KW, BV_KNWIN>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre,
+                       kst, u12, key_table, rg, status, bits);
+  else
+    hipLaunchKernelGGL((k_verify_q<BV_K12W, BV_K12NWIN>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be,
+                       pre, kst, u12, key_table, rg, status, bits);
   return hipGetLastError();
 }
 
 hipError_t verify_generic(hipStream_t st, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
                           const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst, const uint32_t *kxy,
-                          const uint32_t *u12, const uint32_t *g_table, uint8_t *status, uint64_t *bits) {
+                          const uint32_t *item_msg, const uint32_t *dig, const uint32_t *w, const uint32_t *g_table,
+                          uint8_t *status, uint64_t *bits) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_verify_generic, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, kxy, u12,
-                     g_table, status, bits);
+  hipLaunchKernelGGL(k_verify_generic, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, kxy,
+                     item_msg, dig, w, g_table, status, bits);
   return hipGetLastError();
 }
 

@@ -12,20 +12,32 @@
 
 // Fixed-base tables: T[j][d] = d * 2^(W j) * P (affine, 64 bytes), d < 2^W.
 // The generator table is built once per context with wide windows over the
-// full 256-bit u1.  Key tables are built per batch with 8-bit windows over
-// 128 bits only: u2 is split GLV-style (u2 = k1 + k2 lambda, |k1|,|k2| <
-// 2^128) and the second half of a key table holds phi(T) = (beta x, y), so
-// the serial doubling chain per key is 120 doublings instead of 248.
+// full 256-bit u1.  Key tables are built per batch over 128 bits only: u2 is
+// split GLV-style (u2 = k1 + k2 lambda, |k1|,|k2| < 2^128) and the second
+// half of a key table holds phi(T) = (beta x, y), so the serial doubling
+// chain per key covers 128 bits instead of 256.  Two key-table geometries:
+//   K8:  8-bit windows x 16 (+ phi) = 512 KiB per key, 32 adds per item;
+//        entries by per-thread double-and-add (mid-size batches);
+//   K12: 12-bit windows x 11 (+ phi) = 5.5 MiB per key, 22 adds per item;
+//        entries as sums of two 6-bit sub-table points with one batched
+//        inversion per 1024 entries (large batches: ~16k items per key).
 #define BV_ENTRY_U32 16  // affine x, y = 16 words (64 bytes)
 #define BV_GW 16         // G window bits
 #define BV_GNWIN 16      //   x 16 windows x 65536 entries = 64 MiB
-#define BV_KW 8          // key window bits
-#define BV_KNWIN 16      //   x 16 windows (128 bits) x 256 entries, x 2 (T, phi T) = 512 KiB
 #define BV_GTABLE_U32 ((uint64_t)BV_GNWIN * (1ull << BV_GW) * BV_ENTRY_U32)
+#define BV_KW 8          // K8 window bits
+#define BV_KNWIN 16      //   x 16 windows (128 bits) x 256 entries
 #define BV_KHALF_U32 ((uint64_t)BV_KNWIN * (1ull << BV_KW) * BV_ENTRY_U32)
 #define BV_KTABLE_U32 (2 * BV_KHALF_U32)
-// per-item scalars (k_scalar_prep output): u1[8] | k1[4] | k2[4] | signs | pad
-#define BV_U_STRIDE 20
+#define BV_K12W 12       // K12 window bits
+#define BV_K12NWIN 11    //   x 11 windows (132 bits; the top one holds 8)
+#define BV_K12L 6        // K12 sub-table bits: S_k[x] = x 2^(6k) Q, x < 64
+#define BV_K12NSUB 22    //   k < 22 (offsets 0, 6, ..., 126)
+#define BV_K12HALF_U32 ((uint64_t)BV_K12NWIN * (1ull << BV_K12W) * BV_ENTRY_U32)
+#define BV_K12TABLE_U32 (2 * BV_K12HALF_U32)
+#define BV_K12SUB_U32 ((uint64_t)BV_K12NSUB * (1ull << BV_K12L) * BV_ENTRY_U32)
+// per-item GLV halves of u2 (k_verify_g -> k_verify_q): k1[4] | k2[4] | signs | pad
+#define BV_U_STRIDE 12
 
 // key status (k_key_decode output)
 #define KS_OK 0
@@ -216,6 +228,70 @@ DEV void table_store(uint32_t *entry, uint32_t *phi, uint32_t d, const gej &R, b
   }
 }
 
+// K12 entry (j, d) = S_2j[lo] + S_2j+1[hi], lo = d mod 2^L, hi = d >> L,
+// with S_k[x] = x 2^(Lk) Q affine (zeros for x == 0).  The two points are
+// distinct multiples lo 2^(Wj) Q and hi 2^(Wj+L) Q of Q with
+// 0 < lo < 2^L <= hi 2^L and lo + hi 2^L < 2^W << N, so they are neither
+// equal nor opposite and the affine chord formula applies:
+//   lambda = (y2 - y1) / (x2 - x1), x3 = lambda^2 - x1 - x2,
+//   y3 = lambda (x1 - x3) - y1.
+// The denominators H = x2 - x1 of a block are inverted together
+// (Montgomery's trick, k_table_pair).  kind: 0 zero entry, 1 copy S_lo,
+// 2 copy S_hi, 3 chord sum.
+DEV int pair_kind(uint32_t lo, uint32_t hi) { return (lo ? 1 : 0) | (hi ? 2 : 0); }
+
+DEV void pair_load(const uint32_t *s_lo, const uint32_t *s_hi, uint32_t lo, uint32_t hi, fe &x1, fe &y1, fe &x2,
+                   fe &y2) {
+  fe_load(x1, s_lo + BV_ENTRY_U32 * lo);
+  fe_load(y1, s_lo + BV_ENTRY_U32 * lo + 8);
+  fe_load(x2, s_hi + BV_ENTRY_U32 * hi);
+  fe_load(y2, s_hi + BV_ENTRY_U32 * hi + 8);
+}
+
+// the value joining the batch inversion (1 unless the entry is a sum)
+DEV void pair_denominator(fe &H, int kind, const fe &x1, const fe &x2) {
+  if (kind == 3) fe_sub(H, x2, x1);
+  else fe_set(H, 1);
+}
+
+DEV void pair_store(uint32_t *entry, uint32_t *phi, int kind, const fe &x1, const fe &y1, const fe &x2, const fe &y2,
+                    const fe &Hinv) {
+  fe x, y;
+  if (kind == 3) {
+    fe lam, t;
+    fe_sub(t, y2, y1);
+    fe_mul(lam, t, Hinv);
+    fe_sqr(x, lam);
+    fe_sub(x, x, x1);
+    fe_sub(x, x, x2);
+    fe_sub(t, x1, x);
+    fe_mul(y, lam, t);
+    fe_sub(y, y, y1);
+  } else if (kind == 1) {
+    x = x1;
+    y = y1;
+  } else {
+    x = x2;  // kind 2, or kind 0 with S_hi[0] = zeros
+    y = y2;
+  }
+  fe_canon(x);
+  fe_canon(y);
+  uint32_t v[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    v[i] = x.v[i];
+    v[8 + i] = y.v[i];
+  }
+  store16(entry, v);
+  fe beta, bx;
+  fe_load(beta, FE_BETA);
+  fe_mul(bx, x, beta);
+  fe_canon(bx);
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = bx.v[i];
+  store16(phi, v);
+}
+
 // ---------------------------------------------------------------------------
 // Scalars: u1 = e * s^-1, u2 = r * s^-1 (mod N)  (ecdsa.Verify steps 4-6)
 // ---------------------------------------------------------------------------
@@ -265,11 +341,14 @@ DEV bool s_usable(const uint8_t *pre, uint64_t i, const sc &s) {
   return (pre == nullptr || pre[i] == 0) && !u256_is_zero(s.v) && u256_lt(s.v, SC_N);
 }
 
-// Thread t of T owns items t, t+T, ..., t+(M-1)T; one Fermat inversion for
-// all of them (Montgomery's trick).  Unusable items contribute s = 1.
-DEV void scalar_prep_thread(uint64_t t, uint64_t T, uint64_t n_items, uint32_t M, const uint32_t *r_be,
-                            const uint32_t *s_be, const uint8_t *pre, const uint32_t *item_msg,
-                            const uint32_t *digest_words, uint32_t *scratch, uint32_t *u12) {
+// k_sinv, thread t of T: w_i = s_i^-1 R mod N (Montgomery form) for items
+// t, t+T, ..., t+(M-1)T with one Fermat inversion (Montgomery's trick).
+// Needs only s and pre, so it runs on its own stream concurrently with
+// SHA-256 and the key tables; the digest-dependent products u1 = e w and
+// u2 = r w are formed by k_verify_g (item_scalars).  Unusable items
+// contribute s = 1 and get a w that is never read.
+DEV void sinv_thread(uint64_t t, uint64_t T, uint64_t n_items, uint32_t M, const uint32_t *s_be, const uint8_t *pre,
+                     uint32_t *w_out) {
   sc R2, R1;
   sc_load_const(R2, SC_R2);
   sc_load_const(R1, SC_R1);
@@ -281,8 +360,9 @@ DEV void scalar_prep_thread(uint64_t t, uint64_t T, uint64_t n_items, uint32_t M
     sc_load_be_words(s, s_be + 8 * i);
     if (s_usable(pre, i, s)) sc_mont(sM, s, R2);
     else sM = R1;
-#pragma unroll
-    for (int k = 0; k < 8; k++) scratch[8 * i + k] = acc.v[k];
+    uint4 *q = (uint4 *)(w_out + 8 * i);
+    q[0] = make_uint4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
+    q[1] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
     sc_mont(acc, acc, sM);
   }
   sc inv;
@@ -290,35 +370,38 @@ DEV void scalar_prep_thread(uint64_t t, uint64_t T, uint64_t n_items, uint32_t M
   for (int m = (int)M - 1; m >= 0; m--) {
     const uint64_t i = t + (uint64_t)m * T;
     if (i >= n_items) continue;
-    sc s, sM, pfx, w, e, r, u1, u2;
+    sc s, sM, pfx, w;
     sc_load_be_words(s, s_be + 8 * i);
-    const bool ok = s_usable(pre, i, s);
-    if (ok) sc_mont(sM, s, R2);
+    if (s_usable(pre, i, s)) sc_mont(sM, s, R2);
     else sM = R1;
-#pragma unroll
-    for (int k = 0; k < 8; k++) pfx.v[k] = scratch[8 * i + k];
+    uint4 *q = (uint4 *)(w_out + 8 * i);
+    const uint4 a = q[0], b = q[1];
+    pfx.v[0] = a.x; pfx.v[1] = a.y; pfx.v[2] = a.z; pfx.v[3] = a.w;
+    pfx.v[4] = b.x; pfx.v[5] = b.y; pfx.v[6] = b.z; pfx.v[7] = b.w;
     sc_mont(w, inv, pfx);  // s^-1 R
     sc_mont(inv, inv, sM);
-    sc_load_be_words(e, digest_words + 8 * (uint64_t)item_msg[i]);  // hashToInt: 256 bits, unreduced
-    sc_load_be_words(r, r_be + 8 * i);
-    uint32_t v[20];
-    if (!ok || u256_is_zero(r.v) || !u256_lt(r.v, SC_N)) {
-#pragma unroll
-      for (int k = 0; k < 20; k++) v[k] = 0;  // never used: the item does not reach the math
-    } else {
-      sc_mont(u1, e, w);  // e * s^-1 mod N  (e < 2^256 = R, w < N)
-      sc_mont(u2, r, w);
-      uint32_t signs;
-      glv_split(v + 8, v + 12, signs, u2);
-#pragma unroll
-      for (int k = 0; k < 8; k++) v[k] = u1.v[k];
-      v[16] = signs;
-      v[17] = v[18] = v[19] = 0;
-    }
-    uint4 *q = (uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i);
-#pragma unroll
-    for (int c = 0; c < 5; c++) q[c] = make_uint4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+    q[0] = make_uint4(w.v[0], w.v[1], w.v[2], w.v[3]);
+    q[1] = make_uint4(w.v[4], w.v[5], w.v[6], w.v[7]);
   }
+}
+
+// u1 = e s^-1 and the GLV split of u2 = r s^-1 (mod N) for an item that
+// reaches the math (ecdsa.Verify steps 4-6: e = the 256-bit digest,
+// unreduced; w = s^-1 R from k_sinv).
+DEV void item_scalars(uint64_t i, const uint32_t *r_be, const uint32_t *item_msg, const uint32_t *digest_words,
+                      const uint32_t *w_in, uint32_t u1[8], uint32_t k1[4], uint32_t k2[4], uint32_t &signs) {
+  sc w, e, r, a, b;
+  const uint4 *q = (const uint4 *)(w_in + 8 * i);
+  const uint4 x = q[0], y = q[1];
+  w.v[0] = x.x; w.v[1] = x.y; w.v[2] = x.z; w.v[3] = x.w;
+  w.v[4] = y.x; w.v[5] = y.y; w.v[6] = y.z; w.v[7] = y.w;
+  sc_load_be_words(e, digest_words + 8 * (uint64_t)item_msg[i]);
+  sc_load_be_words(r, r_be + 8 * i);
+  sc_mont(a, e, w);  // e * s^-1 mod N  (e < 2^256 = R, w < N)
+  sc_mont(b, r, w);  // r * s^-1 mod N
+#pragma unroll
+  for (int k = 0; k < 8; k++) u1[k] = a.v[k];
+  glv_split(k1, k2, signs, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -394,15 +477,9 @@ DEV void table_add(gej &R, bool &inf, const uint32_t *tab, const uint32_t *u, bo
   if (neg) fe_neg(R.Y, R.Y);
 }
 
-DEV void load_u1(uint32_t u[8], const uint32_t *u12, uint64_t i) {
-  const uint4 *q = (const uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i);
-  uint4 a = q[0], b = q[1];
-  u[0] = a.x; u[1] = a.y; u[2] = a.z; u[3] = a.w;
-  u[4] = b.x; u[5] = b.y; u[6] = b.z; u[7] = b.w;
-}
 // k1 magnitude, k2 magnitude (4 limbs each) and the sign word
 DEV void load_k(uint32_t k1[4], uint32_t k2[4], uint32_t &signs, const uint32_t *u12, uint64_t i) {
-  const uint4 *q = (const uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i + 8);
+  const uint4 *q = (const uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i);
   uint4 a = q[0], b = q[1], c = q[2];
   k1[0] = a.x; k1[1] = a.y; k1[2] = a.z; k1[3] = a.w;
   k2[0] = b.x; k2[1] = b.y; k2[2] = b.z; k2[3] = b.w;
@@ -434,12 +511,17 @@ DEV void rg_load(const uint32_t *rg, uint64_t n, uint64_t i, gej &R, bool &inf) 
 // Phase 1 (overlaps the key-table build): R_G = u1 G for items that reach
 // the math.
 DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
-                       const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12, const uint32_t *g_table,
+                       const uint8_t *pre, const uint8_t *kstatus, const uint32_t *item_msg,
+                       const uint32_t *digest_words, const uint32_t *w_in, uint32_t *u12, const uint32_t *g_table,
                        uint32_t *rg) {
   fe r;
   if (classify_item(i, item_key, r_be, s_be, pre, kstatus, r) != 0xFF) return;
-  uint32_t u[8];
-  load_u1(u, u12, i);
+  uint32_t u[8], k1[4], k2[4], signs;
+  item_scalars(i, r_be, item_msg, digest_words, w_in, u, k1, k2, signs);
+  uint4 *q = (uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i);
+  q[0] = make_uint4(k1[0], k1[1], k1[2], k1[3]);
+  q[1] = make_uint4(k2[0], k2[1], k2[2], k2[3]);
+  q[2] = make_uint4(signs, 0u, 0u, 0u);
   gej R;
   bool inf = true;
   fe_set(R.X, 0);
@@ -449,11 +531,35 @@ DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const u
   rg_store(rg, n, i, R, inf);
 }
 
+// R += sum_j T[j][digit_j(k)] over a 128-bit GLV half k (4 limbs; consumed:
+// shifted right W bits per window, so digits never straddle limbs).
+template <int W, int NWIN>
+DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bool neg) {
+  if (neg) fe_neg(R.Y, R.Y);
+  for (int j = 0; j < NWIN; j++) {
+    const uint32_t d = k[0] & ((1u << W) - 1u);
+    k[0] = (k[0] >> W) | (k[1] << (32 - W));
+    k[1] = (k[1] >> W) | (k[2] << (32 - W));
+    k[2] = (k[2] >> W) | (k[3] << (32 - W));
+    k[3] >>= W;
+    if (d) {
+      const uint32_t *e = tab + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
+      fe x, y;
+      fe_load4(x, e);
+      fe_load4(y, e + 8);
+      gej_add_ge(R, inf, x, y);
+    }
+  }
+  if (neg) fe_neg(R.Y, R.Y);
+}
+
 // Phase 2: R = R_G + k1 Q + k2 phi(Q) with the key's two half-tables;
 // final check -> status.
+template <int W, int NWIN>
 DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
                           const uint32_t *s_be, const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12,
                           const uint32_t *key_table, const uint32_t *rg) {
+  constexpr uint64_t half = (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
   fe r;
   const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
   if (st != 0xFF) return st;
@@ -462,15 +568,15 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
   gej R;
   bool inf;
   rg_load(rg, n, i, R, inf);
-  const uint32_t *tab = key_table + (uint64_t)item_key[i] * BV_KTABLE_U32;
+  const uint32_t *tab = key_table + (uint64_t)item_key[i] * 2 * half;
   // One loop body for both GLV halves (one inlined copy of the point
-  // addition: smaller code, fewer live registers than two table_add calls).
+  // addition: smaller code, fewer live registers than two calls).
 #pragma unroll 1
   for (int h = 0; h < 2; h++) {
     uint32_t kk[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) kk[c] = h ? k2[c] : k1[c];
-    table_add<BV_KW, BV_KNWIN>(R, inf, tab + (h ? BV_KHALF_U32 : 0), kk, (signs >> h) & 1u);
+    key_table_add<W, NWIN>(R, inf, tab + (h ? half : 0), kk, (signs >> h) & 1u);
   }
   fe_load_be_words(r, r_be + 8 * i);  // reloaded: not kept live through the loop
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
@@ -480,14 +586,14 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
 // (Strauss-Shamir) per-lane double-and-add over the 128-bit GLV halves.
 DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
                                 const uint8_t *pre, const uint8_t *kstatus, const uint32_t *kxy,
-                                const uint32_t *u12, const uint32_t *g_table) {
+                                const uint32_t *item_msg, const uint32_t *digest_words, const uint32_t *w_in,
+                                const uint32_t *g_table) {
   fe r;
   const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
   if (st != 0xFF) return st;
   const uint32_t k = item_key[i];
   uint32_t u1[8], k1[4], k2[4], signs;
-  load_u1(u1, u12, i);
-  load_k(k1, k2, signs, u12, i);
+  item_scalars(i, r_be, item_msg, digest_words, w_in, u1, k1, k2, signs);
   fe q1x, q1y, q2x, q2y, beta;
   fe_load(q1x, kxy + 16 * k);
   fe_load(q1y, kxy + 16 * k + 8);

@@ -23,7 +23,9 @@ REJECT, ACCEPT, REJECT_ERR, REF_PANIC = 0, 1, 2, 3
 SC_OK, SC_NIL, SC_NONPOS, SC_GE_N = 0, 1, 2, 3
 PRE_PARTS_BAD = 0x80
 F_DEFAULT = 0
+ABI_VERSION = 2
 F_KEY_CACHE = 1
+F_K8 = 2
 
 # Every symbol include/babbleverify.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -68,6 +70,7 @@ class BvTiming(ctypes.Structure):
         ("ms_verify", ctypes.c_float),
         ("ms_h2d", ctypes.c_float),
         ("ms_d2h", ctypes.c_float),
+        ("key_path", ctypes.c_uint32),
     ]
 
 
@@ -116,7 +119,7 @@ def lib() -> ctypes.CDLL:
     L.bv_decode_signature.restype = ctypes.c_uint8
     L.bv_hex_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, P]
     L.bv_hex_decode.restype = ctypes.c_int64
-    if L.bv_abi_version() != 1:
+    if L.bv_abi_version() != ABI_VERSION:
         raise BvError(BV_E_ARGS, "ABI version mismatch")
     _lib = L
     return L

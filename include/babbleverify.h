@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define BV_ABI_VERSION 1
+#define BV_ABI_VERSION 2
 
 /* Return codes (per-item outcomes are never errors; they go to status[]). */
 #define BV_OK 0
@@ -64,6 +64,8 @@ extern "C" {
 #define BV_F_DEFAULT 0u
 #define BV_F_KEY_CACHE 1u /* keep per-key tables across calls (validator sets
                              are stable); off by default                       */
+#define BV_F_K8 2u        /* never use the 12-bit key tables (5.5 MiB per key);
+                             8-bit tables only (512 KiB per key)               */
 
 typedef struct bv_ctx bv_ctx;
 
@@ -97,11 +99,12 @@ typedef struct {
   float ms_sha256;   /* k_sha256: message hashing                              */
   float ms_keyprep;  /* key decode + per-key table build (own stream, overlaps
                         hashing, s^-1 and the u1 G phase)                       */
-  float ms_scalar;   /* k_scalar_prep: batched s^-1, u1, u2                     */
-  float ms_verify_g; /* k_verify_g: u1 G from the generator table               */
+  float ms_scalar;   /* k_sinv: batched s^-1 (own stream, from batch start)     */
+  float ms_verify_g; /* k_verify_g: u1, u2 + GLV split, u1 G from the G table   */
   float ms_verify;   /* k_verify_q (+ u2 Q, decision, bits) or k_verify_generic */
   float ms_h2d;      /* host -> device staging (host-buffer entry point only)   */
   float ms_d2h;      /* device -> host results                                  */
+  uint32_t key_path; /* 0: per-lane generic path; 8 / 12: K8 / K12 key tables  */
 } bv_timing;
 
 int bv_abi_version(void);

@@ -26,42 +26,101 @@ void parallel_for(uint64_t n, int nt, F f) {
   for (auto &x : th) x.join();
 }
 
-// k_table_bases + k_table_fill<w>: one (b, window, chunk) block per task; the
-// block's prefix/suffix scans run serially.
-void emu_build_tables(bool key, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, uint32_t *table,
-                      int nt) {
-  const int w = key ? BV_KW : BV_GW;
-  const uint32_t nwin = key ? BV_KNWIN : BV_GNWIN, chunks = (1u << w) / 256u;
+// k_table_bases + k_table_fill<w, nwin, phi, block>: one (b, window, chunk)
+// block per task; the block's prefix/suffix scans run serially.
+void emu_fill(uint32_t n_bases, const uint8_t *bstatus, const uint32_t *bases, int w, uint32_t nwin, bool phi,
+              uint32_t block, uint32_t *table, int nt) {
+  const uint32_t chunks = (1u << w) / block;
   const uint64_t half_u32 = (uint64_t)nwin * (1ull << w) * BV_ENTRY_U32;
-  std::vector<uint32_t> bases((size_t)n_bases * nwin * 24);
-  parallel_for(n_bases, nt, [&](uint64_t b) {
-    if (bstatus && bstatus[b] != KS_OK) return;
-    table_bases_one((uint32_t)b, bxy, bases.data(), w, nwin);
-  });
   parallel_for((uint64_t)n_bases * nwin * chunks, nt, [&](uint64_t task) {
     const uint32_t b = (uint32_t)(task / ((uint64_t)nwin * chunks));
     const uint32_t jc = (uint32_t)(task % ((uint64_t)nwin * chunks));
     const uint32_t j = jc / chunks, c = jc % chunks;
     if (bstatus && bstatus[b] != KS_OK) return;
     fe bx, by;
-    jac_to_affine(bx, by, bases.data() + ((uint64_t)b * nwin + j) * 24);
-    std::vector<gej> R(256);
-    std::vector<fe> Z(256), pre(256), suf(256);
-    bool inf[256];
-    for (uint32_t t = 0; t < 256; t++) table_point(R[t], inf[t], Z[t], bx, by, c * 256 + t, w);
+    jac_to_affine(bx, by, bases + ((uint64_t)b * nwin + j) * 24);
+    std::vector<gej> R(block);
+    std::vector<fe> Z(block), pre(block), suf(block);
+    std::vector<char> inf(block);
+    for (uint32_t t = 0; t < block; t++) {
+      bool f;
+      table_point(R[t], f, Z[t], bx, by, c * block + t, w);
+      inf[t] = f;
+    }
     pre[0] = Z[0];
-    for (int t = 1; t < 256; t++) fe_mul(pre[t], pre[t - 1], Z[t]);
-    suf[255] = Z[255];
-    for (int t = 254; t >= 0; t--) fe_mul(suf[t], suf[t + 1], Z[t]);
+    for (uint32_t t = 1; t < block; t++) fe_mul(pre[t], pre[t - 1], Z[t]);
+    suf[block - 1] = Z[block - 1];
+    for (int t = (int)block - 2; t >= 0; t--) fe_mul(suf[t], suf[t + 1], Z[t]);
     fe inv;
-    fe_inv(inv, pre[255]);
-    for (uint32_t t = 0; t < 256; t++) {
+    fe_inv(inv, pre[block - 1]);
+    for (uint32_t t = 0; t < block; t++) {
       fe zi = inv;
       if (t > 0) fe_mul(zi, zi, pre[t - 1]);
-      if (t < 255) fe_mul(zi, zi, suf[t + 1]);
-      const uint32_t d = c * 256 + t;
-      uint32_t *entry = table + (uint64_t)b * (key ? 2 : 1) * half_u32 + (((uint64_t)j << w) + d) * BV_ENTRY_U32;
-      table_store(entry, key ? entry + half_u32 : nullptr, d, R[t], inf[t], zi);
+      if (t < block - 1) fe_mul(zi, zi, suf[t + 1]);
+      const uint32_t d = c * block + t;
+      uint32_t *entry = table + (uint64_t)b * (phi ? 2 : 1) * half_u32 + (((uint64_t)j << w) + d) * BV_ENTRY_U32;
+      table_store(entry, phi ? entry + half_u32 : nullptr, d, R[t], inf[t] != 0, zi);
+    }
+  });
+}
+
+void emu_bases(uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, std::vector<uint32_t> &bases, int w,
+               uint32_t nwin, int nt) {
+  bases.assign((size_t)n_bases * nwin * 24, 0);
+  parallel_for(n_bases, nt, [&](uint64_t b) {
+    if (bstatus && bstatus[b] != KS_OK) return;
+    table_bases_one((uint32_t)b, bxy, bases.data(), w, nwin);
+  });
+}
+
+// kw = 0: generator table; 8: K8 key tables; 12: K12 key tables (sub-tables,
+// then k_table_pair's blocks of 1024 entries with one batched inversion).
+void emu_build_tables(int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, uint32_t *table,
+                      int nt) {
+  std::vector<uint32_t> bases;
+  if (kw == 0 || kw == 8) {
+    const int w = kw ? BV_KW : BV_GW;
+    const uint32_t nwin = kw ? BV_KNWIN : BV_GNWIN;
+    emu_bases(n_bases, bxy, bstatus, bases, w, nwin, nt);
+    emu_fill(n_bases, bstatus, bases.data(), w, nwin, kw != 0, 256, table, nt);
+    return;
+  }
+  constexpr uint32_t W = BV_K12W, L = BV_K12L, NWIN = BV_K12NWIN, NS = 1u << L, PB = 1024;
+  emu_bases(n_bases, bxy, bstatus, bases, L, BV_K12NSUB, nt);
+  std::vector<uint32_t> sub((size_t)n_bases * BV_K12SUB_U32 + 16);
+  emu_fill(n_bases, bstatus, bases.data(), L, BV_K12NSUB, false, NS, sub.data(), nt);
+  const uint64_t half_u32 = BV_K12HALF_U32;
+  const uint32_t chunks = (1u << W) / PB;
+  parallel_for((uint64_t)n_bases * NWIN * chunks, nt, [&](uint64_t task) {
+    const uint32_t b = (uint32_t)(task / ((uint64_t)NWIN * chunks));
+    const uint32_t j = (uint32_t)(task % ((uint64_t)NWIN * chunks)) / chunks, c = (uint32_t)(task % chunks);
+    if (bstatus && bstatus[b] != KS_OK) return;
+    const int live_bits = 128 - (int)(W * j);
+    if (live_bits < (int)W && ((c * PB) >> live_bits) != 0) return;
+    const uint32_t *s_lo = sub.data() + ((uint64_t)b * 2 * NWIN + 2 * j) * NS * BV_ENTRY_U32;
+    const uint32_t *s_hi = s_lo + NS * BV_ENTRY_U32;
+    std::vector<fe> H(PB), pre(PB);
+    fe acc;
+    fe_set(acc, 1);
+    for (uint32_t e = 0; e < PB; e++) {
+      const uint32_t d = c * PB + e;
+      fe x1, y1, x2, y2;
+      pair_load(s_lo, s_hi, d & (NS - 1), d >> L, x1, y1, x2, y2);
+      pair_denominator(H[e], pair_kind(d & (NS - 1), d >> L), x1, x2);
+      pre[e] = acc;
+      fe_mul(acc, acc, H[e]);
+    }
+    fe q;
+    fe_inv(q, acc);
+    uint32_t *base = table + (uint64_t)b * 2 * half_u32 + ((uint64_t)j << W) * BV_ENTRY_U32;
+    for (int e = PB - 1; e >= 0; e--) {
+      const uint32_t d = c * PB + e;
+      fe x1, y1, x2, y2, Hinv;
+      pair_load(s_lo, s_hi, d & (NS - 1), d >> L, x1, y1, x2, y2);
+      fe_mul(Hinv, q, pre[e]);
+      fe_mul(q, q, H[e]);
+      uint32_t *entry = base + (uint64_t)d * BV_ENTRY_U32;
+      pair_store(entry, entry + half_u32, pair_kind(d & (NS - 1), d >> L), x1, y1, x2, y2, Hinv);
     }
   });
 }
@@ -78,7 +137,7 @@ const uint32_t *emu_g_table(int nt) {
                                                0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu,
                                                0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
                                                0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
-    emu_build_tables(false, 1, G, nullptr, gt, nt);
+    emu_build_tables(0, 1, G, nullptr, gt, nt);
   });
   return gt;
 }
@@ -95,7 +154,8 @@ T *aligned(std::vector<uint8_t> &store, size_t bytes) {
 extern "C" {
 
 // Same pipeline and mode choice as bv_api.cpp run_device, on the host.
-// force_mode: -1 = same rule as the library, 0 = generic, 1 = tables.
+// force_mode: -1 = same rule as the library, 0 = generic, 1 = K8 tables,
+// 2 = K12 tables.  Returns the mode used (0, 1 or 2).
 int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint64_t *bits, int n_threads,
                      int force_mode) {
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
@@ -118,30 +178,37 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
   uint32_t *u12 = aligned<uint32_t>(s_u12, n_items * BV_U_STRIDE * 4 + 64);
   parallel_for(n_msgs, n_threads, [&](uint64_t m) { sha256_one(m, msg, b->msg_off, dig); });
   for (uint32_t k = 0; k < n_keys; k++) key_decode_one(k, b->key_bytes, b->key_off, kst, kxy);
-  const bool table_mode = force_mode >= 0 ? force_mode == 1 : (n_keys <= 8192 && n_items >= 16ull * n_keys);
+  int mode = force_mode;
+  if (mode < 0) {
+    mode = (n_keys <= 8192 && n_items >= 16ull * n_keys) ? 1 : 0;
+    if (mode == 1 && n_keys <= 1024 && n_items >= 2048ull * n_keys) mode = 2;
+  }
+  const bool table_mode = mode != 0;
   const uint32_t *gt = emu_g_table(n_threads);
   uint32_t *kt = nullptr;
   if (table_mode) {
-    kt = aligned<uint32_t>(s_kt, (uint64_t)(n_keys ? n_keys : 1) * BV_KTABLE_U32 * 4);
-    emu_build_tables(true, n_keys, kxy, kst, kt, n_threads);
+    const uint64_t per_key = mode == 2 ? BV_K12TABLE_U32 : BV_KTABLE_U32;
+    kt = aligned<uint32_t>(s_kt, (uint64_t)(n_keys ? n_keys : 1) * per_key * 4);
+    emu_build_tables(mode == 2 ? 12 : 8, n_keys, kxy, kst, kt, n_threads);
   }
   std::vector<uint8_t> s_rg;
   uint32_t *rg = table_mode ? aligned<uint32_t>(s_rg, (n_items + 1) * RG_WORDS * 4) : nullptr;
   const uint32_t M = 16;
   const uint64_t T = ((n_items + M - 1) / M + 255) / 256 * 256;  // kernel grid size
-  parallel_for(T, n_threads, [&](uint64_t t) {
-    scalar_prep_thread(t, T, n_items, M, r, s, b->pre, b->item_msg, dig, scratch, u12);
-  });
+  parallel_for(T, n_threads, [&](uint64_t t) { sinv_thread(t, T, n_items, M, s, b->pre, scratch); });
   std::vector<uint8_t> st(n_items + 1);
   if (table_mode) {
     parallel_for(n_items, n_threads,
-                 [&](uint64_t i) { verify_item_g(i, n_items, b->item_key, r, s, b->pre, kst, u12, gt, rg); });
+                 [&](uint64_t i) {
+                   verify_item_g(i, n_items, b->item_key, r, s, b->pre, kst, b->item_msg, dig, scratch, u12, gt, rg);
+                 });
     parallel_for(n_items, n_threads, [&](uint64_t i) {
-      st[i] = verify_item_q(i, n_items, b->item_key, r, s, b->pre, kst, u12, kt, rg);
+      st[i] = mode == 2 ? verify_item_q<BV_K12W, BV_K12NWIN>(i, n_items, b->item_key, r, s, b->pre, kst, u12, kt, rg)
+                        : verify_item_q<BV_KW, BV_KNWIN>(i, n_items, b->item_key, r, s, b->pre, kst, u12, kt, rg);
     });
   } else {
     parallel_for(n_items, n_threads, [&](uint64_t i) {
-      st[i] = verify_item_generic(i, b->item_key, r, s, b->pre, kst, kxy, u12, gt);
+      st[i] = verify_item_generic(i, b->item_key, r, s, b->pre, kst, kxy, b->item_msg, dig, scratch, gt);
     });
   }
   if (msg_hash && n_msgs) memcpy(msg_hash, dig, n_msgs * 32);
@@ -152,7 +219,7 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
     for (uint64_t i = 0; i < n_items; i++)
       if (st[i] == BV_ACCEPT) bits[i / 64] |= 1ull << (i % 64);
   }
-  return table_mode ? 1 : 0;
+  return mode;
 }
 
 // s^-1 mod N through the device chain (Montgomery in/out handled here).

@@ -72,7 +72,7 @@ def test_glv_constants_and_split():
         assert (k1 + k2 * LAMBDA - k) % N == 0, hex(k)
 
 
-@pytest.mark.parametrize("mode", [1, 0])
+@pytest.mark.parametrize("mode", [2, 1, 0])
 def test_golden_items(mode):
     batch, expected, _ = golden_items_batch()
     h, st, bits, m = emu.verify_batch(batch.as_dict(), force_mode=mode)
@@ -80,7 +80,7 @@ def test_golden_items(mode):
     assert np.array_equal(st, expected)
 
 
-@pytest.mark.parametrize("mode", [1, 0])
+@pytest.mark.parametrize("mode", [2, 1, 0])
 def test_adversarial_mix(mode):
     b = synth.adversarial(2500, seed=21, n_creators=4, scale_per_million=dict(
         rflip=20000, sflip=20000, body=10000, highs=10000, range=8000, fmt=8000, key=12000))
@@ -96,7 +96,7 @@ def test_c1_hashgraph_10k_events():
     """C1: 4 peers, 10k events in the InsertEvent play order; all ACCEPT."""
     b = synth.events(10_000, n_creators=4, seed=1)
     h2, st2, bits2, m = emu.verify_batch(b.as_dict())
-    assert m == 1 and np.all(st2 == 1)
+    assert m == 2 and np.all(st2 == 1)
     for i in (0, 1, 5, 9999):
         assert h2[i].tobytes() == gs.SHA256(b.message(i))
 

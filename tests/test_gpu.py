@@ -102,6 +102,27 @@ def test_c4_adversarial_full_rate(verifier):
     """C4 at 10^5 items with the exact per-million corruption mix."""
     b = synth.adversarial(100_000, seed=44)
     check_against_oracle(verifier, b)
+    assert verifier.timing()["key_path"] == 8
+
+
+def test_k12_tables_adversarial(verifier):
+    """>= 2048 items per key: 12-bit key tables (sub-table chord sums)."""
+    b = synth.adversarial(120_000, seed=12, n_creators=16, scale_per_million=MIX)
+    check_against_oracle(verifier, b)
+    assert verifier.timing()["key_path"] == 12
+
+
+def test_k8_tables_forced_by_flag():
+    """BV_F_K8 keeps the 8-bit key tables on a batch that would take K12."""
+    from babble_amd.verifier import Verifier
+
+    v = Verifier(device=0, flags=native.F_K8)
+    try:
+        b = synth.adversarial(40_000, seed=13, n_creators=8, scale_per_million=MIX)
+        check_against_oracle(v, b)
+        assert v.timing()["key_path"] == 8
+    finally:
+        v.close()
 
 
 def test_generic_path_few_items_per_key(verifier):
@@ -109,6 +130,7 @@ def test_generic_path_few_items_per_key(verifier):
     b = synth.adversarial(640, seed=9, n_creators=64, scale_per_million=MIX)
     assert b.n_items < 16 * b.n_keys
     check_against_oracle(verifier, b)
+    assert verifier.timing()["key_path"] == 0
 
 
 def test_c5_blocks_check_block(verifier):
