@@ -21,7 +21,7 @@ namespace bvk {
 hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
 hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
 hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
-                        uint32_t *);
+                        uint32_t *, uint32_t *);
 hipError_t sinv(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *);
 hipError_t verify_g(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
                     const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
@@ -44,6 +44,7 @@ constexpr uint64_t kGTableBytes = kGNwin * (1ull << 16) * 64ull;
 constexpr uint64_t kKTableBytes = 2ull * kKNwin * (1ull << 8) * 64ull;
 constexpr uint64_t kK12TableBytes = 2ull * 11 * (1ull << 12) * 64ull;
 constexpr uint64_t kK12SubBytes = 22ull * 64 * 64;
+constexpr uint64_t kK12PrefixBytes = 11ull * (1ull << 12) * 32;  // one fe per entry
 constexpr uint32_t kBasesPerKey = 22;       // max(K8 16 windows, K12 22 sub-tables)
 constexpr uint64_t kK12MinItemsPerKey = 2048;  // K12 pays for its 11x larger build above this
 constexpr uint32_t kUStride = 12;  // per-item GLV words (k1, k2, signs)
@@ -101,7 +102,7 @@ struct bv_ctx {
   // staging for the host entry point
   DevBuf h_msg_bytes, h_msg_off, h_key_bytes, h_key_off, h_item_msg, h_item_key, h_r, h_s, h_pre;
   // work buffers
-  DevBuf digests, kstatus, kxy, bases_jac, key_sub, key_table, scratch, u12, rg, status, bits;
+  DevBuf digests, kstatus, kxy, bases_jac, key_sub, key_pscr, key_table, scratch, u12, rg, status, bits;
   hipEvent_t ev[E_COUNT] = {};
   bool table_mode = false;
   int key_w = 0;  // 8 or 12 in table mode
@@ -156,6 +157,7 @@ static int create_impl(bv_ctx *ctx) {
     }
   HIPCHK(hipMemcpyAsync(ctx->g_xy.p, gxy, sizeof gxy, hipMemcpyHostToDevice, ctx->stream), BV_E_LAUNCH, "copy G");
   HIPCHK(bvk::build_tables(ctx->stream, 0, 1, ctx->g_xy.as<uint32_t>(), nullptr, ctx->g_bases.as<uint32_t>(), nullptr,
+                           nullptr,
                            ctx->g_table.as<uint32_t>()),
          BV_E_LAUNCH, "G table");
   HIPCHK(hipStreamSynchronize(ctx->stream), BV_E_LAUNCH, "G table sync");
@@ -195,7 +197,7 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   DevBuf *bufs[] = {&ctx->g_table,     &ctx->g_xy,      &ctx->g_bases,    &ctx->h_msg_bytes, &ctx->h_msg_off,
                     &ctx->h_key_bytes, &ctx->h_key_off, &ctx->h_item_msg, &ctx->h_item_key,  &ctx->h_r,
                     &ctx->h_s,         &ctx->h_pre,     &ctx->digests,    &ctx->kstatus,     &ctx->kxy,
-                    &ctx->bases_jac,   &ctx->key_sub,     &ctx->key_table, &ctx->scratch,    &ctx->u12,         &ctx->rg,
+                    &ctx->bases_jac,   &ctx->key_sub,     &ctx->key_pscr,    &ctx->key_table, &ctx->scratch,    &ctx->u12,         &ctx->rg,
                     &ctx->status,      &ctx->bits};
   for (auto *b : bufs) b->release();
   for (auto &e : ctx->ev)
@@ -258,7 +260,10 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
   if (table_mode) {
     const uint64_t nk = std::max<uint32_t>(n_keys, 1);
     HIPCHK(ctx->bases_jac.ensure(nk * kBasesPerKey * 96ull), BV_E_OOM, "alloc bases");
-    if (key_w == 12) HIPCHK(ctx->key_sub.ensure(nk * kK12SubBytes), BV_E_OOM, "alloc key sub-tables");
+    if (key_w == 12) {
+      HIPCHK(ctx->key_sub.ensure(nk * kK12SubBytes), BV_E_OOM, "alloc key sub-tables");
+      HIPCHK(ctx->key_pscr.ensure(nk * kK12PrefixBytes), BV_E_OOM, "alloc key prefix scratch");
+    }
     HIPCHK(ctx->key_table.ensure(nk * (key_w == 12 ? kK12TableBytes : kKTableBytes)), BV_E_OOM,
            "alloc key tables");
     HIPCHK(ctx->rg.ensure(std::max<uint64_t>(n_items, 1) * kRgWords * 4), BV_E_OOM, "alloc R_G");
@@ -279,7 +284,7 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
     HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_FORK], 0), BV_E_LAUNCH, "fork");
     HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
                              ctx->bases_jac.as<uint32_t>(), ctx->key_sub.as<uint32_t>(),
-                             ctx->key_table.as<uint32_t>()),
+                             ctx->key_pscr.as<uint32_t>(), ctx->key_table.as<uint32_t>()),
            BV_E_LAUNCH, "key tables");
     HIPCHK(hipEventRecord(ev[E_KEYS], ctx->kstream), BV_E_LAUNCH, "event");
   }

@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict
   }
   if (t == 0) {
     fe x;
-    fe_inv(x, sPre[BLOCK - 1]);
+    fe_inv_var(x, sPre[BLOCK - 1]);
     sInvTotal = x;
   }
   __syncthreads();
@@ -99,21 +99,24 @@ __global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict
 }
 
 // K12 key tables from the 6-bit sub-tables (verify_core.h: pair_*).
-// blockDim 256, E entries per thread, grid (NWIN * 2^W / (256 E), n_keys).
-// S_2j and S_2j+1 are staged in LDS; the block's chord denominators are
-// inverted with one field inversion (per-thread running products, then
-// block prefix/suffix products in LDS).  Blocks of the top window that hold
-// only digits >= 2^(128 - W j) (never read) exit at once.
-template <int W, int L, int NWIN, int E>
+// One block of 256 threads per (window j, key): entry d = 256 e + t for
+// e < E (E = 2^W / 256), so a wave shares hi and reads 64 distinct lo.
+// S_2j and S_2j+1 are staged in LDS; the window's chord denominators are
+// inverted with ONE field inversion (per-thread running products whose
+// prefixes go to `pscr`, then block prefix/suffix products in LDS), so the
+// serial inversion latency is paid once per window and the whole grid is
+// resident in one round.  The top window only needs digits
+// < 2^(128 - W j): its blocks stop after the live entries.
+template <int W, int L, int NWIN>
 __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__ sub,
                                                     const uint8_t *__restrict__ bstatus,
-                                                    uint32_t *__restrict__ table) {
-  constexpr uint32_t per_block = 256u * E, chunks = (1u << W) / per_block, NS = 1u << L;
+                                                    uint32_t *__restrict__ table, uint4 *__restrict__ pscr) {
+  constexpr uint32_t E = (1u << W) / 256u, NS = 1u << L;
   constexpr uint64_t half_u32 = (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
-  const uint32_t b = blockIdx.y, j = blockIdx.x / chunks, c = blockIdx.x % chunks, t = threadIdx.x;
+  const uint32_t b = blockIdx.y, j = blockIdx.x, t = threadIdx.x;
   if (bstatus && bstatus[b] != KS_OK) return;
   const int live_bits = 128 - W * (int)j;
-  if (live_bits < W && ((c * per_block) >> live_bits) != 0) return;
+  const uint32_t e_live = live_bits >= W ? E : ((1u << live_bits) + 255u) / 256u;
   __shared__ uint32_t sLo[NS * BV_ENTRY_U32], sHi[NS * BV_ENTRY_U32];
   __shared__ fe sPre[256], sSuf[256], sInv;
   const uint32_t *sk = sub + ((uint64_t)b * 2 * NWIN + 2 * j) * NS * BV_ENTRY_U32;
@@ -122,16 +125,17 @@ __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__
     sHi[x] = sk[NS * BV_ENTRY_U32 + x];
   }
   __syncthreads();
-  const uint32_t d0 = c * per_block + t * E;
-  fe pre[E], acc;
+  uint4 *ps = pscr + ((uint64_t)b * NWIN + j) * E * 2 * 256 + t;
+  fe acc;
   fe_set(acc, 1);
-#pragma unroll
-  for (int e = 0; e < E; e++) {
-    const uint32_t d = d0 + e, lo = d & (NS - 1), hi = d >> L;
+#pragma unroll 1
+  for (uint32_t e = 0; e < e_live; e++) {
+    const uint32_t d = 256 * e + t, lo = d & (NS - 1), hi = d >> L;
     fe x1, y1, x2, y2, H;
     pair_load(sLo, sHi, lo, hi, x1, y1, x2, y2);
     pair_denominator(H, pair_kind(lo, hi), x1, x2);
-    pre[e] = acc;
+    ps[(2 * e) * 256] = make_uint4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
+    ps[(2 * e + 1) * 256] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
     fe_mul(acc, acc, H);
   }
   sPre[t] = acc;
@@ -148,7 +152,7 @@ __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__
   }
   if (t == 0) {
     fe x;
-    fe_inv(x, sPre[255]);
+    fe_inv_var(x, sPre[255]);
     sInv = x;
   }
   __syncthreads();
@@ -156,14 +160,17 @@ __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__
   if (t > 0) fe_mul(q, q, sPre[t - 1]);
   if (t < 255) fe_mul(q, q, sSuf[t + 1]);
   uint32_t *base = table + (uint64_t)b * 2 * half_u32 + ((uint64_t)j << W) * BV_ENTRY_U32;
-#pragma unroll
-  for (int e = E - 1; e >= 0; e--) {
-    const uint32_t d = d0 + e, lo = d & (NS - 1), hi = d >> L;
+#pragma unroll 1
+  for (int e = (int)e_live - 1; e >= 0; e--) {
+    const uint32_t d = 256 * e + t, lo = d & (NS - 1), hi = d >> L;
     const int kind = pair_kind(lo, hi);
-    fe x1, y1, x2, y2, H, Hinv;
+    fe x1, y1, x2, y2, H, Hinv, pre;
     pair_load(sLo, sHi, lo, hi, x1, y1, x2, y2);
     pair_denominator(H, kind, x1, x2);
-    fe_mul(Hinv, q, pre[e]);
+    const uint4 p0 = ps[(2 * e) * 256], p1 = ps[(2 * e + 1) * 256];
+    pre.v[0] = p0.x; pre.v[1] = p0.y; pre.v[2] = p0.z; pre.v[3] = p0.w;
+    pre.v[4] = p1.x; pre.v[5] = p1.y; pre.v[6] = p1.z; pre.v[7] = p1.w;
+    fe_mul(Hinv, q, pre);
     fe_mul(q, q, H);
     uint32_t *entry = base + (uint64_t)d * BV_ENTRY_U32;
     pair_store(entry, entry + half_u32, kind, x1, y1, x2, y2, Hinv);
@@ -249,9 +256,10 @@ hipError_t key_decode(hipStream_t st, uint32_t n, const uint8_t *kb, const uint6
 
 // kw = 0: the generator table (16-bit windows over 256 bits, built once per
 // ctx); kw = 8 / 12: the K8 / K12 GLV key tables (verify_core.h).  `sub`
-// is the K12 sub-table scratch (n_bases * BV_K12SUB_U32 words).
+// is the K12 sub-table scratch (n_bases * BV_K12SUB_U32 words), `pscr` the
+// K12 prefix-product scratch (n_bases * BV_K12HALF_U32 / 2 words).
 hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
-                        uint32_t *bases_jac, uint32_t *sub, uint32_t *table) {
+                        uint32_t *bases_jac, uint32_t *sub, uint32_t *pscr, uint32_t *table) {
   if (n_bases == 0) return hipSuccess;
   const int w = kw == 0 ? BV_GW : kw == 8 ? BV_KW : BV_K12L;
   const int nwin = kw == 0 ? BV_GNWIN : kw == 8 ? BV_KNWIN : BV_K12NSUB;
@@ -269,10 +277,8 @@ hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t
                        dim3(1 << BV_K12L), 0, st, bases_jac, bstatus, sub);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    constexpr int E = 4;
-    hipLaunchKernelGGL((k_table_pair<BV_K12W, BV_K12L, BV_K12NWIN, E>),
-                       dim3(BV_K12NWIN * ((1u << BV_K12W) / (256u * E)), n_bases), dim3(256), 0, st, sub, bstatus,
-                       table);
+    hipLaunchKernelGGL((k_table_pair<BV_K12W, BV_K12L, BV_K12NWIN>), dim3(BV_K12NWIN, n_bases), dim3(256), 0, st, sub,
+                       bstatus, table, (uint4 *)pscr);
   }
   return hipGetLastError();
 }

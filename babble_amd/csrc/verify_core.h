@@ -174,7 +174,7 @@ DEV void jac_to_affine(fe &x, fe &y, const uint32_t *jac) {
   fe_load(X, jac);
   fe_load(Y, jac + 8);
   fe_load(Z, jac + 16);
-  fe_inv(zi, Z);
+  fe_inv_var(zi, Z);
   fe_sqr(zi2, zi);
   fe_mul(zi3, zi2, zi);
   fe_mul(x, X, zi2);
@@ -366,7 +366,7 @@ DEV void sinv_thread(uint64_t t, uint64_t T, uint64_t n_items, uint32_t M, const
     sc_mont(acc, acc, sM);
   }
   sc inv;
-  sc_inverse(inv, acc);
+  sc_inverse_var(inv, acc);
   for (int m = (int)M - 1; m >= 0; m--) {
     const uint64_t i = t + (uint64_t)m * T;
     if (i >= n_items) continue;

@@ -52,7 +52,7 @@ void emu_fill(uint32_t n_bases, const uint8_t *bstatus, const uint32_t *bases, i
     suf[block - 1] = Z[block - 1];
     for (int t = (int)block - 2; t >= 0; t--) fe_mul(suf[t], suf[t + 1], Z[t]);
     fe inv;
-    fe_inv(inv, pre[block - 1]);
+    fe_inv_var(inv, pre[block - 1]);
     for (uint32_t t = 0; t < block; t++) {
       fe zi = inv;
       if (t > 0) fe_mul(zi, zi, pre[t - 1]);
@@ -85,40 +85,38 @@ void emu_build_tables(int kw, uint32_t n_bases, const uint32_t *bxy, const uint8
     emu_fill(n_bases, bstatus, bases.data(), w, nwin, kw != 0, 256, table, nt);
     return;
   }
-  constexpr uint32_t W = BV_K12W, L = BV_K12L, NWIN = BV_K12NWIN, NS = 1u << L, PB = 1024;
+  constexpr uint32_t W = BV_K12W, L = BV_K12L, NWIN = BV_K12NWIN, NS = 1u << L;
   emu_bases(n_bases, bxy, bstatus, bases, L, BV_K12NSUB, nt);
   std::vector<uint32_t> sub((size_t)n_bases * BV_K12SUB_U32 + 16);
   emu_fill(n_bases, bstatus, bases.data(), L, BV_K12NSUB, false, NS, sub.data(), nt);
   const uint64_t half_u32 = BV_K12HALF_U32;
-  const uint32_t chunks = (1u << W) / PB;
-  parallel_for((uint64_t)n_bases * NWIN * chunks, nt, [&](uint64_t task) {
-    const uint32_t b = (uint32_t)(task / ((uint64_t)NWIN * chunks));
-    const uint32_t j = (uint32_t)(task % ((uint64_t)NWIN * chunks)) / chunks, c = (uint32_t)(task % chunks);
+  // k_table_pair: one block per (window, key); the top window stops after
+  // its live digits.  Entry order within the block does not change results.
+  parallel_for((uint64_t)n_bases * NWIN, nt, [&](uint64_t task) {
+    const uint32_t b = (uint32_t)(task / NWIN), j = (uint32_t)(task % NWIN);
     if (bstatus && bstatus[b] != KS_OK) return;
     const int live_bits = 128 - (int)(W * j);
-    if (live_bits < (int)W && ((c * PB) >> live_bits) != 0) return;
+    const uint32_t n_live = live_bits >= (int)W ? (1u << W) : (((1u << live_bits) + 255u) / 256u) * 256u;
     const uint32_t *s_lo = sub.data() + ((uint64_t)b * 2 * NWIN + 2 * j) * NS * BV_ENTRY_U32;
     const uint32_t *s_hi = s_lo + NS * BV_ENTRY_U32;
-    std::vector<fe> H(PB), pre(PB);
+    std::vector<fe> H(n_live), pre(n_live);
     fe acc;
     fe_set(acc, 1);
-    for (uint32_t e = 0; e < PB; e++) {
-      const uint32_t d = c * PB + e;
+    for (uint32_t d = 0; d < n_live; d++) {
       fe x1, y1, x2, y2;
       pair_load(s_lo, s_hi, d & (NS - 1), d >> L, x1, y1, x2, y2);
-      pair_denominator(H[e], pair_kind(d & (NS - 1), d >> L), x1, x2);
-      pre[e] = acc;
-      fe_mul(acc, acc, H[e]);
+      pair_denominator(H[d], pair_kind(d & (NS - 1), d >> L), x1, x2);
+      pre[d] = acc;
+      fe_mul(acc, acc, H[d]);
     }
     fe q;
-    fe_inv(q, acc);
+    fe_inv_var(q, acc);
     uint32_t *base = table + (uint64_t)b * 2 * half_u32 + ((uint64_t)j << W) * BV_ENTRY_U32;
-    for (int e = PB - 1; e >= 0; e--) {
-      const uint32_t d = c * PB + e;
+    for (int d = (int)n_live - 1; d >= 0; d--) {
       fe x1, y1, x2, y2, Hinv;
       pair_load(s_lo, s_hi, d & (NS - 1), d >> L, x1, y1, x2, y2);
-      fe_mul(Hinv, q, pre[e]);
-      fe_mul(q, q, H[e]);
+      fe_mul(Hinv, q, pre[d]);
+      fe_mul(q, q, H[d]);
       uint32_t *entry = base + (uint64_t)d * BV_ENTRY_U32;
       pair_store(entry, entry + half_u32, pair_kind(d & (NS - 1), d >> L), x1, y1, x2, y2, Hinv);
     }
@@ -234,6 +232,18 @@ void emu_sc_inverse(const uint32_t s_le[8], uint32_t out_le[8]) {
   for (int i = 0; i < 8; i++) out_le[i] = r.v[i];
 }
 
+// the same through the variable-time divsteps inversion (modinv.h)
+void emu_sc_inverse_var(const uint32_t s_le[8], uint32_t out_le[8]) {
+  sc s, sM, R2, inv, one, r;
+  for (int i = 0; i < 8; i++) s.v[i] = s_le[i];
+  sc_load_const(R2, SC_R2);
+  sc_mont(sM, s, R2);
+  sc_inverse_var(inv, sM);
+  for (int i = 0; i < 8; i++) one.v[i] = i == 0;
+  sc_mont(r, inv, one);
+  for (int i = 0; i < 8; i++) out_le[i] = r.v[i];
+}
+
 // GLV split of k (< N): magnitudes |k1|, |k2| (4 limbs each) and signs
 void emu_glv_split(const uint32_t k_le[8], uint32_t out[9]) {
   sc k;
@@ -285,6 +295,13 @@ void emu_fe_inv(const uint32_t a[8], uint32_t out[8]) {
   fe x, z;
   for (int i = 0; i < 8; i++) x.v[i] = a[i];
   fe_inv(z, x);
+  fe_canon(z);
+  for (int i = 0; i < 8; i++) out[i] = z.v[i];
+}
+void emu_fe_inv_var(const uint32_t a[8], uint32_t out[8]) {
+  fe x, z;
+  for (int i = 0; i < 8; i++) x.v[i] = a[i];
+  fe_inv_var(z, x);
   fe_canon(z);
   for (int i = 0; i < 8; i++) out[i] = z.v[i];
 }

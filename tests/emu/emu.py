@@ -32,7 +32,7 @@ def lib():
         L.emu_verify_batch.restype = ctypes.c_int
         for f in ("emu_fe_mul", "emu_fe_add", "emu_fe_sub", "emu_sc_mont"):
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-        for f in ("emu_fe_sqr", "emu_fe_inv", "emu_sc_inverse"):
+        for f in ("emu_fe_sqr", "emu_fe_inv", "emu_sc_inverse", "emu_fe_inv_var", "emu_sc_inverse_var"):
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib

@@ -44,6 +44,23 @@ def test_scalar_montgomery_and_inverse():
         assert emu.unop("emu_sc_inverse", s) == pow(s, -1, N)
 
 
+def test_divsteps_inversion():
+    """modinv.h (variable-time Bernstein-Yang) against Python ints, both moduli,
+    including weakly reduced field inputs in [p, 2^256) and sparse operands."""
+    rng = random.Random(5)
+    fe_vals = [1, 2, 3, P - 1, P - 2, P + 1, P + 2, 2**256 - 1, 2**255, 2**32 + 977, 2**128, 2**30, 2**30 - 1]
+    fe_vals += [rng.getrandbits(256) for _ in range(3000)]
+    fe_vals += [1 << rng.randrange(256) for _ in range(100)]
+    fe_vals += [2**256 - 1 - (1 << rng.randrange(256)) for _ in range(100)]
+    for a in fe_vals:
+        if a % P:
+            assert emu.unop("emu_fe_inv_var", a) == pow(a, -1, P), hex(a)
+    sc_vals = [1, 2, 3, N - 1, N - 2, (N + 1) // 2, 2**128, 2**255] + [rng.randrange(1, N) for _ in range(3000)]
+    sc_vals += [1 << rng.randrange(255) for _ in range(100)]
+    for s in sc_vals:
+        assert emu.unop("emu_sc_inverse_var", s) == pow(s, -1, N), hex(s)
+
+
 LAMBDA = 0x5363AD4CC05C30E0A5261C028812645A122E22EA20816678DF02967C1B23BD72
 BETA = 0x7AE96A2B657C07106E64479EAC3434E99CF0497512F58995C1396C28719501EE
 
