@@ -16,6 +16,7 @@
 #include <string>
 
 #include "../../include/babbleverify.h"
+#include "geometry.h"
 
 namespace bvk {
 hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
@@ -39,8 +40,10 @@ namespace {
 // (64 MiB, once per ctx); GLV key tables K8 (8-bit windows x 16 + phi,
 // 512 KiB per key) or K12 (12-bit windows x 11 + phi, 5.5 MiB per key, from
 // 22 six-bit sub-tables).
-constexpr uint32_t kGNwin = 16, kKNwin = 16;
-constexpr uint64_t kGTableBytes = kGNwin * (1ull << 16) * 64ull;
+constexpr uint32_t kKNwin = 16;
+constexpr uint64_t kGTableBytes = BV_GTABLE_U32 * 4;                 // 10.7 GB (geometry.h)
+constexpr uint64_t kGSubBytes = BV_GSUB_U32 * 4;
+constexpr uint64_t kGPrefixBytes = (uint64_t)BV_GPAIR_BLOCKS * 4096 * 32;  // one k_table_pair_g launch
 constexpr uint64_t kKTableBytes = 2ull * kKNwin * (1ull << 8) * 64ull;
 constexpr uint64_t kK12TableBytes = 2ull * 11 * (1ull << 12) * 64ull;
 constexpr uint64_t kK12SubBytes = 22ull * 64 * 64;
@@ -98,7 +101,7 @@ struct bv_ctx {
   hipStream_t sstream = nullptr;  // batched s^-1
   std::mutex mu;
   std::string err;
-  DevBuf g_table, g_xy, g_bases;
+  const uint32_t *g_table = nullptr;  // process-wide, per device (gtable_acquire)
   // staging for the host entry point
   DevBuf h_msg_bytes, h_msg_off, h_key_bytes, h_key_off, h_item_msg, h_item_key, h_r, h_s, h_pre;
   // work buffers
@@ -139,28 +142,71 @@ extern "C" const char *bv_last_error(const bv_ctx *ctx) { return ctx ? ctx->err.
 
 extern "C" void bv_destroy(bv_ctx *ctx);
 
+// The generator table is a constant: one copy per device and process,
+// shared by every context (refcounted), built on first use.
+// T[j][d] = d 2^(BV_GW j) G, j < BV_GNWIN, d < 2^BV_GW (geometry.h);
+// sub-tables and prefix scratch are freed after the build.
+namespace {
+struct GTableSlot {
+  void *table = nullptr;
+  int refs = 0;
+};
+std::mutex g_gtable_mu;
+GTableSlot g_gtables[64];
+}  // namespace
+
+static const uint32_t *gtable_acquire(int device, hipStream_t st) {
+  if (device < 0 || device >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_gtable_mu);
+  GTableSlot &slot = g_gtables[device];
+  if (slot.table) {
+    slot.refs++;
+    return (const uint32_t *)slot.table;
+  }
+  void *table = nullptr, *xy = nullptr, *bases = nullptr, *sub = nullptr, *pscr = nullptr;
+  bool ok = hipMalloc(&table, kGTableBytes) == hipSuccess && hipMalloc(&xy, 64) == hipSuccess &&
+            hipMalloc(&bases, BV_GNSUB * 96) == hipSuccess && hipMalloc(&sub, kGSubBytes) == hipSuccess &&
+            hipMalloc(&pscr, kGPrefixBytes) == hipSuccess;
+  if (ok) {
+    uint32_t gxy[16];
+    for (int half = 0; half < 2; half++)
+      for (int i = 0; i < 8; i++) {
+        const uint8_t *q = kGenerator + 32 * half + 4 * (7 - i);
+        gxy[8 * half + i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+      }
+    ok = hipMemcpyAsync(xy, gxy, sizeof gxy, hipMemcpyHostToDevice, st) == hipSuccess &&
+         bvk::build_tables(st, 0, 1, (const uint32_t *)xy, nullptr, (uint32_t *)bases, (uint32_t *)sub,
+                           (uint32_t *)pscr, (uint32_t *)table) == hipSuccess &&
+         hipStreamSynchronize(st) == hipSuccess;
+  }
+  for (void *p : {xy, bases, sub, pscr})
+    if (p) (void)hipFree(p);
+  if (!ok) {
+    if (table) (void)hipFree(table);
+    return nullptr;
+  }
+  slot.table = table;
+  slot.refs = 1;
+  return (const uint32_t *)table;
+}
+
+static void gtable_release(int device) {
+  std::lock_guard<std::mutex> lk(g_gtable_mu);
+  GTableSlot &slot = g_gtables[device];
+  if (--slot.refs == 0) {
+    (void)hipFree(slot.table);
+    slot.table = nullptr;
+  }
+}
+
 static int create_impl(bv_ctx *ctx) {
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
   HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
   HIPCHK(hipStreamCreateWithFlags(&ctx->kstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
   HIPCHK(hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
   for (auto &e : ctx->ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
-  // G table: T[j][d] = d * 2^(16j) * G, built once on the device.
-  HIPCHK(ctx->g_table.ensure(kGTableBytes), BV_E_OOM, "alloc G table");
-  HIPCHK(ctx->g_xy.ensure(64), BV_E_OOM, "alloc G");
-  HIPCHK(ctx->g_bases.ensure(kGNwin * 24 * 4), BV_E_OOM, "alloc G bases");
-  uint32_t gxy[16];
-  for (int half = 0; half < 2; half++)
-    for (int i = 0; i < 8; i++) {
-      const uint8_t *q = kGenerator + 32 * half + 4 * (7 - i);
-      gxy[8 * half + i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
-    }
-  HIPCHK(hipMemcpyAsync(ctx->g_xy.p, gxy, sizeof gxy, hipMemcpyHostToDevice, ctx->stream), BV_E_LAUNCH, "copy G");
-  HIPCHK(bvk::build_tables(ctx->stream, 0, 1, ctx->g_xy.as<uint32_t>(), nullptr, ctx->g_bases.as<uint32_t>(), nullptr,
-                           nullptr,
-                           ctx->g_table.as<uint32_t>()),
-         BV_E_LAUNCH, "G table");
-  HIPCHK(hipStreamSynchronize(ctx->stream), BV_E_LAUNCH, "G table sync");
+  ctx->g_table = gtable_acquire(ctx->device, ctx->stream);
+  if (!ctx->g_table) return fail(ctx, BV_E_OOM, "generator table (geometry.h, ~10.7 GB of HBM) build failed");
   return BV_OK;
 }
 
@@ -194,7 +240,8 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->kstream) (void)hipStreamSynchronize(ctx->kstream);
   if (ctx->sstream) (void)hipStreamSynchronize(ctx->sstream);
-  DevBuf *bufs[] = {&ctx->g_table,     &ctx->g_xy,      &ctx->g_bases,    &ctx->h_msg_bytes, &ctx->h_msg_off,
+  if (ctx->g_table) gtable_release(ctx->device);
+  DevBuf *bufs[] = {&ctx->h_msg_bytes, &ctx->h_msg_off,
                     &ctx->h_key_bytes, &ctx->h_key_off, &ctx->h_item_msg, &ctx->h_item_key,  &ctx->h_r,
                     &ctx->h_s,         &ctx->h_pre,     &ctx->digests,    &ctx->kstatus,     &ctx->kxy,
                     &ctx->bases_jac,   &ctx->key_sub,     &ctx->key_pscr,    &ctx->key_table, &ctx->scratch,    &ctx->u12,         &ctx->rg,
@@ -294,7 +341,7 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
   HIPCHK(hipEventRecord(ev[E_SCALAR], st), BV_E_LAUNCH, "event");
   if (table_mode) {
     HIPCHK(bvk::verify_g(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(), b->item_msg, dig, w,
-                         u12, ctx->g_table.as<uint32_t>(), ctx->rg.as<uint32_t>()),
+                         u12, ctx->g_table, ctx->rg.as<uint32_t>()),
            BV_E_LAUNCH, "k_verify_g");
     HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
@@ -306,7 +353,7 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
     HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
     HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
     HIPCHK(bvk::verify_generic(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(),
-                               ctx->kxy.as<uint32_t>(), b->item_msg, dig, w, ctx->g_table.as<uint32_t>(), status,
+                               ctx->kxy.as<uint32_t>(), b->item_msg, dig, w, ctx->g_table, status,
                                bits),
            BV_E_LAUNCH, "k_verify_generic");
   }

@@ -1,0 +1,48 @@
+// geometry.h — fixed-base table geometry shared by the kernels (verify_core.h)
+// and the host driver (bv_api.cpp).
+//
+// Fixed-base tables: T[j][d] = d * 2^(W j) * P (affine, 64 bytes), d < 2^W.
+//
+// Generator table: a constant, built once per process and device with wide
+// windows over the full 256-bit u1, sized for the GPU's 288 GB of HBM:
+// 24-bit windows x 11 (264 bits; the top window holds 16) = 10.7 GB, so
+// u1 G costs 11 mixed additions and no doublings.  Entries are chord sums of
+// two 12-bit sub-table points S_k[x] = x 2^(12 k) G.  The host emulator
+// (tests/emu, test infrastructure) overrides BV_GW/BV_GNWIN/BV_GL/BV_GNSUB
+// with a 22-bit geometry to keep its host-memory table at 3 GB; the code
+// paths are the same templates.
+//
+// Key tables are built per batch over 128 bits only: u2 is split GLV-style
+// (u2 = k1 + k2 lambda, |k1|, |k2| < 2^128) and the second half of a key
+// table holds phi(T) = (beta x, y), so the serial doubling chain per key
+// covers 128 bits instead of 256.  Two key-table geometries:
+//   K8:  8-bit windows x 16 (+ phi) = 512 KiB per key, 32 adds per item;
+//        entries by per-thread double-and-add (mid-size batches);
+//   K12: 12-bit windows x 11 (+ phi) = 5.5 MiB per key, 22 adds per item;
+//        entries as chord sums of two 6-bit sub-table points with one
+//        batched inversion per window (large batches: ~16k items per key).
+#pragma once
+
+#define BV_ENTRY_U32 16  // affine x, y = 16 words (64 bytes)
+#ifndef BV_GW
+#define BV_GW 24         // G window bits
+#define BV_GNWIN 11      //   x 11 windows (264 bits) x 16M entries = 10.7 GB
+#define BV_GL 12         // G sub-table bits: S_k[x] = x 2^(12k) G, x < 4096
+#define BV_GNSUB 22      //   k < 22
+#endif
+#define BV_GTABLE_U32 ((uint64_t)BV_GNWIN * (1ull << BV_GW) * BV_ENTRY_U32)
+#define BV_GSUB_U32 ((uint64_t)BV_GNSUB * (1ull << BV_GL) * BV_ENTRY_U32)
+#define BV_GPAIR_BLOCKS 1024  // k_table_pair_g blocks per launch (4096 entries each)
+#define BV_KW 8          // K8 window bits
+#define BV_KNWIN 16      //   x 16 windows (128 bits) x 256 entries
+#define BV_KHALF_U32 ((uint64_t)BV_KNWIN * (1ull << BV_KW) * BV_ENTRY_U32)
+#define BV_KTABLE_U32 (2 * BV_KHALF_U32)
+#define BV_K12W 12       // K12 window bits
+#define BV_K12NWIN 11    //   x 11 windows (132 bits; the top one holds 8)
+#define BV_K12L 6        // K12 sub-table bits: S_k[x] = x 2^(6k) Q, x < 64
+#define BV_K12NSUB 22    //   k < 22 (offsets 0, 6, ..., 126)
+#define BV_K12HALF_U32 ((uint64_t)BV_K12NWIN * (1ull << BV_K12W) * BV_ENTRY_U32)
+#define BV_K12TABLE_U32 (2 * BV_K12HALF_U32)
+#define BV_K12SUB_U32 ((uint64_t)BV_K12NSUB * (1ull << BV_K12L) * BV_ENTRY_U32)
+// per-item GLV halves of u2 (k_verify_g -> k_verify_q): k1[4] | k2[4] | signs | pad
+#define BV_U_STRIDE 12

@@ -177,6 +177,70 @@ __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__
   }
 }
 
+// Generator table window j from the 11-bit G sub-tables: block c holds
+// entries d = 4096 c + 256 e + t (e < 16) of window j, so a wave reads 64
+// consecutive S_lo points and one S_hi point (the sub-tables, 3 MiB, stay
+// in L2/MALL; no LDS staging).  One field inversion per block; prefix
+// products in `pscr` (4096 fe per block).  Launched once per window.
+template <int W, int L>
+__global__ void __launch_bounds__(256) k_table_pair_g(const uint32_t *__restrict__ sub, uint32_t *__restrict__ table,
+                                                      uint4 *__restrict__ pscr, uint32_t j, uint32_t c0) {
+  constexpr uint32_t E = 16, NS = 1u << L;
+  const uint32_t c = c0 + blockIdx.x, t = threadIdx.x;
+  const uint32_t *s_lo = sub + (uint64_t)(2 * j) * NS * BV_ENTRY_U32;
+  const uint32_t *s_hi = s_lo + (uint64_t)NS * BV_ENTRY_U32;
+  __shared__ fe sPre[256], sSuf[256], sInv;
+  uint4 *ps = pscr + (uint64_t)blockIdx.x * E * 2 * 256 + t;
+  fe acc;
+  fe_set(acc, 1);
+#pragma unroll 1
+  for (uint32_t e = 0; e < E; e++) {
+    const uint32_t d = 4096u * c + 256u * e + t, lo = d & (NS - 1), hi = d >> L;
+    fe x1, y1, x2, y2, H;
+    pair_load(s_lo, s_hi, lo, hi, x1, y1, x2, y2);
+    pair_denominator(H, pair_kind(lo, hi), x1, x2);
+    ps[(2 * e) * 256] = make_uint4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
+    ps[(2 * e + 1) * 256] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
+    fe_mul(acc, acc, H);
+  }
+  sPre[t] = acc;
+  sSuf[t] = acc;
+  __syncthreads();
+  for (uint32_t s = 1; s < 256; s <<= 1) {
+    fe p = sPre[t], q = sSuf[t];
+    if (t >= s) fe_mul(p, p, sPre[t - s]);
+    if (t + s < 256) fe_mul(q, q, sSuf[t + s]);
+    __syncthreads();
+    sPre[t] = p;
+    sSuf[t] = q;
+    __syncthreads();
+  }
+  if (t == 0) {
+    fe x;
+    fe_inv_var(x, sPre[255]);
+    sInv = x;
+  }
+  __syncthreads();
+  fe q = sInv;
+  if (t > 0) fe_mul(q, q, sPre[t - 1]);
+  if (t < 255) fe_mul(q, q, sSuf[t + 1]);
+  uint32_t *base = table + ((uint64_t)j << W) * BV_ENTRY_U32;
+#pragma unroll 1
+  for (int e = (int)E - 1; e >= 0; e--) {
+    const uint32_t d = 4096u * c + 256u * e + t, lo = d & (NS - 1), hi = d >> L;
+    const int kind = pair_kind(lo, hi);
+    fe x1, y1, x2, y2, H, Hinv, pre;
+    pair_load(s_lo, s_hi, lo, hi, x1, y1, x2, y2);
+    pair_denominator(H, kind, x1, x2);
+    const uint4 p0 = ps[(2 * e) * 256], p1 = ps[(2 * e + 1) * 256];
+    pre.v[0] = p0.x; pre.v[1] = p0.y; pre.v[2] = p0.z; pre.v[3] = p0.w;
+    pre.v[4] = p1.x; pre.v[5] = p1.y; pre.v[6] = p1.z; pre.v[7] = p1.w;
+    fe_mul(Hinv, q, pre);
+    fe_mul(q, q, H);
+    pair_store(base + (uint64_t)d * BV_ENTRY_U32, nullptr, kind, x1, y1, x2, y2, Hinv);
+  }
+}
+
 __global__ void __launch_bounds__(256) k_sinv(uint64_t n_items, uint32_t M, const uint32_t *__restrict__ s_be,
                                               const uint8_t *__restrict__ pre, uint32_t *__restrict__ w_out) {
   const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
@@ -254,21 +318,36 @@ hipError_t key_decode(hipStream_t st, uint32_t n, const uint8_t *kb, const uint6
   return hipGetLastError();
 }
 
-// kw = 0: the generator table (16-bit windows over 256 bits, built once per
-// ctx); kw = 8 / 12: the K8 / K12 GLV key tables (verify_core.h).  `sub`
+// kw = 0: the generator table (BV_GW-bit windows over 256 bits from
+// BV_GL-bit sub-tables, built once per process and device); kw = 8 / 12: the K8 / K12
+// GLV key tables (verify_core.h).  `sub`
 // is the K12 sub-table scratch (n_bases * BV_K12SUB_U32 words), `pscr` the
 // K12 prefix-product scratch (n_bases * BV_K12HALF_U32 / 2 words).
 hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
                         uint32_t *bases_jac, uint32_t *sub, uint32_t *pscr, uint32_t *table) {
   if (n_bases == 0) return hipSuccess;
-  const int w = kw == 0 ? BV_GW : kw == 8 ? BV_KW : BV_K12L;
-  const int nwin = kw == 0 ? BV_GNWIN : kw == 8 ? BV_KNWIN : BV_K12NSUB;
+  const int w = kw == 0 ? BV_GL : kw == 8 ? BV_KW : BV_K12L;
+  const int nwin = kw == 0 ? BV_GNSUB : kw == 8 ? BV_KNWIN : BV_K12NSUB;
   hipLaunchKernelGGL(k_table_bases, grid1(n_bases, 64), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w, nwin);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (kw == 0) {
-    hipLaunchKernelGGL((k_table_fill<BV_GW, BV_GNWIN, false>), dim3(BV_GNWIN * ((1u << BV_GW) / 256u), n_bases),
-                       dim3(256), 0, st, bases_jac, bstatus, table);
+  if (kw == 0) {  // n_bases == 1 (G); `pscr` holds BV_GPAIR_BLOCKS blocks x 4096 fe
+    hipLaunchKernelGGL((k_table_fill<BV_GL, BV_GNSUB, false>), dim3(BV_GNSUB * ((1u << BV_GL) / 256u), 1), dim3(256),
+                       0, st, bases_jac, bstatus, sub);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    for (uint32_t j = 0; j < BV_GNWIN; j++) {
+      const int live_bits = 256 - BV_GW * (int)j;
+      const uint64_t live = live_bits >= BV_GW ? (1ull << BV_GW) : (1ull << live_bits);
+      const uint32_t blocks = (uint32_t)((live + 4095) / 4096);
+      for (uint32_t c0 = 0; c0 < blocks; c0 += BV_GPAIR_BLOCKS) {
+        const uint32_t nb = blocks - c0 < BV_GPAIR_BLOCKS ? blocks - c0 : BV_GPAIR_BLOCKS;
+        hipLaunchKernelGGL((k_table_pair_g<BV_GW, BV_GL>), dim3(nb), dim3(256), 0, st, sub, table, (uint4 *)pscr, j,
+                           c0);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+      }
+    }
   } else if (kw == 8) {
     hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
                        dim3(256), 0, st, bases_jac, bstatus, table);

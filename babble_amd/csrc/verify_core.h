@@ -7,37 +7,9 @@
 #include <stdint.h>
 
 #include "../../include/babbleverify.h"
+#include "geometry.h"
 #include "point.h"
 #include "sha256.h"
-
-// Fixed-base tables: T[j][d] = d * 2^(W j) * P (affine, 64 bytes), d < 2^W.
-// The generator table is built once per context with wide windows over the
-// full 256-bit u1.  Key tables are built per batch over 128 bits only: u2 is
-// split GLV-style (u2 = k1 + k2 lambda, |k1|,|k2| < 2^128) and the second
-// half of a key table holds phi(T) = (beta x, y), so the serial doubling
-// chain per key covers 128 bits instead of 256.  Two key-table geometries:
-//   K8:  8-bit windows x 16 (+ phi) = 512 KiB per key, 32 adds per item;
-//        entries by per-thread double-and-add (mid-size batches);
-//   K12: 12-bit windows x 11 (+ phi) = 5.5 MiB per key, 22 adds per item;
-//        entries as sums of two 6-bit sub-table points with one batched
-//        inversion per 1024 entries (large batches: ~16k items per key).
-#define BV_ENTRY_U32 16  // affine x, y = 16 words (64 bytes)
-#define BV_GW 16         // G window bits
-#define BV_GNWIN 16      //   x 16 windows x 65536 entries = 64 MiB
-#define BV_GTABLE_U32 ((uint64_t)BV_GNWIN * (1ull << BV_GW) * BV_ENTRY_U32)
-#define BV_KW 8          // K8 window bits
-#define BV_KNWIN 16      //   x 16 windows (128 bits) x 256 entries
-#define BV_KHALF_U32 ((uint64_t)BV_KNWIN * (1ull << BV_KW) * BV_ENTRY_U32)
-#define BV_KTABLE_U32 (2 * BV_KHALF_U32)
-#define BV_K12W 12       // K12 window bits
-#define BV_K12NWIN 11    //   x 11 windows (132 bits; the top one holds 8)
-#define BV_K12L 6        // K12 sub-table bits: S_k[x] = x 2^(6k) Q, x < 64
-#define BV_K12NSUB 22    //   k < 22 (offsets 0, 6, ..., 126)
-#define BV_K12HALF_U32 ((uint64_t)BV_K12NWIN * (1ull << BV_K12W) * BV_ENTRY_U32)
-#define BV_K12TABLE_U32 (2 * BV_K12HALF_U32)
-#define BV_K12SUB_U32 ((uint64_t)BV_K12NSUB * (1ull << BV_K12L) * BV_ENTRY_U32)
-// per-item GLV halves of u2 (k_verify_g -> k_verify_q): k1[4] | k2[4] | signs | pad
-#define BV_U_STRIDE 12
 
 // key status (k_key_decode output)
 #define KS_OK 0
@@ -283,6 +255,7 @@ DEV void pair_store(uint32_t *entry, uint32_t *phi, int kind, const fe &x1, cons
     v[8 + i] = y.v[i];
   }
   store16(entry, v);
+  if (!phi) return;
   fe beta, bx;
   fe_load(beta, FE_BETA);
   fe_mul(bx, x, beta);
@@ -450,22 +423,15 @@ DEV bool final_check(const gej &R, bool inf, const fe &r) {
   return false;
 }
 
-// W-bit digit j of the 256-bit little-endian limb array u (W divides 32 or
-// is 16/8).
-template <int W>
-DEV uint32_t digit(const uint32_t *u, int j) {
-  const int bit = j * W;
-  return (u[bit >> 5] >> (bit & 31)) & ((1u << W) - 1u);
-}
-
-// R += sum_{j < NWIN} T[j][digit_j(u)].  With `neg` (a negative GLV half)
-// the sum is subtracted instead: R - T = -((-R) + T), so R is negated before
-// and after the additions rather than negating every entry.
+// R += sum_j T[j][digit_j(u)] over the 256-bit u1 (8 limbs; consumed:
+// shifted right W bits per window, so digits never straddle limbs).
 template <int W, int NWIN>
-DEV void table_add(gej &R, bool &inf, const uint32_t *tab, const uint32_t *u, bool neg = false) {
-  if (neg) fe_neg(R.Y, R.Y);
+DEV void g_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t u[8]) {
   for (int j = 0; j < NWIN; j++) {
-    const uint32_t d = digit<W>(u, j);
+    const uint32_t d = u[0] & ((1u << W) - 1u);
+#pragma unroll
+    for (int c = 0; c < 7; c++) u[c] = (u[c] >> W) | (u[c + 1] << (32 - W));
+    u[7] >>= W;
     if (d) {
       const uint32_t *e = tab + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
       fe x, y;
@@ -474,7 +440,6 @@ DEV void table_add(gej &R, bool &inf, const uint32_t *tab, const uint32_t *u, bo
       gej_add_ge(R, inf, x, y);
     }
   }
-  if (neg) fe_neg(R.Y, R.Y);
 }
 
 // k1 magnitude, k2 magnitude (4 limbs each) and the sign word
@@ -527,7 +492,7 @@ DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const u
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
   fe_set(R.Z, 0);
-  table_add<BV_GW, BV_GNWIN>(R, inf, g_table, u);
+  g_table_add<BV_GW, BV_GNWIN>(R, inf, g_table, u);
   rg_store(rg, n, i, R, inf);
 }
 
@@ -612,6 +577,6 @@ DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint
     if ((k1[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge(R, inf, q1x, q1y);
     if ((k2[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge(R, inf, q2x, q2y);
   }
-  table_add<BV_GW, BV_GNWIN>(R, inf, g_table, u1);
+  g_table_add<BV_GW, BV_GNWIN>(R, inf, g_table, u1);
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
 }

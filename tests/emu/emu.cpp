@@ -73,16 +73,60 @@ void emu_bases(uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, st
   });
 }
 
-// kw = 0: generator table; 8: K8 key tables; 12: K12 key tables (sub-tables,
-// then k_table_pair's blocks of 1024 entries with one batched inversion).
+// One chunk of chord-sum entries d in [d0, d0 + n) of a window (k_table_pair
+// / k_table_pair_g): one batched inversion, then pair_store.
+void emu_pair_chunk(const uint32_t *s_lo, const uint32_t *s_hi, uint32_t L, uint32_t d0, uint32_t n, uint32_t *base,
+                    uint64_t phi_off) {
+  const uint32_t NS = 1u << L;
+  std::vector<fe> H(n), pre(n);
+  fe acc;
+  fe_set(acc, 1);
+  for (uint32_t k = 0; k < n; k++) {
+    const uint32_t d = d0 + k;
+    fe x1, y1, x2, y2;
+    pair_load(s_lo, s_hi, d & (NS - 1), d >> L, x1, y1, x2, y2);
+    pair_denominator(H[k], pair_kind(d & (NS - 1), d >> L), x1, x2);
+    pre[k] = acc;
+    fe_mul(acc, acc, H[k]);
+  }
+  fe q;
+  fe_inv_var(q, acc);
+  for (int k = (int)n - 1; k >= 0; k--) {
+    const uint32_t d = d0 + k;
+    fe x1, y1, x2, y2, Hinv;
+    pair_load(s_lo, s_hi, d & (NS - 1), d >> L, x1, y1, x2, y2);
+    fe_mul(Hinv, q, pre[k]);
+    fe_mul(q, q, H[k]);
+    uint32_t *entry = base + (uint64_t)d * BV_ENTRY_U32;
+    pair_store(entry, phi_off ? entry + phi_off : nullptr, pair_kind(d & (NS - 1), d >> L), x1, y1, x2, y2, Hinv);
+  }
+}
+
+// kw = 0: generator table (11-bit sub-tables, then k_table_pair_g's chunks
+// of 4096 entries); 8: K8 key tables; 12: K12 key tables (sub-tables, then
+// k_table_pair's one block per window).
 void emu_build_tables(int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, uint32_t *table,
                       int nt) {
   std::vector<uint32_t> bases;
-  if (kw == 0 || kw == 8) {
-    const int w = kw ? BV_KW : BV_GW;
-    const uint32_t nwin = kw ? BV_KNWIN : BV_GNWIN;
-    emu_bases(n_bases, bxy, bstatus, bases, w, nwin, nt);
-    emu_fill(n_bases, bstatus, bases.data(), w, nwin, kw != 0, 256, table, nt);
+  if (kw == 8) {
+    emu_bases(n_bases, bxy, bstatus, bases, BV_KW, BV_KNWIN, nt);
+    emu_fill(n_bases, bstatus, bases.data(), BV_KW, BV_KNWIN, true, 256, table, nt);
+    return;
+  }
+  if (kw == 0) {
+    emu_bases(1, bxy, nullptr, bases, BV_GL, BV_GNSUB, nt);
+    std::vector<uint32_t> sub(BV_GSUB_U32 + 16);
+    emu_fill(1, nullptr, bases.data(), BV_GL, BV_GNSUB, false, 256, sub.data(), nt);
+    const uint32_t NS = 1u << BV_GL;
+    for (uint32_t j = 0; j < BV_GNWIN; j++) {
+      const int live_bits = 256 - BV_GW * (int)j;
+      const uint64_t live = live_bits >= BV_GW ? (1ull << BV_GW) : (1ull << live_bits);
+      const uint32_t *s_lo = sub.data() + (uint64_t)(2 * j) * NS * BV_ENTRY_U32, *s_hi = s_lo + NS * BV_ENTRY_U32;
+      uint32_t *base = table + ((uint64_t)j << BV_GW) * BV_ENTRY_U32;
+      parallel_for((live + 4095) / 4096, nt, [&](uint64_t c) {
+        emu_pair_chunk(s_lo, s_hi, BV_GL, (uint32_t)(c * 4096), 4096, base, 0);
+      });
+    }
     return;
   }
   constexpr uint32_t W = BV_K12W, L = BV_K12L, NWIN = BV_K12NWIN, NS = 1u << L;
@@ -99,27 +143,8 @@ void emu_build_tables(int kw, uint32_t n_bases, const uint32_t *bxy, const uint8
     const uint32_t n_live = live_bits >= (int)W ? (1u << W) : (((1u << live_bits) + 255u) / 256u) * 256u;
     const uint32_t *s_lo = sub.data() + ((uint64_t)b * 2 * NWIN + 2 * j) * NS * BV_ENTRY_U32;
     const uint32_t *s_hi = s_lo + NS * BV_ENTRY_U32;
-    std::vector<fe> H(n_live), pre(n_live);
-    fe acc;
-    fe_set(acc, 1);
-    for (uint32_t d = 0; d < n_live; d++) {
-      fe x1, y1, x2, y2;
-      pair_load(s_lo, s_hi, d & (NS - 1), d >> L, x1, y1, x2, y2);
-      pair_denominator(H[d], pair_kind(d & (NS - 1), d >> L), x1, x2);
-      pre[d] = acc;
-      fe_mul(acc, acc, H[d]);
-    }
-    fe q;
-    fe_inv_var(q, acc);
     uint32_t *base = table + (uint64_t)b * 2 * half_u32 + ((uint64_t)j << W) * BV_ENTRY_U32;
-    for (int d = (int)n_live - 1; d >= 0; d--) {
-      fe x1, y1, x2, y2, Hinv;
-      pair_load(s_lo, s_hi, d & (NS - 1), d >> L, x1, y1, x2, y2);
-      fe_mul(Hinv, q, pre[d]);
-      fe_mul(q, q, H[d]);
-      uint32_t *entry = base + (uint64_t)d * BV_ENTRY_U32;
-      pair_store(entry, entry + half_u32, pair_kind(d & (NS - 1), d >> L), x1, y1, x2, y2, Hinv);
-    }
+    emu_pair_chunk(s_lo, s_hi, L, 0, n_live, base, half_u32);
   });
 }
 
