@@ -39,10 +39,13 @@ IMUL32_PER_VERIFY_POINT = 3_755 * 80
 # profiles/r01_ubench_int.txt): the VALU integer peak denominator.
 PEAK_IMUL32_PER_S = 31.76e12
 # v_mad_u64_u32 executed per item by the verify kernels (gfx950 ISA of
-# field.h: a 7M+4S mixed add = 7*64 + 4*36 product mads + 11*8 reduction
-# mads = 680; 16 G-table adds (16-bit windows) + 32 key-table adds (8-bit
-# windows), less the ~1/256 zero digits; + ~250 for the final check).
-EXEC_MAD_PER_ITEM_POINT = 680 * (16 * (1 - 2**-16) + 32 * (1 - 1 / 256)) + 250
+# field_asm.h: an 8M+3S mixed add = 8*64 + 3*36 product mads + 11*8
+# reduction mads = 708; 11 G-table adds (24-bit windows) + 22 K12 key-table
+# adds (GLV halves, 12-bit windows), less the rare zero digits; + ~250 for
+# u1/u2, the GLV split and the final check).
+EXEC_MAD_PER_ITEM_POINT = 708 * (11 * (1 - 2**-24) + 22 * (1 - 2**-12)) + 250
+# VALU wave64 instruction issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles.
+PEAK_VALU_WAVE_INSTS_PER_S = 256 * 4 * 2.4e9 / 4
 
 
 def parse():
@@ -169,10 +172,18 @@ def main():
         achieved = args.events * IMUL32_PER_VERIFY_POINT / (kv_ms * 1e-3)
         executed = args.events * EXEC_MAD_PER_ITEM_POINT / (kv_ms * 1e-3)
         traffic = None
+        issue_frac = None
         tfile = os.path.join(ROOT, "profiles", "kverify_traffic.json")
         if os.path.exists(tfile):
             with open(tfile) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                tj = json.load(f)
+            if tj.get("items_per_launch") == args.events:
+                traffic = tj.get("hbm_bytes_per_launch")
+                # VALU issue utilisation: PMC wave-instruction count of the
+                # two verify kernels (profiles/, same workload) over their
+                # live HIP-event duration, against 1024 SIMDs x 2.4 GHz / 4
+                # cycles per wave64 VALU instruction.
+                issue_frac = tj["valu_wave_insts_per_launch"] / (kv_ms * 1e-3) / PEAK_VALU_WAVE_INSTS_PER_S
         line = {
             "metric": "ECDSA event verifies/sec",
             "value": value,
@@ -211,9 +222,12 @@ def main():
                 "traffic": traffic,
                 "executed_mad_per_s": executed / 1e12,
                 "executed_frac": executed / PEAK_IMUL32_PER_S,
+                "valu_issue_frac": issue_frac,
                 "note": "frac > 1 is possible: fixed-base per-key tables need ~7x fewer modmuls than the canonical "
                         "Strauss schedule the algorithmic count assumes; executed_frac is the physical "
-                        "v_mad_u64_u32 utilisation",
+                        "v_mad_u64_u32 utilisation; valu_issue_frac is PMC VALU wave-instructions "
+                        "(profiles/kverify_traffic.json) / live duration / issue peak; traffic is "
+                        "PMC FETCH_SIZE(x2)+WRITE_SIZE bytes per launch of the two kernels",
             },
         }
         if not args.no_cpu:
