@@ -34,7 +34,7 @@ def _operands(seed, n):
     return edge + top + limbs + [rng.getrandbits(256) for _ in range(n)]
 
 
-OPS = {"fe_mul": lambda a, b: a * b, "fe_add": lambda a, b: a + b, "fe_sub": lambda a, b: a - b}
+OPS = {"fe_mul": lambda a, b: a * b, "fe_sqr": lambda a, b: a * a, "fe_add": lambda a, b: a + b, "fe_sub": lambda a, b: a - b}
 
 
 @pytest.mark.parametrize("name", sorted(OPS))

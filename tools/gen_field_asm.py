@@ -8,6 +8,8 @@ v_mad_u64_u32) and 30 s_nop (VCC carry-chain hazards); fe_add/fe_sub are
 bound (profiles/r01_pmc_summary.json), so instruction count is the roofline.
 
 Programs emitted:
+  fe_sqr  Comba squaring: 28 off-diagonal products once, doubled, plus the
+          8 diagonal squares (36 mads instead of 64), then fe_mul's fold.
   fe_mul  product-scanning (Comba) 8x8 using v_mad_u64_u32's carry-out: each
           column accumulates in a 64-bit pair P_k, carry-outs are counted in
           the high word of the next column's pair, so a product costs one mad
@@ -57,6 +59,7 @@ OPS = {
     "cnd": ((1,), (2, 3, 4), (4,)),        # d = mask ? s1 : s0
     "mul24": ((1,), (2, 3), ()),           # d = a * b (24-bit operands)
     "mul_lo": ((1,), (2, 3), ()),          # d = lo32(a * b)
+    "alignbit": ((1,), (2, 3), ()),        # d = lo32(({a, b} 64-bit) >> sh), sh = x[4]
     "nop": ((), (), ()),
 }
 
@@ -107,6 +110,9 @@ class Prog:
 
     def mul_lo(self, d, a, b):
         self.emit("mul_lo", d, a, b)
+
+    def alignbit(self, d, hi, lo, sh):
+        self.emit("alignbit", d, hi, lo, sh)
 
 
 # ---------------------------------------------------------------------------
@@ -290,6 +296,8 @@ class Machine:
                 self.put(x[1], self.get(x[3]) if self.get(x[4]) else self.get(x[2]))
             elif op == "mul_lo":
                 self.put(x[1], (self.get(x[2]) * self.get(x[3])) & M32)
+            elif op == "alignbit":
+                self.put(x[1], (((self.get(x[2]) << 32) | self.get(x[3])) >> x[4]) & M32)
             elif op == "mul24":
                 a, b = self.get(x[2]), self.get(x[3])
                 assert a < 2**24 and b < 2**24
@@ -315,8 +323,6 @@ def gen_mul(base: int = MUL_BASE) -> Prog:
     Pl = [v(base + 2 * k) for k in range(15)]
     Ph = [v(base + 2 * k + 1) for k in range(15)]
     PP = [pair(x) for x in Pl]
-    K977 = v(base + 30)
-    T0, T1, T2, T3 = v(base + 30), v(base + 31), v(base + 32), v(base + 33)
 
     # ---- 512-bit product ----
     for k in range(15):
@@ -336,6 +342,14 @@ def gen_mul(base: int = MUL_BASE) -> Prog:
                 g.mov(c2, 0)
             if k < 8:
                 g.mov(Ph[k], 0)  # {L_k, 0} pair for the fold
+    return _fold(g, base, R, Pl, Ph, PP)
+
+
+def _fold(g: Prog, base: int, R, Pl, Ph, PP) -> Prog:
+    """Reduce the 512-bit value w_0..w_15 (w_k = P_k.lo, w_15 = P_14.hi,
+    with P_k.hi = 0 for k < 8) mod p into %[r0..7] (weak)."""
+    K977 = v(base + 30)
+    T0, T1, T2, T3 = v(base + 30), v(base + 31), v(base + 32), v(base + 33)
     W = Pl + [Ph[14]]  # w_0 .. w_15
     L, H = W[:8], W[8:]
 
@@ -388,6 +402,60 @@ def gen_mul(base: int = MUL_BASE) -> Prog:
     s.addc(R[2], cG, R[2], 0, cG)
     g.slow = (cF, s)
     return g
+
+
+def gen_sqr(base: int = MUL_BASE) -> Prog:
+    """r = a^2 mod p, weakly reduced.  Comba squaring: the 28 off-diagonal
+    products a_i a_j (i < j) once, in the column scheme of gen_mul; then
+    W = 2 D + sum a_i^2 2^(64 i) as a doubling carry chain and a diagonal
+    carry chain; then the same fold.  36 mads instead of 64."""
+    g = Prog("fe_sqr")
+    A = [f"%[a{i}]" for i in range(8)]
+    R = [f"%[r{i}]" for i in range(8)]
+    Pl = [v(base + 2 * k) for k in range(15)]
+    Ph = [v(base + 2 * k + 1) for k in range(15)]
+    PP = [pair(x) for x in Pl]
+    T01, T23 = pair(v(base + 30)), pair(v(base + 32))
+
+    # ---- off-diagonal D = sum_{i<j} a_i a_j 2^(32(i+j)): columns 1..13 ----
+    for k in range(1, 14):
+        terms = [(i, k - i) for i in range(8) if i < k - i <= 7]
+        src = 0 if k == 1 else PP[k]
+        counted = k > 1  # column 1: one product, zero addend: no carry
+        c2 = Ph[k + 1]
+        for j, (i, jj) in enumerate(terms):
+            cy = CY[j % 3]
+            g.mad(PP[k], cy, A[i], A[jj], src)
+            src = PP[k]
+            if counted:
+                g.addc(c2, cy, 0 if j == 0 else c2, 0, cy)
+        if not counted:
+            g.mov(c2, 0)
+        g.mov(Pl[k + 1], Ph[k])
+        if k < 8:
+            g.mov(Ph[k], 0)  # {L_k, 0} pair for the fold
+    # D: d_0 = 0, d_m = P_m.lo (1 <= m <= 14), d_15 = P_14.hi
+    Dw = [None] + [Pl[m] for m in range(1, 15)] + [Ph[14]]
+
+    # ---- E = 2 D (carry chain, 2 D < 2^512; it interleaves with the
+    # diagonal chain below, so the carry hazards need no s_nop) ----
+    cE = CY[0]
+    g.add_co(Dw[1], cE, Dw[1], Dw[1])
+    for m in range(2, 16):
+        g.addc(Dw[m], cE, Dw[m], Dw[m], cE)
+
+    # ---- W = E + sum a_i^2 2^(64 i) ----
+    cQ = CY[1]
+    g.mad(PP[0], CY[3], A[0], A[0], 0)           # w_0, and a_0^2 hi -> w_1
+    g.add_co(Dw[1], cQ, Dw[1], Ph[0])
+    g.mov(Ph[0], 0)
+    for i in range(1, 8):
+        tp = T01 if i % 2 else T23
+        tl, th = halves(tp)
+        g.mad(tp, CY[2] if i % 2 else CY[3], A[i], A[i], 0)
+        g.addc(Dw[2 * i], cQ, Dw[2 * i], tl, cQ)
+        g.addc(Dw[2 * i + 1], cQ, Dw[2 * i + 1], th, cQ)
+    return _fold(g, base, R, Pl, Ph, PP)
 
 
 def _addsub(name: str, sub: bool) -> Prog:
@@ -503,7 +571,7 @@ def gen_mont(base: int = MONT_BASE) -> Prog:
     return g
 
 
-PROGRAMS = {"fe_mul": gen_mul, "fe_add": gen_add, "fe_sub": gen_sub, "sc_mont": gen_mont}
+PROGRAMS = {"fe_mul": gen_mul, "fe_sqr": gen_sqr, "fe_add": gen_add, "fe_sub": gen_sub, "sc_mont": gen_mont}
 
 
 def build(name: str) -> Prog:
@@ -545,6 +613,8 @@ def asm_line(x) -> str:
         return f"v_mul_u32_u24_e64 {x[1]}, {fmt(x[2])}, {fmt(x[3])}"
     if op == "mul_lo":
         return f"v_mul_lo_u32 {x[1]}, {fmt(x[2])}, {fmt(x[3])}"
+    if op == "alignbit":
+        return f"v_alignbit_b32 {x[1]}, {fmt(x[2])}, {fmt(x[3])}, {x[4]}"
     raise ValueError(op)
 
 
@@ -573,6 +643,7 @@ def stats(g: Prog) -> dict:
 
 def header() -> str:
     mul = build("fe_mul")
+    sqr = build("fe_sqr")
     add = build("fe_add")
     sub = build("fe_sub")
     mont = build("sc_mont")
@@ -594,6 +665,7 @@ def header() -> str:
 // inputs < 2^256, outputs weakly reduced (< 2^256, congruent mod p).
 // Instruction mix (after scheduling):
 //   fe_mul: {st['fe_mul']}
+//   fe_sqr: {st['fe_sqr']}
 //   fe_add: {st['fe_add']}
 //   fe_sub: {st['fe_sub']}
 //   sc_mont: {st['sc_mont']}
@@ -610,6 +682,16 @@ __device__ __forceinline__ void fe_mul_asm(fe &r, const fe &a, const fe &b) {{
 {asm_body(mul)}
       : {r_out}, {c_out}
       : {a_in}, {b_in}
+      : {clob}, "scc");
+}}
+
+// r = a^2 mod p (weak), Comba squaring.  Temporaries as fe_mul.
+__device__ __forceinline__ void fe_sqr_asm(fe &r, const fe &a) {{
+  uint64_t c0, c1, c2, c3;
+  asm volatile(
+{asm_body(sqr)}
+      : {r_out}, {c_out}
+      : {a_in}
       : {clob}, "scc");
 }}
 
