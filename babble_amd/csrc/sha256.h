@@ -23,6 +23,15 @@ static constexpr uint32_t SHA_K[64] = {
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 
 DEV uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+// a ^ b ^ c in one v_bitop3_b32 (truth table 0x96) on gfx950; the compiler
+// does not fuse the xor pairs of the Sigma / sigma functions by itself.
+DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
 DEV uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 // bytes sh..sh+3 of the little-endian pair (lo, hi) (v_alignbyte_b32 on gfx950)
 DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
@@ -38,13 +47,13 @@ DEV void sha256_compress(uint32_t h[8], uint32_t w[16]) {
       wi = w[i];
     } else {
       uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+      uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
       wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
       w[i & 15] = wi;
     }
-    uint32_t t1 = hh + (rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25)) + ((e & f) ^ (~e & g)) + SHA_K[i] + wi;
-    uint32_t t2 = (rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    uint32_t t1 = hh + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g)) + SHA_K[i] + wi;
+    uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
     hh = g;
     g = f;
     f = e;

@@ -15,9 +15,9 @@ Programs emitted:
           the high word of the next column's pair, so a product costs one mad
           + one addc and a column one v_mov; then the fold 2^256 = 2^32 + 977
           as two interleaved carry chains and a short tail.
-  fe_add  s = a + b and t = s + (2^32 + 977) as two interleaved chains, then a
-          lane select (no s_nop on the main path).
-  fe_sub  same with borrows and t = s - (2^32 + 977).
+  fe_add  s = a + b, then s + c0 (2^32 + 977) on the carry-out c0 (18 VALU);
+          the once-in-2^222 second wrap goes to a uniform slow block.
+  fe_sub  same with borrows and s - c0 (2^32 + 977).
 
 Each program is written in logical order over named registers, then list-
 scheduled: an instruction issues once its register dependences (RAW, WAR,
@@ -459,35 +459,41 @@ def gen_sqr(base: int = MUL_BASE) -> Prog:
 
 
 def _addsub(name: str, sub: bool) -> Prog:
-    """r = a +/- b mod p, weakly reduced.  Chain s = a +/- b (carry c0) and
-    chain t = s +/- K (carry c1) interleave; r = c0 ? t : s.  When both
-    chains carried (only possible with a result within K of the wrap) K is
-    applied once more on limbs 0..2."""
+    """r = a +/- b mod p, weakly reduced.  Chain s = a +/- b (carry c0);
+    then s -/+ (c0 ? 0 : K)... i.e. on a wrap past 2^256 apply
+    K = 2^256 - p = 2^32 + 977 once (chain 2, carry c1): 18 VALU.  Only a
+    result within K of the wrap carries again (probability ~2^-222 for
+    random operands); that lane needs K applied once more, done in a
+    uniform slow block entered iff some lane's c1 is set."""
     g = Prog(name)
     A = [f"%[a{i}]" for i in range(8)]
     B = [f"%[b{i}]" for i in range(8)]
     R = [f"%[r{i}]" for i in range(8)]
-    T = [f"%[t{i}]" for i in range(8)]
-    k977 = "%[k]"
+    k0, k1 = "%[k0]", "%[k1]"
     c0, c1, c2 = CY[0], CY[1], CY[2]
     first = g.sub_co if sub else g.add_co
     nxt = g.subb if sub else g.addc
-    g.mov(k977, 977)
-    Kl = [k977, 1, 0, 0, 0, 0, 0, 0]
     first(R[0], c0, A[0], B[0])
     for i in range(1, 8):
         nxt(R[i], c0, A[i], B[i], c0)
-    first(T[0], c1, R[0], Kl[0])
-    for i in range(1, 8):
-        nxt(T[i], c1, R[i], Kl[i], c1)
-    for i in range(8):
-        g.cnd(R[i], R[i], T[i], c0)
-    g.cnd(T[0], 0, 1, c1)
-    g.cnd(T[0], 0, T[0], c0)                # u = c0 & c1
-    g.mul24(T[1], T[0], k977)               # 977 u
-    first(R[0], c2, R[0], T[1])
-    nxt(R[1], c2, R[1], T[0], c2)
-    nxt(R[2], c2, R[2], 0, c2)
+    g.mov(k1, 977)
+    g.cnd(k0, 0, k1, c0)                     # 977 c0
+    g.cnd(k1, 0, 1, c0)                      # c0 (limb 1 of K c0)
+    first(R[0], c1, R[0], k0)
+    nxt(R[1], c1, R[1], k1, c1)
+    for i in range(2, 8):
+        nxt(R[i], c1, R[i], 0, c1)
+    s = Prog(name + "_tail")
+    sf = s.sub_co if sub else s.add_co
+    sn = s.subb if sub else s.addc
+    s.mov(k1, 977)
+    s.cnd(k0, 0, k1, c1)
+    s.cnd(k1, 0, 1, c1)
+    sf(R[0], c2, R[0], k0)
+    sn(R[1], c2, R[1], k1, c2)
+    for i in range(2, 8):
+        sn(R[i], c2, R[i], 0, c2)
+    g.slow = (c1, s)
     return g
 
 
@@ -698,21 +704,23 @@ __device__ __forceinline__ void fe_sqr_asm(fe &r, const fe &a) {{
 // r = a + b mod p (weak)
 __device__ __forceinline__ void fe_add_asm(fe &r, const fe &a, const fe &b) {{
   uint64_t c0, c1, c2;
-  uint32_t t[8], k;
+  uint32_t k0, k1;
   asm volatile(
 {asm_body(add)}
-      : {r_out}, {t_out}, [k] "=&v"(k), {c3_out}
-      : {a_in}, {b_in});
+      : {r_out}, [k0] "=&v"(k0), [k1] "=&v"(k1), {c3_out}
+      : {a_in}, {b_in}
+      : "scc");
 }}
 
 // r = a - b mod p (weak)
 __device__ __forceinline__ void fe_sub_asm(fe &r, const fe &a, const fe &b) {{
   uint64_t c0, c1, c2;
-  uint32_t t[8], k;
+  uint32_t k0, k1;
   asm volatile(
 {asm_body(sub)}
-      : {r_out}, {t_out}, [k] "=&v"(k), {c3_out}
-      : {a_in}, {b_in});
+      : {r_out}, [k0] "=&v"(k0), [k1] "=&v"(k1), {c3_out}
+      : {a_in}, {b_in}
+      : "scc");
 }}
 
 // r = a * b * 2^-256 mod N (Montgomery), a < 2^256, b < N; r < N.
