@@ -5,8 +5,9 @@ Same type names, fields and method semantics as sikoba/babble v0.8.4:
   InternalTransaction(Body)      src/hashgraph/internal_transaction.go
   BlockBody / Block / BlockSignature  src/hashgraph/block.go
   EventBody / Event              src/hashgraph/event.go
-  check_block / process_sig_pool / insert_event_verify
-                                 src/hashgraph/hashgraph.go:1599-1630, 1295-1367, 672-687
+  check_block / process_sig_pool / insert_event_verify / bootstrap
+                                 src/hashgraph/hashgraph.go:1599-1630, 1295-1367, 672-687,
+                                 1481-1536
 Every hash and every signature check goes through libbabbleverify.so
 (`Verifier`); there is no CPU path.  Go's panics are raised as
 `ReferencePanic` by the single-object methods and reported as `panic=True`
@@ -408,4 +409,51 @@ def insert_event_verify(event: Event, outcome: Optional[Outcome] = None, verifie
         raise ReferencePanic(o.err or "reference panic")
     if not o.ok:
         return o.err if o.err else "Invalid Event signature %s" % event.Hex(verifier)
+    return None
+
+
+def bootstrap(topological_events: Callable[[int, int], List[Event]],
+              insert_and_run_consensus: Callable[[Event], Optional[str]],
+              process_sig_pool_step: Callable[[], Optional[str]], batch_size: int = 100,
+              verify_window: int = 100_000, verifier=None) -> Optional[str]:
+    """The event replay of Hashgraph.Bootstrap (hashgraph.go:1481-1536) with
+    batched verification.  Go reads the DB in batches of 100 topological
+    events, inserts each (InsertEventAndRunConsensus -> InsertEvent, whose
+    first step is Event.Verify, hashgraph.go:672-687) and runs
+    ProcessSigPool after every DB batch, returning the first error.
+
+    Here DB batches are read ahead until `verify_window` events are pending
+    and verified in ONE device batch; insertion, ProcessSigPool calls and
+    the error that ends the replay happen in exactly Go's order (a DB read is
+    a pure function of (offset, limit), so reading ahead changes nothing).
+    `insert_and_run_consensus(ev)` is the caller's non-verify part of the
+    insert (ancestry checks, consensus); it returns an error text or None.
+    """
+    index = 0
+    done = False
+    while not done:
+        window: List[List[Event]] = []
+        n = 0
+        while n < verify_window:  # read ahead whole DB batches
+            evs = topological_events(index * batch_size, batch_size)
+            window.append(evs)
+            n += len(evs)
+            index += 1
+            if len(evs) < batch_size:
+                done = True
+                break
+        flat = [e for evs in window for e in evs]
+        outcomes = verify_events(flat, verifier) if flat else []
+        k = 0
+        for evs in window:
+            for ev in evs:
+                err = insert_event_verify(ev, outcomes[k], verifier)
+                k += 1
+                if err is None:
+                    err = insert_and_run_consensus(ev)
+                if err is not None:
+                    return err
+            err = process_sig_pool_step()
+            if err is not None:
+                return err
     return None
