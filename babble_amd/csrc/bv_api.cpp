@@ -38,21 +38,21 @@ namespace {
 
 // Table geometry (must match verify_core.h): generator 16-bit windows x 16
 // (64 MiB, once per ctx); GLV key tables K8 (8-bit windows x 16 + phi,
-// 512 KiB per key) or K12 (12-bit windows x 11 + phi, 5.5 MiB per key, from
+// 512 KiB per key) or K12 (12-bit signed windows x 11 + phi, 2.75 MiB per key, from
 // 22 six-bit sub-tables).
 constexpr uint32_t kKNwin = 16;
 constexpr uint64_t kGTableBytes = BV_GTABLE_U32 * 4;                 // 10.7 GB (geometry.h)
 constexpr uint64_t kGSubBytes = BV_GSUB_U32 * 4;
 constexpr uint64_t kGPrefixBytes = (uint64_t)BV_GPAIR_BLOCKS * 4096 * 32;  // one k_table_pair_g launch
 constexpr uint64_t kKTableBytes = 2ull * kKNwin * (1ull << 8) * 64ull;
-constexpr uint64_t kK12TableBytes = 2ull * 11 * (1ull << 12) * 64ull;
+constexpr uint64_t kK12TableBytes = BV_K12TABLE_U32 * 4ull;
 constexpr uint64_t kK12SubBytes = 22ull * 64 * 64;
-constexpr uint64_t kK12PrefixBytes = 11ull * (1ull << 12) * 32;  // one fe per entry
+constexpr uint64_t kK12PrefixBytes = (uint64_t)BV_K12NWIN * BV_K12ENT * 32;  // one fe per entry
 constexpr uint32_t kBasesPerKey = 22;       // max(K8 16 windows, K12 22 sub-tables)
 constexpr uint64_t kK12MinItemsPerKey = 2048;  // K12 pays for its 11x larger build above this
 constexpr uint32_t kUStride = 12;  // per-item GLV words (k1, k2, signs)
 constexpr uint32_t kMaxTableKeys = 8192;                                // K8: 4 GiB of key tables
-constexpr uint32_t kMaxK12Keys = 1024;                                  // K12: 5.6 GiB
+constexpr uint32_t kMaxK12Keys = 1024;                                  // K12: 2.8 GiB
 constexpr uint32_t kPrepM = 16;                                         // items per s^-1 batch
 constexpr uint32_t kRgWords = 25;                                       // R_G words per item
 

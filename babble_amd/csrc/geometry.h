@@ -18,9 +18,12 @@
 // covers 128 bits instead of 256.  Two key-table geometries:
 //   K8:  8-bit windows x 16 (+ phi) = 512 KiB per key, 32 adds per item;
 //        entries by per-thread double-and-add (mid-size batches);
-//   K12: 12-bit windows x 11 (+ phi) = 5.5 MiB per key, 22 adds per item;
-//        entries as chord sums of two 6-bit sub-table points with one
-//        batched inversion per window (large batches: ~16k items per key).
+//   K12: 12-bit signed-digit windows x 11 (+ phi) = 2.75 MiB per key, 22
+//        adds per item; digits |d| <= 2^11, so a window holds 2^11 entries
+//        (entry 2^11 of window j lives in the never-read slot 0 of window
+//        j+1; one pad entry after the top window); entries as chord sums of
+//        two 6-bit sub-table points with one batched inversion per window
+//        (large batches: ~16k items per key).
 #pragma once
 
 #define BV_ENTRY_U32 16  // affine x, y = 16 words (64 bytes)
@@ -41,7 +44,8 @@
 #define BV_K12NWIN 11    //   x 11 windows (132 bits; the top one holds 8)
 #define BV_K12L 6        // K12 sub-table bits: S_k[x] = x 2^(6k) Q, x < 64
 #define BV_K12NSUB 22    //   k < 22 (offsets 0, 6, ..., 126)
-#define BV_K12HALF_U32 ((uint64_t)BV_K12NWIN * (1ull << BV_K12W) * BV_ENTRY_U32)
+#define BV_K12ENT (1u << (BV_K12W - 1))  // entry slots per window (signed digits)
+#define BV_K12HALF_U32 (((uint64_t)BV_K12NWIN * BV_K12ENT + 1) * BV_ENTRY_U32)
 #define BV_K12TABLE_U32 (2 * BV_K12HALF_U32)
 #define BV_K12SUB_U32 ((uint64_t)BV_K12NSUB * (1ull << BV_K12L) * BV_ENTRY_U32)
 // per-item GLV halves of u2 (k_verify_g -> k_verify_q): k1[4] | k2[4] | signs | pad

@@ -99,24 +99,27 @@ __global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict
 }
 
 // K12 key tables from the 6-bit sub-tables (verify_core.h: pair_*).
-// One block of 256 threads per (window j, key): entry d = 256 e + t for
-// e < E (E = 2^W / 256), so a wave shares hi and reads 64 distinct lo.
+// One block of 256 threads per (window j, key): digit d = 256 e + t for
+// e < E (E = 2^(W-1) / 256; signed digits, geometry.h), so a wave shares hi
+// and reads 64 distinct lo; d = 0 stands for digit 2^(W-1), stored in slot 0
+// of window j+1 (k12_digit).
 // S_2j and S_2j+1 are staged in LDS; the window's chord denominators are
 // inverted with ONE field inversion (per-thread running products whose
 // prefixes go to `pscr`, then block prefix/suffix products in LDS), so the
 // serial inversion latency is paid once per window and the whole grid is
 // resident in one round.  The top window only needs digits
-// < 2^(128 - W j): its blocks stop after the live entries.
+// <= 2^(128 - W j): its blocks stop after the live entries.
 template <int W, int L, int NWIN>
 __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__ sub,
                                                     const uint8_t *__restrict__ bstatus,
                                                     uint32_t *__restrict__ table, uint4 *__restrict__ pscr) {
-  constexpr uint32_t E = (1u << W) / 256u, NS = 1u << L;
-  constexpr uint64_t half_u32 = (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
+  constexpr uint32_t ENT = 1u << (W - 1), E = ENT / 256u, NS = 1u << L;
+  constexpr uint64_t half_u32 = ((uint64_t)NWIN * ENT + 1) * BV_ENTRY_U32;
+  static_assert(half_u32 == BV_K12HALF_U32, "K12 geometry");
   const uint32_t b = blockIdx.y, j = blockIdx.x, t = threadIdx.x;
   if (bstatus && bstatus[b] != KS_OK) return;
   const int live_bits = 128 - W * (int)j;
-  const uint32_t e_live = live_bits >= W ? E : ((1u << live_bits) + 255u) / 256u;
+  const uint32_t e_live = live_bits >= W - 1 ? E : ((1u << live_bits) + 1u + 255u) / 256u;
   __shared__ uint32_t sLo[NS * BV_ENTRY_U32], sHi[NS * BV_ENTRY_U32];
   __shared__ fe sPre[256], sSuf[256], sInv;
   const uint32_t *sk = sub + ((uint64_t)b * 2 * NWIN + 2 * j) * NS * BV_ENTRY_U32;
@@ -130,7 +133,7 @@ __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__
   fe_set(acc, 1);
 #pragma unroll 1
   for (uint32_t e = 0; e < e_live; e++) {
-    const uint32_t d = 256 * e + t, lo = d & (NS - 1), hi = d >> L;
+    const uint32_t d = k12_digit(256 * e + t, ENT), lo = d & (NS - 1), hi = d >> L;
     fe x1, y1, x2, y2, H;
     pair_load(sLo, sHi, lo, hi, x1, y1, x2, y2);
     pair_denominator(H, pair_kind(lo, hi), x1, x2);
@@ -159,10 +162,10 @@ __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__
   fe q = sInv;  // (this thread's product)^-1 = prefix(t-1) * suffix(t+1) * total^-1
   if (t > 0) fe_mul(q, q, sPre[t - 1]);
   if (t < 255) fe_mul(q, q, sSuf[t + 1]);
-  uint32_t *base = table + (uint64_t)b * 2 * half_u32 + ((uint64_t)j << W) * BV_ENTRY_U32;
+  uint32_t *base = table + (uint64_t)b * 2 * half_u32 + (uint64_t)j * ENT * BV_ENTRY_U32;
 #pragma unroll 1
   for (int e = (int)e_live - 1; e >= 0; e--) {
-    const uint32_t d = 256 * e + t, lo = d & (NS - 1), hi = d >> L;
+    const uint32_t d = k12_digit(256 * e + t, ENT), lo = d & (NS - 1), hi = d >> L;
     const int kind = pair_kind(lo, hi);
     fe x1, y1, x2, y2, H, Hinv, pre;
     pair_load(sLo, sHi, lo, hi, x1, y1, x2, y2);

@@ -212,6 +212,10 @@ DEV void table_store(uint32_t *entry, uint32_t *phi, uint32_t d, const gej &R, b
 // 2 copy S_hi, 3 chord sum.
 DEV int pair_kind(uint32_t lo, uint32_t hi) { return (lo ? 1 : 0) | (hi ? 2 : 0); }
 
+// K12 builder slot -> digit: slot 0 of a window block builds the window's
+// top digit 2^(W-1) = ENT (stored at window j+1's unused slot 0).
+DEV uint32_t k12_digit(uint32_t d, uint32_t ent) { return d ? d : ent; }
+
 DEV void pair_load(const uint32_t *s_lo, const uint32_t *s_hi, uint32_t lo, uint32_t hi, fe &x1, fe &y1, fe &x2,
                    fe &y2) {
   fe_load(x1, s_lo + BV_ENTRY_U32 * lo);
@@ -498,20 +502,35 @@ DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const u
 
 // R += sum_j T[j][digit_j(k)] over a 128-bit GLV half k (4 limbs; consumed:
 // shifted right W bits per window, so digits never straddle limbs).
-template <int W, int NWIN>
+// SIGNED (K12): digits in (-2^(W-1), 2^(W-1)] by carry recoding, T[j][|d|]
+// with y negated for d < 0; a window holds ENT = 2^(W-1) slots.  k < 2^128
+// and W NWIN >= 129 bits, so no carry is left after the top window.
+template <int W, int NWIN, bool SIGNED>
 DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bool neg) {
+  constexpr uint32_t ENT = SIGNED ? (1u << (W - 1)) : (1u << W);
+  static_assert(!SIGNED || W * NWIN >= 129, "signed windows must absorb the last carry");
   if (neg) fe_neg(R.Y, R.Y);
+  uint32_t carry = 0;
   for (int j = 0; j < NWIN; j++) {
-    const uint32_t d = k[0] & ((1u << W) - 1u);
+    uint32_t d = (k[0] & ((1u << W) - 1u)) + carry;
     k[0] = (k[0] >> W) | (k[1] << (32 - W));
     k[1] = (k[1] >> W) | (k[2] << (32 - W));
     k[2] = (k[2] >> W) | (k[3] << (32 - W));
     k[3] >>= W;
+    bool dneg = false;
+    if (SIGNED) {
+      carry = d > ENT ? 1u : 0u;
+      if (carry) {
+        d = (1u << W) - d;  // |d - 2^W|, 0 when d == 2^W
+        dneg = true;
+      }
+    }
     if (d) {
-      const uint32_t *e = tab + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
+      const uint32_t *e = tab + ((uint64_t)j * ENT + d) * BV_ENTRY_U32;
       fe x, y;
       fe_load4(x, e);
       fe_load4(y, e + 8);
+      if (dneg) fe_neg(y, y);
       gej_add_ge(R, inf, x, y);
     }
   }
@@ -524,7 +543,8 @@ template <int W, int NWIN>
 DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
                           const uint32_t *s_be, const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12,
                           const uint32_t *key_table, const uint32_t *rg) {
-  constexpr uint64_t half = (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
+  constexpr bool SIGNED = W == BV_K12W;
+  constexpr uint64_t half = SIGNED ? BV_K12HALF_U32 : (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
   fe r;
   const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
   if (st != 0xFF) return st;
@@ -541,7 +561,7 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
     uint32_t kk[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) kk[c] = h ? k2[c] : k1[c];
-    key_table_add<W, NWIN>(R, inf, tab + (h ? half : 0), kk, (signs >> h) & 1u);
+    key_table_add<W, NWIN, SIGNED>(R, inf, tab + (h ? half : 0), kk, (signs >> h) & 1u);
   }
   fe_load_be_words(r, r_be + 8 * i);  // reloaded: not kept live through the loop
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;

@@ -76,13 +76,13 @@ void emu_bases(uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, st
 // One chunk of chord-sum entries d in [d0, d0 + n) of a window (k_table_pair
 // / k_table_pair_g): one batched inversion, then pair_store.
 void emu_pair_chunk(const uint32_t *s_lo, const uint32_t *s_hi, uint32_t L, uint32_t d0, uint32_t n, uint32_t *base,
-                    uint64_t phi_off) {
+                    uint64_t phi_off, uint32_t zero_as = 0) {
   const uint32_t NS = 1u << L;
   std::vector<fe> H(n), pre(n);
   fe acc;
   fe_set(acc, 1);
   for (uint32_t k = 0; k < n; k++) {
-    const uint32_t d = d0 + k;
+    const uint32_t d = zero_as ? k12_digit(d0 + k, zero_as) : d0 + k;
     fe x1, y1, x2, y2;
     pair_load(s_lo, s_hi, d & (NS - 1), d >> L, x1, y1, x2, y2);
     pair_denominator(H[k], pair_kind(d & (NS - 1), d >> L), x1, x2);
@@ -92,7 +92,7 @@ void emu_pair_chunk(const uint32_t *s_lo, const uint32_t *s_hi, uint32_t L, uint
   fe q;
   fe_inv_var(q, acc);
   for (int k = (int)n - 1; k >= 0; k--) {
-    const uint32_t d = d0 + k;
+    const uint32_t d = zero_as ? k12_digit(d0 + k, zero_as) : d0 + k;
     fe x1, y1, x2, y2, Hinv;
     pair_load(s_lo, s_hi, d & (NS - 1), d >> L, x1, y1, x2, y2);
     fe_mul(Hinv, q, pre[k]);
@@ -140,11 +140,12 @@ void emu_build_tables(int kw, uint32_t n_bases, const uint32_t *bxy, const uint8
     const uint32_t b = (uint32_t)(task / NWIN), j = (uint32_t)(task % NWIN);
     if (bstatus && bstatus[b] != KS_OK) return;
     const int live_bits = 128 - (int)(W * j);
-    const uint32_t n_live = live_bits >= (int)W ? (1u << W) : (((1u << live_bits) + 255u) / 256u) * 256u;
+    const uint32_t n_live =
+        live_bits >= (int)W - 1 ? BV_K12ENT : (((1u << live_bits) + 1u + 255u) / 256u) * 256u;
     const uint32_t *s_lo = sub.data() + ((uint64_t)b * 2 * NWIN + 2 * j) * NS * BV_ENTRY_U32;
     const uint32_t *s_hi = s_lo + NS * BV_ENTRY_U32;
-    uint32_t *base = table + (uint64_t)b * 2 * half_u32 + ((uint64_t)j << W) * BV_ENTRY_U32;
-    emu_pair_chunk(s_lo, s_hi, L, 0, n_live, base, half_u32);
+    uint32_t *base = table + (uint64_t)b * 2 * half_u32 + (uint64_t)j * BV_K12ENT * BV_ENTRY_U32;
+    emu_pair_chunk(s_lo, s_hi, L, 0, n_live, base, half_u32, BV_K12ENT);
   });
 }
 
