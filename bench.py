@@ -223,7 +223,7 @@ def main():
                 "executed_mad_per_s": executed / 1e12,
                 "executed_frac": executed / PEAK_IMUL32_PER_S,
                 "valu_issue_frac": issue_frac,
-                "note": "frac > 1 is possible: fixed-base per-key tables need ~7x fewer modmuls than the canonical "
+                "note": "frac > 1 is possible: fixed-base G and per-key GLV tables need ~11x fewer modmuls than the canonical "
                         "Strauss schedule the algorithmic count assumes; executed_frac is the physical "
                         "v_mad_u64_u32 utilisation; valu_issue_frac is PMC VALU wave-instructions "
                         "(profiles/kverify_traffic.json) / live duration / issue peak; traffic is "
