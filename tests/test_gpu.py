@@ -105,6 +105,18 @@ def test_c4_adversarial_full_rate(verifier):
     assert verifier.timing()["key_path"] == 8
 
 
+def test_c4_adversarial_1m(verifier):
+    """C4 exactly as SURVEY §8d specifies it: 10^6 events (seed 4, 64
+    creators), the per-million corruption and malformed-key mix; every
+    digest, status and accept bit equal to the C oracle's.  At 15.6k items
+    per key this runs the signed-digit K12 tables (incl. digits 2^11 and the
+    top-window carry at scale)."""
+    b = synth.adversarial(1_000_000, seed=4)
+    res = check_against_oracle(verifier, b)
+    assert verifier.timing()["key_path"] == 12
+    assert set(np.unique(res.status)) == {0, 1, 2, 3}
+
+
 def test_k12_tables_adversarial(verifier):
     """>= 2048 items per key: 12-bit key tables (sub-table chord sums)."""
     b = synth.adversarial(120_000, seed=12, n_creators=16, scale_per_million=MIX)
