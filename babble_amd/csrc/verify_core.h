@@ -319,44 +319,50 @@ DEV bool s_usable(const uint8_t *pre, uint64_t i, const sc &s) {
 }
 
 // k_sinv, thread t of T: w_i = s_i^-1 R mod N (Montgomery form) for items
-// t, t+T, ..., t+(M-1)T with one Fermat inversion (Montgomery's trick).
+// t, t+T, ..., t+(M-1)T with one inversion (Montgomery's trick).
 // Needs only s and pre, so it runs on its own stream concurrently with
 // SHA-256 and the key tables; the digest-dependent products u1 = e w and
 // u2 = r w are formed by k_verify_g (item_scalars).  Unusable items
 // contribute s = 1 and get a w that is never read.
+//
+// The raw s_k enter the Montgomery products unconverted (no s R^2 -> s R
+// step): after k items the prefix is acc_k = R^(1-k) prod_{i<=k} s_i, the
+// inverse of the total (xR -> x^-1 R) is R^(1+K) / prod s, one extra
+// product by 1 makes it R^K / prod s, and walking back w_k = inv acc_(k-1)
+// / R = R / s_k while inv loses one s_k and one R per step.
 DEV void sinv_thread(uint64_t t, uint64_t T, uint64_t n_items, uint32_t M, const uint32_t *s_be, const uint8_t *pre,
                      uint32_t *w_out) {
-  sc R2, R1;
-  sc_load_const(R2, SC_R2);
+  sc R1, one;
   sc_load_const(R1, SC_R1);
+#pragma unroll
+  for (int k = 0; k < 8; k++) one.v[k] = k == 0 ? 1u : 0u;
   sc acc = R1;
   for (uint32_t m = 0; m < M; m++) {
     const uint64_t i = t + (uint64_t)m * T;
     if (i >= n_items) break;
-    sc s, sM;
+    sc s;
     sc_load_be_words(s, s_be + 8 * i);
-    if (s_usable(pre, i, s)) sc_mont(sM, s, R2);
-    else sM = R1;
+    if (!s_usable(pre, i, s)) s = one;
     uint4 *q = (uint4 *)(w_out + 8 * i);
     q[0] = make_uint4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
     q[1] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
-    sc_mont(acc, acc, sM);
+    sc_mont(acc, acc, s);
   }
   sc inv;
   sc_inverse_var(inv, acc);
+  sc_mont(inv, inv, one);
   for (int m = (int)M - 1; m >= 0; m--) {
     const uint64_t i = t + (uint64_t)m * T;
     if (i >= n_items) continue;
-    sc s, sM, pfx, w;
+    sc s, pfx, w;
     sc_load_be_words(s, s_be + 8 * i);
-    if (s_usable(pre, i, s)) sc_mont(sM, s, R2);
-    else sM = R1;
+    if (!s_usable(pre, i, s)) s = one;
     uint4 *q = (uint4 *)(w_out + 8 * i);
     const uint4 a = q[0], b = q[1];
     pfx.v[0] = a.x; pfx.v[1] = a.y; pfx.v[2] = a.z; pfx.v[3] = a.w;
     pfx.v[4] = b.x; pfx.v[5] = b.y; pfx.v[6] = b.z; pfx.v[7] = b.w;
     sc_mont(w, inv, pfx);  // s^-1 R
-    sc_mont(inv, inv, sM);
+    sc_mont(inv, inv, s);
     q[0] = make_uint4(w.v[0], w.v[1], w.v[2], w.v[3]);
     q[1] = make_uint4(w.v[4], w.v[5], w.v[6], w.v[7]);
   }
