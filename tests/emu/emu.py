@@ -91,3 +91,26 @@ def verify_batch(arrs: dict, n_threads: int = 0, force_mode: int = -1):
     mode = L.emu_verify_batch(ctypes.byref(b), h.ctypes.data, st.ctypes.data, bits.ctypes.data, n_threads,
                               force_mode)
     return h[:n_msgs], st[:n_items], bits[: (n_items + 63) // 64], mode
+
+
+def dump_batch(path: str, arrs: dict) -> None:
+    """Write a batch in emu_main.cpp's "BVB1" format (sanitizer driver input)."""
+    n_msgs = len(arrs["msg_off"]) - 1
+    n_keys = len(arrs["key_off"]) - 1
+    n_items = len(arrs["item_msg"])
+    pre = arrs.get("pre")
+    msg = np.ascontiguousarray(arrs["msg_bytes"], np.uint8)
+    key = np.ascontiguousarray(arrs["key_bytes"], np.uint8)
+    with open(path, "wb") as f:
+        f.write(b"BVB1")
+        f.write(np.array([n_msgs, n_keys, n_items, msg.size, key.size, pre is not None], np.uint64).tobytes())
+        f.write(np.ascontiguousarray(arrs["msg_off"], np.uint64).tobytes())
+        f.write(msg.tobytes())
+        f.write(np.ascontiguousarray(arrs["key_off"], np.uint64).tobytes())
+        f.write(key.tobytes())
+        f.write(np.ascontiguousarray(arrs["item_msg"], np.uint32).tobytes())
+        f.write(np.ascontiguousarray(arrs["item_key"], np.uint32).tobytes())
+        f.write(np.ascontiguousarray(arrs["r_be"], np.uint8).tobytes())
+        f.write(np.ascontiguousarray(arrs["s_be"], np.uint8).tobytes())
+        if pre is not None:
+            f.write(np.ascontiguousarray(pre, np.uint8).tobytes())

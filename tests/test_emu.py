@@ -136,3 +136,23 @@ def test_empty_and_ragged():
     h, st, bits = coracle.verify_batch(b.as_dict())
     h2, st2, bits2, _ = emu.verify_batch(b.as_dict())
     assert np.array_equal(st, st2) and len(bits2) == 2 and np.array_equal(bits, bits2)
+
+
+def test_asan_ubsan_emulator(tmp_path):
+    """Host-only AddressSanitizer + UBSan build of the device per-unit source
+    (tests/emu/Makefile `asan`, emu_main.cpp) on the golden items plus an
+    adversarial mix, in all three key-table modes, against the C oracle."""
+    import subprocess
+
+    subprocess.run(["make", "-s", "-C", emu._HERE, "asan"], check=True)
+    exe = emu._HERE + "/_build/emu_asan"
+    golden, _, _ = golden_items_batch()
+    adv = synth.adversarial(700, seed=23, n_creators=3, scale_per_million=dict(
+        rflip=20000, sflip=20000, body=10000, highs=10000, range=8000, fmt=8000, key=12000))
+    for name, b in (("golden", golden), ("adv", adv)):
+        path = str(tmp_path / f"{name}.bin")
+        emu.dump_batch(path, b.as_dict())
+        r = subprocess.run([exe, path, "4"], capture_output=True, text=True, timeout=600,
+                           env={"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "PATH": "/usr/bin:/bin"})
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert r.stdout.count("equal") == 3 and "MISMATCH" not in r.stdout, r.stdout
