@@ -1,118 +1,170 @@
 // bv_api.cpp — host side of libbabbleverify.so: the C ABI declared in
-// include/babbleverify.h.
+// include/babbleverify.h (single-device contexts; bv_group.cpp adds the
+// multi-device group on top).
 //
-// One bv_ctx owns two HIP streams (main + keys), the generator table (16-bit
-// windows, 64 MiB, built on the device at bv_create and kept resident in
-// HBM) and growable device work buffers.  bv_verify_batch stages host
-// buffers to HBM and runs the same device pipeline as
-// bv_verify_batch_device.  There is no CPU fallback: a missing or
-// non-gfx950 device is BV_E_NODEVICE.
-#include <hip/hip_runtime.h>
+// One bv_ctx owns three HIP streams (main, keys, s^-1) plus a copy stream
+// for the host entry point, growable device work buffers, pinned
+// (hipHostMalloc) staging buffers, and optionally the key cache
+// (BV_F_KEY_CACHE).  The generator table (geometry.h: 24-bit windows,
+// 10.7 GB) is a per-process, per-device constant shared by every ctx.  There
+// is no CPU fallback: a missing or non-gfx950 device is BV_E_NODEVICE.
+//
+// Host entry point (bv_verify_batch, what cgo calls): every input array is
+// staged into one pinned buffer by a small thread pool and streamed to HBM on
+// the copy stream in ~16 MB chunks; the message bytes go last, chunked on
+// message boundaries, and each chunk is hashed (k_sha256 on the main stream)
+// as soon as it lands, so hashing overlaps the PCIe transfer of the next
+// chunk.  Digests are copied back as soon as hashing ends (overlapping the
+// verify kernels), statuses and bits after the last kernel.
+#include "bv_internal.h"
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
-#include <mutex>
-#include <string>
-
-#include "../../include/babbleverify.h"
-#include "geometry.h"
-
-namespace bvk {
-hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
-hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
-hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
-                        uint32_t *, uint32_t *);
-hipError_t sinv(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *);
-hipError_t verify_g(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
-                    const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
-                    const uint32_t *, uint32_t *);
-hipError_t verify_q(hipStream_t, int, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
-                    const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
-hipError_t verify_generic(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
-                          const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
-                          const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
-}  // namespace bvk
+#include <functional>
+#include <thread>
 
 namespace {
 
-// Table geometry (must match verify_core.h): generator 16-bit windows x 16
-// (64 MiB, once per ctx); GLV key tables K8 (8-bit windows x 16 + phi,
-// 512 KiB per key) or K12 (12-bit signed windows x 11 + phi, 2.75 MiB per key, from
-// 22 six-bit sub-tables).
-constexpr uint32_t kKNwin = 16;
-constexpr uint64_t kGTableBytes = BV_GTABLE_U32 * 4;                 // 10.7 GB (geometry.h)
+constexpr uint64_t kGTableBytes = BV_GTABLE_U32 * 4;                       // 10.7 GB (geometry.h)
 constexpr uint64_t kGSubBytes = BV_GSUB_U32 * 4;
 constexpr uint64_t kGPrefixBytes = (uint64_t)BV_GPAIR_BLOCKS * 4096 * 32;  // one k_table_pair_g launch
-constexpr uint64_t kKTableBytes = 2ull * kKNwin * (1ull << 8) * 64ull;
-constexpr uint64_t kK12TableBytes = BV_K12TABLE_U32 * 4ull;
-constexpr uint64_t kK12SubBytes = 22ull * 64 * 64;
+constexpr uint64_t kKTableBytes = BV_KTABLE_U32 * 4;
+constexpr uint64_t kK12TableBytes = BV_K12TABLE_U32 * 4;
+constexpr uint64_t kK12SubBytes = BV_K12SUB_U32 * 4;
 constexpr uint64_t kK12PrefixBytes = (uint64_t)BV_K12NWIN * BV_K12ENT * 32;  // one fe per entry
-constexpr uint32_t kBasesPerKey = 22;       // max(K8 16 windows, K12 22 sub-tables)
+constexpr uint64_t kKcTableBytes = BV_KCTABLE_U32 * 4;                      // 470 MB per cached key
+constexpr uint64_t kKcSubBytes = BV_KCSUB_U32 * 4;
+constexpr uint32_t kBasesPerKey = 22;       // max(K8 16, K12 22, KC 14) bases per key
 constexpr uint64_t kK12MinItemsPerKey = 2048;  // K12 pays for its 11x larger build above this
-constexpr uint32_t kUStride = 12;  // per-item GLV words (k1, k2, signs)
-constexpr uint32_t kMaxTableKeys = 8192;                                // K8: 4 GiB of key tables
-constexpr uint32_t kMaxK12Keys = 1024;                                  // K12: 2.8 GiB
-constexpr uint32_t kPrepM = 16;                                         // items per s^-1 batch
-constexpr uint32_t kRgWords = 25;                                       // R_G words per item
-
-struct DevBuf {
-  void *p = nullptr;
-  size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) {
-      hipError_t e = hipFree(p);
-      if (e != hipSuccess) return e;
-      p = nullptr;
-      cap = 0;
-    }
-    size_t want = std::max(bytes, cap * 3 / 2);
-    want = (want + 255) & ~(size_t)255;
-    hipError_t e = hipMalloc(&p, want);
-    if (e != hipSuccess) {
-      p = nullptr;
-      return e;
-    }
-    cap = want;
-    return hipSuccess;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-  template <class T>
-  T *as() const {
-    return (T *)p;
-  }
-};
-
-// timing events (see read_timing)
-enum { E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_SINV, E_COUNT };
+constexpr uint32_t kMaxTableKeys = 8192;       // K8: 4 GiB of key tables
+constexpr uint32_t kMaxK12Keys = 1024;         // K12: 2.8 GiB
+constexpr uint32_t kKcMaxBatchKeys = 4096;     // key cache: batches with more keys use per-batch tables
+constexpr uint32_t kKcBuildGroup = 16;         // keys per KC build launch (pscr: 117 MB per key)
+constexpr uint32_t kPrepM = 16;                // items per s^-1 batch
+constexpr uint32_t kRgWords = 25;              // R_G words per item
+constexpr size_t kChunk = 16ull << 20;         // host-entry staging / PCIe chunk
 
 }  // namespace
 
-struct bv_ctx {
-  int device = 0;
-  uint32_t flags = 0;
-  hipStream_t stream = nullptr;   // main
-  hipStream_t kstream = nullptr;  // key tables
-  hipStream_t sstream = nullptr;  // batched s^-1
+// ---------------------------------------------------------------------------
+// buffers
+// ---------------------------------------------------------------------------
+hipError_t DevBuf::ensure(size_t bytes) {
+  if (bytes <= cap) return hipSuccess;
+  if (p) {
+    hipError_t e = hipFree(p);
+    if (e != hipSuccess) return e;
+    p = nullptr;
+    cap = 0;
+  }
+  size_t want = std::max(bytes, cap * 3 / 2);
+  want = (want + 255) & ~(size_t)255;
+  hipError_t e = hipMalloc(&p, want);
+  if (e != hipSuccess) {
+    p = nullptr;
+    (void)hipGetLastError();
+    return e;
+  }
+  cap = want;
+  return hipSuccess;
+}
+void DevBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+}
+hipError_t PinnedBuf::ensure(size_t bytes) {
+  if (bytes <= cap) return hipSuccess;
+  if (p) {
+    hipError_t e = hipHostFree(p);
+    if (e != hipSuccess) return e;
+    p = nullptr;
+    cap = 0;
+  }
+  size_t want = std::max(bytes, cap * 3 / 2);
+  want = (want + 4095) & ~(size_t)4095;
+  hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    p = nullptr;
+    (void)hipGetLastError();
+    return e;
+  }
+  cap = want;
+  return hipSuccess;
+}
+void PinnedBuf::release() {
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  cap = 0;
+}
+
+// ---------------------------------------------------------------------------
+// host copy pool: parallel memcpy into / out of pinned staging
+// ---------------------------------------------------------------------------
+struct CopyPool {
+  std::vector<std::thread> th;
   std::mutex mu;
-  std::string err;
-  const uint32_t *g_table = nullptr;  // process-wide, per device (gtable_acquire)
-  // staging for the host entry point
-  DevBuf h_msg_bytes, h_msg_off, h_key_bytes, h_key_off, h_item_msg, h_item_key, h_r, h_s, h_pre;
-  // work buffers
-  DevBuf digests, kstatus, kxy, bases_jac, key_sub, key_pscr, key_table, scratch, u12, rg, status, bits;
-  hipEvent_t ev[E_COUNT] = {};
-  bool table_mode = false;
-  int key_w = 0;  // 8 or 12 in table mode
-  bv_timing timing = {};
+  std::condition_variable cv, done_cv;
+  std::vector<std::function<void()>> q;
+  size_t pending = 0;
+  bool stop = false;
+  explicit CopyPool(int n) {
+    for (int i = 0; i < n; i++)
+      th.emplace_back([this]() {
+        for (;;) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [this]() { return stop || !q.empty(); });
+            if (stop && q.empty()) return;
+            f = std::move(q.back());
+            q.pop_back();
+          }
+          f();
+          std::lock_guard<std::mutex> lk(mu);
+          if (--pending == 0) done_cv.notify_all();
+        }
+      });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+  }
+  // dst <- src (n bytes); returns when done.  Small copies stay on the caller.
+  void copy(void *dst, const void *src, size_t n) {
+    constexpr size_t kPiece = 2ull << 20;
+    if (n <= kPiece || th.empty()) {
+      if (n) memcpy(dst, src, n);
+      return;
+    }
+    const size_t pieces = (n + kPiece - 1) / kPiece;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (size_t i = 1; i < pieces; i++) {
+        const size_t o = i * kPiece, len = std::min(kPiece, n - o);
+        q.push_back([=]() { memcpy((uint8_t *)dst + o, (const uint8_t *)src + o, len); });
+        pending++;
+      }
+    }
+    cv.notify_all();
+    memcpy(dst, src, std::min(kPiece, n));  // the caller copies the first piece
+    std::unique_lock<std::mutex> lk(mu);
+    done_cv.wait(lk, [this]() { return pending == 0; });
+  }
 };
 
-static int fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess) {
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e) {
   if (c) {
     char buf[256];
     if (e != hipSuccess)
@@ -124,10 +176,10 @@ static int fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess
   return code;
 }
 
-#define HIPCHK(expr, code, what)                            \
-  do {                                                      \
-    hipError_t _e = (expr);                                 \
-    if (_e != hipSuccess) return fail(ctx, code, what, _e); \
+#define HIPCHK(expr, code, what)                               \
+  do {                                                         \
+    hipError_t _e = (expr);                                    \
+    if (_e != hipSuccess) return bv_fail(ctx, code, what, _e); \
   } while (0)
 
 static const uint8_t kGenerator[64] = {
@@ -139,8 +191,6 @@ static const uint8_t kGenerator[64] = {
 extern "C" int bv_abi_version(void) { return BV_ABI_VERSION; }
 
 extern "C" const char *bv_last_error(const bv_ctx *ctx) { return ctx ? ctx->err.c_str() : "null ctx"; }
-
-extern "C" void bv_destroy(bv_ctx *ctx);
 
 // The generator table is a constant: one copy per device and process,
 // shared by every context (refcounted), built on first use.
@@ -183,6 +233,7 @@ static const uint32_t *gtable_acquire(int device, hipStream_t st) {
     if (p) (void)hipFree(p);
   if (!ok) {
     if (table) (void)hipFree(table);
+    (void)hipGetLastError();
     return nullptr;
   }
   slot.table = table;
@@ -201,18 +252,34 @@ static void gtable_release(int device) {
 
 static int create_impl(bv_ctx *ctx) {
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  // the key-table stream runs a latency-bound chain (k_table_bases): give it
+  // the higher priority so its waves are scheduled ahead of the bulk kernels
+  int lo = 0, hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
   HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
-  HIPCHK(hipStreamCreateWithFlags(&ctx->kstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
+  HIPCHK(hipStreamCreateWithPriority(&ctx->kstream, hipStreamNonBlocking, hi), BV_E_NODEVICE, "hipStreamCreate");
   HIPCHK(hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
+  HIPCHK(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
   for (auto &e : ctx->ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
+  HIPCHK(hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming), BV_E_NODEVICE, "hipEventCreate");
+  ctx->chunk_ev.resize(64);
+  for (auto &e : ctx->chunk_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming), BV_E_NODEVICE, "event");
   ctx->g_table = gtable_acquire(ctx->device, ctx->stream);
-  if (!ctx->g_table) return fail(ctx, BV_E_OOM, "generator table (geometry.h, ~10.7 GB of HBM) build failed");
+  if (!ctx->g_table) return bv_fail(ctx, BV_E_OOM, "generator table (geometry.h, ~10.7 GB of HBM) build failed");
+  const unsigned hw = std::thread::hardware_concurrency();
+  ctx->pool = new CopyPool((int)std::min<unsigned>(hw ? hw - 1 : 0, 7));
+  if (ctx->flags & BV_F_KEY_CACHE) {
+    double gb = 64.0;
+    if (const char *s = getenv("BV_KEY_CACHE_GB")) gb = atof(s);
+    ctx->kc_budget = (uint64_t)(std::max(gb, 0.0) * 1e9);
+  }
   return BV_OK;
 }
 
 extern "C" int bv_create(bv_ctx **out, int device, uint32_t flags) {
   if (!out) return BV_E_ARGS;
   *out = nullptr;
+  if (flags & ~BV_F_KNOWN) return BV_E_ARGS;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return BV_E_NODEVICE;
   if (device < 0) {
@@ -237,21 +304,27 @@ extern "C" int bv_create(bv_ctx **out, int device, uint32_t flags) {
 extern "C" void bv_destroy(bv_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->kstream) (void)hipStreamSynchronize(ctx->kstream);
-  if (ctx->sstream) (void)hipStreamSynchronize(ctx->sstream);
+  for (hipStream_t s : {ctx->stream, ctx->kstream, ctx->sstream, ctx->cstream})
+    if (s) (void)hipStreamSynchronize(s);
   if (ctx->g_table) gtable_release(ctx->device);
-  DevBuf *bufs[] = {&ctx->h_msg_bytes, &ctx->h_msg_off,
-                    &ctx->h_key_bytes, &ctx->h_key_off, &ctx->h_item_msg, &ctx->h_item_key,  &ctx->h_r,
-                    &ctx->h_s,         &ctx->h_pre,     &ctx->digests,    &ctx->kstatus,     &ctx->kxy,
-                    &ctx->bases_jac,   &ctx->key_sub,     &ctx->key_pscr,    &ctx->key_table, &ctx->scratch,    &ctx->u12,         &ctx->rg,
-                    &ctx->status,      &ctx->bits};
+  DevBuf *bufs[] = {&ctx->d_in,      &ctx->digests,  &ctx->kstatus,  &ctx->kxy,     &ctx->bases_jac,
+                    &ctx->key_sub,   &ctx->key_pscr, &ctx->key_table, &ctx->scratch, &ctx->u12,
+                    &ctx->rg,        &ctx->status,   &ctx->bits,     &ctx->kc_tabs, &ctx->kc_kst,
+                    &ctx->kc_kxy,    &ctx->kc_btabs};
   for (auto *b : bufs) b->release();
+  for (auto &s : ctx->kc_slots)
+    if (s.table) (void)hipFree(s.table);
+  ctx->pin_in.release();
+  ctx->pin_out.release();
+  ctx->pin_small.release();
   for (auto &e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
-  if (ctx->kstream) (void)hipStreamDestroy(ctx->kstream);
-  if (ctx->sstream) (void)hipStreamDestroy(ctx->sstream);
-  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  for (auto &e : ctx->chunk_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
+  for (hipStream_t s : {ctx->kstream, ctx->sstream, ctx->cstream, ctx->stream})
+    if (s) (void)hipStreamDestroy(s);
+  delete ctx->pool;
   delete ctx;
 }
 
@@ -261,22 +334,172 @@ extern "C" int bv_get_timing(const bv_ctx *ctx, bv_timing *out) {
   return BV_OK;
 }
 
-// Device pipeline over device-resident inputs.  msg_hash/status/bits may be
-// null (ctx buffers are used).  Caller holds ctx->mu and has set the device.
-static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
-                      hipStream_t st) {
+// ---------------------------------------------------------------------------
+// key cache (BV_F_KEY_CACHE)
+// ---------------------------------------------------------------------------
+// Resolves the batch's keys against the cache: hits need nothing; valid
+// misses get a KC table built now (cold); malformed keys are remembered with
+// their status and no table.  On success fills ctx->kc_tabs / kc_kst (device,
+// per batch key) and returns BV_OK with *use = true; *use = false when the
+// batch cannot use the cache (too many keys, budget) and must take the
+// per-batch path.  hkb/hko: host copies of the key bytes; dkb/dko: device.
+static int kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
+                      const uint64_t *dko, hipStream_t st, bool *use) {
+  *use = false;
+  if (n_keys == 0 || n_keys > kKcMaxBatchKeys) return BV_OK;
+  ctx->kc_clock++;
+  std::vector<int> slot_of(n_keys, -1);
+  std::vector<uint32_t> miss;
+  uint32_t hits = 0;
+  for (uint32_t k = 0; k < n_keys; k++) {
+    std::string key((const char *)hkb + hko[k], (size_t)(hko[k + 1] - hko[k]));
+    auto it = ctx->kc_index.find(key);
+    if (it != ctx->kc_index.end()) {
+      slot_of[k] = it->second;
+      ctx->kc_slots[it->second].last_use = ctx->kc_clock;
+      hits++;
+    } else {
+      miss.push_back(k);
+    }
+  }
+  uint32_t builds = 0;
+  if (!miss.empty()) {
+    // statuses of the missing keys: k_key_decode on the device (the product
+    // path for elliptic.Unmarshal), then one small synchronous copy back
+    HIPCHK(ctx->kstatus.ensure(n_keys), BV_E_OOM, "alloc kstatus");
+    HIPCHK(ctx->kxy.ensure((uint64_t)n_keys * 64), BV_E_OOM, "alloc kxy");
+    HIPCHK(bvk::key_decode(st, n_keys, dkb, dko, ctx->kstatus.as<uint8_t>(), ctx->kxy.as<uint32_t>()), BV_E_LAUNCH,
+           "k_key_decode");
+    std::vector<uint8_t> kst(n_keys);
+    HIPCHK(hipMemcpyAsync(kst.data(), ctx->kstatus.p, n_keys, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h kst");
+    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+    std::vector<uint32_t> build;  // valid misses
+    for (uint32_t k : miss)
+      if (kst[k] == KS_OK) build.push_back(k);
+    // budget: evict least-recently-used tables not used by this batch
+    uint64_t need = (uint64_t)build.size() * kKcTableBytes;
+    if (need > ctx->kc_budget) return BV_OK;  // this batch's keys alone exceed the budget
+    while (ctx->kc_bytes + need > ctx->kc_budget) {
+      int victim = -1;
+      for (size_t i = 0; i < ctx->kc_slots.size(); i++) {
+        const auto &s = ctx->kc_slots[i];
+        if (s.table && s.last_use != ctx->kc_clock && (victim < 0 || s.last_use < ctx->kc_slots[victim].last_use))
+          victim = (int)i;
+      }
+      if (victim < 0) return BV_OK;
+      HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync before eviction");
+      auto &s = ctx->kc_slots[victim];
+      HIPCHK(hipFree(s.table), BV_E_LAUNCH, "free cached table");
+      s.table = nullptr;
+      ctx->kc_bytes -= kKcTableBytes;
+      ctx->kc_index.erase(s.bytes);
+      s.bytes.clear();
+      s.free = true;
+    }
+    // allocate slots for every miss (malformed keys: status only, no table)
+    for (uint32_t k : miss) {
+      int si = -1;
+      for (size_t i = 0; i < ctx->kc_slots.size(); i++)
+        if (ctx->kc_slots[i].free) {
+          si = (int)i;
+          break;
+        }
+      if (si < 0) {
+        ctx->kc_slots.emplace_back();
+        si = (int)ctx->kc_slots.size() - 1;
+      }
+      auto &s = ctx->kc_slots[si];
+      s.free = false;
+      s.bytes.assign((const char *)hkb + hko[k], (size_t)(hko[k + 1] - hko[k]));
+      s.status = kst[k];
+      s.last_use = ctx->kc_clock;
+      s.table = nullptr;
+      if (kst[k] == KS_OK) {
+        hipError_t e = hipMalloc(&s.table, kKcTableBytes);
+        if (e != hipSuccess) {
+          (void)hipGetLastError();
+          s.table = nullptr;
+          s.free = true;
+          s.bytes.clear();
+          return BV_OK;  // HBM exhausted: per-batch path for this call
+        }
+        ctx->kc_bytes += kKcTableBytes;
+      }
+      ctx->kc_index[s.bytes] = si;
+      slot_of[k] = si;
+    }
+    // build the new tables, kKcBuildGroup keys per launch
+    const uint32_t G = std::min<uint32_t>(kKcBuildGroup, (uint32_t)std::max<size_t>(build.size(), 1));
+    HIPCHK(ctx->kc_kxy.ensure((uint64_t)G * 64), BV_E_OOM, "alloc kc kxy");
+    HIPCHK(ctx->kc_btabs.ensure((uint64_t)G * 8), BV_E_OOM, "alloc kc tabs");
+    HIPCHK(ctx->bases_jac.ensure((uint64_t)G * kBasesPerKey * 96), BV_E_OOM, "alloc bases");
+    HIPCHK(ctx->key_sub.ensure((uint64_t)G * kKcSubBytes), BV_E_OOM, "alloc kc sub-tables");
+    HIPCHK(ctx->key_pscr.ensure((uint64_t)G * bvk::kc_pscr_bytes()), BV_E_OOM, "alloc kc prefix scratch");
+    HIPCHK(ctx->pin_small.ensure(4096), BV_E_OOM, "alloc pinned");
+    for (size_t g0 = 0; g0 < build.size(); g0 += G) {
+      const uint32_t n = (uint32_t)std::min<size_t>(G, build.size() - g0);
+      uint64_t *tabs = (uint64_t *)ctx->pin_small.p;
+      HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");  // pin_small reuse
+      for (uint32_t i = 0; i < n; i++) {
+        const uint32_t k = build[g0 + i];
+        HIPCHK(hipMemcpyAsync(ctx->kc_kxy.as<uint8_t>() + 64ull * i, ctx->kxy.as<uint8_t>() + 64ull * k, 64,
+                              hipMemcpyDeviceToDevice, st),
+               BV_E_LAUNCH, "gather kxy");
+        tabs[i] = (uint64_t)(uintptr_t)ctx->kc_slots[slot_of[k]].table;
+      }
+      HIPCHK(hipMemcpyAsync(ctx->kc_btabs.p, tabs, n * 8ull, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d tabs");
+      HIPCHK(bvk::build_kc(st, n, ctx->kc_kxy.as<uint32_t>(), nullptr, ctx->bases_jac.as<uint32_t>(),
+                           ctx->key_sub.as<uint32_t>(), ctx->key_pscr.as<uint32_t>(), ctx->kc_btabs.as<uint64_t>()),
+             BV_E_LAUNCH, "KC key tables");
+      builds += n;
+    }
+    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+  }
+  // per-batch arrays: table address and status of every batch key
+  HIPCHK(ctx->pin_small.ensure((uint64_t)n_keys * 9 + 64), BV_E_OOM, "alloc pinned");
+  HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync");  // pin_small may feed an earlier async call
+  uint64_t *tabs = (uint64_t *)ctx->pin_small.p;
+  uint8_t *kst = (uint8_t *)(tabs + n_keys);
+  for (uint32_t k = 0; k < n_keys; k++) {
+    const auto &s = ctx->kc_slots[slot_of[k]];
+    tabs[k] = (uint64_t)(uintptr_t)s.table;
+    kst[k] = s.status;
+  }
+  HIPCHK(ctx->kc_tabs.ensure((uint64_t)n_keys * 8), BV_E_OOM, "alloc kc tabs");
+  HIPCHK(ctx->kc_kst.ensure(n_keys), BV_E_OOM, "alloc kc kst");
+  HIPCHK(hipMemcpyAsync(ctx->kc_tabs.p, tabs, n_keys * 8ull, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d tabs");
+  HIPCHK(hipMemcpyAsync(ctx->kc_kst.p, kst, n_keys, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d kst");
+  ctx->timing.kc_hits = hits;
+  ctx->timing.kc_builds = builds;
+  ctx->timing.kc_keys = (uint32_t)ctx->kc_index.size();
+  *use = true;
+  return BV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// device pipeline
+// ---------------------------------------------------------------------------
+// Over device-resident inputs.  msg_hash/status/bits may be null (ctx
+// buffers are used).  Caller holds ctx->mu and has set the device.
+// `hashed`: the digests are already in ctx->digests (host entry point,
+// hashed chunk by chunk as the bytes landed).  `kc`: use the key cache
+// arrays prepared by kc_prepare.  Every call starts after the previous call
+// on this ctx has finished on the device (ev_done), whatever its stream:
+// work buffers are shared between calls.
+int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
+                  hipStream_t st, bool hashed, bool kc) {
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
   if (n_items > 0 && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be))
-    return fail(ctx, BV_E_ARGS, "null item arrays");
-  if (n_msgs > 0 && !b->msg_off) return fail(ctx, BV_E_ARGS, "null msg_off");
-  if (n_items > 0 && n_keys == 0) return fail(ctx, BV_E_ARGS, "items without keys");
-  if (n_keys > 0 && !b->key_off) return fail(ctx, BV_E_ARGS, "null key_off");
+    return bv_fail(ctx, BV_E_ARGS, "null item arrays");
+  if (n_msgs > 0 && !b->msg_off) return bv_fail(ctx, BV_E_ARGS, "null msg_off");
+  if (n_items > 0 && n_keys == 0) return bv_fail(ctx, BV_E_ARGS, "items without keys");
+  if (n_keys > 0 && !b->key_off) return bv_fail(ctx, BV_E_ARGS, "null key_off");
   if (((uintptr_t)b->r_be | (uintptr_t)b->s_be) & 15)
-    return fail(ctx, BV_E_ARGS, "r_be/s_be must be 16-byte aligned");
+    return bv_fail(ctx, BV_E_ARGS, "r_be/s_be must be 16-byte aligned");
 
   uint32_t *dig = (uint32_t *)d_msg_hash;
-  if (!dig || ((uintptr_t)dig & 15)) {
+  if (hashed || !dig || ((uintptr_t)dig & 15)) {
     HIPCHK(ctx->digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
     dig = ctx->digests.as<uint32_t>();
   }
@@ -293,73 +516,84 @@ static int run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8
   HIPCHK(ctx->kstatus.ensure(std::max<uint32_t>(n_keys, 1)), BV_E_OOM, "alloc kstatus");
   HIPCHK(ctx->kxy.ensure(std::max<uint32_t>(n_keys, 1) * 64ull), BV_E_OOM, "alloc kxy");
   HIPCHK(ctx->scratch.ensure(std::max<uint64_t>(n_items, 1) * 32), BV_E_OOM, "alloc scratch");
-  HIPCHK(ctx->u12.ensure(std::max<uint64_t>(n_items, 1) * kUStride * 4), BV_E_OOM, "alloc u12");
+  HIPCHK(ctx->u12.ensure(std::max<uint64_t>(n_items, 1) * BV_U_STRIDE * 4), BV_E_OOM, "alloc u12");
 
-  // Per-key fixed-base tables pay off once a key signs enough items; with
-  // few items per key the generic per-lane path is cheaper.
-  const bool table_mode = n_keys <= kMaxTableKeys && n_items >= 16ull * n_keys;
-  const int key_w = !table_mode ? 0
+  // Key path: the key cache when prepared; otherwise per-batch fixed-base
+  // tables once a key signs enough items (K12 for large batches, K8 for
+  // mid-size), else the generic per-lane path.
+  const bool table_mode = kc || (n_keys <= kMaxTableKeys && n_items >= 16ull * n_keys);
+  const int key_w = kc ? BV_KCW
+                    : !table_mode ? 0
                     : (n_keys <= kMaxK12Keys && n_items >= kK12MinItemsPerKey * n_keys && !(ctx->flags & BV_F_K8))
                         ? 12
                         : 8;
   ctx->table_mode = table_mode;
   ctx->key_w = key_w;
   if (table_mode) {
-    const uint64_t nk = std::max<uint32_t>(n_keys, 1);
-    HIPCHK(ctx->bases_jac.ensure(nk * kBasesPerKey * 96ull), BV_E_OOM, "alloc bases");
-    if (key_w == 12) {
-      HIPCHK(ctx->key_sub.ensure(nk * kK12SubBytes), BV_E_OOM, "alloc key sub-tables");
-      HIPCHK(ctx->key_pscr.ensure(nk * kK12PrefixBytes), BV_E_OOM, "alloc key prefix scratch");
-    }
-    HIPCHK(ctx->key_table.ensure(nk * (key_w == 12 ? kK12TableBytes : kKTableBytes)), BV_E_OOM,
-           "alloc key tables");
     HIPCHK(ctx->rg.ensure(std::max<uint64_t>(n_items, 1) * kRgWords * 4), BV_E_OOM, "alloc R_G");
+    if (!kc) {
+      const uint64_t nk = std::max<uint32_t>(n_keys, 1);
+      HIPCHK(ctx->bases_jac.ensure(nk * kBasesPerKey * 96ull), BV_E_OOM, "alloc bases");
+      if (key_w == 12) {
+        HIPCHK(ctx->key_sub.ensure(nk * kK12SubBytes), BV_E_OOM, "alloc key sub-tables");
+        HIPCHK(ctx->key_pscr.ensure(nk * kK12PrefixBytes), BV_E_OOM, "alloc key prefix scratch");
+      }
+      HIPCHK(ctx->key_table.ensure(nk * (key_w == 12 ? kK12TableBytes : kKTableBytes)), BV_E_OOM,
+             "alloc key tables");
+    }
   }
+  const uint8_t *kst = kc ? ctx->kc_kst.as<uint8_t>() : ctx->kstatus.as<uint8_t>();
 
   hipEvent_t *ev = ctx->ev;
   const uint32_t *r32 = (const uint32_t *)b->r_be, *s32 = (const uint32_t *)b->s_be;
   uint32_t *w = ctx->scratch.as<uint32_t>(), *u12 = ctx->u12.as<uint32_t>();
+  if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order after previous call");
   HIPCHK(hipEventRecord(ev[E_START], st), BV_E_LAUNCH, "event");
   // s^-1 needs only s: its own stream, concurrent with everything up to k_verify_g
   HIPCHK(hipStreamWaitEvent(ctx->sstream, ev[E_START], 0), BV_E_LAUNCH, "fork");
   HIPCHK(bvk::sinv(ctx->sstream, n_items, kPrepM, s32, b->pre, w), BV_E_LAUNCH, "k_sinv");
   HIPCHK(hipEventRecord(ev[E_SINV], ctx->sstream), BV_E_LAUNCH, "event");
-  HIPCHK(bvk::key_decode(st, n_keys, b->key_bytes, b->key_off, ctx->kstatus.as<uint8_t>(), ctx->kxy.as<uint32_t>()),
-         BV_E_LAUNCH, "k_key_decode");
+  if (!kc)
+    HIPCHK(bvk::key_decode(st, n_keys, b->key_bytes, b->key_off, ctx->kstatus.as<uint8_t>(),
+                           ctx->kxy.as<uint32_t>()),
+           BV_E_LAUNCH, "k_key_decode");
   HIPCHK(hipEventRecord(ev[E_FORK], st), BV_E_LAUNCH, "event");
-  if (table_mode) {  // key tables on the keys stream, concurrent with the main stream below
+  if (table_mode && !kc) {  // key tables on the keys stream, concurrent with the main stream below
     HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_FORK], 0), BV_E_LAUNCH, "fork");
     HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
                              ctx->bases_jac.as<uint32_t>(), ctx->key_sub.as<uint32_t>(),
                              ctx->key_pscr.as<uint32_t>(), ctx->key_table.as<uint32_t>()),
            BV_E_LAUNCH, "key tables");
     HIPCHK(hipEventRecord(ev[E_KEYS], ctx->kstream), BV_E_LAUNCH, "event");
+  } else {
+    HIPCHK(hipEventRecord(ev[E_KEYS], st), BV_E_LAUNCH, "event");
   }
-  HIPCHK(bvk::sha256(st, n_msgs, b->msg_bytes, b->msg_off, dig), BV_E_LAUNCH, "k_sha256");
+  if (!hashed) HIPCHK(bvk::sha256(st, n_msgs, b->msg_bytes, b->msg_off, dig), BV_E_LAUNCH, "k_sha256");
   HIPCHK(hipEventRecord(ev[E_SHA], st), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamWaitEvent(st, ev[E_SINV], 0), BV_E_LAUNCH, "join");
   HIPCHK(hipEventRecord(ev[E_SCALAR], st), BV_E_LAUNCH, "event");
   if (table_mode) {
-    HIPCHK(bvk::verify_g(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(), b->item_msg, dig, w,
-                         u12, ctx->g_table, ctx->rg.as<uint32_t>()),
+    HIPCHK(bvk::verify_g(st, n_items, b->item_key, r32, s32, b->pre, kst, b->item_msg, dig, w, u12, ctx->g_table,
+                         ctx->rg.as<uint32_t>()),
            BV_E_LAUNCH, "k_verify_g");
     HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
     HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
-    HIPCHK(bvk::verify_q(st, key_w, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(), u12,
-                         ctx->key_table.as<uint32_t>(), ctx->rg.as<uint32_t>(), status, bits),
+    HIPCHK(bvk::verify_q(st, key_w, n_items, b->item_key, r32, s32, b->pre, kst, u12, ctx->key_table.as<uint32_t>(),
+                         kc ? ctx->kc_tabs.as<uint64_t>() : nullptr, ctx->rg.as<uint32_t>(), status, bits),
            BV_E_LAUNCH, "k_verify_q");
   } else {
     HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
     HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
-    HIPCHK(bvk::verify_generic(st, n_items, b->item_key, r32, s32, b->pre, ctx->kstatus.as<uint8_t>(),
-                               ctx->kxy.as<uint32_t>(), b->item_msg, dig, w, ctx->g_table, status,
-                               bits),
+    HIPCHK(bvk::verify_generic(st, n_items, b->item_key, r32, s32, b->pre, kst, ctx->kxy.as<uint32_t>(), b->item_msg,
+                               dig, w, ctx->g_table, status, bits),
            BV_E_LAUNCH, "k_verify_generic");
   }
   HIPCHK(hipEventRecord(ev[E_END], st), BV_E_LAUNCH, "event");
   if (d_msg_hash && (uint8_t *)dig != d_msg_hash)
     HIPCHK(hipMemcpyAsync(d_msg_hash, dig, n_msgs * 32, hipMemcpyDeviceToDevice, st), BV_E_LAUNCH, "copy digests");
+  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
+  ctx->has_done = true;
   return BV_OK;
 }
 
@@ -368,7 +602,7 @@ static float elapsed(hipEvent_t a, hipEvent_t b) {
   return hipEventElapsedTime(&t, a, b) == hipSuccess ? t : -1.f;
 }
 
-static void read_timing(bv_ctx *ctx) {
+void bv_read_timing(bv_ctx *ctx) {
   hipEvent_t *ev = ctx->ev;
   bv_timing &t = ctx->timing;
   t.ms_sha256 = elapsed(ev[E_FORK], ev[E_SHA]);
@@ -385,13 +619,236 @@ extern "C" int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_re
   if (!ctx || !dbatch || !dresult) return BV_E_ARGS;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  const auto t0 = std::chrono::steady_clock::now();
   hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
-  int rc = run_device(ctx, dbatch, dresult->msg_hash, dresult->status, dresult->accept_bits, st);
+  ctx->timing = bv_timing{};
+  bool kc = false;
+  if ((ctx->flags & BV_F_KEY_CACHE) && dbatch->n_keys && dbatch->n_keys <= kKcMaxBatchKeys) {
+    // the cache is keyed by the raw key bytes: bring them (small) to the host
+    const uint32_t nk = dbatch->n_keys;
+    if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order");
+    std::vector<uint64_t> hko(nk + 1);
+    HIPCHK(hipMemcpyAsync(hko.data(), dbatch->key_off, (nk + 1) * 8ull, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
+           "d2h key_off");
+    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+    if (hko[0] != 0) return bv_fail(ctx, BV_E_ARGS, "key_off[0] != 0");
+    for (uint32_t k = 0; k < nk; k++)
+      if (hko[k] > hko[k + 1]) return bv_fail(ctx, BV_E_ARGS, "key_off not monotone");
+    std::vector<uint8_t> hkb(hko[nk] + 1);
+    if (hko[nk]) {
+      HIPCHK(hipMemcpyAsync(hkb.data(), dbatch->key_bytes, hko[nk], hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
+             "d2h key bytes");
+      HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+    }
+    int rc = kc_prepare(ctx, nk, hkb.data(), hko.data(), dbatch->key_bytes, dbatch->key_off, st, &kc);
+    if (rc != BV_OK) return rc;
+  }
+  int rc = bv_run_device(ctx, dbatch, dresult->msg_hash, dresult->status, dresult->accept_bits, st, false, kc);
   if (rc != BV_OK) return rc;
   if (!async) {
     HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "verify sync");
-    read_timing(ctx);
+    bv_read_timing(ctx);
+    ctx->timing.ms_host =
+        std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
+  return BV_OK;
+}
+
+extern "C" int bv_sync(bv_ctx *ctx) {
+  if (!ctx) return BV_E_ARGS;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!ctx->has_done) return BV_OK;
+  HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync");
+  bv_read_timing(ctx);
+  return BV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// host entry point
+// ---------------------------------------------------------------------------
+int bv_validate_host_batch(bv_ctx *ctx, const bv_batch *b) {
+  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
+  const uint32_t n_keys = b->n_keys;
+  if ((n_msgs && !b->msg_off) || (n_keys && !b->key_off) ||
+      (n_items && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be)))
+    return bv_fail(ctx, BV_E_ARGS, "null input array");
+  if (n_items && !n_keys) return bv_fail(ctx, BV_E_ARGS, "items without keys");
+  const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
+  const uint64_t key_len = n_keys ? b->key_off[n_keys] : 0;
+  // byte arrays may be null only when empty (all-empty messages or keys)
+  if ((msg_len && !b->msg_bytes) || (key_len && !b->key_bytes)) return bv_fail(ctx, BV_E_ARGS, "null byte array");
+  // validate host offsets (a bad offset must not become an OOB device read)
+  if (n_msgs && b->msg_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "msg_off[0] != 0");
+  if (n_keys && b->key_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "key_off[0] != 0");
+  for (uint64_t m = 0; m < n_msgs; m++)
+    if (b->msg_off[m] > b->msg_off[m + 1]) return bv_fail(ctx, BV_E_ARGS, "msg_off not monotone");
+  for (uint32_t k = 0; k < n_keys; k++)
+    if (b->key_off[k] > b->key_off[k + 1]) return bv_fail(ctx, BV_E_ARGS, "key_off not monotone");
+  for (uint64_t i = 0; i < n_items; i++)
+    if (b->item_msg[i] >= n_msgs || b->item_key[i] >= n_keys)
+      return bv_fail(ctx, BV_E_ARGS, "item index out of range");
+  return BV_OK;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Stage a host batch into HBM (pinned chunks on the copy stream), hash the
+// messages chunk by chunk as they land and launch the verify pipeline.
+// Returns with the work enqueued; bv_host_finish waits and copies results.
+int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
+  const auto t0 = std::chrono::steady_clock::now();
+  call->t0 = t0;
+  int rc = bv_validate_host_batch(ctx, b);
+  if (rc != BV_OK) return rc;
+  hipStream_t st = ctx->stream, cs = ctx->cstream;
+  ctx->timing = bv_timing{};
+  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
+  const uint32_t n_keys = b->n_keys;
+  const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
+  const uint64_t key_len = n_keys ? b->key_off[n_keys] : 0;
+
+  // one staging layout, identical in pinned host memory and in HBM
+  struct Seg {
+    const void *src;
+    size_t n;
+    size_t off;
+  };
+  Seg segs[9];
+  size_t total = 0;
+  auto add = [&](int i, const void *src, size_t n, size_t pad) {
+    segs[i] = {src, n, total};
+    total += align256(n + pad);
+  };
+  add(0, b->msg_off, n_msgs ? (n_msgs + 1) * 8 : 0, 0);
+  add(1, b->key_off, n_keys ? (n_keys + 1) * 8ull : 0, 0);
+  add(2, b->key_bytes, key_len, 64);
+  add(3, b->item_msg, n_items * 4, 0);
+  add(4, b->item_key, n_items * 4, 0);
+  add(5, b->r_be, n_items * 32, 0);
+  add(6, b->s_be, n_items * 32, 0);
+  add(7, b->pre, b->pre ? n_items : 0, 0);
+  add(8, b->msg_bytes, msg_len, 64);
+  // previous work on this ctx must be done before its staging is reused
+  if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
+  HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
+  HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
+  uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
+  HIPCHK(hipEventRecord(ctx->ev[E_CALL], cs), BV_E_LAUNCH, "event");
+
+  // keys and item arrays first (one contiguous region of the layout), in
+  // kChunk pieces: the pool fills piece c+1 while the DMA engine moves piece c
+  size_t ev_i = 0;
+  auto chunk_event = [&]() -> hipEvent_t {
+    hipEvent_t e = ctx->chunk_ev[ev_i % ctx->chunk_ev.size()];
+    ev_i++;
+    return e;
+  };
+  const size_t small_end = segs[8].off;
+  for (size_t a = 0; a < small_end; a += kChunk) {
+    const size_t z = std::min(small_end, a + kChunk);
+    for (int i = 0; i < 8; i++) {  // the parts of segments 0-7 inside [a, z)
+      const Seg &s = segs[i];
+      const size_t lo = std::max(a, s.off), hi = std::min(z, s.off + s.n);
+      if (lo < hi) ctx->pool->copy(pin + lo, (const uint8_t *)s.src + (lo - s.off), hi - lo);
+    }
+    HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
+  }
+  // zero the message-bytes pad in the staging (the SHA kernel over-reads
+  // the last dword of a message into it)
+  if (msg_len) memset(pin + segs[8].off + msg_len, 0, 64);
+  HIPCHK(hipEventRecord(ctx->ev[E_SMALL], cs), BV_E_LAUNCH, "event");
+
+  bv_batch d = {};
+  d.n_msgs = n_msgs;
+  d.msg_bytes = dev + segs[8].off;
+  d.msg_off = (const uint64_t *)(dev + segs[0].off);
+  d.n_keys = n_keys;
+  d.key_bytes = dev + segs[2].off;
+  d.key_off = (const uint64_t *)(dev + segs[1].off);
+  d.n_items = n_items;
+  d.item_msg = (const uint32_t *)(dev + segs[3].off);
+  d.item_key = (const uint32_t *)(dev + segs[4].off);
+  d.r_be = dev + segs[5].off;
+  d.s_be = dev + segs[6].off;
+  d.pre = b->pre ? dev + segs[7].off : nullptr;
+
+  // key cache resolution needs the keys on the device (decode of misses)
+  bool kc = false;
+  if ((ctx->flags & BV_F_KEY_CACHE) && n_keys && n_keys <= kKcMaxBatchKeys) {
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SMALL], 0), BV_E_LAUNCH, "join");
+    rc = kc_prepare(ctx, n_keys, b->key_bytes, b->key_off, d.key_bytes, d.key_off, st, &kc);
+    if (rc != BV_OK) return rc;
+  }
+
+  // message bytes: chunks on message boundaries, each hashed once it lands
+  HIPCHK(ctx->digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
+  if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order");
+  HIPCHK(hipEventRecord(ctx->ev[E_HASH0], st), BV_E_LAUNCH, "event");
+  uint64_t m0 = 0;
+  while (m0 < n_msgs) {
+    // messages [m0, m1) holding about kChunk bytes (at least one message)
+    const uint64_t base = b->msg_off[m0];
+    uint64_t m1 = std::upper_bound(b->msg_off + m0 + 1, b->msg_off + n_msgs + 1, base + kChunk) - b->msg_off - 1;
+    if (m1 <= m0) m1 = m0 + 1;
+    const uint64_t end = b->msg_off[m1];
+    const size_t len = end - base + (m1 == n_msgs ? 64 : 0);
+    ctx->pool->copy(pin + segs[8].off + base, b->msg_bytes + base, end - base);
+    HIPCHK(hipMemcpyAsync(dev + segs[8].off + base, pin + segs[8].off + base, len, hipMemcpyHostToDevice, cs),
+           BV_E_LAUNCH, "h2d msgs");
+    hipEvent_t e = chunk_event();
+    HIPCHK(hipEventRecord(e, cs), BV_E_LAUNCH, "event");
+    HIPCHK(hipStreamWaitEvent(st, e, 0), BV_E_LAUNCH, "join chunk");
+    if (m0 == 0) HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SMALL], 0), BV_E_LAUNCH, "join offsets");
+    HIPCHK(bvk::sha256(st, m1 - m0, d.msg_bytes, d.msg_off + m0, ctx->digests.as<uint32_t>() + 8 * m0), BV_E_LAUNCH,
+           "k_sha256");
+    m0 = m1;
+  }
+  HIPCHK(hipEventRecord(ctx->ev[E_STAGED], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_STAGED], 0), BV_E_LAUNCH, "join staging");
+  HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
+  rc = bv_run_device(ctx, &d, nullptr, nullptr, nullptr, st, true, kc);
+  if (rc != BV_OK) return rc;
+
+  // results into pinned memory: digests as soon as hashing ended (overlaps
+  // the verify kernels, on the copy stream), statuses and bits at the end
+  const size_t o_st = align256(n_msgs * 32), o_bits = o_st + align256(n_items);
+  HIPCHK(ctx->pin_out.ensure(o_bits + align256((n_items + 63) / 64 * 8) + 256), BV_E_OOM, "alloc pinned results");
+  uint8_t *pout = (uint8_t *)ctx->pin_out.p;
+  call->pout = pout;
+  call->o_st = o_st;
+  call->o_bits = o_bits;
+  if (n_msgs) {
+    HIPCHK(hipStreamWaitEvent(cs, ctx->ev[E_HASHED], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipMemcpyAsync(pout, ctx->digests.p, n_msgs * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH, "d2h digests");
+  }
+  if (n_items) {
+    HIPCHK(hipMemcpyAsync(pout + o_st, ctx->status.p, n_items, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
+    HIPCHK(hipMemcpyAsync(pout + o_bits, ctx->bits.p, (n_items + 63) / 64 * 8, hipMemcpyDeviceToHost, st),
+           BV_E_LAUNCH, "d2h bits");
+  }
+  HIPCHK(hipEventRecord(ctx->ev[E_OUT], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_STAGED], 0), BV_E_LAUNCH, "join");  // staging free after this point
+  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_HASHED], 0), BV_E_LAUNCH, "join");
+  // the digests' d2h on the copy stream also precedes ev_done
+  HIPCHK(hipEventRecord(ctx->ev[E_CSDONE], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_CSDONE], 0), BV_E_LAUNCH, "join");
+  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
+  return BV_OK;
+}
+
+int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call *call, bool bits_out) {
+  HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "verify sync");
+  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
+  if (res->msg_hash && n_msgs) ctx->pool->copy(res->msg_hash, call->pout, n_msgs * 32);
+  if (res->status && n_items) ctx->pool->copy(res->status, call->pout + call->o_st, n_items);
+  if (bits_out && res->accept_bits && n_items)
+    memcpy(res->accept_bits, call->pout + call->o_bits, (n_items + 63) / 64 * 8);
+  bv_read_timing(ctx);
+  ctx->timing.ms_h2d = elapsed(ctx->ev[E_CALL], ctx->ev[E_STAGED]);
+  ctx->timing.ms_d2h = elapsed(ctx->ev[E_END], ctx->ev[E_OUT]);
+  ctx->timing.ms_host =
+      std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call->t0).count();
   return BV_OK;
 }
 
@@ -399,83 +856,10 @@ extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   if (!ctx || !b || !res) return BV_E_ARGS;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
-  hipStream_t st = ctx->stream;
-  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
-  const uint32_t n_keys = b->n_keys;
-  if ((n_msgs && !b->msg_off) || (n_keys && !b->key_off) ||
-      (n_items && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be)))
-    return fail(ctx, BV_E_ARGS, "null input array");
-  const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
-  const uint64_t key_len = n_keys ? b->key_off[n_keys] : 0;
-  // byte arrays may be null only when empty (all-empty messages or keys)
-  if ((msg_len && !b->msg_bytes) || (key_len && !b->key_bytes)) return fail(ctx, BV_E_ARGS, "null byte array");
-  // validate host offsets (a bad offset must not become an OOB device read)
-  if (n_msgs && b->msg_off[0] != 0) return fail(ctx, BV_E_ARGS, "msg_off[0] != 0");
-  if (n_keys && b->key_off[0] != 0) return fail(ctx, BV_E_ARGS, "key_off[0] != 0");
-  for (uint64_t m = 0; m < n_msgs; m++)
-    if (b->msg_off[m] > b->msg_off[m + 1]) return fail(ctx, BV_E_ARGS, "msg_off not monotone");
-  for (uint32_t k = 0; k < n_keys; k++)
-    if (b->key_off[k] > b->key_off[k + 1]) return fail(ctx, BV_E_ARGS, "key_off not monotone");
-  for (uint64_t i = 0; i < n_items; i++)
-    if (b->item_msg[i] >= n_msgs || b->item_key[i] >= n_keys) return fail(ctx, BV_E_ARGS, "item index out of range");
-
-  hipEvent_t e0, e1;
-  HIPCHK(hipEventCreate(&e0), BV_E_LAUNCH, "event");
-  HIPCHK(hipEventCreate(&e1), BV_E_LAUNCH, "event");
-  HIPCHK(hipEventRecord(e0, st), BV_E_LAUNCH, "event");
-  HIPCHK(ctx->h_msg_bytes.ensure(msg_len + 64), BV_E_OOM, "alloc msg bytes");
-  HIPCHK(ctx->h_msg_off.ensure((n_msgs + 1) * 8), BV_E_OOM, "alloc msg off");
-  HIPCHK(ctx->h_key_bytes.ensure(key_len + 64), BV_E_OOM, "alloc key bytes");
-  HIPCHK(ctx->h_key_off.ensure((uint64_t)(n_keys + 1) * 8), BV_E_OOM, "alloc key off");
-  HIPCHK(ctx->h_item_msg.ensure(std::max<uint64_t>(n_items, 1) * 4), BV_E_OOM, "alloc item msg");
-  HIPCHK(ctx->h_item_key.ensure(std::max<uint64_t>(n_items, 1) * 4), BV_E_OOM, "alloc item key");
-  HIPCHK(ctx->h_r.ensure(std::max<uint64_t>(n_items, 1) * 32), BV_E_OOM, "alloc r");
-  HIPCHK(ctx->h_s.ensure(std::max<uint64_t>(n_items, 1) * 32), BV_E_OOM, "alloc s");
-  HIPCHK(ctx->h_pre.ensure(std::max<uint64_t>(n_items, 1)), BV_E_OOM, "alloc pre");
-  auto h2d = [&](DevBuf &d, const void *src, size_t n) -> hipError_t {
-    if (n == 0) return hipSuccess;
-    return hipMemcpyAsync(d.p, src, n, hipMemcpyHostToDevice, st);
-  };
-  HIPCHK(h2d(ctx->h_msg_bytes, b->msg_bytes, msg_len), BV_E_LAUNCH, "h2d msg");
-  if (n_msgs) HIPCHK(h2d(ctx->h_msg_off, b->msg_off, (n_msgs + 1) * 8), BV_E_LAUNCH, "h2d msg off");
-  HIPCHK(h2d(ctx->h_key_bytes, b->key_bytes, key_len), BV_E_LAUNCH, "h2d keys");
-  if (n_keys) HIPCHK(h2d(ctx->h_key_off, b->key_off, (uint64_t)(n_keys + 1) * 8), BV_E_LAUNCH, "h2d key off");
-  HIPCHK(h2d(ctx->h_item_msg, b->item_msg, n_items * 4), BV_E_LAUNCH, "h2d item msg");
-  HIPCHK(h2d(ctx->h_item_key, b->item_key, n_items * 4), BV_E_LAUNCH, "h2d item key");
-  HIPCHK(h2d(ctx->h_r, b->r_be, n_items * 32), BV_E_LAUNCH, "h2d r");
-  HIPCHK(h2d(ctx->h_s, b->s_be, n_items * 32), BV_E_LAUNCH, "h2d s");
-  if (b->pre) HIPCHK(h2d(ctx->h_pre, b->pre, n_items), BV_E_LAUNCH, "h2d pre");
-  bv_batch d = {};
-  d.n_msgs = n_msgs;
-  d.msg_bytes = ctx->h_msg_bytes.as<uint8_t>();
-  d.msg_off = ctx->h_msg_off.as<uint64_t>();
-  d.n_keys = n_keys;
-  d.key_bytes = ctx->h_key_bytes.as<uint8_t>();
-  d.key_off = ctx->h_key_off.as<uint64_t>();
-  d.n_items = n_items;
-  d.item_msg = ctx->h_item_msg.as<uint32_t>();
-  d.item_key = ctx->h_item_key.as<uint32_t>();
-  d.r_be = ctx->h_r.as<uint8_t>();
-  d.s_be = ctx->h_s.as<uint8_t>();
-  d.pre = b->pre ? ctx->h_pre.as<uint8_t>() : nullptr;
-  int rc = run_device(ctx, &d, nullptr, nullptr, nullptr, st);
+  bv_host_call call;
+  int rc = bv_host_launch(ctx, b, &call);
   if (rc != BV_OK) return rc;
-  if (res->msg_hash && n_msgs)
-    HIPCHK(hipMemcpyAsync(res->msg_hash, ctx->digests.p, n_msgs * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
-           "d2h digests");
-  if (res->status && n_items)
-    HIPCHK(hipMemcpyAsync(res->status, ctx->status.p, n_items, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
-  if (res->accept_bits && n_items)
-    HIPCHK(hipMemcpyAsync(res->accept_bits, ctx->bits.p, (n_items + 63) / 64 * 8, hipMemcpyDeviceToHost, st),
-           BV_E_LAUNCH, "d2h bits");
-  HIPCHK(hipEventRecord(e1, st), BV_E_LAUNCH, "event");
-  HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "verify sync");
-  read_timing(ctx);
-  ctx->timing.ms_h2d = elapsed(e0, ctx->ev[E_START]);
-  ctx->timing.ms_d2h = elapsed(ctx->ev[E_END], e1);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  return BV_OK;
+  return bv_host_finish(ctx, b, res, &call, true);
 }
 
 extern "C" int bv_sha256_batch(bv_ctx *ctx, uint64_t n_msgs, const uint8_t *msg_bytes, const uint64_t *msg_off,
@@ -484,20 +868,28 @@ extern "C" int bv_sha256_batch(bv_ctx *ctx, uint64_t n_msgs, const uint8_t *msg_
   if (n_msgs == 0) return BV_OK;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
-  if (msg_off[0] != 0) return fail(ctx, BV_E_ARGS, "msg_off[0] != 0");
+  if (msg_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "msg_off[0] != 0");
   for (uint64_t m = 0; m < n_msgs; m++)
-    if (msg_off[m] > msg_off[m + 1]) return fail(ctx, BV_E_ARGS, "msg_off not monotone");
+    if (msg_off[m] > msg_off[m + 1]) return bv_fail(ctx, BV_E_ARGS, "msg_off not monotone");
   hipStream_t st = ctx->stream;
   const uint64_t len = msg_off[n_msgs];
-  HIPCHK(ctx->h_msg_bytes.ensure(len + 64), BV_E_OOM, "alloc msg bytes");
-  HIPCHK(ctx->h_msg_off.ensure((n_msgs + 1) * 8), BV_E_OOM, "alloc msg off");
+  if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
+  const size_t o_off = align256(len + 64), total = o_off + align256((n_msgs + 1) * 8);
+  HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
+  HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
+  HIPCHK(ctx->pin_out.ensure(n_msgs * 32), BV_E_OOM, "alloc pinned results");
   HIPCHK(ctx->digests.ensure(n_msgs * 32), BV_E_OOM, "alloc digests");
-  if (len) HIPCHK(hipMemcpyAsync(ctx->h_msg_bytes.p, msg_bytes, len, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
-  HIPCHK(hipMemcpyAsync(ctx->h_msg_off.p, msg_off, (n_msgs + 1) * 8, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
-  HIPCHK(bvk::sha256(st, n_msgs, ctx->h_msg_bytes.as<uint8_t>(), ctx->h_msg_off.as<uint64_t>(),
-                     ctx->digests.as<uint32_t>()),
-         BV_E_LAUNCH, "k_sha256");
-  HIPCHK(hipMemcpyAsync(out_hash, ctx->digests.p, n_msgs * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h");
+  uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
+  ctx->pool->copy(pin, msg_bytes, len);
+  memset(pin + len, 0, 64);
+  memcpy(pin + o_off, msg_off, (n_msgs + 1) * 8);
+  HIPCHK(hipMemcpyAsync(dev, pin, total, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
+  HIPCHK(bvk::sha256(st, n_msgs, dev, (const uint64_t *)(dev + o_off), ctx->digests.as<uint32_t>()), BV_E_LAUNCH,
+         "k_sha256");
+  HIPCHK(hipMemcpyAsync(ctx->pin_out.p, ctx->digests.p, n_msgs * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h");
+  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
+  ctx->has_done = true;
   HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+  memcpy(out_hash, ctx->pin_out.p, n_msgs * 32);
   return BV_OK;
 }

@@ -1,0 +1,287 @@
+// bv_group.cpp — multi-GPU verifier behind the C ABI (include/babbleverify.h,
+// bv_group_*): one process, one bv_ctx per device, items sharded by index,
+// one RCCL all-gather of the accept bitmasks.
+//
+// The north star's multi-GPU step: VerifyBatch items are
+// independent, so device g verifies a contiguous item range and no data
+// crosses devices except the accept bits.  Shards never split the items of
+// one message (bv_plan_shards): a BlockBody's 100 validator signatures
+// (block.go:343, hashgraph.go:1599-1630) stay on one device, so the body is
+// hashed once and a CheckBlock count is local.  Each device's bitmask
+// (its shard's bits from bit 0, padded to the largest shard) is all-gathered
+// with ONE ncclAllGather into device 0 and copied to the host once; the
+// host merges the shard-local words into the global bitmask (bit shifts).
+// RCCL is loaded with dlopen at bv_group_create (the PyTorch process may
+// already hold it), so libbabbleverify.so has no link-time RCCL dependency
+// and single-device users never load it.
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+
+#include "bv_internal.h"
+
+namespace {
+
+// the RCCL entry points used (rccl.h; ncclUint64 = 5, ncclSuccess = 0)
+typedef void *nccl_comm;
+typedef int (*fn_init_all)(nccl_comm *, int, const int *);
+typedef int (*fn_destroy)(nccl_comm);
+typedef int (*fn_all_gather)(const void *, void *, size_t, int, nccl_comm, hipStream_t);
+typedef int (*fn_group)(void);
+typedef const char *(*fn_errstr)(int);
+constexpr int kNcclUint64 = 5;
+
+struct Rccl {
+  void *h = nullptr;
+  fn_init_all init_all = nullptr;
+  fn_destroy destroy = nullptr;
+  fn_all_gather all_gather = nullptr;
+  fn_group group_start = nullptr, group_end = nullptr;
+  fn_errstr errstr = nullptr;
+  bool load(std::string &err) {
+    if (h) return true;
+    const char *names[] = {"librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so.1"};
+    for (const char *n : names) {  // prefer a copy already in the process (PyTorch's)
+      h = dlopen(n, RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+      if (h) break;
+    }
+    for (const char *n : names) {
+      if (h) break;
+      h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+    }
+    if (!h) {
+      err = "RCCL (librccl.so) not found";
+      return false;
+    }
+    init_all = (fn_init_all)dlsym(h, "ncclCommInitAll");
+    destroy = (fn_destroy)dlsym(h, "ncclCommDestroy");
+    all_gather = (fn_all_gather)dlsym(h, "ncclAllGather");
+    group_start = (fn_group)dlsym(h, "ncclGroupStart");
+    group_end = (fn_group)dlsym(h, "ncclGroupEnd");
+    errstr = (fn_errstr)dlsym(h, "ncclGetErrorString");
+    if (!init_all || !destroy || !all_gather || !group_start || !group_end || !errstr) {
+      err = "RCCL symbols missing";
+      return false;
+    }
+    return true;
+  }
+};
+Rccl g_rccl;
+std::mutex g_rccl_mu;
+
+}  // namespace
+
+struct bv_group {
+  std::vector<int> devices;
+  std::vector<bv_ctx *> ctx;
+  std::vector<nccl_comm> comms;
+  std::vector<DevBuf> send, recv;  // per device: shard bits, gathered bits
+  std::vector<std::vector<uint64_t>> sub_off, sub_msg;
+  std::string err;
+  std::mutex mu;
+};
+
+static int gfail(bv_group *g, int code, const std::string &what) {
+  if (g) g->err = what;
+  return code;
+}
+
+extern "C" const char *bv_group_last_error(const bv_group *g) { return g ? g->err.c_str() : "null group"; }
+
+// Contiguous item ranges balanced by count, cut only where the next item
+// names a different message than the previous one (message-aligned), so the
+// items of one message are never split.  Empty shards are allowed.
+extern "C" int bv_plan_shards(const bv_batch *b, int n_shards, uint64_t *bounds) {
+  if (!b || n_shards <= 0 || !bounds) return BV_E_ARGS;
+  const uint64_t n = b->n_items;
+  if (n && !b->item_msg) return BV_E_ARGS;
+  bounds[0] = 0;
+  for (int g = 1; g < n_shards; g++) {
+    uint64_t c = std::max<uint64_t>(bounds[g - 1], (uint64_t)((__uint128_t)n * g / n_shards));
+    while (c > 0 && c < n && b->item_msg[c] == b->item_msg[c - 1]) c++;
+    bounds[g] = std::min(c, n);
+  }
+  bounds[n_shards] = n;
+  return BV_OK;
+}
+
+extern "C" void bv_group_destroy(bv_group *g) {
+  if (!g) return;
+  for (size_t i = 0; i < g->ctx.size(); i++) {
+    if (i < g->comms.size() && g->comms[i]) {
+      (void)hipSetDevice(g->devices[i]);
+      g_rccl.destroy(g->comms[i]);
+    }
+    (void)hipSetDevice(g->devices[i]);
+    if (i < g->send.size()) g->send[i].release();
+    if (i < g->recv.size()) g->recv[i].release();
+    bv_destroy(g->ctx[i]);
+  }
+  delete g;
+}
+
+extern "C" int bv_group_create(bv_group **out, const int *devices, int n_devices, uint32_t flags) {
+  if (!out || !devices || n_devices <= 0 || n_devices > 64) return BV_E_ARGS;
+  *out = nullptr;
+  for (int i = 0; i < n_devices; i++)
+    for (int j = 0; j < i; j++)
+      if (devices[i] == devices[j]) return BV_E_ARGS;
+  bv_group *g = new bv_group();
+  g->devices.assign(devices, devices + n_devices);
+  for (int i = 0; i < n_devices; i++) {
+    bv_ctx *c = nullptr;
+    int rc = bv_create(&c, devices[i], flags);
+    if (rc != BV_OK) {
+      bv_group_destroy(g);
+      return rc;
+    }
+    g->ctx.push_back(c);
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    std::string e;
+    if (!g_rccl.load(e)) {
+      bv_group_destroy(g);
+      return BV_E_COMM;
+    }
+  }
+  g->comms.assign(n_devices, nullptr);
+  const int r = g_rccl.init_all(g->comms.data(), n_devices, devices);
+  if (r != 0) {
+    g->comms.assign(n_devices, nullptr);
+    bv_group_destroy(g);
+    return BV_E_COMM;
+  }
+  g->send.resize(n_devices);
+  g->recv.resize(n_devices);
+  g->sub_off.resize(n_devices);
+  g->sub_msg.resize(n_devices);
+  *out = g;
+  return BV_OK;
+}
+
+extern "C" int bv_group_get_timing(const bv_group *g, int i, bv_timing *out) {
+  if (!g || i < 0 || i >= (int)g->ctx.size()) return BV_E_ARGS;
+  return bv_get_timing(g->ctx[i], out);
+}
+
+extern "C" int bv_group_verify_batch(bv_group *g, const bv_batch *b, bv_result *res) {
+  if (!g || !b || !res) return BV_E_ARGS;
+  std::lock_guard<std::mutex> lk(g->mu);
+  const int D = (int)g->ctx.size();
+  int rc = bv_validate_host_batch(g->ctx[0], b);
+  if (rc != BV_OK) return gfail(g, rc, g->ctx[0]->err);
+  std::vector<uint64_t> bounds(D + 1);
+  bv_plan_shards(b, D, bounds.data());
+
+  // per-device sub-batches: the shard's items and the message range they
+  // name (re-based offsets and indices); keys are replicated (small)
+  std::vector<bv_batch> sb(D);
+  std::vector<uint64_t> mlo(D, 0), mhi(D, 0);
+  std::vector<std::vector<uint32_t>> item_msg(D);
+  for (int d = 0; d < D; d++) {
+    const uint64_t a = bounds[d], z = bounds[d + 1];
+    uint64_t lo = b->n_msgs, hi = 0;
+    for (uint64_t i = a; i < z; i++) {
+      lo = std::min<uint64_t>(lo, b->item_msg[i]);
+      hi = std::max<uint64_t>(hi, b->item_msg[i] + 1ull);
+    }
+    if (a == z) lo = hi = 0;
+    mlo[d] = lo;
+    mhi[d] = hi;
+    auto &off = g->sub_off[d];
+    off.resize(hi - lo + 1);
+    for (uint64_t m = lo; m <= hi; m++) off[m - lo] = b->msg_off[m] - b->msg_off[lo];
+    item_msg[d].resize(z - a);
+    for (uint64_t i = a; i < z; i++) item_msg[d][i - a] = (uint32_t)(b->item_msg[i] - lo);
+    bv_batch &s = sb[d];
+    s = *b;
+    s.n_msgs = hi - lo;
+    s.msg_bytes = b->msg_bytes ? b->msg_bytes + (hi > lo ? b->msg_off[lo] : 0) : nullptr;
+    s.msg_off = off.data();
+    s.n_items = z - a;
+    s.item_msg = item_msg[d].data();
+    s.item_key = b->item_key ? b->item_key + a : nullptr;
+    s.r_be = b->r_be ? b->r_be + 32 * a : nullptr;
+    s.s_be = b->s_be ? b->s_be + 32 * a : nullptr;
+    s.pre = b->pre ? b->pre + a : nullptr;
+  }
+  uint64_t words = 1;
+  for (int d = 0; d < D; d++) words = std::max<uint64_t>(words, (bounds[d + 1] - bounds[d] + 63) / 64);
+
+  // stage + launch every shard concurrently (one host thread per device)
+  std::vector<bv_host_call> calls(D);
+  std::vector<int> rcs(D, BV_OK);
+  std::vector<std::thread> th;
+  for (int d = 0; d < D; d++)
+    th.emplace_back([&, d]() {
+      bv_ctx *c = g->ctx[d];
+      std::lock_guard<std::mutex> clk(c->mu);
+      if (hipSetDevice(c->device) != hipSuccess) {
+        rcs[d] = BV_E_NODEVICE;
+        return;
+      }
+      rcs[d] = bv_host_launch(c, &sb[d], &calls[d]);
+      if (rcs[d] != BV_OK) return;
+      // the shard's bits, zero-padded to `words`, as the all-gather send buffer
+      if (g->send[d].ensure(words * 8) != hipSuccess || g->recv[d].ensure(words * 8 * D) != hipSuccess) {
+        rcs[d] = BV_E_OOM;
+        return;
+      }
+      const uint64_t sw = (sb[d].n_items + 63) / 64;
+      if (hipMemsetAsync(g->send[d].p, 0, words * 8, c->stream) != hipSuccess ||
+          (sw && hipMemcpyAsync(g->send[d].p, c->bits.p, sw * 8, hipMemcpyDeviceToDevice, c->stream) != hipSuccess))
+        rcs[d] = BV_E_LAUNCH;
+    });
+  for (auto &t : th) t.join();
+  for (int d = 0; d < D; d++)
+    if (rcs[d] != BV_OK) return gfail(g, rcs[d], "device " + std::to_string(g->devices[d]) + ": " + g->ctx[d]->err);
+
+  // ONE all-gather of the accept bitmasks over RCCL (xGMI)
+  int r = g_rccl.group_start();
+  for (int d = 0; d < D && r == 0; d++) {
+    (void)hipSetDevice(g->devices[d]);
+    r = g_rccl.all_gather(g->send[d].p, g->recv[d].p, words, kNcclUint64, g->comms[d], g->ctx[d]->stream);
+  }
+  const int r2 = g_rccl.group_end();
+  if (r != 0 || r2 != 0) return gfail(g, BV_E_COMM, std::string("ncclAllGather: ") + g_rccl.errstr(r ? r : r2));
+  std::vector<uint64_t> gathered(words * D);
+  (void)hipSetDevice(g->devices[0]);
+  if (hipMemcpyAsync(gathered.data(), g->recv[0].p, words * 8 * D, hipMemcpyDeviceToHost, g->ctx[0]->stream) !=
+      hipSuccess)
+    return gfail(g, BV_E_LAUNCH, "d2h gathered bits");
+
+  // per-device results (digests, statuses) straight into the caller's arrays
+  for (int d = 0; d < D; d++) {
+    bv_ctx *c = g->ctx[d];
+    std::lock_guard<std::mutex> clk(c->mu);
+    (void)hipSetDevice(c->device);
+    if (hipEventRecord(c->ev_done, c->stream) != hipSuccess) return gfail(g, BV_E_LAUNCH, "event");
+    bv_result sr = {};
+    sr.msg_hash = res->msg_hash ? res->msg_hash + 32 * mlo[d] : nullptr;
+    sr.status = res->status ? res->status + bounds[d] : nullptr;
+    rc = bv_host_finish(c, &sb[d], &sr, &calls[d], false);
+    if (rc != BV_OK) return gfail(g, rc, c->err);
+  }
+  // merge the shard-local words into the global bitmask
+  if (res->accept_bits && b->n_items) {
+    const uint64_t W = (b->n_items + 63) / 64;
+    memset(res->accept_bits, 0, W * 8);
+    for (int d = 0; d < D; d++) {
+      const uint64_t a = bounds[d], n = bounds[d + 1] - a;
+      const uint64_t *src = gathered.data() + (uint64_t)d * words;
+      for (uint64_t w = 0; w < (n + 63) / 64; w++) {
+        uint64_t v = src[w];
+        const uint64_t valid = std::min<uint64_t>(64, n - 64 * w);
+        if (valid < 64) v &= (1ull << valid) - 1;
+        const uint64_t bit = a + 64 * w, q = bit / 64, s = bit % 64;
+        res->accept_bits[q] |= v << s;
+        if (s && q + 1 < W) res->accept_bits[q + 1] |= v >> (64 - s);
+      }
+    }
+  }
+  return BV_OK;
+}

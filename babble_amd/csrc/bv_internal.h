@@ -1,0 +1,114 @@
+// bv_internal.h — ctx layout and internal entry points shared by bv_api.cpp
+// (single device) and bv_group.cpp (multi-device group).  Not installed.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/babbleverify.h"
+#include "geometry.h"
+
+#define KS_OK 0  // k_key_decode statuses (verify_core.h)
+
+namespace bvk {
+hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
+hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
+hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
+                        uint32_t *, uint32_t *);
+hipError_t build_kc(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *, uint32_t *,
+                    const uint64_t *);
+size_t kc_pscr_bytes();
+hipError_t sinv(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *);
+hipError_t verify_g(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
+                    const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
+                    const uint32_t *, uint32_t *);
+hipError_t verify_q(hipStream_t, int, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
+                    const uint8_t *, const uint32_t *, const uint32_t *, const uint64_t *, const uint32_t *,
+                    uint8_t *, uint64_t *);
+hipError_t verify_generic(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
+                          const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
+                          const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
+}  // namespace bvk
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes);
+  void release();
+  template <class T>
+  T *as() const {
+    return (T *)p;
+  }
+};
+
+struct PinnedBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes);
+  void release();
+};
+
+struct CopyPool;
+
+// timing / ordering events (see bv_read_timing)
+enum {
+  E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_SINV,
+  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_COUNT
+};
+
+struct KcSlot {
+  std::string bytes;      // raw pubkey bytes (the cache key)
+  uint8_t status = 0;     // k_key_decode status
+  void *table = nullptr;  // KC table (valid keys only)
+  uint64_t last_use = 0;
+  bool free = false;
+};
+
+struct bv_ctx {
+  int device = 0;
+  uint32_t flags = 0;
+  hipStream_t stream = nullptr;   // main
+  hipStream_t kstream = nullptr;  // per-batch key tables (high priority)
+  hipStream_t sstream = nullptr;  // batched s^-1
+  hipStream_t cstream = nullptr;  // host-entry copies
+  std::mutex mu;
+  std::string err;
+  const uint32_t *g_table = nullptr;  // process-wide, per device (gtable_acquire)
+  CopyPool *pool = nullptr;
+  // host-entry staging: one layout in pinned memory and in HBM
+  PinnedBuf pin_in, pin_out, pin_small;
+  DevBuf d_in;
+  // work buffers
+  DevBuf digests, kstatus, kxy, bases_jac, key_sub, key_pscr, key_table, scratch, u12, rg, status, bits;
+  hipEvent_t ev[E_COUNT] = {};
+  std::vector<hipEvent_t> chunk_ev;
+  hipEvent_t ev_done = nullptr;  // end of the last call's device work
+  bool has_done = false;
+  bool table_mode = false;
+  int key_w = 0;  // 8, 12 or 20 (KC) in table mode
+  bv_timing timing = {};
+  // key cache (BV_F_KEY_CACHE)
+  std::unordered_map<std::string, int> kc_index;
+  std::vector<KcSlot> kc_slots;
+  uint64_t kc_clock = 0, kc_bytes = 0, kc_budget = 0;
+  DevBuf kc_tabs, kc_kst, kc_kxy, kc_btabs;
+};
+
+// one in-flight host-entry call (bv_host_launch -> bv_host_finish)
+struct bv_host_call {
+  std::chrono::steady_clock::time_point t0;
+  uint8_t *pout = nullptr;
+  size_t o_st = 0, o_bits = 0;
+};
+
+int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess);
+int bv_validate_host_batch(bv_ctx *ctx, const bv_batch *b);
+int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
+                  hipStream_t st, bool hashed, bool kc);
+int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call);
+int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call *call, bool bits_out);
+void bv_read_timing(bv_ctx *ctx);

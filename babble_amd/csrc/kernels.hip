@@ -276,12 +276,88 @@ __global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, const uint32
                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
                                                   const uint32_t *__restrict__ u12,
                                                   const uint32_t *__restrict__ key_table,
+                                                  const uint64_t *__restrict__ key_tabs,
                                                   const uint32_t *__restrict__ rg, uint8_t *__restrict__ status,
                                                   uint64_t *__restrict__ bits) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t st = BV_REJECT;
-  if (i < n_items) st = verify_item_q<W, NWIN>(i, n_items, item_key, r_be, s_be, pre, kstatus, u12, key_table, rg);
+  if (i < n_items)
+    st = verify_item_q<W, NWIN>(i, n_items, item_key, r_be, s_be, pre, kstatus, u12, key_table, key_tabs, rg);
   write_status(i, n_items, st, status, bits);
+}
+
+// Key-cache (KC) table windows from the 10-bit sub-tables: block (c, key)
+// holds slots s = BV_KCPAIR_ENT c' + 256 e + t (e < 16) of window
+// j = c / (ENT / BV_KCPAIR_ENT), c' = c mod that; digit k12_digit(s) (signed
+// windows: slot 0 builds digit ENT, stored in window j+1's slot 0).  A wave
+// reads 64 consecutive S_lo points and one S_hi point from L2 (the key's
+// sub-tables are 0.9 MB).  One field inversion per block (Montgomery's trick
+// over 4096 chord denominators, prefix products in `pscr`), then each entry
+// and its phi image are stored.  Blocks beyond the top window's live digits
+// (<= 2^(128 - W j) + 1) return at once.  `tabs[b]` is key b's table.
+template <int W, int L, int NWIN>
+__global__ void __launch_bounds__(256) k_table_pair_kc(const uint32_t *__restrict__ sub,
+                                                       const uint8_t *__restrict__ bstatus,
+                                                       const uint64_t *__restrict__ tabs, uint4 *__restrict__ pscr) {
+  constexpr uint32_t ENT = 1u << (W - 1), NS = 1u << L, E = BV_KCPAIR_ENT / 256u, CH = ENT / BV_KCPAIR_ENT;
+  constexpr uint64_t half_u32 = ((uint64_t)NWIN * ENT + 1) * BV_ENTRY_U32;
+  const uint32_t b = blockIdx.y, j = blockIdx.x / CH, c = blockIdx.x % CH, t = threadIdx.x;
+  if (bstatus && bstatus[b] != KS_OK) return;
+  const int live_bits = 128 - W * (int)j;
+  if (live_bits < W - 1 && (uint64_t)BV_KCPAIR_ENT * c > (1ull << live_bits) + 1) return;  // uniform per block
+  const uint32_t *s_lo = sub + ((uint64_t)b * 2 * NWIN + 2 * j) * NS * BV_ENTRY_U32;
+  const uint32_t *s_hi = s_lo + (uint64_t)NS * BV_ENTRY_U32;
+  __shared__ fe sPre[256], sSuf[256], sInv;
+  uint4 *ps = pscr + ((uint64_t)b * gridDim.x + blockIdx.x) * E * 2 * 256 + t;
+  fe acc;
+  fe_set(acc, 1);
+#pragma unroll 1
+  for (uint32_t e = 0; e < E; e++) {
+    const uint32_t d = k12_digit(BV_KCPAIR_ENT * c + 256u * e + t, ENT), lo = d & (NS - 1), hi = d >> L;
+    fe x1, y1, x2, y2, H;
+    pair_load(s_lo, s_hi, lo, hi, x1, y1, x2, y2);
+    pair_denominator(H, pair_kind(lo, hi), x1, x2);
+    ps[(2 * e) * 256] = make_uint4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
+    ps[(2 * e + 1) * 256] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
+    fe_mul(acc, acc, H);
+  }
+  sPre[t] = acc;
+  sSuf[t] = acc;
+  __syncthreads();
+  for (uint32_t s = 1; s < 256; s <<= 1) {
+    fe p = sPre[t], q = sSuf[t];
+    if (t >= s) fe_mul(p, p, sPre[t - s]);
+    if (t + s < 256) fe_mul(q, q, sSuf[t + s]);
+    __syncthreads();
+    sPre[t] = p;
+    sSuf[t] = q;
+    __syncthreads();
+  }
+  if (t == 0) {
+    fe x;
+    fe_inv_var(x, sPre[255]);
+    sInv = x;
+  }
+  __syncthreads();
+  fe q = sInv;
+  if (t > 0) fe_mul(q, q, sPre[t - 1]);
+  if (t < 255) fe_mul(q, q, sSuf[t + 1]);
+  uint32_t *base = (uint32_t *)tabs[b] + (uint64_t)j * ENT * BV_ENTRY_U32;
+#pragma unroll 1
+  for (int e = (int)E - 1; e >= 0; e--) {
+    const uint32_t d = k12_digit(BV_KCPAIR_ENT * c + 256u * e + t, ENT), lo = d & (NS - 1), hi = d >> L;
+    const int kind = pair_kind(lo, hi);
+    fe x1, y1, x2, y2, H, Hinv, pre;
+    pair_load(s_lo, s_hi, lo, hi, x1, y1, x2, y2);
+    pair_denominator(H, kind, x1, x2);
+    const uint4 p0 = ps[(2 * e) * 256], p1 = ps[(2 * e + 1) * 256];
+    pre.v[0] = p0.x; pre.v[1] = p0.y; pre.v[2] = p0.z; pre.v[3] = p0.w;
+    pre.v[4] = p1.x; pre.v[5] = p1.y; pre.v[6] = p1.z; pre.v[7] = p1.w;
+    fe_mul(Hinv, q, pre);
+    fe_mul(q, q, H);
+    uint32_t *entry = base + (uint64_t)d * BV_ENTRY_U32;
+    pair_store(entry, entry + half_u32, kind, x1, y1, x2, y2, Hinv);
+  }
 }
 
 __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, const uint32_t *__restrict__ item_key,
@@ -381,16 +457,44 @@ hipError_t verify_g(hipStream_t st, uint64_t n, const uint32_t *item_key, const 
   return hipGetLastError();
 }
 
+// kw = 8 / 12: contiguous per-batch tables in key_table; kw = 20: the key
+// cache (KC), table base address per batch key in key_tabs.
 hipError_t verify_q(hipStream_t st, int kw, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
                     const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst, const uint32_t *u12,
-                    const uint32_t *key_table, const uint32_t *rg, uint8_t *status, uint64_t *bits) {
+                    const uint32_t *key_table, const uint64_t *key_tabs, const uint32_t *rg, uint8_t *status,
+                    uint64_t *bits) {
   if (n == 0) return hipSuccess;
   if (kw == 8)
     hipLaunchKernelGGL((k_verify_q<BV_KW, BV_KNWIN>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre,
-                       kst, u12, key_table, rg, status, bits);
-  else
+                       kst, u12, key_table, nullptr, rg, status, bits);
+  else if (kw == 12)
     hipLaunchKernelGGL((k_verify_q<BV_K12W, BV_K12NWIN>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be,
-                       pre, kst, u12, key_table, rg, status, bits);
+                       pre, kst, u12, key_table, nullptr, rg, status, bits);
+  else
+    hipLaunchKernelGGL((k_verify_q<BV_KCW, BV_KCNWIN>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be,
+                       pre, kst, u12, nullptr, key_tabs, rg, status, bits);
+  return hipGetLastError();
+}
+
+// Key-cache tables for n keys (decoded affine points kxy, statuses kst):
+// bases 2^(10 k) Q (k < 14), the 10-bit sub-tables into `sub`
+// (n * BV_KCSUB_U32 words), then every window's chord sums + phi half into
+// tabs[b] (BV_KCTABLE_U32 words each).  `pscr`: n * kc_pscr_bytes() bytes.
+size_t kc_pscr_bytes() {
+  return (size_t)BV_KCNWIN * (BV_KCENT / BV_KCPAIR_ENT) * BV_KCPAIR_ENT * 32;
+}
+hipError_t build_kc(hipStream_t st, uint32_t n, const uint32_t *kxy, const uint8_t *kst, uint32_t *bases_jac,
+                    uint32_t *sub, uint32_t *pscr, const uint64_t *tabs) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_table_bases, grid1(n, 64), dim3(64), 0, st, n, kxy, kst, bases_jac, BV_KCL, BV_KCNSUB);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_table_fill<BV_KCL, BV_KCNSUB, false>), dim3(BV_KCNSUB * ((1u << BV_KCL) / 256u), n),
+                     dim3(256), 0, st, bases_jac, kst, sub);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_table_pair_kc<BV_KCW, BV_KCL, BV_KCNWIN>),
+                     dim3(BV_KCNWIN * (BV_KCENT / BV_KCPAIR_ENT), n), dim3(256), 0, st, sub, kst, tabs, (uint4 *)pscr);
   return hipGetLastError();
 }
 

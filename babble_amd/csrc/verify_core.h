@@ -545,12 +545,17 @@ DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bo
 
 // Phase 2: R = R_G + k1 Q + k2 phi(Q) with the key's two half-tables;
 // final check -> status.
+// key_tabs != null (key cache): per-batch-key table base addresses, else
+// the tables are contiguous in key_table (per-batch K8 / K12 build).
 template <int W, int NWIN>
 DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
                           const uint32_t *s_be, const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12,
-                          const uint32_t *key_table, const uint32_t *rg) {
-  constexpr bool SIGNED = W == BV_K12W;
-  constexpr uint64_t half = SIGNED ? BV_K12HALF_U32 : (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
+                          const uint32_t *key_table, const uint64_t *key_tabs, const uint32_t *rg) {
+  constexpr bool SIGNED = W != BV_KW;
+  constexpr uint64_t half =
+      SIGNED ? ((uint64_t)NWIN * (1ull << (W - 1)) + 1) * BV_ENTRY_U32 : (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
+  static_assert(W != BV_K12W || half == BV_K12HALF_U32, "K12 geometry");
+  static_assert(W != BV_KCW || half == BV_KCHALF_U32, "KC geometry");
   fe r;
   const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
   if (st != 0xFF) return st;
@@ -559,7 +564,8 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
   gej R;
   bool inf;
   rg_load(rg, n, i, R, inf);
-  const uint32_t *tab = key_table + (uint64_t)item_key[i] * 2 * half;
+  const uint32_t *tab = key_tabs ? (const uint32_t *)key_tabs[item_key[i]]
+                                 : key_table + (uint64_t)item_key[i] * 2 * half;
   // One loop body for both GLV halves (one inlined copy of the point
   // addition: smaller code, fewer live registers than two calls).
 #pragma unroll 1

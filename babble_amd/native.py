@@ -23,7 +23,7 @@ REJECT, ACCEPT, REJECT_ERR, REF_PANIC = 0, 1, 2, 3
 SC_OK, SC_NIL, SC_NONPOS, SC_GE_N = 0, 1, 2, 3
 PRE_PARTS_BAD = 0x80
 F_DEFAULT = 0
-ABI_VERSION = 2
+ABI_VERSION = 3
 F_KEY_CACHE = 1
 F_K8 = 2
 
@@ -31,7 +31,8 @@ F_K8 = 2
 EXPORTS = (
     "bv_abi_version", "bv_create", "bv_destroy", "bv_last_error", "bv_verify_batch",
     "bv_verify_batch_device", "bv_sha256_batch", "bv_get_timing", "bv_decode_signature",
-    "bv_hex_decode",
+    "bv_hex_decode", "bv_group_create", "bv_group_destroy", "bv_group_last_error", "bv_group_verify_batch",
+    "bv_group_get_timing", "bv_plan_shards", "bv_sync",
 )
 
 
@@ -70,7 +71,11 @@ class BvTiming(ctypes.Structure):
         ("ms_verify", ctypes.c_float),
         ("ms_h2d", ctypes.c_float),
         ("ms_d2h", ctypes.c_float),
+        ("ms_host", ctypes.c_float),
         ("key_path", ctypes.c_uint32),
+        ("kc_hits", ctypes.c_uint32),
+        ("kc_builds", ctypes.c_uint32),
+        ("kc_keys", ctypes.c_uint32),
     ]
 
 
@@ -119,6 +124,19 @@ def lib() -> ctypes.CDLL:
     L.bv_decode_signature.restype = ctypes.c_uint8
     L.bv_hex_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, P]
     L.bv_hex_decode.restype = ctypes.c_int64
+    L.bv_group_create.argtypes = [ctypes.POINTER(P), ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_uint32]
+    L.bv_group_create.restype = ctypes.c_int
+    L.bv_group_destroy.argtypes = [P]
+    L.bv_group_last_error.argtypes = [P]
+    L.bv_group_last_error.restype = ctypes.c_char_p
+    L.bv_group_verify_batch.argtypes = [P, ctypes.POINTER(BvBatch), ctypes.POINTER(BvResult)]
+    L.bv_group_verify_batch.restype = ctypes.c_int
+    L.bv_group_get_timing.argtypes = [P, ctypes.c_int, ctypes.POINTER(BvTiming)]
+    L.bv_group_get_timing.restype = ctypes.c_int
+    L.bv_sync.argtypes = [P]
+    L.bv_sync.restype = ctypes.c_int
+    L.bv_plan_shards.argtypes = [ctypes.POINTER(BvBatch), ctypes.c_int, P]
+    L.bv_plan_shards.restype = ctypes.c_int
     if L.bv_abi_version() != ABI_VERSION:
         raise BvError(BV_E_ARGS, "ABI version mismatch")
     _lib = L

@@ -73,6 +73,10 @@ class DeviceBatch:
         b.s_be = self.s_be.data_ptr()
         b.pre = self.pre.data_ptr() if self.pre is not None else 0
         self.cbatch = b
+        # the copies above run on torch's stream; the library may run on its
+        # own non-blocking stream, so they must be complete before any call
+        torch.cuda.current_stream(dev).synchronize()
+        self._pending = None
         r = native.BvResult()
         r.msg_hash = self.msg_hash.data_ptr()
         r.status = self.status.data_ptr()
@@ -80,6 +84,12 @@ class DeviceBatch:
         self.cresult = r
 
     def result(self) -> VerifyResult:
+        # .cpu() runs on torch's current stream: ordered after a verify that
+        # was enqueued on it; an async verify on the library's own stream is
+        # waited for explicitly
+        if self._pending is not None:
+            self._pending.sync()
+            self._pending = None
         return VerifyResult(
             self.msg_hash.cpu().numpy()[: self.n_msgs * 32].reshape(self.n_msgs, 32),
             self.status.cpu().numpy()[: self.n_items],
@@ -113,26 +123,8 @@ class Verifier:
             raise native.BvError(rc, self._L.bv_last_error(self._ctx).decode(errors="replace"))
 
     def verify(self, b: PackedBatch) -> VerifyResult:
-        keep = []
-
-        def c(a, dt):
-            a = np.ascontiguousarray(a, dtype=dt)
-            keep.append(a)
-            return a
-
-        cb = native.BvBatch()
-        cb.n_msgs = b.n_msgs
-        cb.msg_bytes = _p(c(b.msg_bytes, np.uint8))
-        cb.msg_off = _p(c(b.msg_off, np.uint64))
-        cb.n_keys = b.n_keys
-        cb.key_bytes = _p(c(b.key_bytes, np.uint8))
-        cb.key_off = _p(c(b.key_off, np.uint64))
-        cb.n_items = b.n_items
-        cb.item_msg = _p(c(b.item_msg, np.uint32))
-        cb.item_key = _p(c(b.item_key, np.uint32))
-        cb.r_be = _p(c(b.r_be, np.uint8))
-        cb.s_be = _p(c(b.s_be, np.uint8))
-        cb.pre = _p(c(b.pre, np.uint8)) if b.pre is not None else 0
+        keep: list = []
+        cb = _cbatch(b, keep)
         h = np.zeros((max(b.n_msgs, 1), 32), np.uint8)
         st = np.zeros(max(b.n_items, 1), np.uint8)
         bits = np.zeros(max((b.n_items + 63) // 64, 1), np.uint64)
@@ -144,8 +136,24 @@ class Verifier:
         return DeviceBatch(b, self.device)
 
     def verify_device(self, d: DeviceBatch, stream: Optional[int] = None, sync: bool = True) -> None:
+        """bv_verify_batch_device on `stream` (a hipStream_t handle).  The
+        default is PyTorch's current stream on this device, so the work is
+        ordered after the tensor copies that filled `d` and before any later
+        torch op (DeviceBatch.result()'s copies) without extra syncs."""
+        if stream is None:
+            import torch
+
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        # (handle 0 = torch's legacy default stream: the library then uses its
+        # own stream; DeviceBatch synchronised its copies at construction and
+        # result() waits for an async call through bv_sync)
         self._check(self._L.bv_verify_batch_device(self._ctx, ctypes.byref(d.cbatch), ctypes.byref(d.cresult),
                                                    stream or 0, 0 if sync else 1))
+        d._pending = None if sync else self
+
+    def sync(self) -> None:
+        """bv_sync: wait for this ctx's last (async) call."""
+        self._check(self._L.bv_sync(self._ctx))
 
     def sha256(self, msgs: Sequence[bytes]) -> list:
         msgs = [bytes(m) for m in msgs]
@@ -161,4 +169,82 @@ class Verifier:
     def timing(self) -> dict:
         t = native.BvTiming()
         self._check(self._L.bv_get_timing(self._ctx, ctypes.byref(t)))
+        return {k: getattr(t, k) for k, _ in native.BvTiming._fields_}
+
+
+def _cbatch(b: PackedBatch, keep: list) -> "native.BvBatch":
+    def c(a, dt):
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a
+
+    cb = native.BvBatch()
+    cb.n_msgs = b.n_msgs
+    cb.msg_bytes = _p(c(b.msg_bytes, np.uint8))
+    cb.msg_off = _p(c(b.msg_off, np.uint64))
+    cb.n_keys = b.n_keys
+    cb.key_bytes = _p(c(b.key_bytes, np.uint8))
+    cb.key_off = _p(c(b.key_off, np.uint64))
+    cb.n_items = b.n_items
+    cb.item_msg = _p(c(b.item_msg, np.uint32))
+    cb.item_key = _p(c(b.item_key, np.uint32))
+    cb.r_be = _p(c(b.r_be, np.uint8))
+    cb.s_be = _p(c(b.s_be, np.uint8))
+    cb.pre = _p(c(b.pre, np.uint8)) if b.pre is not None else 0
+    return cb
+
+
+def plan_shards(b: PackedBatch, n_shards: int) -> np.ndarray:
+    """bv_plan_shards: the item bounds bv_group_verify_batch uses (host only)."""
+    keep: list = []
+    cb = _cbatch(b, keep)
+    out = np.zeros(n_shards + 1, np.uint64)
+    rc = native.lib().bv_plan_shards(ctypes.byref(cb), n_shards, out.ctypes.data)
+    if rc != native.BV_OK:
+        raise native.BvError(rc, "bv_plan_shards")
+    return out
+
+
+class Group:
+    """bv_group: one verifier over several devices of this process; items
+    sharded message-aligned, accept bitmasks all-gathered over RCCL."""
+
+    def __init__(self, devices: Sequence[int], flags: int = native.F_DEFAULT):
+        self._L = native.lib()
+        self.devices = list(devices)
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        g = ctypes.c_void_p()
+        rc = self._L.bv_group_create(ctypes.byref(g), arr, len(self.devices), flags)
+        if rc != native.BV_OK:
+            raise native.BvError(rc, "bv_group_create failed")
+        self._g = g
+
+    def close(self):
+        if self._g:
+            self._L.bv_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def verify(self, b: PackedBatch) -> VerifyResult:
+        keep: list = []
+        cb = _cbatch(b, keep)
+        h = np.zeros((max(b.n_msgs, 1), 32), np.uint8)
+        st = np.zeros(max(b.n_items, 1), np.uint8)
+        bits = np.zeros(max((b.n_items + 63) // 64, 1), np.uint64)
+        res = native.BvResult(h.ctypes.data, st.ctypes.data, bits.ctypes.data)
+        rc = self._L.bv_group_verify_batch(self._g, ctypes.byref(cb), ctypes.byref(res))
+        if rc != native.BV_OK:
+            raise native.BvError(rc, self._L.bv_group_last_error(self._g).decode(errors="replace"))
+        return VerifyResult(h[: b.n_msgs], st[: b.n_items], bits[: (b.n_items + 63) // 64])
+
+    def timing(self, i: int = 0) -> dict:
+        t = native.BvTiming()
+        rc = self._L.bv_group_get_timing(self._g, i, ctypes.byref(t))
+        if rc != native.BV_OK:
+            raise native.BvError(rc, "bv_group_get_timing")
         return {k: getattr(t, k) for k, _ in native.BvTiming._fields_}

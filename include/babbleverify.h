@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define BV_ABI_VERSION 2
+#define BV_ABI_VERSION 3
 
 /* Return codes (per-item outcomes are never errors; they go to status[]). */
 #define BV_OK 0
@@ -60,12 +60,19 @@ extern "C" {
 #define BV_PRE_PARTS_BAD 0x80
 #define BV_PRE(rc, sc) ((uint8_t)((rc) | ((sc) << 2)))
 
-/* Flags for bv_create. */
+/* Flags for bv_create (any other bit is BV_E_ARGS). */
 #define BV_F_DEFAULT 0u
-#define BV_F_KEY_CACHE 1u /* keep per-key tables across calls (validator sets
-                             are stable); off by default                       */
-#define BV_F_K8 2u        /* never use the 12-bit key tables (5.5 MiB per key);
-                             8-bit tables only (512 KiB per key)               */
+#define BV_F_KEY_CACHE 1u /* keep per-key tables in HBM across calls, keyed by
+                             the raw pubkey bytes (validator sets are stable,
+                             peers/peer_set.go): 20-bit signed-window GLV
+                             tables, 470 MB per valid key, built on first use,
+                             LRU-evicted past the cache budget (env
+                             BV_KEY_CACHE_GB, default 64).  Malformed keys are
+                             never given a table.  Off by default: tables are
+                             then rebuilt for every batch.                     */
+#define BV_F_K8 2u        /* per-batch tables: never use the 12-bit tables
+                             (2.75 MiB per key); 8-bit only (512 KiB per key) */
+#define BV_F_KNOWN (BV_F_KEY_CACHE | BV_F_K8)
 
 typedef struct bv_ctx bv_ctx;
 
@@ -102,9 +109,16 @@ typedef struct {
   float ms_scalar;   /* k_sinv: batched s^-1 (own stream, from batch start)     */
   float ms_verify_g; /* k_verify_g: u1, u2 + GLV split, u1 G from the G table   */
   float ms_verify;   /* k_verify_q (+ u2 Q, decision, bits) or k_verify_generic */
-  float ms_h2d;      /* host -> device staging (host-buffer entry point only)   */
-  float ms_d2h;      /* device -> host results                                  */
-  uint32_t key_path; /* 0: per-lane generic path; 8 / 12: K8 / K12 key tables  */
+  float ms_h2d;      /* host -> device staging (host-buffer entry point only):
+                        call start -> last input byte in HBM                    */
+  float ms_d2h;      /* device -> host results after the last kernel            */
+  float ms_host;     /* wall clock of the whole call on the host (host entry
+                        point: staging, PCIe, kernels, copy-out)                */
+  uint32_t key_path; /* 0: per-lane generic path; 8 / 12: per-batch K8 / K12
+                        key tables; 20: key-cache (KC) tables                   */
+  uint32_t kc_hits;   /* batch keys found in the key cache                      */
+  uint32_t kc_builds; /* key tables built into the cache by this call           */
+  uint32_t kc_keys;   /* keys held by the cache after the call                  */
 } bv_timing;
 
 int bv_abi_version(void);
@@ -123,6 +137,32 @@ int bv_verify_batch(bv_ctx *ctx, const bv_batch *batch, bv_result *result);
  * `async` != 0, else after it completes. */
 int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresult,
                            void *stream, int async);
+/* Calls on one ctx are ordered on the device whatever their streams: a call's
+ * work starts after the previous call's work has finished (the ctx's work
+ * buffers are shared).  bv_sync waits for the last call's work (after an
+ * async call) and updates bv_get_timing. */
+int bv_sync(bv_ctx *ctx);
+
+/* Multi-GPU: one verifier over several devices of this process (one bv_ctx
+ * per device, the caller's device ordinals).  bv_group_verify_batch shards
+ * the items into contiguous ranges that never split the items of one
+ * message (a BlockBody's signatures stay on one device), balanced by item
+ * count (bv_plan_shards); each device stages, hashes and verifies its shard
+ * (messages of the shard only), and the per-device accept bitmasks come back
+ * through ONE RCCL all-gather (ncclAllGather over xGMI, librccl loaded at
+ * bv_group_create) into device 0, from which the merged bitmask is copied
+ * once.  Digests and statuses come back per device.  Errors: BV_E_COMM if
+ * RCCL is unavailable or a collective fails. */
+typedef struct bv_group bv_group;
+int bv_group_create(bv_group **out, const int *devices, int n_devices, uint32_t flags);
+void bv_group_destroy(bv_group *g);
+const char *bv_group_last_error(const bv_group *g);
+int bv_group_verify_batch(bv_group *g, const bv_batch *batch, bv_result *result);
+/* Timing of the last group call on device slot `i` (its ctx's bv_timing). */
+int bv_group_get_timing(const bv_group *g, int i, bv_timing *out);
+/* Host helper (no device): the shard plan bv_group_verify_batch uses.
+ * Writes n_shards + 1 item bounds (bounds[0] = 0, bounds[n] = n_items). */
+int bv_plan_shards(const bv_batch *batch, int n_shards, uint64_t *bounds);
 
 /* SHA-256 of n messages (host buffers) -> 32*n bytes. */
 int bv_sha256_batch(bv_ctx *ctx, uint64_t n_msgs, const uint8_t *msg_bytes,

@@ -89,6 +89,56 @@ def scalar_base_mult(k: int):
     return int.from_bytes(out.raw[:32], "big"), int.from_bytes(out.raw[32:], "big")
 
 
+def _cbatch(arrs: dict, keep: list) -> _Batch:
+    def ptr(a):
+        a = np.ascontiguousarray(a)
+        keep.append(a)
+        return a.ctypes.data if a.size else 0
+
+    b = _Batch()
+    b.n_msgs = len(arrs["msg_off"]) - 1
+    b.msg_bytes = ptr(arrs["msg_bytes"])
+    b.msg_off = ptr(arrs["msg_off"].astype(np.uint64))
+    b.n_keys = len(arrs["key_off"]) - 1
+    b.key_bytes = ptr(arrs["key_bytes"])
+    b.key_off = ptr(arrs["key_off"].astype(np.uint64))
+    b.n_items = len(arrs["item_msg"])
+    b.item_msg = ptr(arrs["item_msg"].astype(np.uint32))
+    b.item_key = ptr(arrs["item_key"].astype(np.uint32))
+    b.r_be = ptr(arrs["r_be"])
+    b.s_be = ptr(arrs["s_be"])
+    b.pre = ptr(arrs["pre"]) if arrs.get("pre") is not None else 0
+    return b
+
+
+OSSL_SKIP = 0xFE
+_ossl = None
+
+
+def ossl_lib():
+    global _ossl
+    if _ossl is None:
+        path = os.path.join(_HERE, "_build", "libosslref.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.ossl_verify_batch.argtypes = [ctypes.POINTER(_Batch), ctypes.c_void_p, ctypes.c_int]
+        L.ossl_verify_batch.restype = ctypes.c_int
+        _ossl = L
+    return _ossl
+
+
+def ossl_verify_batch(arrs: dict, n_threads: int = 0) -> np.ndarray:
+    """OpenSSL libcrypto over a packed batch (oracle/openssl_ref.c): per item
+    SHA-256 + SEC1 decode + ECDSA_do_verify; 1 / 0 for well-formed items,
+    OSSL_SKIP for items OpenSSL is no oracle for."""
+    keep: list = []
+    b = _cbatch(arrs, keep)
+    st = np.zeros(max(b.n_items, 1), np.uint8)
+    ossl_lib().ossl_verify_batch(ctypes.byref(b), st.ctypes.data, n_threads or default_threads())
+    return st[: b.n_items]
+
+
 def verify_batch(arrs: dict, n_threads: int = 0):
     """Run the oracle over a packed batch (dict of numpy arrays, see
     babble_amd.batch.pack layout).  Returns (msg_hash[n_msgs,32], status[n], bits)."""

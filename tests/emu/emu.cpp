@@ -227,8 +227,8 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
                    verify_item_g(i, n_items, b->item_key, r, s, b->pre, kst, b->item_msg, dig, scratch, u12, gt, rg);
                  });
     parallel_for(n_items, n_threads, [&](uint64_t i) {
-      st[i] = mode == 2 ? verify_item_q<BV_K12W, BV_K12NWIN>(i, n_items, b->item_key, r, s, b->pre, kst, u12, kt, rg)
-                        : verify_item_q<BV_KW, BV_KNWIN>(i, n_items, b->item_key, r, s, b->pre, kst, u12, kt, rg);
+      st[i] = mode == 2 ? verify_item_q<BV_K12W, BV_K12NWIN>(i, n_items, b->item_key, r, s, b->pre, kst, u12, kt, nullptr, rg)
+                        : verify_item_q<BV_KW, BV_KNWIN>(i, n_items, b->item_key, r, s, b->pre, kst, u12, kt, nullptr, rg);
     });
   } else {
     parallel_for(n_items, n_threads, [&](uint64_t i) {

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_code_object():
     L = native.lib()
-    assert L.bv_abi_version() == native.ABI_VERSION == 2
+    assert L.bv_abi_version() == native.ABI_VERSION == 3
     # the library carries gfx950 device code (offload bundle entry name)
     blob = open(native.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
@@ -59,3 +59,50 @@ def test_null_args():
     assert L.bv_verify_batch_device(None, None, None, None, 0) == native.BV_E_ARGS
     assert L.bv_sha256_batch(None, 0, None, None, None) == native.BV_E_ARGS
     assert L.bv_get_timing(None, None) == native.BV_E_ARGS
+
+
+def test_unknown_flags_rejected_before_any_device_call():
+    ctx = ctypes.c_void_p()
+    assert native.lib().bv_create(ctypes.byref(ctx), 0, 0x80) == native.BV_E_ARGS and not ctx.value
+    g = ctypes.c_void_p()
+    devs = (ctypes.c_int * 2)(0, 0)  # duplicate device
+    assert native.lib().bv_group_create(ctypes.byref(g), devs, 2, 0) == native.BV_E_ARGS
+
+
+def test_group_null_args():
+    L = native.lib()
+    assert L.bv_group_verify_batch(None, None, None) == native.BV_E_ARGS
+    assert L.bv_sync(None) == native.BV_E_ARGS
+    assert L.bv_plan_shards(None, 2, None) == native.BV_E_ARGS
+
+
+def test_plan_shards_balanced_and_message_aligned():
+    """bv_plan_shards (the group's sharding): contiguous, covering, balanced,
+    and never splitting the items of one message (C5: a block's 100
+    signatures stay on one device)."""
+    import numpy as np
+
+    from babble_amd.batch import PackedBatch
+    from babble_amd.verifier import plan_shards
+
+    def batch(item_msg):
+        n = len(item_msg)
+        nm = int(item_msg.max()) + 1 if n else 0
+        return PackedBatch(np.zeros(0, np.uint8), np.zeros(nm + 1, np.uint64), np.zeros(0, np.uint8),
+                           np.zeros(2, np.uint64), np.asarray(item_msg, np.uint32), np.zeros(n, np.uint32),
+                           np.zeros((n, 32), np.uint8), np.zeros((n, 32), np.uint8), None)
+
+    # events: one item per message -> exact balance
+    b = batch(np.arange(1000))
+    assert plan_shards(b, 8).tolist() == [0, 125, 250, 375, 500, 625, 750, 875, 1000]
+    # blocks: 100 items per message, 10^4 blocks over 8 devices
+    im = np.repeat(np.arange(10_000), 100)
+    bd = plan_shards(batch(im), 8)
+    assert bd[0] == 0 and bd[-1] == im.size and np.all(np.diff(bd.astype(np.int64)) >= 0)
+    for c in bd[1:-1]:
+        assert im[c] != im[c - 1]  # a cut never splits a block
+    sizes = np.diff(bd.astype(np.int64))
+    assert sizes.max() - sizes.min() <= 100
+    # ragged: more shards than messages, empty batch
+    assert plan_shards(batch(np.repeat([0, 1], 5)), 4).tolist() == [0, 5, 5, 10, 10]
+    assert plan_shards(batch(np.zeros(0, np.int64)), 3).tolist() == [0, 0, 0, 0]

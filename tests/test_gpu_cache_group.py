@@ -1,0 +1,184 @@
+"""GPU parity for the key cache (BV_F_KEY_CACHE), the pinned host entry
+point, call ordering across streams / async calls, the multi-device group
+(bv_group_*, RCCL all-gather) and C5 at its full size — all through the C
+ABI against the C oracle (bit-exact statuses, digests and accept bits)."""
+import os
+
+import numpy as np
+import pytest
+
+from babble_amd import native, synth
+from oracle import coracle
+from oracle import gosemantics as gs
+
+pytestmark = pytest.mark.gpu
+
+MIX = dict(rflip=20000, sflip=20000, body=10000, highs=10000, range=8000, fmt=8000, key=12000)
+
+
+def oracle_check(res, b):
+    h, st, bits = coracle.verify_batch(b.as_dict())
+    assert np.array_equal(res.msg_hash, h), "digests differ from oracle"
+    bad = np.flatnonzero(res.status != st)
+    assert bad.size == 0, f"{bad.size} statuses differ, first {bad[:8]}: gpu {res.status[bad[:8]]} oracle {st[bad[:8]]}"
+    assert np.array_equal(res.accept_bits, bits)
+    return st
+
+
+@pytest.fixture(scope="module")
+def cached():
+    from babble_amd.verifier import Verifier
+
+    v = Verifier(device=0, flags=native.F_KEY_CACHE)
+    yield v
+    v.close()
+
+
+@pytest.fixture(scope="module")
+def verifier_default():
+    from babble_amd.verifier import Verifier
+
+    v = Verifier(device=0)
+    yield v
+    v.close()
+
+
+def test_key_cache_cold_then_warm(cached):
+    """First call builds a KC table per valid key (malformed keys get none);
+    the second call hits every key and builds nothing; both bit-exact."""
+    b = synth.adversarial(30_000, seed=41, n_creators=6, scale_per_million=MIX)
+    st = oracle_check(cached.verify(b), b)
+    t = cached.timing()
+    assert t["key_path"] == 20
+    n_valid = sum(1 for k in range(b.n_keys) if gs.Unmarshal(b.key(k)) is not None)
+    assert 0 < n_valid < b.n_keys  # the mix carries malformed keys
+    assert t["kc_builds"] == n_valid and t["kc_hits"] == 0
+    assert set(np.unique(st)) == {0, 1, 2, 3}
+    oracle_check(cached.verify(b), b)
+    t = cached.timing()
+    assert t["kc_builds"] == 0 and t["kc_hits"] == b.n_keys and t["key_path"] == 20
+
+
+def test_key_cache_small_batches(cached):
+    """Latency-sized batches (1, 100, 1000 = SyncLimit, config.go:44) on the
+    cached tables: same results as the oracle."""
+    for n in (1, 100, 1000):
+        b = synth.events(n, n_creators=4, seed=100 + n)
+        oracle_check(cached.verify(b), b)
+        assert cached.timing()["key_path"] == 20
+
+
+def test_key_cache_device_entry(cached):
+    b = synth.adversarial(20_000, seed=42, n_creators=6, scale_per_million=MIX)
+    d = cached.to_device(b)
+    cached.verify_device(d)
+    oracle_check(d.result(), b)
+    assert cached.timing()["key_path"] == 20
+
+
+def test_key_cache_eviction(monkeypatch):
+    """A 1.5 GB budget holds 3 tables: a batch with 2 new keys after a batch
+    with 2 others evicts the least recently used; results stay exact."""
+    from babble_amd.verifier import Verifier
+
+    monkeypatch.setenv("BV_KEY_CACHE_GB", "1.5")
+    v = Verifier(device=0, flags=native.F_KEY_CACHE)
+    try:
+        a = synth.events(3000, n_creators=2, seed=51)
+        b = synth.events(3000, n_creators=2, seed=52)
+        oracle_check(v.verify(a), a)
+        assert v.timing()["kc_builds"] == 2
+        oracle_check(v.verify(b), b)
+        t = v.timing()
+        assert t["kc_builds"] == 2 and t["kc_keys"] <= 3
+        oracle_check(v.verify(a), a)
+    finally:
+        v.close()
+
+
+def test_host_entry_equals_device_entry_1m(cached):
+    """The pinned, chunked host entry point (digests hashed chunk by chunk
+    as they land) at C2 size gives the device entry's results, and reports
+    its PCIe staging time."""
+    from babble_amd.verifier import Verifier
+
+    b = synth.events(1_000_000, n_creators=64, seed=2)
+    v = Verifier(device=0)
+    try:
+        res = v.verify(b)
+        t = v.timing()
+        assert t["ms_h2d"] > 0 and t["ms_host"] >= t["ms_h2d"]
+        d = v.to_device(b)
+        v.verify_device(d)
+        res2 = d.result()
+        assert np.array_equal(res.msg_hash, res2.msg_hash)
+        assert np.array_equal(res.status, res2.status) and np.all(res.status == 1)
+        assert np.array_equal(res.accept_bits, res2.accept_bits)
+    finally:
+        v.close()
+
+
+def test_async_calls_on_two_streams_are_ordered():
+    """two async device calls on different streams share the ctx
+    work buffers; the library orders them (ev_done), so both are exact."""
+    import torch
+
+    from babble_amd.verifier import Verifier
+
+    v = Verifier(device=0)
+    try:
+        b1 = synth.adversarial(60_000, seed=61, n_creators=8, scale_per_million=MIX)
+        b2 = synth.adversarial(50_000, seed=62, n_creators=8, scale_per_million=MIX)
+        d1, d2 = v.to_device(b1), v.to_device(b2)
+        s1, s2 = torch.cuda.Stream(0), torch.cuda.Stream(0)
+        v.verify_device(d1, stream=s1.cuda_stream, sync=False)
+        v.verify_device(d2, stream=s2.cuda_stream, sync=False)
+        s1.synchronize()
+        s2.synchronize()
+        oracle_check(d1.result(), b1)
+        oracle_check(d2.result(), b2)
+        # async on the library's own stream: result() waits through bv_sync
+        v.verify_device(d1, stream=0, sync=False)
+        oracle_check(d1.result(), b1)
+    finally:
+        v.close()
+
+
+def test_group_one_device():
+    """bv_group over the box's device(s): shards, per-device staging and the
+    RCCL all-gather of the bitmask; equal to the oracle."""
+    import torch
+
+    from babble_amd.verifier import Group
+
+    g = Group(list(range(torch.cuda.device_count())))
+    try:
+        b = synth.adversarial(40_000, seed=71, n_creators=8, scale_per_million=MIX)
+        oracle_check(g.verify(b), b)
+        wb = synth.blocks(300, n_validators=100, seed=72)
+        oracle_check(g.verify(wb.batch), wb.batch)
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("key_cache", [True, False])
+def test_c5_full_size_check_block(cached, verifier_default, key_cache):
+    """C5 as SURVEY §8d specifies it: 10^4 blocks x 100 validators (10^6
+    signature items over 10^4 BlockBodies, each hashed once), 5 % invalid
+    signatures; every status equal to the oracle, and the per-block valid
+    counts decide CheckBlock (count > TrustCount, hashgraph.go:1599-1630)."""
+    wb = synth.blocks(10_000, n_validators=100, seed=5)
+    b = wb.batch
+    rng = np.random.default_rng(5)
+    bad = rng.choice(b.n_items, size=b.n_items // 20, replace=False)
+    b.s_be[bad, 7] ^= 0x40
+    v = cached if key_cache else verifier_default
+    res = v.verify(b)
+    assert v.timing()["key_path"] == (20 if key_cache else 12)
+    st = oracle_check(res, b)
+    valid = (st == 1).reshape(wb.n_blocks, wb.n_validators).sum(axis=1)
+    got = (res.status == 1).reshape(wb.n_blocks, wb.n_validators).sum(axis=1)
+    assert np.array_equal(valid, got)
+    tc = gs.trust_count(wb.n_validators)
+    assert int(valid.sum()) == b.n_items - len(bad)
+    assert np.all(valid > tc)
