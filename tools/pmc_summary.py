@@ -8,9 +8,13 @@ counter per dispatch of each kernel, and derives:
     memory-side counter tallies 128-B requests at 64 B for wide 16-B/lane
     reads — MI355X_MICROARCH.md §HBM; our table gathers are dwordx4)
   * hbm_write_bytes = WRITE_SIZE (KiB) x 1024       (exact for wide stores)
-  * valu_busy_pct   = 100 x SQ_ACTIVE_INST_VALU x 4 / CU_NUM / GRBM_GUI_ACTIVE
-    (SQ_* count quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs, so
-    the per-XCD active cycles are GRBM/8)
+  * valu_issue_util = (SQ_INSTS_VALU_INT64 x 5.39 + other SQ_INSTS_VALU x 3.03)
+    / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the fraction of SIMD cycles spent
+    issuing VALU instructions, with the per-class issue costs measured on
+    gfx950 (profiles/r01_ubench_ops.txt: v_mad_u64_u32 5.39 cycles per wave64
+    instruction, 32-bit VALU 3.03).  On ROCm 7.2 / gfx950 SQ_ACTIVE_INST_VALU
+    equals SQ_INSTS_VALU (an instruction count, not quad-cycles), so the
+    gfx94x VALUBusy formula over-counts; this one is <= 1 up to noise.
   * valu_insts_per_s (wave instructions x 64 lanes / kernel time)
 Writes nothing itself; bench.py reads profiles/kverify_traffic.json, which is
 this script's output for k_verify_q copied into profiles/.
@@ -26,6 +30,7 @@ from collections import defaultdict
 
 N_CU = 256
 N_XCD = 8
+CYC_MAD64, CYC_VALU32 = 5.39, 3.03  # profiles/r01_ubench_ops.txt
 
 
 def short(name: str) -> str:
@@ -75,9 +80,10 @@ def summarise(root: str) -> dict:
             e["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024
         if "hbm_read_bytes" in e and "hbm_write_bytes" in e:
             e["hbm_bytes"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
-        if "SQ_ACTIVE_INST_VALU" in avg and avg.get("GRBM_GUI_ACTIVE"):
-            # SQ_ACTIVE_INST_VALU counts quad-cycles, summed over SEs/SIMDs
-            e["valu_busy_pct"] = 100.0 * avg["SQ_ACTIVE_INST_VALU"] * 4 / N_CU / (avg["GRBM_GUI_ACTIVE"] / N_XCD)
+        if "SQ_INSTS_VALU" in avg and "SQ_INSTS_VALU_INT64" in avg and avg.get("GRBM_GUI_ACTIVE"):
+            i64 = avg["SQ_INSTS_VALU_INT64"]
+            cyc = i64 * CYC_MAD64 + (avg["SQ_INSTS_VALU"] - i64) * CYC_VALU32
+            e["valu_issue_util"] = cyc / (N_CU * 4) / (avg["GRBM_GUI_ACTIVE"] / N_XCD)
         if "SQ_INSTS_VALU" in avg and t:
             e["valu_wave_insts"] = avg["SQ_INSTS_VALU"]
             e["valu_lane_ops_per_s"] = avg["SQ_INSTS_VALU"] * 64 / t
@@ -87,6 +93,24 @@ def summarise(root: str) -> dict:
     return out
 
 
+def kverify(summary: dict, items: int, source: str) -> dict:
+    """The record bench.py reads (profiles/r02_kverify_pmc.json): PMC totals
+    of k_verify_g + k_verify_q<12,11> per launch pair."""
+    ks = [k for k in summary if k.startswith("k_verify_g") or k.startswith("k_verify_q<12")]
+    tot = lambda f: sum(summary[k].get(f, 0.0) for k in ks)  # noqa: E731
+    cnt = lambda c: sum(summary[k]["counters"].get(c, 0.0) for k in ks)  # noqa: E731
+    return {"source": source, "kernels": ks, "items_per_launch": items,
+            "hbm_bytes_per_launch": tot("hbm_bytes"), "hbm_read_bytes_uncorrected": cnt("FETCH_SIZE") * 1024,
+            "algorithmic_table_bytes": items * 33 * 64,
+            "valu_wave_insts": cnt("SQ_INSTS_VALU"), "valu_int64_wave_insts": cnt("SQ_INSTS_VALU_INT64"),
+            "valu_issue_util": {k: summary[k].get("valu_issue_util") for k in ks}}
+
+
 if __name__ == "__main__":
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-    print(json.dumps(summarise(root), indent=1, sort_keys=True))
+    s = summarise(root)
+    if len(sys.argv) > 3:  # <root> <items> <kverify-out.json>
+        with open(sys.argv[3], "w") as f:
+            json.dump(kverify(s, int(sys.argv[2]), f"{sys.argv[3]} <- tools/gpu_pmc.sh passes over bench.py "
+                              f"--no-extras --events {sys.argv[2]}"), f, indent=1)
+    print(json.dumps(s, indent=1, sort_keys=True))
