@@ -352,7 +352,11 @@ def verify_block_signatures(block: Block, sigs: Sequence[BlockSignature], verifi
 
 def check_block(block: Block, peer_set: PeerSet, verifier=None) -> Optional[str]:
     """Hashgraph.CheckBlock (hashgraph.go:1599-1630): None or the error text."""
-    if peer_set.Hash(verifier) != (block.PeersHash() or b""):
+    # reflect.DeepEqual(psh, block.PeersHash()) (hashgraph.go:1605): the
+    # computed hash is never nil ([]byte{} for an empty set), so a nil
+    # PeersHash never matches, while an empty one matches an empty set
+    bph = block.PeersHash()
+    if bph is None or peer_set.Hash(verifier) != bph:
         return "Wrong PeerSet"
     sigs = [s for s in block.GetSignatures() if s.ValidatorHex() in peer_set.ByPubKey]
     outcomes = verify_block_signatures(block, sigs, verifier)

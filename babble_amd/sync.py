@@ -73,7 +73,26 @@ class WireEvent:
 
 # participant_event(pubkey_string, index) -> hex hash or None (not found);
 # the Store.ParticipantEvent of inmem_store.go:143-145 before the sync.
-ParticipantEvent = Callable[[str, int], Optional[str]]
+class StoreError(Exception):
+    """common.StoreErr (src/common/store_errors.go:29-63): its Error() text is
+    "<dataType>, <key>, <kind>" and ReadWireInfo returns it unchanged for a
+    missing self-parent (hashgraph.go:1556-1559)."""
+
+    KEY_NOT_FOUND, TOO_LATE, SKIPPED_INDEX, UNKNOWN_PARTICIPANT, EMPTY, KEY_ALREADY_EXISTS = range(6)
+    _KIND = ("Not Found", "Too Late", "Skipped Index", "Unknown Participant", "Empty", "Key Already Exists")
+
+    def __init__(self, data_type: str, err_type: int, key: str):
+        super().__init__(data_type, err_type, key)
+        self.data_type, self.err_type, self.key = data_type, err_type, key
+
+    def __str__(self) -> str:
+        return "%s, %s, %s" % (self.data_type, self.key, self._KIND[self.err_type])
+
+
+# Store.ParticipantEvent (inmem_store.go:143-145 -> caches.go:84-95 ->
+# rolling_index.go:55-66) before the sync: the hex hash, or the StoreError
+# the store returns (None = a plain KeyNotFound).
+ParticipantEvent = Callable[[str, int], object]
 
 
 @dataclass
@@ -116,15 +135,15 @@ def read_wire_batch(wevents: Sequence[WireEvent], repertoire_by_id: Dict[int, Pe
         err = None
         if we.Body.SelfParentIndex >= 0:
             parents[0] = _resolve(cpk, we.Body.SelfParentIndex, participant_event, in_batch)
-            if parents[0] is None:
-                err = "Participant %s, index %d not found" % (cpk, we.Body.SelfParentIndex)
+            if isinstance(parents[0], StoreError):
+                err = str(parents[0])  # returned unchanged (hashgraph.go:1556-1559)
         if err is None and we.Body.OtherParentIndex >= 0:
             opc = repertoire_by_id.get(we.Body.OtherParentCreatorID)
             if opc is None:
                 err = "Participant %d not found" % we.Body.OtherParentCreatorID
             else:
                 parents[1] = _resolve(opc.PubKeyString(), we.Body.OtherParentIndex, participant_event, in_batch)
-                if parents[1] is None:
+                if isinstance(parents[1], StoreError):
                     err = "OtherParent (creator: %d, index: %d) not found" % (we.Body.OtherParentCreatorID,
                                                                               we.Body.OtherParentIndex)
         if err is not None:
@@ -157,10 +176,17 @@ def read_wire_batch(wevents: Sequence[WireEvent], repertoire_by_id: Dict[int, Pe
 
 
 def _resolve(pk: str, index: int, participant_event: ParticipantEvent, in_batch: Dict[Tuple[str, int], int]):
+    """hex hash (store), in-batch event index, or the StoreError Go would see.
+    Only a KeyNotFound can be satisfied by an event inserted earlier in the
+    same sync; TooLate / UnknownParticipant stand as they are."""
     h = participant_event(pk, index)
-    if h is not None:
+    if isinstance(h, str):
         return h
-    return in_batch.get((pk, index))
+    if h is None:
+        h = StoreError("ParticipantEvents", StoreError.KEY_NOT_FOUND, str(index))
+    if h.err_type == StoreError.KEY_NOT_FOUND and (pk, index) in in_batch:
+        return in_batch[(pk, index)]
+    return h
 
 
 def sync_verify(wevents: Sequence[WireEvent], repertoire_by_id: Dict[int, Peer], participant_event: ParticipantEvent,

@@ -273,12 +273,12 @@ def main():
             },
             "roofline": roof,
         }
-    if rank == 0 and not args.no_extras:
+    if rank == 0 and world == 1 and not args.no_extras:
         line["warm"] = warm_leg(args, dev, world, dist, local, step_with)
         line["host_entry"] = host_entry_leg(args, v, batch)
         line["latency_ms"] = latency_leg(args)
     if rank == 0:
-        if not args.no_cpu:
+        if world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(batch, args.cpu_seconds)
             line["gpu_over_cpu"] = line["value"] / line["cpu_baseline"]["value"]
         print(json.dumps(line), flush=True)

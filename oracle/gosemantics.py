@@ -699,7 +699,10 @@ def check_block(body: BlockBody, signatures: Sequence[Tuple[str, GoStr]], peers:
     since errors count as invalid). A panicking Verify would crash the node;
     it is reported as ReferencePanic.
     """
-    if peer_set_hash(peers) != (body.PeersHash or b""):
+    # reflect.DeepEqual(psh, block.PeersHash()) (hashgraph.go:1605):
+    # psh is []byte{} (non-nil) for an empty set, so a nil PeersHash never
+    # matches and an empty one matches only the empty set
+    if body.PeersHash is None or peer_set_hash(peers) != body.PeersHash:
         return False, 0
     by_pub = {EncodeToString(p.PubKeyBytes()) for p in peers}
     digest = body.Hash()

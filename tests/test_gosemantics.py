@@ -164,3 +164,32 @@ def test_item_status_order():
     assert gs.item_status(b"\x04", d, 1, N) == gs.REJECT
     assert gs.item_status(b"\x04", d, 1, 1) == gs.REF_PANIC
     assert gs.item_status(good, d, 1, 1) == gs.REJECT
+
+
+def test_check_block_deepequal_nil_vs_empty_peers_hash():
+    """CheckBlock compares with reflect.DeepEqual (hashgraph.go:1605):
+    PeerSet.Hash of an empty set is []byte{} (peer_set.go:104-115), which
+    equals an empty PeersHash ("" in JSON) but not a nil one (null)."""
+    from oracle import gosemantics as gs
+
+    empty = gs.BlockBody(Index=1, RoundReceived=1, Timestamp=1, StateHash=b"", FrameHash=b"", PeersHash=b"",
+                         Transactions=None, InternalTransactions=None, InternalTransactionReceipts=None)
+    nil = gs.BlockBody(Index=1, RoundReceived=1, Timestamp=1, StateHash=b"", FrameHash=b"", PeersHash=None,
+                       Transactions=None, InternalTransactions=None, InternalTransactionReceipts=None)
+    # empty set: count 0 > TrustCount 0 is false either way, but only the nil
+    # hash fails at the PeerSet comparison (valid count not reached)
+    assert gs.peer_set_hash([]) == b""
+    assert gs.check_block(empty, [], []) == (False, 0)
+    assert gs.check_block(nil, [], []) == (False, 0)
+
+
+def test_mirror_check_block_wrong_peerset_for_nil_hash():
+    from babble_amd import hashgraph as H
+
+    nil_block = H.Block(Body=H.BlockBody(Index=1, RoundReceived=1, Timestamp=1, StateHash=b"", FrameHash=b"",
+                                         PeersHash=None), Signatures={})
+    empty_block = H.Block(Body=H.BlockBody(Index=1, RoundReceived=1, Timestamp=1, StateHash=b"", FrameHash=b"",
+                                           PeersHash=b""), Signatures={})
+    ps = H.PeerSet([])
+    assert H.check_block(nil_block, ps) == "Wrong PeerSet"
+    assert H.check_block(empty_block, ps) == "Not enough valid signatures: got 0, need 0"

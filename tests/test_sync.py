@@ -127,3 +127,40 @@ def test_sync_verify_read_error_prefix():
     events, outcomes, read_err = S.sync_verify(wevents, rep, pe)
     assert read_err == "Creator 99 not found" and len(events) == 30
     assert all(o.ok for o in outcomes)
+
+
+def test_self_parent_store_error_text_passes_through():
+    """ReadWireInfo returns the store's error unchanged for a missing
+    self-parent (hashgraph.go:1556-1559): common.StoreErr text
+    "<dataType>, <key>, <kind>" (store_errors.go:46-63); a TooLate stands
+    even if the index is in the batch, a KeyNotFound can be satisfied by an
+    event inserted earlier in the same sync."""
+    wevents, bodies, rep, pe = make_sync(seed=9, n=40)
+    # the 12th event's self-parent: make the pre-sync store report TooLate
+    t = next(i for i, we in enumerate(wevents) if we.Body.SelfParentIndex >= 0 and i > 10)
+    we = wevents[t]
+    cpk = rep[we.Body.CreatorID].PubKeyString()
+
+    def pe_late(p, i):
+        if p == cpk and i == we.Body.SelfParentIndex:
+            return S.StoreError("ParticipantEvents[%d]" % we.Body.CreatorID, S.StoreError.TOO_LATE, str(i))
+        return pe(p, i)
+
+    reads, _ = S.read_wire_batch(wevents, rep, pe_late, verifier=HashlibStub())
+    assert reads[t].err == "ParticipantEvents[%d], %d, Too Late" % (we.Body.CreatorID, we.Body.SelfParentIndex)
+    assert all(r.err is None for r in reads[:t])
+    # an explicit KeyNotFound (or None) for an in-batch self-parent is resolved in the batch
+    reads, _ = S.read_wire_batch(wevents, rep, lambda p, i: pe(p, i) or S.StoreError(
+        "ParticipantEvents[0]", S.StoreError.KEY_NOT_FOUND, str(i)), verifier=HashlibStub())
+    assert all(r.err is None for r in reads)
+
+
+def test_missing_self_parent_not_found_text():
+    wevents, bodies, rep, pe = make_sync(seed=10, n=30)
+    t = next(i for i, we in enumerate(wevents) if we.Body.SelfParentIndex >= 0)
+    we = wevents[t]
+    cpk = rep[we.Body.CreatorID].PubKeyString()
+    we.Body.SelfParentIndex += 1000  # nowhere: not in the store, not in the batch
+    reads, _ = S.read_wire_batch(wevents, rep, pe, verifier=HashlibStub())
+    assert reads[t].err == "ParticipantEvents, %d, Not Found" % we.Body.SelfParentIndex
+    del cpk
