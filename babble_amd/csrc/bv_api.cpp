@@ -893,3 +893,39 @@ extern "C" int bv_sha256_batch(bv_ctx *ctx, uint64_t n_msgs, const uint8_t *msg_
   memcpy(out_hash, ctx->pin_out.p, n_msgs * 32);
   return BV_OK;
 }
+
+extern "C" int bv_peer_set_hash(bv_ctx *ctx, uint32_t n_peers, const uint8_t *key_bytes, const uint64_t *key_off,
+                                uint8_t out_hash[32]) {
+  if (!ctx || !out_hash || (n_peers && !key_off)) return BV_E_ARGS;
+  if (n_peers == 0) return BV_OK;  // []byte{}: nothing written
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  if (key_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "key_off[0] != 0");
+  uint64_t maxlen = 0;
+  for (uint32_t i = 0; i < n_peers; i++) {
+    if (key_off[i] > key_off[i + 1]) return bv_fail(ctx, BV_E_ARGS, "key_off not monotone");
+    maxlen = std::max<uint64_t>(maxlen, key_off[i + 1] - key_off[i]);
+  }
+  const uint64_t len = key_off[n_peers];
+  if (len && !key_bytes) return bv_fail(ctx, BV_E_ARGS, "null key bytes");
+  hipStream_t st = ctx->stream;
+  if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
+  const size_t o_off = align256(len + 8), o_scr = o_off + align256((n_peers + 1) * 8ull);
+  const size_t total = o_scr + align256(32 + maxlen + 72);
+  HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
+  HIPCHK(ctx->d_in.ensure(total + 32), BV_E_OOM, "alloc device staging");
+  HIPCHK(ctx->pin_out.ensure(32), BV_E_OOM, "alloc pinned results");
+  uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
+  if (len) memcpy(pin, key_bytes, len);
+  memcpy(pin + o_off, key_off, (n_peers + 1) * 8ull);
+  HIPCHK(hipMemcpyAsync(dev, pin, o_scr, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
+  uint32_t *dout = (uint32_t *)(dev + total);
+  HIPCHK(bvk::sha256_chain(st, n_peers, dev, (const uint64_t *)(dev + o_off), dev + o_scr, dout), BV_E_LAUNCH,
+         "k_sha256_chain");
+  HIPCHK(hipMemcpyAsync(ctx->pin_out.p, dout, 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h");
+  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
+  ctx->has_done = true;
+  HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+  memcpy(out_hash, ctx->pin_out.p, 32);
+  return BV_OK;
+}

@@ -17,6 +17,7 @@
 namespace bvk {
 hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
 hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
+hipError_t sha256_chain(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
 hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
                         uint32_t *, uint32_t *);
 hipError_t build_kc(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *, uint32_t *,

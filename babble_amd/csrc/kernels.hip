@@ -27,6 +27,31 @@ __global__ void __launch_bounds__(256) k_sha256(uint64_t n_msgs, const uint8_t *
   if (m < n_msgs) sha256_one(m, bytes, off, digest_words);
 }
 
+// PeerSet.Hash (src/peers/peer_set.go:104-115): h = [] then, for each peer
+// in order, h = SHA256(h || pubkey) (crypto.SimpleHashFromTwoHashes,
+// src/crypto/hash.go:17-22).  An inherently serial chain: ONE lane walks it
+// in one launch (instead of one host round trip per peer); `scratch` holds
+// 32 + max key length + 64 bytes.
+__global__ void __launch_bounds__(64) k_sha256_chain(uint32_t n, const uint8_t *__restrict__ bytes,
+                                                     const uint64_t *__restrict__ off, uint8_t *__restrict__ scratch,
+                                                     uint32_t *__restrict__ out_words) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t hlen = 0;  // 0 before the first peer ([]byte{}), then 32
+  for (uint32_t i = 0; i < n; i++) {
+    const uint64_t o = off[i], len = off[i + 1] - o;
+    for (int k = 0; k < 8; k++) {  // previous digest, big-endian bytes
+      const uint32_t be = bswap32(h[k]);
+      for (int q = 0; q < 4; q++) scratch[4 * k + q] = (uint8_t)(be >> (8 * q));
+    }
+    for (uint64_t q = 0; q < len; q++) scratch[hlen + q] = bytes[o + q];
+    for (int q = 0; q < 8; q++) scratch[hlen + len + q] = 0;  // the over-read pad
+    sha256_msg(h, scratch, 0, hlen + len);
+    hlen = 32;  // re-serialised at the top of the next iteration
+  }
+  for (int k = 0; k < 8; k++) out_words[k] = bswap32(h[k]);
+}
+
 __global__ void __launch_bounds__(64) k_key_decode(uint32_t n_keys, const uint8_t *__restrict__ kbytes,
                                                    const uint64_t *__restrict__ koff, uint8_t *__restrict__ kstatus,
                                                    uint32_t *__restrict__ kxy) {
@@ -388,6 +413,12 @@ static inline dim3 grid1(uint64_t n, uint32_t block) { return dim3((uint32_t)((n
 hipError_t sha256(hipStream_t st, uint64_t n, const uint8_t *bytes, const uint64_t *off, uint32_t *dig) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sha256, grid1(n, 256), dim3(256), 0, st, n, bytes, off, dig);
+  return hipGetLastError();
+}
+
+hipError_t sha256_chain(hipStream_t st, uint32_t n, const uint8_t *bytes, const uint64_t *off, uint8_t *scratch,
+                        uint32_t *out) {
+  hipLaunchKernelGGL(k_sha256_chain, dim3(1), dim3(64), 0, st, n, bytes, off, scratch, out);
   return hipGetLastError();
 }
 

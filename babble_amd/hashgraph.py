@@ -99,10 +99,15 @@ class PeerSet:
     def Hash(self, verifier=None) -> bytes:
         """peer_set.go:104-115: h = SHA256(h || pubkey) over the peers in order."""
         if self._hash is None:
-            h = b""
-            for p in self.Peers:
-                h = SHA256(h + p.PubKeyBytes(), verifier)
-            self._hash = h
+            v = verifier or default_verifier()
+            pks = [p.PubKeyBytes() for p in self.Peers]
+            if hasattr(v, "peer_set_hash"):  # the whole chain in one device launch
+                self._hash = v.peer_set_hash(pks)
+            else:
+                h = b""
+                for pk in pks:
+                    h = SHA256(h + pk, v)
+                self._hash = h
         return self._hash
 
     def TrustCount(self) -> int:

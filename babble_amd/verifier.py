@@ -166,6 +166,20 @@ class Verifier:
         self._check(self._L.bv_sha256_batch(self._ctx, len(msgs), buf.ctypes.data, off.ctypes.data, out.ctypes.data))
         return [out[i].tobytes() for i in range(len(msgs))]
 
+    def peer_set_hash(self, pubkeys: Sequence[bytes]) -> bytes:
+        """bv_peer_set_hash: PeerSet.Hash over the peers' key bytes (b"" for
+        an empty set, as Go's []byte{})."""
+        pubkeys = [bytes(k) for k in pubkeys]
+        if not pubkeys:
+            return b""
+        buf = np.frombuffer(b"".join(pubkeys) or b"\0", np.uint8).copy()
+        off = np.zeros(len(pubkeys) + 1, np.uint64)
+        off[1:] = np.cumsum([len(k) for k in pubkeys], dtype=np.uint64)
+        out = np.zeros(32, np.uint8)
+        self._check(self._L.bv_peer_set_hash(self._ctx, len(pubkeys), buf.ctypes.data, off.ctypes.data,
+                                             out.ctypes.data))
+        return out.tobytes()
+
     def timing(self) -> dict:
         t = native.BvTiming()
         self._check(self._L.bv_get_timing(self._ctx, ctypes.byref(t)))

@@ -168,6 +168,13 @@ int bv_plan_shards(const bv_batch *batch, int n_shards, uint64_t *bounds);
 int bv_sha256_batch(bv_ctx *ctx, uint64_t n_msgs, const uint8_t *msg_bytes,
                     const uint64_t *msg_off, uint8_t *out_hash);
 
+/* PeerSet.Hash (src/peers/peer_set.go:104-115): h = [] then h = SHA256(h ||
+ * pubkey) over the n peers' raw key bytes in order (PubKeyBytes), as ONE
+ * device launch (the chain is serial).  n_peers == 0: the hash is empty
+ * ([]byte{}) and out_hash is not written. */
+int bv_peer_set_hash(bv_ctx *ctx, uint32_t n_peers, const uint8_t *key_bytes, const uint64_t *key_off,
+                     uint8_t out_hash[32]);
+
 /* Device-timing breakdown of the last verify call on this ctx. */
 int bv_get_timing(const bv_ctx *ctx, bv_timing *out);
 

@@ -717,3 +717,137 @@ def check_block(body: BlockBody, signatures: Sequence[Tuple[str, GoStr]], peers:
         if st == ACCEPT:
             valid += 1
     return valid > trust_count(len(peers)), valid
+
+
+# ----------------------------------------------------------------------------
+# github.com/ugorji/go/codec v1.1.7 JsonHandle{Canonical: true} (go.mod:24),
+# as used by Frame.Marshal (src/hashgraph/frame.go:35-46).  Restated from the
+# published codec (encode.go kStruct / kMapCanonical, json.go quoteStr),
+# schema-driven: every Go type the Frame graph holds is described by its
+# type string below, and one recursive encoder walks values against it.
+# PARITY UNPINNED: neither Go nor the ugorji module is in this container and
+# the reference holds no serialized Frame.
+# ----------------------------------------------------------------------------
+@dataclass
+class Event:
+    """hashgraph.Event exported fields (event.go:102-105)."""
+    Body: EventBody = field(default_factory=EventBody)
+    Signature: GoStr = ""
+
+
+@dataclass
+class FrameEvent:
+    """event.go:455-463."""
+    Core: Optional[Event] = None
+    Round: int = 0
+    LamportTimestamp: int = 0
+    Witness: bool = False
+
+
+@dataclass
+class Root:
+    """root.go:11-14."""
+    Events: Optional[list] = None
+
+
+@dataclass
+class Frame:
+    """frame.go:12-20."""
+    Round: int = 0
+    Peers: Optional[list] = None
+    Roots: Optional[dict] = None
+    Events: Optional[list] = None
+    PeerSets: Optional[dict] = None
+    Timestamp: int = 0
+
+
+UGORJI_SCHEMA = {
+    "Frame": [("Round", "int"), ("Peers", "[]*Peer"), ("Roots", "map[string]*Root"), ("Events", "[]*FrameEvent"),
+              ("PeerSets", "map[int][]*Peer"), ("Timestamp", "int64")],
+    "Root": [("Events", "[]*FrameEvent")],
+    "FrameEvent": [("Core", "*Event"), ("Round", "int"), ("LamportTimestamp", "int"), ("Witness", "bool")],
+    "Event": [("Body", "EventBody"), ("Signature", "string")],
+    "EventBody": [("Transactions", "[][]byte"), ("InternalTransactions", "[]InternalTransaction"),
+                  ("Parents", "[]string"), ("Creator", "[]byte"), ("Index", "int"),
+                  ("BlockSignatures", "[]BlockSignature"), ("Timestamp", "int64")],
+    "InternalTransaction": [("Body", "InternalTransactionBody"), ("Signature", "string")],
+    "InternalTransactionBody": [("Type", "uint8"), ("Peer", "Peer")],
+    "BlockSignature": [("Validator", "[]byte"), ("Index", "int"), ("Signature", "string")],
+    "Peer": [("NetAddr", "string"), ("PubKeyHex", "string"), ("Moniker", "string")],
+}
+
+
+def ugorji_string(s: GoStr) -> bytes:
+    """json.go quoteStr (HTMLCharsAsIs false): short escapes for " \\ \\n \\r
+    \\b \\f \\t, \\u00XX for other bytes < 0x20 and < > &, U+2028/2029
+    escaped, each invalid UTF-8 byte -> \\ufffd."""
+    b = _b(s)
+    out = bytearray(b'"')
+    i = 0
+    short = {ord('"'): b'\\"', ord("\\"): b"\\\\", ord("\n"): b"\\n", ord("\r"): b"\\r", 8: b"\\b", 12: b"\\f",
+             ord("\t"): b"\\t"}
+    while i < len(b):
+        c = b[i]
+        if c < 0x80:
+            if c in short:
+                out += short[c]
+            elif c < 0x20 or c in (ord("<"), ord(">"), ord("&")):
+                out += b"\\u%04x" % c
+            else:
+                out.append(c)
+            i += 1
+            continue
+        n, ok = _utf8_rune(b, i)
+        if not ok:
+            out += b"\\ufffd"
+            i += 1
+            continue
+        if b[i:i + 3] in (b"\xe2\x80\xa8", b"\xe2\x80\xa9"):
+            out += b"\\u%04x" % (0x2000 + (b[i + 2] - 0x80))
+        else:
+            out += b[i:i + n]
+        i += n
+    out += b'"'
+    return bytes(out)
+
+
+def ugorji_encode(v, gotype: str) -> bytes:
+    """Encode value `v` of Go type `gotype` (a UGORJI_SCHEMA type string)."""
+    if gotype.startswith("*"):
+        return b"null" if v is None else ugorji_encode(v, gotype[1:])
+    if gotype == "[]byte":
+        return b"null" if v is None else b'"' + base64.b64encode(bytes(v)) + b'"'
+    if gotype.startswith("[]"):
+        if v is None:
+            return b"null"
+        return b"[" + b",".join(ugorji_encode(x, gotype[2:]) for x in v) + b"]"
+    if gotype.startswith("map["):
+        if v is None:
+            return b"null"
+        ktype, vtype = gotype[4:].split("]", 1)
+        if ktype == "string":  # Canonical: keys sorted by their bytes
+            keys = sorted(v, key=_b)
+            kenc = ugorji_string
+        else:  # integer keys: numeric order, written as quoted decimals
+            keys = sorted(v)
+            kenc = lambda k: b'"%d"' % k  # noqa: E731
+        return b"{" + b",".join(kenc(k) + b":" + ugorji_encode(v[k], vtype) for k in keys) + b"}"
+    if gotype in ("int", "int64", "uint8"):
+        return b"%d" % v
+    if gotype == "bool":
+        return b"true" if v else b"false"
+    if gotype == "string":
+        return ugorji_string(v)
+    # struct: exported fields, name-sorted (encode.go kStruct: toMap uses sfiSort)
+    fields = sorted(UGORJI_SCHEMA[gotype], key=lambda f: f[0])
+    return b"{" + b",".join(b'"' + n.encode() + b'":' + ugorji_encode(getattr(v, n), t) for n, t in fields) + b"}"
+
+
+def frame_marshal(f: Frame) -> bytes:
+    """Frame.Marshal (frame.go:35-46)."""
+    return ugorji_encode(f, "Frame")
+
+
+def frame_hash(f: Frame) -> bytes:
+    """Frame.Hash (frame.go:63-69)."""
+    return SHA256(frame_marshal(f))
