@@ -103,65 +103,6 @@ void PinnedBuf::release() {
 }
 
 // ---------------------------------------------------------------------------
-// host copy pool: parallel memcpy into / out of pinned staging
-// ---------------------------------------------------------------------------
-struct CopyPool {
-  std::vector<std::thread> th;
-  std::mutex mu;
-  std::condition_variable cv, done_cv;
-  std::vector<std::function<void()>> q;
-  size_t pending = 0;
-  bool stop = false;
-  explicit CopyPool(int n) {
-    for (int i = 0; i < n; i++)
-      th.emplace_back([this]() {
-        for (;;) {
-          std::function<void()> f;
-          {
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [this]() { return stop || !q.empty(); });
-            if (stop && q.empty()) return;
-            f = std::move(q.back());
-            q.pop_back();
-          }
-          f();
-          std::lock_guard<std::mutex> lk(mu);
-          if (--pending == 0) done_cv.notify_all();
-        }
-      });
-  }
-  ~CopyPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      stop = true;
-    }
-    cv.notify_all();
-    for (auto &t : th) t.join();
-  }
-  // dst <- src (n bytes); returns when done.  Small copies stay on the caller.
-  void copy(void *dst, const void *src, size_t n) {
-    constexpr size_t kPiece = 2ull << 20;
-    if (n <= kPiece || th.empty()) {
-      if (n) memcpy(dst, src, n);
-      return;
-    }
-    const size_t pieces = (n + kPiece - 1) / kPiece;
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      for (size_t i = 1; i < pieces; i++) {
-        const size_t o = i * kPiece, len = std::min(kPiece, n - o);
-        q.push_back([=]() { memcpy((uint8_t *)dst + o, (const uint8_t *)src + o, len); });
-        pending++;
-      }
-    }
-    cv.notify_all();
-    memcpy(dst, src, std::min(kPiece, n));  // the caller copies the first piece
-    std::unique_lock<std::mutex> lk(mu);
-    done_cv.wait(lk, [this]() { return pending == 0; });
-  }
-};
-
-// ---------------------------------------------------------------------------
 // errors
 // ---------------------------------------------------------------------------
 int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e) {
@@ -310,7 +251,8 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   DevBuf *bufs[] = {&ctx->d_in,      &ctx->digests,  &ctx->kstatus,  &ctx->kxy,     &ctx->bases_jac,
                     &ctx->key_sub,   &ctx->key_pscr, &ctx->key_table, &ctx->scratch, &ctx->u12,
                     &ctx->rg,        &ctx->status,   &ctx->bits,     &ctx->kc_tabs, &ctx->kc_kst,
-                    &ctx->kc_kxy,    &ctx->kc_btabs};
+                    &ctx->kc_kxy,    &ctx->kc_btabs, &ctx->ev_lens,  &ctx->ev_ppos,  &ctx->ev_offs,
+                    &ctx->ev_bodies, &ctx->ev_tmp,   &ctx->ev_iota};
   for (auto *b : bufs) b->release();
   for (auto &s : ctx->kc_slots)
     if (s.table) (void)hipFree(s.table);
@@ -343,7 +285,7 @@ extern "C" int bv_get_timing(const bv_ctx *ctx, bv_timing *out) {
 // per batch key) and returns BV_OK with *use = true; *use = false when the
 // batch cannot use the cache (too many keys, budget) and must take the
 // per-batch path.  hkb/hko: host copies of the key bytes; dkb/dko: device.
-static int kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
+int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
                       const uint64_t *dko, hipStream_t st, bool *use) {
   *use = false;
   if (n_keys == 0 || n_keys > kKcMaxBatchKeys) return BV_OK;
@@ -640,7 +582,7 @@ extern "C" int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_re
              "d2h key bytes");
       HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
     }
-    int rc = kc_prepare(ctx, nk, hkb.data(), hko.data(), dbatch->key_bytes, dbatch->key_off, st, &kc);
+    int rc = bv_kc_prepare(ctx, nk, hkb.data(), hko.data(), dbatch->key_bytes, dbatch->key_off, st, &kc);
     if (rc != BV_OK) return rc;
   }
   int rc = bv_run_device(ctx, dbatch, dresult->msg_hash, dresult->status, dresult->accept_bits, st, false, kc);
@@ -691,7 +633,6 @@ int bv_validate_host_batch(bv_ctx *ctx, const bv_batch *b) {
   return BV_OK;
 }
 
-static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Stage a host batch into HBM (pinned chunks on the copy stream), hash the
 // messages chunk by chunk as they land and launch the verify pipeline.
@@ -777,7 +718,7 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
   bool kc = false;
   if ((ctx->flags & BV_F_KEY_CACHE) && n_keys && n_keys <= kKcMaxBatchKeys) {
     HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SMALL], 0), BV_E_LAUNCH, "join");
-    rc = kc_prepare(ctx, n_keys, b->key_bytes, b->key_off, d.key_bytes, d.key_off, st, &kc);
+    rc = bv_kc_prepare(ctx, n_keys, b->key_bytes, b->key_off, d.key_bytes, d.key_off, st, &kc);
     if (rc != BV_OK) return rc;
   }
 

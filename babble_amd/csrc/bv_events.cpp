@@ -1,0 +1,266 @@
+// bv_events.cpp — bv_verify_events: canonical EventBody JSON built on the
+// device from wire fields, in-batch DAG-level hashing, then the verify
+// pipeline (include/babbleverify.h).
+//
+// Host work is validation, the DAG levels (only when an event names an
+// in-batch parent) and one pinned staging copy of the compact arrays; the
+// bodies never cross PCIe.  Device: k_ev_len -> inclusive scan (hipcub) ->
+// k_ev_write -> level 0 in one grid launch -> the remaining levels, wide ones
+// as grid launches and runs of narrow ones (<= 1024 events) as ONE
+// single-workgroup launch each (k_ev_hash_chain) -> bv_run_device on the
+// hashed bodies.
+#include <algorithm>
+#include <cstring>
+
+#include "bv_internal.h"
+
+#define HIPCHK(expr, code, what)                               \
+  do {                                                         \
+    hipError_t _e = (expr);                                    \
+    if (_e != hipSuccess) return bv_fail(ctx, code, what, _e); \
+  } while (0)
+
+namespace {
+
+constexpr uint32_t kNarrowLevel = 1024;  // events per level run by k_ev_hash_chain
+constexpr size_t kChunk = 16ull << 20;
+
+int validate(bv_ctx *ctx, const bv_event_batch *b) {
+  const uint64_t n = b->n_events;
+  if (!n) return BV_OK;
+  if (!b->creator || !b->index || !b->timestamp || !b->parent_kind || !b->parent_ref || !b->tx_start ||
+      !b->r_be || !b->s_be || !b->key_off)
+    return bv_fail(ctx, BV_E_ARGS, "null event array");
+  if (b->key_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "key_off[0] != 0");
+  for (uint32_t k = 0; k < b->n_keys; k++)
+    if (b->key_off[k] > b->key_off[k + 1]) return bv_fail(ctx, BV_E_ARGS, "key_off not monotone");
+  if (b->key_off[b->n_keys] && !b->key_bytes) return bv_fail(ctx, BV_E_ARGS, "null key bytes");
+  if (b->tx_start[0] != 0) return bv_fail(ctx, BV_E_ARGS, "tx_start[0] != 0");
+  const uint64_t n_tx = b->tx_start[n];
+  if (n_tx && !b->tx_off) return bv_fail(ctx, BV_E_ARGS, "null tx_off");
+  if (n_tx && b->tx_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "tx_off[0] != 0");
+  for (uint64_t t = 0; t < n_tx; t++)
+    if (b->tx_off[t] > b->tx_off[t + 1]) return bv_fail(ctx, BV_E_ARGS, "tx_off not monotone");
+  if (n_tx && b->tx_off[n_tx] && !b->tx_bytes) return bv_fail(ctx, BV_E_ARGS, "null tx bytes");
+  for (const uint64_t *off : {b->itx_off, b->bsig_off}) {
+    if (!off) continue;
+    if (off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "fragment offsets must start at 0");
+    for (uint64_t e = 0; e < n; e++)
+      if (off[e] > off[e + 1]) return bv_fail(ctx, BV_E_ARGS, "fragment offsets not monotone");
+  }
+  if ((b->itx_off && b->itx_off[n] && !b->itx_json) || (b->bsig_off && b->bsig_off[n] && !b->bsig_json))
+    return bv_fail(ctx, BV_E_ARGS, "null fragment bytes");
+  for (uint64_t e = 0; e < n; e++) {
+    if (b->creator[e] >= b->n_keys) return bv_fail(ctx, BV_E_ARGS, "creator index out of range");
+    if (b->tx_start[e] > b->tx_start[e + 1]) return bv_fail(ctx, BV_E_ARGS, "tx_start not monotone");
+    for (int p = 0; p < 2; p++) {
+      const uint8_t k = b->parent_kind[2 * e + p];
+      const uint64_t r = b->parent_ref[2 * e + p];
+      if (k > BV_PARENT_EVENT) return bv_fail(ctx, BV_E_ARGS, "bad parent kind");
+      if (k == BV_PARENT_HASH && (r >= b->n_parent_hashes || !b->parent_hashes))
+        return bv_fail(ctx, BV_E_ARGS, "parent hash index out of range");
+      if (k == BV_PARENT_EVENT && r >= e) return bv_fail(ctx, BV_E_ARGS, "in-batch parent must precede its child");
+    }
+  }
+  return BV_OK;
+}
+
+}  // namespace
+
+extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result *res) {
+  if (!ctx || !eb || !res) return BV_E_ARGS;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  bv_host_call call;
+  call.t0 = std::chrono::steady_clock::now();
+  int rc = validate(ctx, eb);
+  if (rc != BV_OK) return rc;
+  ctx->timing = bv_timing{};
+  const uint64_t n = eb->n_events;
+  hipStream_t st = ctx->stream;
+  if (n == 0) return BV_OK;
+
+  // DAG levels over in-batch parents (refs point backwards: one pass)
+  std::vector<uint32_t> level, order, level_off;
+  bool dag = false;
+  for (uint64_t i = 0; i < 2 * n && !dag; i++) dag = eb->parent_kind[i] == BV_PARENT_EVENT;
+  if (dag) {
+    level.assign(n, 0);
+    uint32_t nl = 1;
+    for (uint64_t e = 0; e < n; e++) {
+      uint32_t l = 0;
+      for (int p = 0; p < 2; p++)
+        if (eb->parent_kind[2 * e + p] == BV_PARENT_EVENT) l = std::max(l, level[eb->parent_ref[2 * e + p]] + 1);
+      level[e] = l;
+      nl = std::max(nl, l + 1);
+    }
+    level_off.assign(nl + 1, 0);
+    for (uint64_t e = 0; e < n; e++) level_off[level[e] + 1]++;
+    for (uint32_t l = 0; l < nl; l++) level_off[l + 1] += level_off[l];
+    order.resize(n);
+    std::vector<uint32_t> fill(level_off.begin(), level_off.end() - 1);
+    for (uint64_t e = 0; e < n; e++) order[fill[level[e]]++] = (uint32_t)e;
+  }
+
+  // staging layout (pinned host and HBM): the compact wire arrays
+  const uint64_t n_tx = eb->tx_start[n];
+  const uint64_t tx_len = n_tx ? eb->tx_off[n_tx] : 0;
+  const uint64_t key_len = eb->key_off[eb->n_keys];
+  const uint64_t itx_len = eb->itx_off ? eb->itx_off[n] : 0, bsig_len = eb->bsig_off ? eb->bsig_off[n] : 0;
+  struct Seg {
+    const void *src;
+    size_t n, off;
+  };
+  std::vector<Seg> segs;
+  size_t total = 0;
+  auto add = [&](const void *src, size_t bytes, size_t pad = 0) -> size_t {
+    segs.push_back({src, bytes, total});
+    const size_t o = total;
+    total += align256(bytes + pad);
+    return o;
+  };
+  const size_t o_koff = add(eb->key_off, (eb->n_keys + 1) * 8ull);
+  const size_t o_kb = add(eb->key_bytes, key_len, 64);
+  const size_t o_cr = add(eb->creator, n * 4);
+  const size_t o_ix = add(eb->index, n * 8);
+  const size_t o_ts = add(eb->timestamp, n * 8);
+  const size_t o_pk = add(eb->parent_kind, n * 2);
+  const size_t o_pr = add(eb->parent_ref, n * 16);
+  const size_t o_ph = add(eb->parent_hashes, eb->parent_hashes ? eb->n_parent_hashes * 32 : 0);
+  const size_t o_txs = add(eb->tx_start, (n + 1) * 8);
+  const size_t o_txo = add(eb->tx_off, n_tx ? (n_tx + 1) * 8 : 0);
+  const size_t o_txb = add(eb->tx_bytes, tx_len);
+  const size_t o_tln = add(eb->tx_list_nil, eb->tx_list_nil ? n : 0);
+  const size_t o_txn = add(eb->tx_nil, eb->tx_nil ? n_tx : 0);
+  const size_t o_io = add(eb->itx_off, eb->itx_off ? (n + 1) * 8 : 0);
+  const size_t o_ij = add(eb->itx_json, itx_len);
+  const size_t o_bo = add(eb->bsig_off, eb->bsig_off ? (n + 1) * 8 : 0);
+  const size_t o_bj = add(eb->bsig_json, bsig_len);
+  const size_t o_r = add(eb->r_be, n * 32);
+  const size_t o_s = add(eb->s_be, n * 32);
+  const size_t o_pre = add(eb->pre, eb->pre ? n : 0);
+  const size_t o_ord = add(dag ? order.data() : nullptr, dag ? n * 4 : 0);
+  const size_t o_lof = add(dag ? level_off.data() : nullptr, dag ? level_off.size() * 4 : 0);
+
+  if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
+  HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
+  HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
+  uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
+  HIPCHK(hipEventRecord(ctx->ev[E_CALL], st), BV_E_LAUNCH, "event");
+  for (size_t a = 0; a < total; a += kChunk) {
+    const size_t z = std::min(total, a + kChunk);
+    for (const Seg &s : segs) {
+      const size_t lo = std::max(a, s.off), hi = std::min(z, s.off + s.n);
+      if (s.src && lo < hi) ctx->pool->copy(pin + lo, (const uint8_t *)s.src + (lo - s.off), hi - lo);
+    }
+    HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
+  }
+  HIPCHK(hipEventRecord(ctx->ev[E_STAGED], st), BV_E_LAUNCH, "event");
+
+  // the same batch over device pointers
+  bv_event_batch d = *eb;
+  d.key_off = (const uint64_t *)(dev + o_koff);
+  d.key_bytes = dev + o_kb;
+  d.creator = (const uint32_t *)(dev + o_cr);
+  d.index = (const int64_t *)(dev + o_ix);
+  d.timestamp = (const int64_t *)(dev + o_ts);
+  d.parent_kind = dev + o_pk;
+  d.parent_ref = (const uint64_t *)(dev + o_pr);
+  d.parent_hashes = eb->parent_hashes ? dev + o_ph : nullptr;
+  d.tx_start = (const uint64_t *)(dev + o_txs);
+  d.tx_off = n_tx ? (const uint64_t *)(dev + o_txo) : nullptr;
+  d.tx_bytes = dev + o_txb;
+  d.tx_list_nil = eb->tx_list_nil ? dev + o_tln : nullptr;
+  d.tx_nil = eb->tx_nil ? dev + o_txn : nullptr;
+  d.itx_off = eb->itx_off ? (const uint64_t *)(dev + o_io) : nullptr;
+  d.itx_json = dev + o_ij;
+  d.bsig_off = eb->bsig_off ? (const uint64_t *)(dev + o_bo) : nullptr;
+  d.bsig_json = dev + o_bj;
+  d.r_be = dev + o_r;
+  d.s_be = dev + o_s;
+  d.pre = eb->pre ? dev + o_pre : nullptr;
+
+  // bodies: an upper bound on their size (exact lengths are on the device)
+  uint64_t kmax = 0;
+  for (uint32_t k = 0; k < eb->n_keys; k++) kmax = std::max<uint64_t>(kmax, eb->key_off[k + 1] - eb->key_off[k]);
+  const uint64_t bound = n * (160 + 2 * 68 + 2 * 20 + 4 * (kmax / 3 + 1) + 16) + 4 * (tx_len / 3 + n_tx) +
+                         8 * n_tx + itx_len + bsig_len + 64;
+  size_t tmp_bytes = 0;
+  HIPCHK(bvk::ev_build(st, d, nullptr, nullptr, nullptr, nullptr, nullptr, &tmp_bytes), BV_E_LAUNCH, "scan size");
+  HIPCHK(ctx->ev_lens.ensure(n * 8), BV_E_OOM, "alloc lens");
+  HIPCHK(ctx->ev_ppos.ensure(n * 8), BV_E_OOM, "alloc ppos");
+  HIPCHK(ctx->ev_offs.ensure((n + 1) * 8), BV_E_OOM, "alloc offs");
+  HIPCHK(ctx->ev_bodies.ensure(bound), BV_E_OOM, "alloc bodies");
+  HIPCHK(ctx->ev_tmp.ensure(std::max<size_t>(tmp_bytes, 256)), BV_E_OOM, "alloc scan scratch");
+  HIPCHK(ctx->ev_iota.ensure(n * 4), BV_E_OOM, "alloc item index");
+  HIPCHK(ctx->digests.ensure(n * 32), BV_E_OOM, "alloc digests");
+  if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order");
+  uint64_t *offs = ctx->ev_offs.as<uint64_t>();
+  uint32_t *ppos = ctx->ev_ppos.as<uint32_t>(), *dig = ctx->digests.as<uint32_t>();
+  uint8_t *bodies = ctx->ev_bodies.as<uint8_t>();
+  HIPCHK(bvk::ev_build(st, d, ctx->ev_lens.as<uint64_t>(), ppos, offs, bodies, ctx->ev_tmp.p, &tmp_bytes),
+         BV_E_LAUNCH, "event bodies");
+
+  // hashing: all at once, or level by level over the in-batch DAG
+  if (!dag) {
+    HIPCHK(bvk::ev_hash(st, n, nullptr, d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
+  } else {
+    const uint32_t *dord = (const uint32_t *)(dev + o_ord), *dlof = (const uint32_t *)(dev + o_lof);
+    const uint32_t nl = (uint32_t)level_off.size() - 1;
+    uint32_t L = 0;
+    while (L < nl) {
+      const uint32_t w = level_off[L + 1] - level_off[L];
+      if (w > kNarrowLevel || L == 0) {
+        HIPCHK(bvk::ev_hash(st, w, dord + level_off[L], d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
+        L++;
+        continue;
+      }
+      uint32_t L1 = L;
+      while (L1 < nl && level_off[L1 + 1] - level_off[L1] <= kNarrowLevel) L1++;
+      HIPCHK(bvk::ev_hash_chain(st, L, L1, dlof, dord, d, ppos, bodies, offs, dig), BV_E_LAUNCH,
+             "k_ev_hash_chain");
+      L = L1;
+    }
+  }
+  HIPCHK(bvk::iota(st, n, ctx->ev_iota.as<uint32_t>()), BV_E_LAUNCH, "k_iota");
+  HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
+
+  // verification: item e = (body e, creator key, r, s)
+  bv_batch vb = {};
+  vb.n_msgs = n;
+  vb.msg_bytes = bodies;
+  vb.msg_off = offs;
+  vb.n_keys = eb->n_keys;
+  vb.key_bytes = d.key_bytes;
+  vb.key_off = d.key_off;
+  vb.n_items = n;
+  vb.item_msg = ctx->ev_iota.as<uint32_t>();
+  vb.item_key = d.creator;
+  vb.r_be = d.r_be;
+  vb.s_be = d.s_be;
+  vb.pre = d.pre;
+  bool kc = false;
+  if (ctx->flags & BV_F_KEY_CACHE) {
+    rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, d.key_bytes, d.key_off, st, &kc);
+    if (rc != BV_OK) return rc;
+  }
+  rc = bv_run_device(ctx, &vb, nullptr, nullptr, nullptr, st, true, kc);
+  if (rc != BV_OK) return rc;
+
+  const size_t o_st = align256(n * 32), o_bits = o_st + align256(n);
+  HIPCHK(ctx->pin_out.ensure(o_bits + align256((n + 63) / 64 * 8) + 256), BV_E_OOM, "alloc pinned results");
+  uint8_t *pout = (uint8_t *)ctx->pin_out.p;
+  call.pout = pout;
+  call.o_st = o_st;
+  call.o_bits = o_bits;
+  HIPCHK(hipMemcpyAsync(pout, ctx->digests.p, n * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h digests");
+  HIPCHK(hipMemcpyAsync(pout + o_st, ctx->status.p, n, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
+  HIPCHK(hipMemcpyAsync(pout + o_bits, ctx->bits.p, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
+         "d2h bits");
+  HIPCHK(hipEventRecord(ctx->ev[E_OUT], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
+  bv_batch sizes = {};
+  sizes.n_msgs = n;
+  sizes.n_items = n;
+  return bv_host_finish(ctx, &sizes, res, &call, true);
+}

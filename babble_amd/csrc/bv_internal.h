@@ -4,7 +4,11 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -18,6 +22,13 @@ namespace bvk {
 hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
 hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
 hipError_t sha256_chain(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
+hipError_t ev_build(hipStream_t, const bv_event_batch &, uint64_t *, uint32_t *, uint64_t *, uint8_t *, void *,
+                    size_t *);
+hipError_t ev_hash(hipStream_t, uint64_t, const uint32_t *, const bv_event_batch &, const uint32_t *, uint8_t *,
+                   const uint64_t *, uint32_t *);
+hipError_t ev_hash_chain(hipStream_t, uint32_t, uint32_t, const uint32_t *, const uint32_t *, const bv_event_batch &,
+                         const uint32_t *, uint8_t *, const uint64_t *, uint32_t *);
+hipError_t iota(hipStream_t, uint64_t, uint32_t *);
 hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
                         uint32_t *, uint32_t *);
 hipError_t build_kc(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *, uint32_t *,
@@ -53,7 +64,67 @@ struct PinnedBuf {
   void release();
 };
 
-struct CopyPool;
+// ---------------------------------------------------------------------------
+// host copy pool: parallel memcpy into / out of pinned staging
+// ---------------------------------------------------------------------------
+struct CopyPool {
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  std::vector<std::function<void()>> q;
+  size_t pending = 0;
+  bool stop = false;
+  explicit CopyPool(int n) {
+    for (int i = 0; i < n; i++)
+      th.emplace_back([this]() {
+        for (;;) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [this]() { return stop || !q.empty(); });
+            if (stop && q.empty()) return;
+            f = std::move(q.back());
+            q.pop_back();
+          }
+          f();
+          std::lock_guard<std::mutex> lk(mu);
+          if (--pending == 0) done_cv.notify_all();
+        }
+      });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+  }
+  // dst <- src (n bytes); returns when done.  Small copies stay on the caller.
+  void copy(void *dst, const void *src, size_t n) {
+    constexpr size_t kPiece = 2ull << 20;
+    if (n <= kPiece || th.empty()) {
+      if (n) memcpy(dst, src, n);
+      return;
+    }
+    const size_t pieces = (n + kPiece - 1) / kPiece;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (size_t i = 1; i < pieces; i++) {
+        const size_t o = i * kPiece, len = std::min(kPiece, n - o);
+        q.push_back([=]() { memcpy((uint8_t *)dst + o, (const uint8_t *)src + o, len); });
+        pending++;
+      }
+    }
+    cv.notify_all();
+    memcpy(dst, src, std::min(kPiece, n));  // the caller copies the first piece
+    std::unique_lock<std::mutex> lk(mu);
+    done_cv.wait(lk, [this]() { return pending == 0; });
+  }
+};
+
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // timing / ordering events (see bv_read_timing)
 enum {
@@ -97,6 +168,8 @@ struct bv_ctx {
   std::vector<KcSlot> kc_slots;
   uint64_t kc_clock = 0, kc_bytes = 0, kc_budget = 0;
   DevBuf kc_tabs, kc_kst, kc_kxy, kc_btabs;
+  // bv_verify_events: body lengths, parent-hex positions, offsets, bodies
+  DevBuf ev_lens, ev_ppos, ev_offs, ev_bodies, ev_tmp, ev_iota;
 };
 
 // one in-flight host-entry call (bv_host_launch -> bv_host_finish)
@@ -110,6 +183,8 @@ int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess);
 int bv_validate_host_batch(bv_ctx *ctx, const bv_batch *b);
 int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc);
+int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
+                  const uint64_t *dko, hipStream_t st, bool *use);
 int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call);
 int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call *call, bool bits_out);
 void bv_read_timing(bv_ctx *ctx);

@@ -18,7 +18,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "evjson.h"
 #include "verify_core.h"
+
+#include <hipcub/hipcub.hpp>
 
 __global__ void __launch_bounds__(256) k_sha256(uint64_t n_msgs, const uint8_t *__restrict__ bytes,
                                                 const uint64_t *__restrict__ off,
@@ -50,6 +53,78 @@ __global__ void __launch_bounds__(64) k_sha256_chain(uint32_t n, const uint8_t *
     hlen = 32;  // re-serialised at the top of the next iteration
   }
   for (int k = 0; k < 8; k++) out_words[k] = bswap32(h[k]);
+}
+
+// ---------------------------------------------------------------------------
+// Events from wire fields (evjson.h): body lengths, bodies, level hashing
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_ev_len(bv_event_batch b, uint64_t *__restrict__ lens,
+                                                uint32_t *__restrict__ ppos) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= b.n_events) return;
+  uint32_t pp[2];
+  lens[e] = evj_len(b, e, pp);
+  ppos[2 * e] = pp[0];
+  ppos[2 * e + 1] = pp[1];
+}
+
+__global__ void __launch_bounds__(256) k_ev_write(bv_event_batch b, const uint64_t *__restrict__ offs,
+                                                  uint8_t *__restrict__ bodies) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < b.n_events) evj_write(b, e, bodies + offs[e]);
+}
+
+// Splice the in-batch parents' hex (their digests final) into event e's
+// body, then hash it.  `coherent`: parents were hashed by other threads of
+// this launch (k_ev_hash_chain), so their digest words are read at agent
+// scope, past the non-coherent vector L1.
+__device__ __forceinline__ void ev_splice_hash(uint64_t e, const bv_event_batch &b, const uint32_t *ppos,
+                                               uint8_t *bodies, const uint64_t *offs, uint32_t *dig,
+                                               bool coherent) {
+  for (int p = 0; p < 2; p++) {
+    const uint32_t pos = ppos[2 * e + p];
+    if (pos == EVJ_NOPOS) continue;
+    const uint64_t q = b.parent_ref[2 * e + p];
+    uint32_t w[8];
+    for (int k = 0; k < 8; k++)
+      w[k] = coherent ? __hip_atomic_load(dig + 8 * q + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : dig[8 * q + k];
+    uint8_t d[32];
+    for (int k = 0; k < 8; k++)
+      for (int c = 0; c < 4; c++) d[4 * k + c] = (uint8_t)(w[k] >> (8 * c));  // words hold BE digest bytes
+    evj_hex32(bodies + offs[e] + pos, d);
+  }
+  sha256_one(e, bodies, offs, dig);
+}
+
+// One DAG level (or all events when list == null): a grid over its events.
+__global__ void __launch_bounds__(256) k_ev_hash(uint64_t count, const uint32_t *__restrict__ list, bv_event_batch b,
+                                                 const uint32_t *__restrict__ ppos, uint8_t *__restrict__ bodies,
+                                                 const uint64_t *__restrict__ offs, uint32_t *__restrict__ dig) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) ev_splice_hash(list ? list[i] : i, b, ppos, bodies, offs, dig, false);
+}
+
+// Consecutive NARROW levels [l0, l1) in one launch of one workgroup: level
+// L's events (order[level_off[L] .. level_off[L+1])) hash in parallel, then
+// a fence + barrier before level L+1 reads their digests.  core.sync's
+// SyncResponse is ~SyncLimit events, a few per level (one per creator).
+__global__ void __launch_bounds__(1024) k_ev_hash_chain(uint32_t l0, uint32_t l1,
+                                                        const uint32_t *__restrict__ level_off,
+                                                        const uint32_t *__restrict__ order, bv_event_batch b,
+                                                        const uint32_t *__restrict__ ppos, uint8_t *__restrict__ bodies,
+                                                        const uint64_t *__restrict__ offs, uint32_t *__restrict__ dig) {
+  for (uint32_t L = l0; L < l1; L++) {
+    for (uint32_t i = level_off[L] + threadIdx.x; i < level_off[L + 1]; i += blockDim.x)
+      ev_splice_hash(order[i], b, ppos, bodies, offs, dig, true);
+    __threadfence();
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) k_iota(uint64_t n, uint32_t *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (uint32_t)i;
 }
 
 __global__ void __launch_bounds__(64) k_key_decode(uint32_t n_keys, const uint8_t *__restrict__ kbytes,
@@ -413,6 +488,47 @@ static inline dim3 grid1(uint64_t n, uint32_t block) { return dim3((uint32_t)((n
 hipError_t sha256(hipStream_t st, uint64_t n, const uint8_t *bytes, const uint64_t *off, uint32_t *dig) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sha256, grid1(n, 256), dim3(256), 0, st, n, bytes, off, dig);
+  return hipGetLastError();
+}
+
+// Bodies of the events of `b` (device pointers): lengths, offsets (offs:
+// n + 1, inclusive scan into offs + 1), then the JSON.  `tmp` / `tmp_bytes`:
+// scan scratch (query with tmp == null).
+hipError_t ev_build(hipStream_t st, const bv_event_batch &b, uint64_t *lens, uint32_t *ppos, uint64_t *offs,
+                    uint8_t *bodies, void *tmp, size_t *tmp_bytes) {
+  const uint64_t n = b.n_events;
+  if (!tmp) return hipcub::DeviceScan::InclusiveSum(nullptr, *tmp_bytes, lens, offs + 1, (int)n, st);
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ev_len, grid1(n, 256), dim3(256), 0, st, b, lens, ppos);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(offs, 0, 8, st);
+  if (e != hipSuccess) return e;
+  e = hipcub::DeviceScan::InclusiveSum(tmp, *tmp_bytes, lens, offs + 1, (int)n, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_ev_write, grid1(n, 256), dim3(256), 0, st, b, offs, bodies);
+  return hipGetLastError();
+}
+
+hipError_t ev_hash(hipStream_t st, uint64_t count, const uint32_t *list, const bv_event_batch &b, const uint32_t *ppos,
+                   uint8_t *bodies, const uint64_t *offs, uint32_t *dig) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ev_hash, grid1(count, 256), dim3(256), 0, st, count, list, b, ppos, bodies, offs, dig);
+  return hipGetLastError();
+}
+
+hipError_t ev_hash_chain(hipStream_t st, uint32_t l0, uint32_t l1, const uint32_t *level_off, const uint32_t *order,
+                         const bv_event_batch &b, const uint32_t *ppos, uint8_t *bodies, const uint64_t *offs,
+                         uint32_t *dig) {
+  if (l1 <= l0) return hipSuccess;
+  hipLaunchKernelGGL(k_ev_hash_chain, dim3(1), dim3(1024), 0, st, l0, l1, level_off, order, b, ppos, bodies, offs,
+                     dig);
+  return hipGetLastError();
+}
+
+hipError_t iota(hipStream_t st, uint64_t n, uint32_t *out) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_iota, grid1(n, 256), dim3(256), 0, st, n, out);
   return hipGetLastError();
 }
 

@@ -32,7 +32,7 @@ EXPORTS = (
     "bv_abi_version", "bv_create", "bv_destroy", "bv_last_error", "bv_verify_batch",
     "bv_verify_batch_device", "bv_sha256_batch", "bv_get_timing", "bv_decode_signature",
     "bv_hex_decode", "bv_group_create", "bv_group_destroy", "bv_group_last_error", "bv_group_verify_batch",
-    "bv_group_get_timing", "bv_plan_shards", "bv_sync", "bv_peer_set_hash",
+    "bv_group_get_timing", "bv_plan_shards", "bv_sync", "bv_peer_set_hash", "bv_verify_events",
 )
 
 
@@ -133,6 +133,8 @@ def lib() -> ctypes.CDLL:
     L.bv_group_verify_batch.restype = ctypes.c_int
     L.bv_group_get_timing.argtypes = [P, ctypes.c_int, ctypes.POINTER(BvTiming)]
     L.bv_group_get_timing.restype = ctypes.c_int
+    L.bv_verify_events.argtypes = [P, P, ctypes.POINTER(BvResult)]
+    L.bv_verify_events.restype = ctypes.c_int
     L.bv_peer_set_hash.argtypes = [P, ctypes.c_uint32, P, P, P]
     L.bv_peer_set_hash.restype = ctypes.c_int
     L.bv_sync.argtypes = [P]

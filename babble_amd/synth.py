@@ -38,6 +38,9 @@ def lib():
         L.synth_events_capacity.restype = u64
         L.synth_events.argtypes = [u64, u32, u64, u32, u32, u32, i64, vp, u64, vp, vp, vp, vp, vp]
         L.synth_events.restype = u64
+        L.synth_events_fields.argtypes = [u64, u32, u64, u32, u32, u32, i64, vp, u64, vp, vp, vp, vp, vp, vp, vp,
+                                          vp, vp, vp]
+        L.synth_events_fields.restype = u64
         L.synth_blocks_capacity.argtypes = [u64, u32, u32]
         L.synth_blocks_capacity.restype = u64
         L.synth_blocks.argtypes = [u64, u32, u64, u32, u32, u32, i64, vp, u64, vp, vp, vp, vp, vp, vp, vp]
@@ -65,6 +68,54 @@ def events(n_events: int, n_creators: int = 64, seed: int = 2, n_tx: int = 1, tx
     key_off = np.arange(n_creators + 1, dtype=np.uint64) * 65
     return PackedBatch(msg[:used].copy(), off, keys, key_off, np.arange(n_events, dtype=np.uint32), item_key, r, s,
                        np.zeros(n_events, np.uint8))
+
+
+def event_fields(n_events: int, n_creators: int = 64, seed: int = 2, n_tx: int = 1, tx_bytes: int = 64,
+                 nonce_pool: int = 64, ts0: int = TS0, parents: str = "event"):
+    """The synth_events hashgraph as (PackedBatch of serialized bodies,
+    events.EventWireBatch of the same events' wire fields).  parents="event":
+    in-batch parents by event index (the core.sync DAG); "hash": every
+    parent by its known hash (a store / bootstrap replay: no in-batch
+    dependency)."""
+    from .events import PARENT_EVENT, PARENT_HASH, PARENT_NONE, EventWireBatch
+
+    L = lib()
+    cap = L.synth_events_capacity(n_events, n_tx, tx_bytes)
+    msg = np.zeros(cap + 64, np.uint8)
+    off = np.zeros(n_events + 1, np.uint64)
+    keys = np.zeros(65 * n_creators, np.uint8)
+    item_key = np.zeros(n_events, np.uint32)
+    r = np.zeros((n_events, 32), np.uint8)
+    s = np.zeros((n_events, 32), np.uint8)
+    dig = np.zeros((n_events, 32), np.uint8)
+    par = np.zeros((n_events, 2), np.int64)
+    idx = np.zeros(n_events, np.int64)
+    ts = np.zeros(n_events, np.int64)
+    tx = np.zeros(n_events * n_tx * tx_bytes, np.uint8)
+    used = L.synth_events_fields(seed, n_creators, n_events, n_tx, tx_bytes, min(nonce_pool, max(n_events, 1)), ts0,
+                                 msg.ctypes.data, cap, off.ctypes.data, keys.ctypes.data, item_key.ctypes.data,
+                                 r.ctypes.data, s.ctypes.data, dig.ctypes.data, par.ctypes.data, idx.ctypes.data,
+                                 ts.ctypes.data, tx.ctypes.data)
+    if used == 0 and n_events > 0:
+        raise RuntimeError("synth_events failed")
+    key_off = np.arange(n_creators + 1, dtype=np.uint64) * 65
+    packed = PackedBatch(msg[:used].copy(), off, keys, key_off, np.arange(n_events, dtype=np.uint32), item_key, r, s,
+                         np.zeros(n_events, np.uint8))
+    kind = np.where(par < 0, PARENT_NONE, PARENT_EVENT if parents == "event" else PARENT_HASH).astype(np.uint8)
+    if parents == "event":
+        ref = np.where(par < 0, 0, par).astype(np.uint64)
+        hashes = np.zeros((0, 32), np.uint8)
+    else:
+        ref = np.where(par < 0, 0, par).astype(np.uint64)  # parent_hashes[i] = digest of event i
+        hashes = dig
+    wire = EventWireBatch(
+        key_bytes=keys, key_off=key_off, creator=item_key, index=idx, timestamp=ts, parent_kind=kind,
+        parent_ref=ref, parent_hashes=hashes, tx_start=np.arange(n_events + 1, dtype=np.uint64) * n_tx,
+        tx_off=np.arange(n_events * n_tx + 1, dtype=np.uint64) * tx_bytes, tx_bytes=tx,
+        tx_list_nil=np.ones(n_events, np.uint8) if n_tx == 0 else None, tx_nil=None, itx_off=None,
+        itx_json=np.zeros(0, np.uint8), bsig_off=None, bsig_json=np.zeros(0, np.uint8), r_be=r.copy(), s_be=s.copy(),
+        pre=np.zeros(n_events, np.uint8))
+    return packed, wire
 
 
 @dataclass

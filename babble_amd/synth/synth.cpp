@@ -210,10 +210,26 @@ uint64_t synth_events_capacity(uint64_t n_events, uint32_t n_tx, uint32_t tx_byt
 
 // Returns total body bytes written, or 0 on failure.
 // Outputs: msg_bytes/msg_off (n_events+1), key_bytes (65 * n_creators),
-// item_key[n_events], r_be/s_be[32 * n_events].
+// item_key[n_events], r_be/s_be[32 * n_events]; optionally (non-null) the
+// wire fields of every event for bv_verify_events: digests (32 * n), parent
+// event indices (2 * n, -1 = none), Index and Timestamp (n each) and the raw
+// transactions (n * n_tx * tx_bytes).
+uint64_t synth_events_fields(uint64_t seed, uint32_t n_creators, uint64_t n_events, uint32_t n_tx, uint32_t tx_bytes,
+                             uint32_t nonce_pool, int64_t ts0, uint8_t *msg_bytes, uint64_t msg_cap,
+                             uint64_t *msg_off, uint8_t *key_bytes, uint32_t *item_key, uint8_t *r_be, uint8_t *s_be,
+                             uint8_t *digest_out, int64_t *parent_out, int64_t *index_out, int64_t *ts_out,
+                             uint8_t *tx_out);
 uint64_t synth_events(uint64_t seed, uint32_t n_creators, uint64_t n_events, uint32_t n_tx, uint32_t tx_bytes,
                       uint32_t nonce_pool, int64_t ts0, uint8_t *msg_bytes, uint64_t msg_cap, uint64_t *msg_off,
                       uint8_t *key_bytes, uint32_t *item_key, uint8_t *r_be, uint8_t *s_be) {
+  return synth_events_fields(seed, n_creators, n_events, n_tx, tx_bytes, nonce_pool, ts0, msg_bytes, msg_cap, msg_off,
+                             key_bytes, item_key, r_be, s_be, nullptr, nullptr, nullptr, nullptr, nullptr);
+}
+uint64_t synth_events_fields(uint64_t seed, uint32_t n_creators, uint64_t n_events, uint32_t n_tx, uint32_t tx_bytes,
+                             uint32_t nonce_pool, int64_t ts0, uint8_t *msg_bytes, uint64_t msg_cap,
+                             uint64_t *msg_off, uint8_t *key_bytes, uint32_t *item_key, uint8_t *r_be, uint8_t *s_be,
+                             uint8_t *digest_out, int64_t *parent_out, int64_t *index_out, int64_t *ts_out,
+                             uint8_t *tx_out) {
   if (n_creators == 0 || nonce_pool == 0) return 0;
   Ctx cx;
   Drbg dr(seed, "keys");
@@ -224,6 +240,7 @@ uint64_t synth_events(uint64_t seed, uint32_t n_creators, uint64_t n_events, uin
   }
   SplitMix rng(seed * 0x2545F4914F6CDD1Dull + 7);
   std::vector<std::string> last_hex(n_creators);  // "0X..." of each creator's latest event
+  std::vector<int64_t> last_ev(n_creators, -1);   // ... and its batch index
   std::vector<int64_t> next_index(n_creators, 0);
   std::vector<std::vector<uint8_t>> txs(n_tx, std::vector<uint8_t>(tx_bytes));
   uint64_t pos = 0;
@@ -238,6 +255,14 @@ uint64_t synth_events(uint64_t seed, uint32_t n_creators, uint64_t n_events, uin
       p0 = last_hex[c];
       p1 = last_hex[other];  // may be "" if the other creator has no event yet
     }
+    if (parent_out) {
+      parent_out[2 * i] = idx > 0 ? last_ev[c] : -1;
+      parent_out[2 * i + 1] = idx > 0 && !p1.empty() ? last_ev[other] : -1;
+    }
+    if (index_out) index_out[i] = idx;
+    if (ts_out) ts_out[i] = ts0 + (int64_t)i;
+    if (tx_out)
+      for (uint32_t t = 0; t < n_tx; t++) memcpy(tx_out + ((uint64_t)i * n_tx + t) * tx_bytes, txs[t].data(), tx_bytes);
     std::string body = event_body(txs, n_tx == 0, p0, p1, sg[c].pub, idx, ts0 + (int64_t)i);
     if (pos + body.size() > msg_cap) return 0;
     memcpy(msg_bytes + pos, body.data(), body.size());
@@ -248,6 +273,8 @@ uint64_t synth_events(uint64_t seed, uint32_t n_creators, uint64_t n_events, uin
     std::string hx = "0X";
     hexup(hx, dig, 32);
     last_hex[c] = hx;
+    last_ev[c] = (int64_t)i;
+    if (digest_out) memcpy(digest_out + 32 * i, dig, 32);
     item_key[i] = c;
     cx.sign(sg[c], (uint32_t)(idx % nonce_pool), dig, r_be + 32 * i, s_be + 32 * i);
   }

@@ -166,6 +166,19 @@ class Verifier:
         self._check(self._L.bv_sha256_batch(self._ctx, len(msgs), buf.ctypes.data, off.ctypes.data, out.ctypes.data))
         return [out[i].tobytes() for i in range(len(msgs))]
 
+    def verify_events(self, eb) -> VerifyResult:
+        """bv_verify_events over an events.EventWireBatch: the device builds,
+        hashes (DAG levels in-batch) and verifies every EventBody."""
+        keep: list = []
+        cb = eb.c_struct(keep)
+        n = eb.n_events
+        h = np.zeros((max(n, 1), 32), np.uint8)
+        st = np.zeros(max(n, 1), np.uint8)
+        bits = np.zeros(max((n + 63) // 64, 1), np.uint64)
+        res = native.BvResult(h.ctypes.data, st.ctypes.data, bits.ctypes.data)
+        self._check(self._L.bv_verify_events(self._ctx, ctypes.byref(cb), ctypes.byref(res)))
+        return VerifyResult(h[:n], st[:n], bits[: (n + 63) // 64])
+
     def peer_set_hash(self, pubkeys: Sequence[bytes]) -> bytes:
         """bv_peer_set_hash: PeerSet.Hash over the peers' key bytes (b"" for
         an empty set, as Go's []byte{})."""

@@ -143,6 +143,59 @@ int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresu
  * async call) and updates bv_get_timing. */
 int bv_sync(bv_ctx *ctx);
 
+/* Events from their wire fields.  Instead of the
+ * serialized bodies, the caller passes what a WireEvent carries
+ * (src/hashgraph/event.go:413-449) with the parents resolved as in
+ * Hashgraph.ReadWireInfo (hashgraph.go:1540-1595); the device builds every
+ * canonical EventBody JSON (event.go:38-45, Go 1.13 encoding/json, bit-exact),
+ * hashes it and verifies the creator's signature over it.  A parent may be an
+ * EARLIER event of the same batch (the in-batch DAG dependency of core.sync,
+ * core.go:214-245): its "0X"+hex is spliced into the child's body once the
+ * parent's digest is known, level by level on the device (one launch for the
+ * narrow levels of a SyncResponse).  ~2-3x fewer bytes cross PCIe than the
+ * serialized bodies (64-B tx: ~250 B per event instead of ~530).
+ * Per-event result: msg_hash (the body digest = Event.Hash) and status of the
+ * event signature (keys.Verify as composed by Event.Verify, event.go:232-247).
+ * InternalTransactions are serialized from the verbatim fragment but their
+ * own signatures are NOT verified here (use bv_verify_batch items, as the Go
+ * shim does for Event.Verify's ITX loop). */
+#define BV_PARENT_NONE 0  /* "" (wire index < 0)                              */
+#define BV_PARENT_HASH 1  /* known hash: parent_ref indexes parent_hashes     */
+#define BV_PARENT_EVENT 2 /* an earlier event of this batch: parent_ref = its
+                             index (< the child's)                            */
+typedef struct {
+  uint64_t n_events;
+  uint32_t n_keys;
+  const uint8_t *key_bytes;      /* creator keys, raw bytes (as bv_batch)      */
+  const uint64_t *key_off;       /* n_keys + 1                                 */
+  const uint32_t *creator;       /* key index per event (EventBody.Creator)    */
+  const int64_t *index;          /* EventBody.Index                            */
+  const int64_t *timestamp;      /* EventBody.Timestamp                        */
+  const uint8_t *parent_kind;    /* 2 per event: self-parent, other-parent     */
+  const uint64_t *parent_ref;    /* 2 per event (see BV_PARENT_*)              */
+  uint64_t n_parent_hashes;
+  const uint8_t *parent_hashes;  /* 32 bytes each                              */
+  const uint64_t *tx_start;      /* n_events + 1: event e has transactions
+                                    [tx_start[e], tx_start[e+1])               */
+  const uint64_t *tx_off;        /* n_tx + 1 byte offsets into tx_bytes        */
+  const uint8_t *tx_bytes;
+  const uint8_t *tx_list_nil;    /* per event, 1: Transactions is nil (NULL: none) */
+  const uint8_t *tx_nil;         /* per tx, 1: that []byte is nil (NULL: none)  */
+  const uint64_t *itx_off;       /* n_events + 1 into itx_json: encoding/json of
+                                    InternalTransactions; empty = nil (NULL: all nil) */
+  const uint8_t *itx_json;
+  const uint64_t *bsig_off;      /* same for BlockSignatures (creator = Validator) */
+  const uint8_t *bsig_json;
+  const uint8_t *r_be;           /* the event signature, as in bv_batch        */
+  const uint8_t *s_be;
+  const uint8_t *pre;
+} bv_event_batch;
+
+/* Host buffers in, results out (msg_hash: 32 * n_events; status, accept_bits
+ * per event).  BV_E_ARGS for a bad reference (an EVENT parent not earlier in
+ * the batch, an out-of-range key / hash / offset). */
+int bv_verify_events(bv_ctx *ctx, const bv_event_batch *events, bv_result *result);
+
 /* Multi-GPU: one verifier over several devices of this process (one bv_ctx
  * per device, the caller's device ordinals).  bv_group_verify_batch shards
  * the items into contiguous ranges that never split the items of one

@@ -11,6 +11,7 @@
 #include <thread>
 #include <vector>
 
+#include "../../babble_amd/csrc/evjson.h"
 #include "../../babble_amd/csrc/verify_core.h"
 
 namespace {
@@ -247,6 +248,29 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
 }
 
 // s^-1 mod N through the device chain (Montgomery in/out handled here).
+// bv_verify_events' body construction and DAG hashing on the host (the
+// device kernels' per-event code, evjson.h + sha256.h), in event order
+// (parents precede children).  bodies: sum of lengths + 64 bytes; offs:
+// n + 1; digests: 32 * n.  Returns the total body bytes.
+uint64_t emu_ev_bodies(const bv_event_batch *b, uint8_t *bodies, uint64_t cap, uint64_t *offs, uint8_t *digests) {
+  const uint64_t n = b->n_events;
+  std::vector<uint32_t> ppos(2 * n);
+  offs[0] = 0;
+  for (uint64_t e = 0; e < n; e++) offs[e + 1] = offs[e] + evj_len(*b, e, &ppos[2 * e]);
+  if (offs[n] + 64 > cap) return 0;
+  memset(bodies + offs[n], 0, 64);
+  for (uint64_t e = 0; e < n; e++) evj_write(*b, e, bodies + offs[e]);
+  std::vector<uint32_t> dig(8 * n + 8);
+  for (uint64_t e = 0; e < n; e++) {
+    for (int p = 0; p < 2; p++)
+      if (ppos[2 * e + p] != EVJ_NOPOS)
+        evj_hex32(bodies + offs[e] + ppos[2 * e + p], (const uint8_t *)&dig[8 * b->parent_ref[2 * e + p]]);
+    sha256_one(e, bodies, offs, dig.data());
+  }
+  memcpy(digests, dig.data(), 32 * n);
+  return offs[n];
+}
+
 void emu_sc_inverse(const uint32_t s_le[8], uint32_t out_le[8]) {
   sc s, sM, R2, inv, one, r;
   for (int i = 0; i < 8; i++) s.v[i] = s_le[i];

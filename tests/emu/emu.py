@@ -114,3 +114,21 @@ def dump_batch(path: str, arrs: dict) -> None:
         f.write(np.ascontiguousarray(arrs["s_be"], np.uint8).tobytes())
         if pre is not None:
             f.write(np.ascontiguousarray(pre, np.uint8).tobytes())
+
+
+def ev_bodies(eb):
+    """emu_ev_bodies over an events.EventWireBatch: (bodies: list[bytes],
+    digests[n, 32]) built by the device's own per-event code on the host."""
+    L = lib()
+    L.emu_ev_bodies.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    L.emu_ev_bodies.restype = ctypes.c_uint64
+    keep: list = []
+    cb = eb.c_struct(keep)
+    n = eb.n_events
+    cap = 1024 * n + 4 * int(eb.tx_bytes.size) + int(eb.itx_json.size) + int(eb.bsig_json.size) + 4096
+    bodies = np.zeros(cap, np.uint8)
+    offs = np.zeros(n + 1, np.uint64)
+    dig = np.zeros((max(n, 1), 32), np.uint8)
+    total = L.emu_ev_bodies(ctypes.byref(cb), bodies.ctypes.data, cap, offs.ctypes.data, dig.ctypes.data)
+    assert total == offs[n]
+    return [bodies[offs[i]:offs[i + 1]].tobytes() for i in range(n)], dig[:n]

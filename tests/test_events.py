@@ -1,0 +1,171 @@
+"""bv_verify_events: canonical EventBody JSON built from wire fields
+(babble_amd/csrc/evjson.h) and in-batch DAG hashing.
+
+CPU: the device's per-event code run by the host emulator equals Go
+encoding/json as restated by the oracle (oracle/gosemantics.py EventBody,
+event.go:38-45) on the synthetic hashgraph and on random edge cases (nil
+and empty transaction lists, nil transactions, ITX / BlockSignature
+fragments, negative Index / Timestamp, HASH / EVENT / no parents, odd key
+lengths), digests included.  GPU: the same through the C ABI, with the
+signatures verified, against the oracle.
+"""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from babble_amd import events as E
+from babble_amd import synth
+from oracle import gosemantics as gs
+from tests.emu import emu
+
+
+def random_wire(seed, n=300):
+    """(EventWireBatch, oracle EventBodies, signatures as (pre, r, s)):
+    parents reference earlier events of the batch or known hashes."""
+    rng = random.Random(seed)
+    b = E.EventBatchBuilder()
+    keys = [bytes(rng.getrandbits(8) for _ in range(rng.choice([65, 65, 65, 33, 0, 70]))) for _ in range(5)]
+    kidx = [b.add_key(k) for k in keys]
+    bodies, digests = [], []
+    for e in range(n):
+        c = rng.randrange(len(keys))
+        parents, pstr = [], []
+        for _ in range(2):
+            r = rng.random()
+            if r < 0.2 or e == 0:
+                parents.append(None)
+                pstr.append("")
+            elif r < 0.5:
+                h = bytes(rng.getrandbits(8) for _ in range(32))
+                parents.append(("hash", h))
+                pstr.append(gs.EncodeToString(h))
+            else:
+                j = rng.randrange(max(0, e - 8), e)
+                parents.append(("event", j))
+                pstr.append(gs.EncodeToString(digests[j]))
+        r = rng.random()
+        txs = None if r < 0.15 else ([] if r < 0.25 else [
+            None if rng.random() < 0.1 else bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 80)))
+            for _ in range(rng.randrange(1, 4))])
+        itxs = None
+        if rng.random() < 0.1:
+            itxs = [gs.InternalTransaction(gs.InternalTransactionBody(rng.randrange(2), gs.Peer(
+                "h:%d" % e, "0X04AB", "<m&>")), "r|s")]
+        bsigs = None
+        if rng.random() < 0.1:
+            bsigs = [gs.BlockSignature(keys[c], rng.randrange(9), "a| b")] if rng.random() < 0.5 else []
+        idx = rng.choice([0, 1, 7, -5, 2**62, -(2**63)])
+        ts = rng.choice([0, 1600000000 + e, -1, 2**63 - 1])
+        body = gs.EventBody(Transactions=txs, InternalTransactions=itxs, Parents=pstr, Creator=keys[c], Index=idx,
+                            BlockSignatures=bsigs, Timestamp=ts)
+        raw = body.Marshal()
+        b.add_event(kidx[c], idx, ts, parents, txs, (0, b"\1" * 32, b"\2" * 32),
+                    itx_json=frag_json(itxs), bsig_json=frag_json(bsigs))
+        bodies.append(raw)
+        digests.append(hashlib.sha256(raw).digest())
+    return b.pack(), bodies, digests
+
+
+def frag_json(xs):
+    """encoding/json of a slice of ITX / BlockSignature (b"" = nil)."""
+    if xs is None:
+        return b""
+    return gs.json_list(xs, lambda t: t.json())
+
+
+@pytest.mark.parametrize("parents", ["event", "hash"])
+def test_emu_bodies_equal_synth_hashgraph(parents):
+    packed, wire = synth.event_fields(600, n_creators=5, seed=7, parents=parents)
+    bodies, dig = emu.ev_bodies(wire)
+    for i in range(packed.n_items):
+        assert bodies[i] == packed.message(i), i
+        assert dig[i].tobytes() == hashlib.sha256(bodies[i]).digest()
+
+
+def test_emu_bodies_equal_oracle_edge_cases():
+    for seed in (1, 2, 3):
+        wire, want, wd = random_wire(seed)
+        bodies, dig = emu.ev_bodies(wire)
+        assert bodies == want
+        assert [d.tobytes() for d in dig] == wd
+
+
+def test_no_transactions_and_wire_bytes():
+    packed, wire = synth.event_fields(50, n_creators=3, seed=9, n_tx=0)
+    bodies, _ = emu.ev_bodies(wire)
+    assert bodies == [packed.message(i) for i in range(50)]
+    assert b'"Transactions":null' in bodies[0]
+    # the wire form is much smaller than the serialized bodies
+    p2, w2 = synth.event_fields(1000, n_creators=4, seed=3)
+    assert E.wire_bytes(w2) * 2 < p2.msg_bytes.nbytes + p2.r_be.nbytes + p2.s_be.nbytes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parents,n", [("event", 2000), ("hash", 200_000)])
+def test_verify_events_matches_oracle(parents, n):
+    from babble_amd.verifier import Verifier
+    from oracle import coracle
+
+    packed, wire = synth.event_fields(n, n_creators=8, seed=11, parents=parents)
+    rng = np.random.default_rng(3)
+    bad = rng.choice(n, size=max(1, n // 100), replace=False)
+    wire.s_be[bad, 5] ^= 0x20
+    packed.s_be[bad, 5] ^= 0x20
+    v = Verifier(0)
+    try:
+        res = v.verify_events(wire)
+        h, st, bits = coracle.verify_batch(packed.as_dict())
+        assert np.array_equal(res.msg_hash, h)
+        assert np.array_equal(res.status, st) and np.array_equal(res.accept_bits, bits)
+        assert int((st != 1).sum()) == len(bad)
+    finally:
+        v.close()
+
+
+@pytest.mark.gpu
+def test_verify_events_edge_cases_digests():
+    from babble_amd.verifier import Verifier
+
+    v = Verifier(0)
+    try:
+        for seed in (4, 5):
+            wire, want, wd = random_wire(seed, n=500)
+            res = v.verify_events(wire)
+            assert [d.tobytes() for d in res.msg_hash] == wd
+    finally:
+        v.close()
+
+
+@pytest.mark.gpu
+def test_verify_events_sync_sized_dag_depth():
+    """A SyncLimit-sized batch (config.go:44) from 4 creators: ~250 DAG
+    levels hashed on the device (narrow levels in one launch)."""
+    from babble_amd.verifier import Verifier
+    from oracle import coracle
+
+    packed, wire = synth.event_fields(1000, n_creators=4, seed=12, parents="event")
+    v = Verifier(0)
+    try:
+        res = v.verify_events(wire)
+        h, st, _ = coracle.verify_batch(packed.as_dict())
+        assert np.array_equal(res.msg_hash, h) and np.all(res.status == 1)
+    finally:
+        v.close()
+
+
+@pytest.mark.gpu
+def test_verify_events_rejects_forward_reference():
+    from babble_amd import native
+    from babble_amd.verifier import Verifier
+
+    _, wire = synth.event_fields(10, n_creators=2, seed=13)
+    wire.parent_kind[3, 0] = E.PARENT_EVENT
+    wire.parent_ref[3, 0] = 5
+    v = Verifier(0)
+    try:
+        with pytest.raises(native.BvError):
+            v.verify_events(wire)
+    finally:
+        v.close()
