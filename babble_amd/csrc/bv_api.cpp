@@ -623,13 +623,22 @@ int bv_validate_host_batch(bv_ctx *ctx, const bv_batch *b) {
   // validate host offsets (a bad offset must not become an OOB device read)
   if (n_msgs && b->msg_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "msg_off[0] != 0");
   if (n_keys && b->key_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "key_off[0] != 0");
-  for (uint64_t m = 0; m < n_msgs; m++)
-    if (b->msg_off[m] > b->msg_off[m + 1]) return bv_fail(ctx, BV_E_ARGS, "msg_off not monotone");
   for (uint32_t k = 0; k < n_keys; k++)
     if (b->key_off[k] > b->key_off[k + 1]) return bv_fail(ctx, BV_E_ARGS, "key_off not monotone");
-  for (uint64_t i = 0; i < n_items; i++)
-    if (b->item_msg[i] >= n_msgs || b->item_key[i] >= n_keys)
-      return bv_fail(ctx, BV_E_ARGS, "item index out of range");
+  // the O(n) checks run on the copy pool (1M items: ~0.3 ms instead of ~3)
+  constexpr uint64_t kGrain = 1 << 17;
+  if (!ctx->pool->parallel_for(n_msgs, kGrain, [b](uint64_t lo, uint64_t hi) {
+        for (uint64_t m = lo; m < hi; m++)
+          if (b->msg_off[m] > b->msg_off[m + 1]) return false;
+        return true;
+      }))
+    return bv_fail(ctx, BV_E_ARGS, "msg_off not monotone");
+  if (!ctx->pool->parallel_for(n_items, kGrain, [b, n_msgs, n_keys](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; i++)
+          if (b->item_msg[i] >= n_msgs || b->item_key[i] >= n_keys) return false;
+        return true;
+      }))
+    return bv_fail(ctx, BV_E_ARGS, "item index out of range");
   return BV_OK;
 }
 
@@ -746,6 +755,7 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
     m0 = m1;
   }
   HIPCHK(hipEventRecord(ctx->ev[E_STAGED], cs), BV_E_LAUNCH, "event");
+  call->ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_STAGED], 0), BV_E_LAUNCH, "join staging");
   HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
   rc = bv_run_device(ctx, &d, nullptr, nullptr, nullptr, st, true, kc);
@@ -780,6 +790,7 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
 
 int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call *call, bool bits_out) {
   HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "verify sync");
+  const auto t_out = std::chrono::steady_clock::now();
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   if (res->msg_hash && n_msgs) ctx->pool->copy(res->msg_hash, call->pout, n_msgs * 32);
   if (res->status && n_items) ctx->pool->copy(res->status, call->pout + call->o_st, n_items);
@@ -788,8 +799,10 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
   bv_read_timing(ctx);
   ctx->timing.ms_h2d = elapsed(ctx->ev[E_CALL], ctx->ev[E_STAGED]);
   ctx->timing.ms_d2h = elapsed(ctx->ev[E_END], ctx->ev[E_OUT]);
-  ctx->timing.ms_host =
-      std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call->t0).count();
+  const auto t_end = std::chrono::steady_clock::now();
+  ctx->timing.ms_host = std::chrono::duration<float, std::milli>(t_end - call->t0).count();
+  ctx->timing.ms_host_prep = call->ms_prep;
+  ctx->timing.ms_host_out = std::chrono::duration<float, std::milli>(t_end - t_out).count();
   return BV_OK;
 }
 

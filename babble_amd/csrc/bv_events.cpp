@@ -39,29 +39,40 @@ int validate(bv_ctx *ctx, const bv_event_batch *b) {
   const uint64_t n_tx = b->tx_start[n];
   if (n_tx && !b->tx_off) return bv_fail(ctx, BV_E_ARGS, "null tx_off");
   if (n_tx && b->tx_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "tx_off[0] != 0");
-  for (uint64_t t = 0; t < n_tx; t++)
-    if (b->tx_off[t] > b->tx_off[t + 1]) return bv_fail(ctx, BV_E_ARGS, "tx_off not monotone");
+  constexpr uint64_t kGrain = 1 << 17;
+  if (!ctx->pool->parallel_for(n_tx, kGrain, [b](uint64_t lo, uint64_t hi) {
+        for (uint64_t t = lo; t < hi; t++)
+          if (b->tx_off[t] > b->tx_off[t + 1]) return false;
+        return true;
+      }))
+    return bv_fail(ctx, BV_E_ARGS, "tx_off not monotone");
   if (n_tx && b->tx_off[n_tx] && !b->tx_bytes) return bv_fail(ctx, BV_E_ARGS, "null tx bytes");
-  for (const uint64_t *off : {b->itx_off, b->bsig_off}) {
-    if (!off) continue;
-    if (off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "fragment offsets must start at 0");
-    for (uint64_t e = 0; e < n; e++)
-      if (off[e] > off[e + 1]) return bv_fail(ctx, BV_E_ARGS, "fragment offsets not monotone");
-  }
+  for (const uint64_t *off : {b->itx_off, b->bsig_off})
+    if (off && off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "fragment offsets must start at 0");
   if ((b->itx_off && b->itx_off[n] && !b->itx_json) || (b->bsig_off && b->bsig_off[n] && !b->bsig_json))
     return bv_fail(ctx, BV_E_ARGS, "null fragment bytes");
-  for (uint64_t e = 0; e < n; e++) {
-    if (b->creator[e] >= b->n_keys) return bv_fail(ctx, BV_E_ARGS, "creator index out of range");
-    if (b->tx_start[e] > b->tx_start[e + 1]) return bv_fail(ctx, BV_E_ARGS, "tx_start not monotone");
-    for (int p = 0; p < 2; p++) {
-      const uint8_t k = b->parent_kind[2 * e + p];
-      const uint64_t r = b->parent_ref[2 * e + p];
-      if (k > BV_PARENT_EVENT) return bv_fail(ctx, BV_E_ARGS, "bad parent kind");
-      if (k == BV_PARENT_HASH && (r >= b->n_parent_hashes || !b->parent_hashes))
-        return bv_fail(ctx, BV_E_ARGS, "parent hash index out of range");
-      if (k == BV_PARENT_EVENT && r >= e) return bv_fail(ctx, BV_E_ARGS, "in-batch parent must precede its child");
-    }
-  }
+  for (const uint64_t *off : {b->itx_off, b->bsig_off})
+    if (off && !ctx->pool->parallel_for(n, kGrain, [off](uint64_t lo, uint64_t hi) {
+          for (uint64_t e = lo; e < hi; e++)
+            if (off[e] > off[e + 1]) return false;
+          return true;
+        }))
+      return bv_fail(ctx, BV_E_ARGS, "fragment offsets not monotone");
+  if (!ctx->pool->parallel_for(n, kGrain, [b](uint64_t lo, uint64_t hi) {
+        for (uint64_t e = lo; e < hi; e++) {
+          if (b->creator[e] >= b->n_keys || b->tx_start[e] > b->tx_start[e + 1]) return false;
+          for (int p = 0; p < 2; p++) {
+            const uint8_t k = b->parent_kind[2 * e + p];
+            const uint64_t r = b->parent_ref[2 * e + p];
+            if (k > BV_PARENT_EVENT) return false;
+            if (k == BV_PARENT_HASH && (r >= b->n_parent_hashes || !b->parent_hashes)) return false;
+            if (k == BV_PARENT_EVENT && r >= e) return false;  // an in-batch parent precedes its child
+          }
+        }
+        return true;
+      }))
+    return bv_fail(ctx, BV_E_ARGS,
+                   "bad event reference (creator, tx_start, or a parent not earlier in the batch / out of range)");
   return BV_OK;
 }
 
@@ -82,8 +93,7 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
 
   // DAG levels over in-batch parents (refs point backwards: one pass)
   std::vector<uint32_t> level, order, level_off;
-  bool dag = false;
-  for (uint64_t i = 0; i < 2 * n && !dag; i++) dag = eb->parent_kind[i] == BV_PARENT_EVENT;
+  const bool dag = memchr(eb->parent_kind, BV_PARENT_EVENT, 2 * n) != nullptr;
   if (dag) {
     level.assign(n, 0);
     uint32_t nl = 1;
@@ -156,6 +166,7 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
     HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
   }
   HIPCHK(hipEventRecord(ctx->ev[E_STAGED], st), BV_E_LAUNCH, "event");
+  call.ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call.t0).count();
 
   // the same batch over device pointers
   bv_event_batch d = *eb;

@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -100,6 +102,28 @@ struct CopyPool {
     cv.notify_all();
     for (auto &t : th) t.join();
   }
+  // fn(lo, hi) over [0, n) in `grain`-sized ranges on the pool and the
+  // caller; returns false if any range returned false.
+  bool parallel_for(uint64_t n, uint64_t grain, const std::function<bool(uint64_t, uint64_t)> &fn) {
+    if (n <= grain || th.empty()) return fn(0, n);
+    const uint64_t parts = (n + grain - 1) / grain;
+    std::atomic<bool> ok{true};
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (uint64_t i = 1; i < parts; i++) {
+        const uint64_t lo = i * grain, hi = std::min(n, lo + grain);
+        q.push_back([&fn, &ok, lo, hi]() {
+          if (!fn(lo, hi)) ok = false;
+        });
+        pending++;
+      }
+    }
+    cv.notify_all();
+    if (!fn(0, std::min(n, grain))) ok = false;
+    std::unique_lock<std::mutex> lk(mu);
+    done_cv.wait(lk, [this]() { return pending == 0; });
+    return ok;
+  }
   // dst <- src (n bytes); returns when done.  Small copies stay on the caller.
   void copy(void *dst, const void *src, size_t n) {
     constexpr size_t kPiece = 2ull << 20;
@@ -175,6 +199,7 @@ struct bv_ctx {
 // one in-flight host-entry call (bv_host_launch -> bv_host_finish)
 struct bv_host_call {
   std::chrono::steady_clock::time_point t0;
+  float ms_prep = 0;
   uint8_t *pout = nullptr;
   size_t o_st = 0, o_bits = 0;
 };

@@ -68,10 +68,36 @@ __global__ void __launch_bounds__(256) k_ev_len(bv_event_batch b, uint64_t *__re
   ppos[2 * e + 1] = pp[1];
 }
 
-__global__ void __launch_bounds__(256) k_ev_write(bv_event_batch b, const uint64_t *__restrict__ offs,
-                                                  uint8_t *__restrict__ bodies) {
-  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < b.n_events) evj_write(b, e, bodies + offs[e]);
+// Bodies of EV_WRITE_NT consecutive events are contiguous in the output:
+// each thread writes its body byte by byte into LDS, then the block stores
+// the whole range with coalesced dword stores (the partial dwords at either
+// end, shared with the neighbouring blocks' bodies, byte by byte).  Blocks
+// whose bodies exceed the LDS buffer write straight to global memory.
+#define EV_WRITE_NT 64
+#define EV_WRITE_CAP (32 * 1024)
+__global__ void __launch_bounds__(EV_WRITE_NT) k_ev_write(bv_event_batch b, const uint64_t *__restrict__ offs,
+                                                          uint8_t *__restrict__ bodies) {
+  __shared__ uint32_t lds[EV_WRITE_CAP / 4 + 4];
+  const uint64_t n = b.n_events;
+  const uint64_t e0 = (uint64_t)blockIdx.x * EV_WRITE_NT, e = e0 + threadIdx.x;
+  const uint64_t e1 = e0 + EV_WRITE_NT < n ? e0 + EV_WRITE_NT : n;
+  const uint64_t base = offs[e0], end = offs[e1], a0 = base & ~(uint64_t)3;
+  if (end - a0 > EV_WRITE_CAP) {  // uniform per block
+    if (e < n) evj_write(b, e, bodies + offs[e]);
+    return;
+  }
+  uint8_t *l = (uint8_t *)lds;
+  if (e < e1) evj_write(b, e, l + (offs[e] - a0));
+  __syncthreads();
+  const uint64_t d0 = (base + 3) & ~(uint64_t)3, d1 = end & ~(uint64_t)3;
+  if (d0 <= d1) {
+    for (uint64_t q = base + threadIdx.x; q < d0; q += EV_WRITE_NT) bodies[q] = l[q - a0];
+    for (uint64_t q = d1 + threadIdx.x; q < end; q += EV_WRITE_NT) bodies[q] = l[q - a0];
+    for (uint64_t q = d0 + 4 * threadIdx.x; q < d1; q += 4 * EV_WRITE_NT)
+      *(uint32_t *)(bodies + q) = lds[(q - a0) >> 2];
+  } else {  // the range lies inside one dword
+    for (uint64_t q = base + threadIdx.x; q < end; q += EV_WRITE_NT) bodies[q] = l[q - a0];
+  }
 }
 
 // Splice the in-batch parents' hex (their digests final) into event e's
@@ -506,7 +532,7 @@ hipError_t ev_build(hipStream_t st, const bv_event_batch &b, uint64_t *lens, uin
   if (e != hipSuccess) return e;
   e = hipcub::DeviceScan::InclusiveSum(tmp, *tmp_bytes, lens, offs + 1, (int)n, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_ev_write, grid1(n, 256), dim3(256), 0, st, b, offs, bodies);
+  hipLaunchKernelGGL(k_ev_write, grid1(n, EV_WRITE_NT), dim3(EV_WRITE_NT), 0, st, b, offs, bodies);
   return hipGetLastError();
 }
 

@@ -324,23 +324,25 @@ def verify_events(events: Sequence[Event], verifier=None) -> List[Outcome]:
     out = []
     for ev, (itx_items, item, m) in zip(events, plan):
         ev._hash = res.msg_hash[m].tobytes()
-        o = None
-        for k in itx_items:  # event.go:222-230, in order; the first failure wins
-            if k is None:
-                o = Outcome(False, "slice bounds out of range", panic=True)
-                break
-            st = int(res.status[k])
-            if st == ACCEPT:
-                continue
-            if st == REJECT_ERR:
-                o = Outcome(False, _ERR_PARTS)
-            elif st == REF_PANIC:
-                o = _item_outcome(st)
-            else:
-                o = Outcome(False, "invalid signature on internal transaction")
-            break
-        out.append(o if o is not None else _item_outcome(int(res.status[item])))
+        itx_st = [None if k is None else int(res.status[k]) for k in itx_items]
+        out.append(compose_event_outcome(itx_st, int(res.status[item])))
     return out
+
+
+def compose_event_outcome(itx_statuses: Sequence[Optional[int]], event_status: int) -> Outcome:
+    """Event.Verify's order (event.go:219-247): each ITX in order, the first
+    failure wins (None = PubKeyBytes panicked); then the event signature."""
+    for st in itx_statuses:  # event.go:222-230
+        if st is None:
+            return Outcome(False, "slice bounds out of range", panic=True)
+        if st == ACCEPT:
+            continue
+        if st == REJECT_ERR:
+            return Outcome(False, _ERR_PARTS)
+        if st == REF_PANIC:
+            return _item_outcome(st)
+        return Outcome(False, "invalid signature on internal transaction")
+    return _item_outcome(event_status)
 
 
 def verify_block_signatures(block: Block, sigs: Sequence[BlockSignature], verifier=None) -> List[Outcome]:

@@ -72,6 +72,8 @@ class BvTiming(ctypes.Structure):
         ("ms_h2d", ctypes.c_float),
         ("ms_d2h", ctypes.c_float),
         ("ms_host", ctypes.c_float),
+        ("ms_host_prep", ctypes.c_float),
+        ("ms_host_out", ctypes.c_float),
         ("key_path", ctypes.c_uint32),
         ("kc_hits", ctypes.c_uint32),
         ("kc_builds", ctypes.c_uint32),

@@ -29,11 +29,13 @@ means it was new to the store.
 """
 from __future__ import annotations
 
+import re
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
+from . import gojson as J
 from .hashgraph import (BlockSignature, Event, EventBody, InternalTransaction, Outcome, Peer, DecodeFromString,
-                        EncodeToString, default_verifier, verify_events)
+                        EncodeToString, _item_outcome, default_verifier, verify_events, verify_itxs)
 
 
 @dataclass
@@ -120,15 +122,49 @@ def read_wire_batch(wevents: Sequence[WireEvent], repertoire_by_id: Dict[int, Pe
     n = len(wevents)
     reads = [WireRead() for _ in range(n)]
     levels = [-1] * n
-    # pending[i] = (creator_bytes, [self, other] as hex str or in-batch index)
+    pending, has_child, err_at, err = _resolve_batch(wevents, repertoire_by_id, participant_event)
+    if err_at is not None:
+        reads[err_at].err = err
+    for i in range(n):
+        if pending[i] is None:
+            continue
+        lvl = 0
+        for p in pending[i][1]:
+            if isinstance(p, int):
+                lvl = max(lvl, levels[p] + 1)
+        levels[i] = lvl
+
+    hexes: Dict[int, str] = {}
+    n_levels = max(levels) + 1 if n else 0
+    for lvl in range(n_levels):
+        idx = [i for i in range(n) if levels[i] == lvl]
+        for i in idx:
+            cb, ps = pending[i]
+            ps = [hexes[p] if isinstance(p, int) else p for p in ps]
+            reads[i].event = Event(Body=_body(wevents[i], cb, ps[0], ps[1]), Signature=wevents[i].Signature)
+        need = [i for i in idx if has_child[i]]
+        if need:  # one device SHA-256 batch per DAG level
+            digests = v.sha256([reads[i].event.Body.Marshal() for i in need])
+            for i, d in zip(need, digests):
+                reads[i].event._hash = d
+                hexes[i] = EncodeToString(d)
+    return reads, levels
+
+
+def _resolve_batch(wevents: Sequence[WireEvent], repertoire_by_id: Dict[int, Peer],
+                   participant_event: ParticipantEvent):
+    """ReadWireInfo's lookups for a whole SyncResponse, without hashing:
+    (pending, has_child, err_at, err) where pending[i] = (creator bytes,
+    [self, other]) with each parent "" / a store hex / an in-batch index, up
+    to the first error (event err_at with Go's text err)."""
+    n = len(wevents)
     pending: List[Optional[Tuple[bytes, List[object]]]] = [None] * n
     in_batch: Dict[Tuple[str, int], int] = {}
     has_child = [False] * n
     for i, we in enumerate(wevents):
         creator = repertoire_by_id.get(we.Body.CreatorID)
         if creator is None:
-            reads[i].err = "Creator %d not found" % we.Body.CreatorID
-            break
+            return pending, has_child, i, "Creator %d not found" % we.Body.CreatorID
         cpk = creator.PubKeyString()
         creator_bytes = DecodeFromString(cpk)
         parents: List[object] = ["", ""]
@@ -147,32 +183,13 @@ def read_wire_batch(wevents: Sequence[WireEvent], repertoire_by_id: Dict[int, Pe
                     err = "OtherParent (creator: %d, index: %d) not found" % (we.Body.OtherParentCreatorID,
                                                                               we.Body.OtherParentIndex)
         if err is not None:
-            reads[i].err = err
-            break
-        lvl = 0
+            return pending, has_child, i, err
         for p in parents:
             if isinstance(p, int):
                 has_child[p] = True
-                lvl = max(lvl, levels[p] + 1)
-        levels[i] = lvl
         pending[i] = (creator_bytes, parents)
         in_batch.setdefault((cpk, we.Body.Index), i)
-
-    hexes: Dict[int, str] = {}
-    n_levels = max(levels) + 1 if n else 0
-    for lvl in range(n_levels):
-        idx = [i for i in range(n) if levels[i] == lvl]
-        for i in idx:
-            cb, ps = pending[i]
-            ps = [hexes[p] if isinstance(p, int) else p for p in ps]
-            reads[i].event = Event(Body=_body(wevents[i], cb, ps[0], ps[1]), Signature=wevents[i].Signature)
-        need = [i for i in idx if has_child[i]]
-        if need:  # one device SHA-256 batch per DAG level
-            digests = v.sha256([reads[i].event.Body.Marshal() for i in need])
-            for i, d in zip(need, digests):
-                reads[i].event._hash = d
-                hexes[i] = EncodeToString(d)
-    return reads, levels
+    return pending, has_child, None, None
 
 
 def _resolve(pk: str, index: int, participant_event: ParticipantEvent, in_batch: Dict[Tuple[str, int], int]):
@@ -214,4 +231,69 @@ def sync_verify(wevents: Sequence[WireEvent], repertoire_by_id: Dict[int, Peer],
     outcomes = verify_events(events, verifier)
     for e, h in zip(events, cached):
         assert h is None or h == e._hash, "level hash disagrees with the verify batch digest"
+    return events, outcomes, read_err
+
+
+_HEX_RE = re.compile(r"0X[0-9A-F]{64}")
+
+
+def sync_verify_device(wevents: Sequence[WireEvent], repertoire_by_id: Dict[int, Peer],
+                       participant_event: ParticipantEvent,
+                       verifier=None) -> Tuple[List[Event], List[Outcome], Optional[str]]:
+    """sync_verify with the bodies built ON THE DEVICE (bv_verify_events): the
+    resolved wire fields cross PCIe, the device serializes every EventBody,
+    hashes the in-batch DAG level by level (narrow levels in one launch) and
+    verifies every signature; events carrying InternalTransactions get their
+    ITX items verified in one more bv_verify_batch (Event.Verify's order,
+    event.go:222-230).  Same results as sync_verify (tests/test_sync.py).
+    Falls back to sync_verify if a store hash is not a canonical Event.Hex()."""
+    from .events import EventBatchBuilder
+
+    v = verifier or default_verifier()
+    pending, _, err_at, read_err = _resolve_batch(wevents, repertoire_by_id, participant_event)
+    n = err_at if err_at is not None else len(wevents)
+    if n == 0:
+        return [], [], read_err
+    if any(isinstance(p, str) and p and not _HEX_RE.fullmatch(p) for i in range(n) for p in pending[i][1]):
+        return sync_verify(wevents, repertoire_by_id, participant_event, verifier)
+    eb = EventBatchBuilder()
+    bsigs = []
+    for i in range(n):
+        we = wevents[i]
+        cb, ps = pending[i]
+        par = [None if p == "" else ("event", p) if isinstance(p, int) else ("hash", bytes.fromhex(p[2:])) for p in ps]
+        itxs = we.Body.InternalTransactions
+        bs = we.BlockSignatures(cb)
+        bsigs.append(bs)
+        eb.add_event(eb.add_key(cb), we.Body.Index, we.Body.Timestamp, par, we.Body.Transactions, we.Signature,
+                     itx_json=b"" if itxs is None else J.slice_(itxs, lambda t: t.json()),
+                     bsig_json=b"" if bs is None else J.slice_(bs, lambda t: t.json()))
+    res = v.verify_events(eb.pack())
+    digests = [res.msg_hash[i].tobytes() for i in range(n)]
+    itx_events = [i for i in range(n) if wevents[i].Body.InternalTransactions]
+    itx_out = {}
+    if itx_events:
+        flat = [t for i in itx_events for t in wevents[i].Body.InternalTransactions]
+        outs = verify_itxs(flat, v)
+        k = 0
+        for i in itx_events:
+            m = len(wevents[i].Body.InternalTransactions)
+            itx_out[i] = outs[k:k + m]
+            k += m
+    events, outcomes = [], []
+    for i in range(n):
+        cb, ps = pending[i]
+        ps = [EncodeToString(digests[p]) if isinstance(p, int) else p for p in ps]
+        we = wevents[i]
+        ev = Event(Body=EventBody(Transactions=we.Body.Transactions, InternalTransactions=we.Body.InternalTransactions,
+                                  BlockSignatures=bsigs[i], Parents=ps, Creator=cb, Index=we.Body.Index,
+                                  Timestamp=we.Body.Timestamp), Signature=we.Signature)
+        ev._hash = digests[i]
+        events.append(ev)
+        o = _item_outcome(int(res.status[i]))
+        for io in itx_out.get(i, []):  # event.go:222-230: the first ITX failure wins
+            if not io.ok or io.panic:
+                o = io if (io.panic or io.err) else Outcome(False, "invalid signature on internal transaction")
+                break
+        outcomes.append(o)
     return events, outcomes, read_err

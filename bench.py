@@ -277,6 +277,7 @@ def main():
         line["warm"] = warm_leg(args, dev, world, dist, local, step_with)
         line["host_entry"] = host_entry_leg(args, v, batch)
         line["latency_ms"] = latency_leg(args)
+        line["events_entry"] = events_entry_leg(args)
     if rank == 0:
         if world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(batch, args.cpu_seconds)
@@ -332,6 +333,53 @@ def host_entry_leg(args, v, batch):
             "pcie_gb_s": staged / (h2d * 1e-3) / 1e9 if h2d > 0 else None,
             "note": "inputs in pageable host memory; staged through pinned chunks, hashing overlaps the transfer; "
                     "PCIe-bound (~520 B per event crosses the link)"}
+
+
+def events_entry_leg(args):
+    """bv_verify_events: wire fields in, the device
+    builds every canonical EventBody, hashes and verifies.  `bulk`: the C2
+    events with every parent a known hash (a store replay, no in-batch
+    dependency), host buffers in / results out; `sync_dag`: a SyncLimit
+    (1000) SyncResponse from 4 creators whose parents are earlier events of
+    the batch (~250 DAG levels hashed on the device), median latency, key
+    cache warm."""
+    import numpy as np
+
+    from babble_amd import events as E
+    from babble_amd import native, synth
+    from babble_amd.verifier import Verifier
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    out = {}
+    packed, wire = synth.event_fields(args.events, n_creators=args.creators, seed=2, parents="hash")
+    del packed
+    v = Verifier(device=local)
+    v.verify_events(wire)
+    reps = max(2, min(5, args.steps))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = v.verify_events(wire)
+    el = (time.perf_counter() - t0) / reps
+    assert np.all(res.status == 1)
+    tm = v.timing()
+    wb = E.wire_bytes(wire)
+    out["bulk"] = {"value": args.events / el, "unit": "verifies/s", "ms_per_call": el * 1e3, "ms_h2d": tm["ms_h2d"],
+                   "bytes_staged": wb, "bytes_per_event": wb / args.events,
+                   "pcie_gb_s": wb / (tm["ms_h2d"] * 1e-3) / 1e9 if tm["ms_h2d"] > 0 else None}
+    v.close()
+    _, dag = synth.event_fields(1000, n_creators=4, seed=31, parents="event")
+    vc = Verifier(device=local, flags=native.F_KEY_CACHE)
+    vc.verify_events(dag)
+    ts = []
+    for _ in range(15):
+        t0 = time.perf_counter()
+        res = vc.verify_events(dag)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    assert np.all(res.status == 1)
+    out["sync_dag_1000"] = {"ms_median": float(np.median(ts)), "creators": 4,
+                            "dag_levels": int(1000 // 4)}
+    vc.close()
+    return out
 
 
 def latency_leg(args):

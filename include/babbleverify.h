@@ -114,6 +114,9 @@ typedef struct {
   float ms_d2h;      /* device -> host results after the last kernel            */
   float ms_host;     /* wall clock of the whole call on the host (host entry
                         point: staging, PCIe, kernels, copy-out)                */
+  float ms_host_prep; /* host: validation + staging copies, call start -> the
+                         last input copy enqueued                               */
+  float ms_host_out;  /* host: results copied out after the device finished    */
   uint32_t key_path; /* 0: per-lane generic path; 8 / 12: per-batch K8 / K12
                         key tables; 20: key-cache (KC) tables                   */
   uint32_t kc_hits;   /* batch keys found in the key cache                      */

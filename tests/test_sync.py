@@ -164,3 +164,33 @@ def test_missing_self_parent_not_found_text():
     reads, _ = S.read_wire_batch(wevents, rep, pe, verifier=HashlibStub())
     assert reads[t].err == "ParticipantEvents, %d, Not Found" % we.Body.SelfParentIndex
     del cpk
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bad", [None, 33])
+def test_sync_verify_device_equals_host_path(bad):
+    """sync_verify_device (bodies serialized and DAG-hashed ON the device,
+    bv_verify_events) == sync_verify (host bodies, per-level hashing): same
+    bodies, digests, outcomes and first read error."""
+    import time
+
+    from babble_amd.verifier import Verifier
+
+    corrupt = {5, 64, 100}
+    wevents, bodies, rep, pe = make_sync(seed=17, n=160, corrupt=corrupt, bad_creator_at=bad)
+    v = Verifier(0)
+    try:
+        t0 = time.perf_counter()
+        ev_h, out_h, err_h = S.sync_verify(wevents, rep, pe, v)
+        t1 = time.perf_counter()
+        ev_d, out_d, err_d = S.sync_verify_device(wevents, rep, pe, v)
+        t2 = time.perf_counter()
+        print(f"host-level path {1e3 * (t1 - t0):.1f} ms, device path {1e3 * (t2 - t1):.1f} ms")
+        assert err_h == err_d and len(ev_h) == len(ev_d)
+        for a, b, (body, _) in zip(ev_h, ev_d, bodies):
+            assert a.Body.Marshal() == b.Body.Marshal() == body.Marshal()
+            assert a.Hash() == b.Hash() == body.Hash()
+        assert [(o.ok, o.err, o.panic) for o in out_h] == [(o.ok, o.err, o.panic) for o in out_d]
+        assert [t for t, o in enumerate(out_d) if not o.ok] == sorted(c for c in corrupt if c < len(out_d))
+    finally:
+        v.close()
