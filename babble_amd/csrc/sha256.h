@@ -90,8 +90,25 @@ DEV void sha256_msg(uint32_t h[8], const uint8_t *base, uint64_t off, uint64_t l
       // full data block: 17 aligned dwords, realigned
       const uint32_t *src = wbase + blk * 16;
       uint32_t d[17];
+#if defined(__HIP_DEVICE_COMPILE__)
+      // 4 dwordx4 loads at dword alignment (gfx950 global loads need not be
+      // 16-byte aligned): a quarter of the load instructions, and each lane
+      // touches a cache line once per load instead of four times
+      typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+      const u32x4a4 *v = (const u32x4a4 *)src;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const u32x4a4 x = v[i];
+        d[4 * i] = x.x;
+        d[4 * i + 1] = x.y;
+        d[4 * i + 2] = x.z;
+        d[4 * i + 3] = x.w;
+      }
+      d[16] = src[16];
+#else
 #pragma unroll
       for (int i = 0; i < 17; i++) d[i] = src[i];
+#endif
 #pragma unroll
       for (int i = 0; i < 16; i++) w[i] = bswap32(alignbyte(d[i + 1], d[i], sh));
     } else {
