@@ -146,6 +146,24 @@ def pmc_profile(n_items: int):
     return tj if tj.get("items_per_launch") == n_items else None
 
 
+def corrupted(rank: int, n: int):
+    """The seeded items of rank `rank`'s shard whose r has a bit flipped."""
+    import numpy as np
+
+    rng = np.random.default_rng(7919 + rank)
+    return np.sort(rng.choice(n, max(1, n // 10_000), replace=False))
+
+
+def expected_words(rank: int, n: int):
+    import numpy as np
+
+    ok = np.ones(n, bool)
+    ok[corrupted(rank, n)] = False
+    packed = np.packbits(ok, bitorder="little")
+    words = (n + 63) // 64
+    return np.concatenate([packed, np.zeros(words * 8 - len(packed), np.uint8)]).view(np.uint64)
+
+
 def timed_steps(step, steps: int, warmup: int, world: int, dist, local: int):
     import torch
 
@@ -193,9 +211,12 @@ def main():
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    # Per-rank shard: same 64 creators (seeded keys), disjoint events.
+    # Per-rank shard: same 64 creators (seeded keys), disjoint events.  One
+    # item in 10^4 (seeded by rank) has an r bit flipped, so the all-gathered
+    # accept bitmask has known zeros and is checked bit for bit below.
     batch = synth.events(args.events, n_creators=args.creators, seed=2,
                          ts0=synth.TS0 + rank * args.events * 8)
+    batch.r_be[corrupted(rank, args.events), 31] ^= 1
     v = Verifier(device=local)
     dev = v.to_device(batch)
     words = dev.accept_bits.numel()
@@ -211,9 +232,14 @@ def main():
 
     elapsed, tms = timed_steps(step_with(v), args.steps, args.warmup, world, dist, local)
     res = dev.result()
-    n_acc = int(np.count_nonzero(res.status == 1))
-    if n_acc != batch.n_items:
-        raise SystemExit(f"rank {rank}: {batch.n_items - n_acc} of {batch.n_items} valid signatures rejected")
+    want = expected_words(rank, args.events)
+    if not np.array_equal(res.accept_bits, want):
+        raise SystemExit(f"rank {rank}: accept bitmask differs from the expected one")
+    if world > 1:  # the all-gathered mask of the last step: every rank's shard, bit for bit
+        got = gathered.cpu().numpy().view(np.uint64).reshape(world, -1)
+        for q in range(world):
+            if not np.array_equal(got[q], expected_words(q, args.events)):
+                raise SystemExit(f"rank {rank}: gathered bitmask of rank {q} differs from the expected one")
 
     line = None
     if rank == 0:
@@ -272,6 +298,8 @@ def main():
                 "device_total": mean(tms, "ms_total"),
             },
             "roofline": roof,
+            "bitmask_check": f"exact: {world} x {args.events} events, accept bits all-gathered and equal to the "
+                             f"expected mask ({len(corrupted(0, args.events))} seeded r-bit flips per rank rejected)",
         }
     if rank == 0 and world == 1 and not args.no_extras:
         line["warm"] = warm_leg(args, dev, world, dist, local, step_with)
@@ -304,7 +332,7 @@ def warm_leg(args, dev, world, dist, local, step_with):
     builds = vc.timing()["kc_builds"]
     elapsed, tms = timed_steps(step_with(vc), args.steps, 1, 1, None, local)
     res = dev.result()
-    assert np.all(res.status == 1)
+    assert np.array_equal(res.accept_bits, expected_words(0, args.events))
     out = {"value": args.events * args.steps / elapsed, "unit": "verifies/s",
            "ms_per_step": elapsed / args.steps * 1e3, "first_call_ms": cold_ms, "tables_built_first_call": builds,
            "key_path": int(tms[-1]["key_path"]),

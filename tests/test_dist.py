@@ -80,3 +80,84 @@ def test_gloo_allgather_matches_oracle(world):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert np.array_equal(got, want)
+
+
+def _worker_blocks(rank, world, port, out_q):
+    """C5-shaped shard: a block's signatures never straddle ranks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from tests.emu import emu
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    wb = synth.blocks(9, n_validators=13, seed=44)
+    b = wb.batch
+    b.s_be[::7, 9] ^= 0x10  # every 7th signature invalid
+    bounds = shard.plan_shards(b.item_msg, world)
+    lo, hi = bounds[rank], bounds[rank + 1]
+    assert len(set(b.item_msg[lo:hi].tolist()) & set(b.item_msg[:lo].tolist() + b.item_msg[hi:].tolist())) == 0
+    sub = shard.slice_batch(b, lo, hi)
+    _, st, bits, _ = emu.verify_batch(sub.as_dict(), n_threads=2) if hi > lo else (None, None,
+                                                                                      np.zeros(1, np.uint64), 0)
+    g = shard.allgather_bits_planned(torch.from_numpy(bits.view(np.int64).copy()), bounds, world)
+    if rank == 0:
+        out_q.put(g.copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_block_aware_shards_match_oracle(world):
+    from oracle import coracle
+
+    wb = synth.blocks(9, n_validators=13, seed=44)
+    b = wb.batch
+    b.s_be[::7, 9] ^= 0x10
+    _, _, want = coracle.verify_batch(b.as_dict())
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_blocks, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.array_equal(got, want)
+
+
+def test_python_plan_equals_c_abi_plan():
+    """shard.plan_shards == bv_plan_shards (the library's group sharding)."""
+    from babble_amd.verifier import plan_shards
+
+    rng = np.random.default_rng(5)
+    for _ in range(50):
+        reps = rng.integers(1, 120, size=rng.integers(1, 40))
+        b = synth.blocks(1, n_validators=2, seed=1).batch
+        im = np.repeat(np.arange(len(reps)), reps).astype(np.uint32)
+        b.item_msg = im
+        b.item_key = np.zeros(len(im), np.uint32)
+        b.r_be = np.zeros((len(im), 32), np.uint8)
+        b.s_be = np.zeros((len(im), 32), np.uint8)
+        b.pre = None
+        b.msg_off = np.zeros(len(reps) + 1, np.uint64)
+        for w in (1, 2, 3, 8):
+            assert shard.plan_shards(im, w) == plan_shards(b, w).tolist()
+
+
+def test_merge_bits_shifts():
+    rng = np.random.default_rng(9)
+    for _ in range(20):
+        n = int(rng.integers(1, 700))
+        ok = rng.random(n) < 0.7
+        bounds = sorted(set([0, n] + rng.integers(0, n, size=3).tolist()))
+        parts = []
+        for a, z in zip(bounds, bounds[1:]):
+            pk = np.packbits(ok[a:z], bitorder="little")
+            pk = np.concatenate([pk, np.zeros((-len(pk)) % 8, np.uint8)])
+            parts.append(pk.view(np.uint64) if len(pk) else np.zeros(1, np.uint64))
+        pk = np.packbits(ok, bitorder="little")
+        want = np.concatenate([pk, np.zeros((-len(pk)) % 8, np.uint8)]).view(np.uint64)
+        assert np.array_equal(shard.merge_bits(parts, bounds), want)
