@@ -5,8 +5,8 @@
 // One bv_ctx owns three HIP streams (main, keys, s^-1) plus a copy stream
 // for the host entry point, growable device work buffers, pinned
 // (hipHostMalloc) staging buffers, and optionally the key cache
-// (BV_F_KEY_CACHE).  The generator table (geometry.h: 24-bit windows,
-// 10.7 GB) is a per-process, per-device constant shared by every ctx.  There
+// (BV_F_KEY_CACHE).  The generator table (geometry.h: 26-bit signed
+// windows, 21.5 GB) is a per-process, per-device constant shared by every ctx.  There
 // is no CPU fallback: a missing or non-gfx950 device is BV_E_NODEVICE.
 //
 // Host entry point (bv_verify_batch, what cgo calls): every input array is
@@ -29,7 +29,7 @@
 
 namespace {
 
-constexpr uint64_t kGTableBytes = BV_GTABLE_U32 * 4;                       // 10.7 GB (geometry.h)
+constexpr uint64_t kGTableBytes = BV_GTABLE_U32 * 4;                       // 21.5 GB (geometry.h)
 constexpr uint64_t kGSubBytes = BV_GSUB_U32 * 4;
 constexpr uint64_t kGPrefixBytes = (uint64_t)BV_GPAIR_BLOCKS * 4096 * 32;  // one k_table_pair_g launch
 constexpr uint64_t kKTableBytes = BV_KTABLE_U32 * 4;
@@ -135,7 +135,7 @@ extern "C" const char *bv_last_error(const bv_ctx *ctx) { return ctx ? ctx->err.
 
 // The generator table is a constant: one copy per device and process,
 // shared by every context (refcounted), built on first use.
-// T[j][d] = d 2^(BV_GW j) G, j < BV_GNWIN, d < 2^BV_GW (geometry.h);
+// T[j][d] = d 2^(BV_GW j) G, j < BV_GNWIN, 0 < d <= 2^(BV_GW-1) (signed, geometry.h);
 // sub-tables and prefix scratch are freed after the build.
 namespace {
 struct GTableSlot {
@@ -206,7 +206,7 @@ static int create_impl(bv_ctx *ctx) {
   ctx->chunk_ev.resize(64);
   for (auto &e : ctx->chunk_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming), BV_E_NODEVICE, "event");
   ctx->g_table = gtable_acquire(ctx->device, ctx->stream);
-  if (!ctx->g_table) return bv_fail(ctx, BV_E_OOM, "generator table (geometry.h, ~10.7 GB of HBM) build failed");
+  if (!ctx->g_table) return bv_fail(ctx, BV_E_OOM, "generator table (geometry.h, ~21.5 GB of HBM) build failed");
   const unsigned hw = std::thread::hardware_concurrency();
   ctx->pool = new CopyPool((int)std::min<unsigned>(hw ? hw - 1 : 0, 7));
   if (ctx->flags & BV_F_KEY_CACHE) {

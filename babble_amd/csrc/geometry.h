@@ -4,14 +4,16 @@
 // Fixed-base tables: T[j][d] = d * 2^(W j) * P (affine, 64 bytes), d < 2^W.
 //
 // Generator table: a constant, built once per process and device with wide
-// windows over the full 256-bit u1, sized for the GPU's 288 GB of HBM:
-// 24-bit windows x 11 (264 bits; the top window holds 16) = 10.7 GB, so
-// u1 G costs 11 mixed additions and no doublings.  Entries are chord sums of
-// two 12-bit sub-table points S_k[x] = x 2^(12 k) G.  The host emulator
-// (tests/emu, test infrastructure) overrides BV_GW/BV_GNWIN/BV_GL/BV_GNSUB
-// with a 22-bit geometry to keep its host-memory table at 3 GB; the code
-// paths are the same templates.
-//
+// SIGNED-digit windows over the 256-bit u1, sized for the GPU's 288 GB of
+// HBM: 26-bit windows x 10 (260 bits >= 257 for the signed recoding; digits
+// in (-2^25, 2^25], y negated for negative digits) = 2^25 entries per window,
+// 21.5 GB, so u1 G costs 9 mixed additions (the first window lands on the
+// identity) and no doublings.  Entries are chord sums of two 13-bit
+// sub-table points S_k[x] = x 2^(13 k) G; the digit 2^25 of window j lives
+// in the never-read slot 0 of window j+1 (one pad entry after the top
+// window), as in the K12 / KC key tables.  The host emulator (tests/emu, test
+// infrastructure) overrides BV_GW/BV_GNWIN/BV_GL/BV_GNSUB with smaller
+// geometries (host memory); the code paths are the same templates.
 // Key tables are built per batch over 128 bits only: u2 is split GLV-style
 // (u2 = k1 + k2 lambda, |k1|, |k2| < 2^128) and the second half of a key
 // table holds phi(T) = (beta x, y), so the serial doubling chain per key
@@ -28,12 +30,13 @@
 
 #define BV_ENTRY_U32 16  // affine x, y = 16 words (64 bytes)
 #ifndef BV_GW
-#define BV_GW 24         // G window bits
-#define BV_GNWIN 11      //   x 11 windows (264 bits) x 16M entries = 10.7 GB
-#define BV_GL 12         // G sub-table bits: S_k[x] = x 2^(12k) G, x < 4096
-#define BV_GNSUB 22      //   k < 22
+#define BV_GW 26         // G window bits (signed digits)
+#define BV_GNWIN 10      //   x 10 windows (260 bits) x 2^25 entries = 21.5 GB
+#define BV_GL 13         // G sub-table bits: S_k[x] = x 2^(13k) G, x < 8192
+#define BV_GNSUB 20      //   k < 20
 #endif
-#define BV_GTABLE_U32 ((uint64_t)BV_GNWIN * (1ull << BV_GW) * BV_ENTRY_U32)
+#define BV_GENT (1u << (BV_GW - 1))  // entry slots per G window
+#define BV_GTABLE_U32 (((uint64_t)BV_GNWIN * BV_GENT + 1) * BV_ENTRY_U32)
 #define BV_GSUB_U32 ((uint64_t)BV_GNSUB * (1ull << BV_GL) * BV_ENTRY_U32)
 #define BV_GPAIR_BLOCKS 1024  // k_table_pair_g blocks per launch (4096 entries each)
 #define BV_KW 8          // K8 window bits

@@ -306,15 +306,17 @@ __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__
   }
 }
 
-// Generator table window j from the 11-bit G sub-tables: block c holds
-// entries d = 4096 c + 256 e + t (e < 16) of window j, so a wave reads 64
-// consecutive S_lo points and one S_hi point (the sub-tables, 3 MiB, stay
-// in L2/MALL; no LDS staging).  One field inversion per block; prefix
-// products in `pscr` (4096 fe per block).  Launched once per window.
+// Generator table window j from the G sub-tables (geometry.h, signed
+// digits): block c holds slots s = 4096 c + 256 e + t (e < 16) of window j,
+// digit k12_digit(s) (slot 0 builds digit 2^(W-1), which lands in window
+// j+1's slot 0), so a wave reads 64 consecutive S_lo points and one S_hi point
+// (the sub-tables, 5 MiB, stay in L2/MALL; no LDS staging).  One field
+// inversion per block; prefix products in `pscr` (4096 fe per block).
+// Launched once per window chunk.
 template <int W, int L>
 __global__ void __launch_bounds__(256) k_table_pair_g(const uint32_t *__restrict__ sub, uint32_t *__restrict__ table,
                                                       uint4 *__restrict__ pscr, uint32_t j, uint32_t c0) {
-  constexpr uint32_t E = 16, NS = 1u << L;
+  constexpr uint32_t E = 16, NS = 1u << L, ENT = 1u << (W - 1);
   const uint32_t c = c0 + blockIdx.x, t = threadIdx.x;
   const uint32_t *s_lo = sub + (uint64_t)(2 * j) * NS * BV_ENTRY_U32;
   const uint32_t *s_hi = s_lo + (uint64_t)NS * BV_ENTRY_U32;
@@ -324,7 +326,7 @@ __global__ void __launch_bounds__(256) k_table_pair_g(const uint32_t *__restrict
   fe_set(acc, 1);
 #pragma unroll 1
   for (uint32_t e = 0; e < E; e++) {
-    const uint32_t d = 4096u * c + 256u * e + t, lo = d & (NS - 1), hi = d >> L;
+    const uint32_t d = k12_digit(4096u * c + 256u * e + t, ENT), lo = d & (NS - 1), hi = d >> L;
     fe x1, y1, x2, y2, H;
     pair_load(s_lo, s_hi, lo, hi, x1, y1, x2, y2);
     pair_denominator(H, pair_kind(lo, hi), x1, x2);
@@ -353,10 +355,10 @@ __global__ void __launch_bounds__(256) k_table_pair_g(const uint32_t *__restrict
   fe q = sInv;
   if (t > 0) fe_mul(q, q, sPre[t - 1]);
   if (t < 255) fe_mul(q, q, sSuf[t + 1]);
-  uint32_t *base = table + ((uint64_t)j << W) * BV_ENTRY_U32;
+  uint32_t *base = table + (uint64_t)j * ENT * BV_ENTRY_U32;
 #pragma unroll 1
   for (int e = (int)E - 1; e >= 0; e--) {
-    const uint32_t d = 4096u * c + 256u * e + t, lo = d & (NS - 1), hi = d >> L;
+    const uint32_t d = k12_digit(4096u * c + 256u * e + t, ENT), lo = d & (NS - 1), hi = d >> L;
     const int kind = pair_kind(lo, hi);
     fe x1, y1, x2, y2, H, Hinv, pre;
     pair_load(s_lo, s_hi, lo, hi, x1, y1, x2, y2);
@@ -589,8 +591,10 @@ hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     for (uint32_t j = 0; j < BV_GNWIN; j++) {
+      // slots needed: all of a full window; the top window's digits are
+      // <= 2^(256 - W j) (its value bits plus the carry)
       const int live_bits = 256 - BV_GW * (int)j;
-      const uint64_t live = live_bits >= BV_GW ? (1ull << BV_GW) : (1ull << live_bits);
+      const uint64_t live = live_bits >= BV_GW - 1 ? BV_GENT : (1ull << live_bits) + 1;
       const uint32_t blocks = (uint32_t)((live + 4095) / 4096);
       for (uint32_t c0 = 0; c0 < blocks; c0 += BV_GPAIR_BLOCKS) {
         const uint32_t nb = blocks - c0 < BV_GPAIR_BLOCKS ? blocks - c0 : BV_GPAIR_BLOCKS;

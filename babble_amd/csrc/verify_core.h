@@ -433,20 +433,30 @@ DEV bool final_check(const gej &R, bool inf, const fe &r) {
   return false;
 }
 
-// R += sum_j T[j][digit_j(u)] over the 256-bit u1 (8 limbs; consumed:
-// shifted right W bits per window, so digits never straddle limbs).
+// R += sum_j T[j][digit_j(u)] over the 256-bit u1 (8 limbs, consumed:
+// shifted right W bits per window, so digits never straddle limbs) with
+// SIGNED digits in (-2^(W-1), 2^(W-1)] by carry recoding: T[j][|d|], y
+// negated for d < 0 (geometry.h).  u < N < 2^256 and W NWIN >= 257, so no
+// carry is left after the top window.
 template <int W, int NWIN>
 DEV void g_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t u[8]) {
+  constexpr uint32_t ENT = 1u << (W - 1);
+  static_assert(W * NWIN >= 257 && W < 32, "signed G windows must absorb the last carry");
+  uint32_t carry = 0;
   for (int j = 0; j < NWIN; j++) {
-    const uint32_t d = u[0] & ((1u << W) - 1u);
+    uint32_t d = (u[0] & ((1u << W) - 1u)) + carry;
 #pragma unroll
     for (int c = 0; c < 7; c++) u[c] = (u[c] >> W) | (u[c + 1] << (32 - W));
     u[7] >>= W;
+    carry = d > ENT ? 1u : 0u;
+    const bool dneg = carry != 0;
+    if (dneg) d = (1u << W) - d;  // |d - 2^W|, 0 when d == 2^W
     if (d) {
-      const uint32_t *e = tab + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
+      const uint32_t *e = tab + ((uint64_t)j * ENT + d) * BV_ENTRY_U32;
       fe x, y;
       fe_load4(x, e);
       fe_load4(y, e + 8);
+      if (dneg) fe_neg(y, y);
       gej_add_ge(R, inf, x, y);
     }
   }

@@ -42,18 +42,18 @@ sys.path.insert(0, ROOT)
 # ~2.1 KB of table gathers per item).  Work per item of the EXECUTED
 # schedule, in 256-bit modular multiplications (squarings included), each
 # 64 schoolbook 32x32 products + 16 reduction products = 80 IMUL32:
-#   u1 G:  11 windows of the 24-bit G table, the first lands on the identity
-#          (a copy), 10 mixed additions x (8M + 3S)         = 110
+#   u1 G:  10 signed windows of the 26-bit G table, the first lands on the
+#          identity (a copy), 9 mixed additions x (8M + 3S) =  99
 #   u2 Q:  22 windows of the K12 GLV key tables, 22 x 11    = 242
 #   u1, u2 = e w, r w (2 Montgomery products), GLV split (2 wide products
 #          + 2 products) and the projective check X == r Z^2 (1S + 1M)
 #                                                           ~   8
-#   = 360 modmuls = 28,800 IMUL32 per item.
+#   = 349 modmuls = 27,920 IMUL32 per item.
 # `achieved` = items x 28,800 / (k_verify_g + k_verify_q time); `peak` = the
 # v_mad_u64_u32 rate measured on MI355X (tools/ubench_int.hip,
 # profiles/r01_ubench_int.txt).  SURVEY §8d's canonical Strauss schedule
 # (4,050 modmuls per verify) is reported only as `speedup_vs_canonical`.
-MODMUL_PER_ITEM_EXEC = 360
+MODMUL_PER_ITEM_EXEC = 349
 IMUL32_PER_MODMUL = 80
 CANONICAL_MODMUL_PER_VERIFY = 4050
 PEAK_IMUL32_PER_S = 31.76e12
@@ -253,7 +253,7 @@ def main():
             "kernel": "k_verify_g + k_verify_q<12,11>",
             "achieved": achieved / 1e12,
             "peak": PEAK_IMUL32_PER_S / 1e12,
-            "unit": "T IMUL32/s (executed schedule: 360 modmuls x 80 IMUL32 per item; bench.py ROOFLINE)",
+            "unit": "T IMUL32/s (executed schedule: 349 modmuls x 80 IMUL32 per item; bench.py ROOFLINE)",
             "frac": achieved / PEAK_IMUL32_PER_S,
             "traffic": None,
             "speedup_vs_canonical": CANONICAL_MODMUL_PER_VERIFY / MODMUL_PER_ITEM_EXEC,

@@ -121,11 +121,11 @@ void emu_build_tables(int kw, uint32_t n_bases, const uint32_t *bxy, const uint8
     const uint32_t NS = 1u << BV_GL;
     for (uint32_t j = 0; j < BV_GNWIN; j++) {
       const int live_bits = 256 - BV_GW * (int)j;
-      const uint64_t live = live_bits >= BV_GW ? (1ull << BV_GW) : (1ull << live_bits);
+      const uint64_t live = live_bits >= BV_GW - 1 ? BV_GENT : (1ull << live_bits) + 1;
       const uint32_t *s_lo = sub.data() + (uint64_t)(2 * j) * NS * BV_ENTRY_U32, *s_hi = s_lo + NS * BV_ENTRY_U32;
-      uint32_t *base = table + ((uint64_t)j << BV_GW) * BV_ENTRY_U32;
+      uint32_t *base = table + (uint64_t)j * BV_GENT * BV_ENTRY_U32;
       parallel_for((live + 4095) / 4096, nt, [&](uint64_t c) {
-        emu_pair_chunk(s_lo, s_hi, BV_GL, (uint32_t)(c * 4096), 4096, base, 0);
+        emu_pair_chunk(s_lo, s_hi, BV_GL, (uint32_t)(c * 4096), 4096, base, 0, BV_GENT);
       });
     }
     return;
