@@ -98,6 +98,8 @@ class PeerSet:
 
     def Hash(self, verifier=None) -> bytes:
         """peer_set.go:104-115: h = SHA256(h || pubkey) over the peers in order."""
+        if self._hash is None and not self.Peers:
+            self._hash = b""  # h := []byte{} with nothing to chain
         if self._hash is None:
             v = verifier or default_verifier()
             pks = [p.PubKeyBytes() for p in self.Peers]
