@@ -45,6 +45,7 @@ K = 2**32 + 977  # 2^256 mod p
 HAZARD_STATES = 2  # VALU writes SGPR -> VALU reads it: 2 wait states (gfx950)
 MUL_BASE = 0       # physical VGPR temporaries of fe_mul: v[MUL_BASE, MUL_BASE+34)
 MUL_NREGS = 34
+NCARRY = 10        # SGPR lane-mask pairs of fe_mul / fe_sqr (%[c0..9])
 
 # ops: name -> (dst-operand positions, src-operand positions, sgpr-src positions)
 #   every op: (op, d, ...); positions index into the tuple
@@ -61,6 +62,8 @@ OPS = {
     "mul_lo": ((1,), (2, 3), ()),          # d = lo32(a * b)
     "alignbit": ((1,), (2, 3), ()),        # d = lo32(({a, b} 64-bit) >> sh), sh = x[4]
     "nop": ((), (), ()),
+    "sor": ((1,), (2, 3), (2, 3)),         # SALU s_or_b64 d, a, b (lane masks)
+    "slow": ((), (), (1,)),                # uniform branch into x[2] (a Prog) iff any lane of mask x[1]
 }
 
 
@@ -113,6 +116,14 @@ class Prog:
 
     def alignbit(self, d, hi, lo, sh):
         self.emit("alignbit", d, hi, lo, sh)
+
+    def sor(self, d, a, b):
+        self.emit("sor", d, a, b)
+
+    def slow_block(self, mask, blk: "Prog"):
+        """Mid-program rare block: run (by the whole wave) iff some lane's
+        `mask` bit is set; it must be a no-op for lanes without the bit."""
+        self.emit("slow", mask, blk)
 
 
 # ---------------------------------------------------------------------------
@@ -169,10 +180,35 @@ def sgpr_reads(ins) -> list[str]:
 BRANCH_STATES = 2  # s_cmp_lg_u64 + s_cbranch_scc0 between the blocks
 
 
-def schedule(g: Prog, ages: dict[str, int] | None = None) -> Prog:
-    """List-schedule g.ins; `ages` = wait states already elapsed since each
-    SGPR's last VALU write at entry (for a slow block after a branch)."""
-    ins = g.ins
+def _block_sgpr_writes(blk: Prog) -> set[str]:
+    out: set[str] = set()
+    for x in blk.ins:
+        if x[0] == "slow":
+            out |= _block_sgpr_writes(x[2])
+            continue
+        out |= {x[p] for p in OPS[x[0]][0] if is_sgpr(x[p])}
+    if blk.slow is not None:
+        out |= _block_sgpr_writes(blk.slow[1])
+    return out
+
+
+SALU_OPS = {"sor"}
+
+
+def _note_sgpr_writes(x: tuple, wtime: dict[str, int], t: int) -> None:
+    """Record the SGPRs x writes: a VALU write starts the hazard window
+    (the next VALU or SALU read waits HAZARD_STATES); an SALU write does
+    not (SALU results are interlocked), so it clears the entry."""
+    for p in OPS[x[0]][0]:
+        if is_sgpr(x[p]):
+            if x[0] in SALU_OPS:
+                wtime.pop(x[p], None)
+            else:
+                wtime[x[p]] = t
+
+
+def _sched_segment(ins: list[tuple], out: Prog, t: int, sgpr_wtime: dict[str, int]) -> int:
+    """List-schedule a straight-line segment into `out`; returns the clock."""
     n = len(ins)
     preds: list[set[int]] = [set() for _ in range(n)]
     last_w: dict[str, int] = {}
@@ -193,9 +229,6 @@ def schedule(g: Prog, ages: dict[str, int] | None = None) -> Prog:
             last_w[w] = j
             last_r[w] = []
     done = [False] * n
-    out = Prog(g.name)
-    t = 0                      # wait-state clock
-    sgpr_wtime: dict[str, int] = {k: -a for k, a in (ages or {}).items()}
     remaining = n
     while remaining:
         pick = None
@@ -212,11 +245,36 @@ def schedule(g: Prog, ages: dict[str, int] | None = None) -> Prog:
         x = ins[pick]
         out.ins.append(x)
         t += 1
-        for p in OPS[x[0]][0]:
-            if is_sgpr(x[p]):
-                sgpr_wtime[x[p]] = t
+        _note_sgpr_writes(x, sgpr_wtime, t)
         done[pick] = True
         remaining -= 1
+    return t
+
+
+def schedule(g: Prog, ages: dict[str, int] | None = None) -> Prog:
+    """List-schedule g.ins; `ages` = wait states already elapsed since each
+    SGPR's last VALU write at entry (for a slow block after a branch).
+    Mid-program slow blocks split the program into segments; after one, the
+    SGPRs it may write count as written at the resume point (conservative
+    for both the taken and the skipped path)."""
+    out = Prog(g.name)
+    t = 0
+    sgpr_wtime: dict[str, int] = {k: -a for k, a in (ages or {}).items()}
+    seg: list[tuple] = []
+    for x in g.ins + [None]:
+        if x is not None and x[0] != "slow":
+            seg.append(x)
+            continue
+        t = _sched_segment(seg, out, t, sgpr_wtime)
+        seg = []
+        if x is None:
+            break
+        mask, blk = x[1], x[2]
+        entry = {k: t - w + BRANCH_STATES for k, w in sgpr_wtime.items()}
+        out.ins.append(("slow", mask, schedule(blk, entry)))
+        t += BRANCH_STATES
+        for sg in _block_sgpr_writes(blk):
+            sgpr_wtime[sg] = t
     if g.slow is not None:
         mask, blk = g.slow
         exit_ages = {k: t - w + BRANCH_STATES for k, w in sgpr_wtime.items()}
@@ -227,14 +285,18 @@ def schedule(g: Prog, ages: dict[str, int] | None = None) -> Prog:
 def check_hazards(g: Prog, wt: dict[str, int] | None = None, t: int = 0) -> None:
     wt = dict(wt or {})
     for x in g.ins:
+        if x[0] == "slow":
+            check_hazards(x[2], wt, t + BRANCH_STATES)
+            t += BRANCH_STATES
+            for sg in _block_sgpr_writes(x[2]):
+                wt[sg] = t
+            continue
         t += 1
         if x[0] == "nop":
             continue
         for s in sgpr_reads(x):
             assert t - 1 - wt.get(s, -99) >= HAZARD_STATES, (g.name, x, t, wt.get(s))
-        for p in OPS[x[0]][0]:
-            if is_sgpr(x[p]):
-                wt[x[p]] = t
+        _note_sgpr_writes(x, wt, t)
     if g.slow is not None:
         check_hazards(g.slow[1], wt, t + BRANCH_STATES)
 
@@ -245,6 +307,7 @@ def check_hazards(g: Prog, wt: dict[str, int] | None = None, t: int = 0) -> None
 class Machine:
     def __init__(self):
         self.r: dict[str, int] = {}
+        self.hits: dict[str, int] = {}  # mid-program slow blocks entered (by program name)
 
     def get(self, x) -> int:
         if isinstance(x, int):
@@ -265,16 +328,24 @@ class Machine:
             self.r[x] = val
 
     def run(self, g: Prog, force_slow: bool = False):
-        self._run(g)
+        self._run(g, force_slow)
         if g.slow is not None:
             mask, blk = g.slow
             if force_slow or self.get(mask):
                 self.run(blk, force_slow)
 
-    def _run(self, g: Prog):
+    def _run(self, g: Prog, force_slow: bool = False):
         for x in g.ins:
             op = x[0]
             if op == "nop":
+                continue
+            if op == "slow":
+                self.hits[g.name] = self.hits.get(g.name, 0) + bool(self.get(x[1]))
+                if force_slow or self.get(x[1]):
+                    self.run(x[2], force_slow)
+                continue
+            if op == "sor":
+                self.put(x[1], 1 if (self.get(x[2]) or self.get(x[3])) else 0)
                 continue
             if op == "mad":
                 s = self.get(x[3]) * self.get(x[4]) + self.get(x[5])
@@ -340,67 +411,88 @@ def gen_mul(base: int = MUL_BASE) -> Prog:
             g.mov(Pl[k + 1], Ph[k])
             if not counted:
                 g.mov(c2, 0)
-            if k < 8:
-                g.mov(Ph[k], 0)  # {L_k, 0} pair for the fold
+        if k >= 8:
+            g.mov(Ph[k - 8], Pl[k])  # P_(k-8) = {w_(k-8), w_k} for the fold
+    g.mov(Ph[7], Ph[14])             # P_7 = {w_7, w_15}
     return _fold(g, base, R, Pl, Ph, PP)
 
 
 def _fold(g: Prog, base: int, R, Pl, Ph, PP) -> Prog:
-    """Reduce the 512-bit value w_0..w_15 (w_k = P_k.lo, w_15 = P_14.hi,
-    with P_k.hi = 0 for k < 8) mod p into %[r0..7] (weak)."""
-    K977 = v(base + 30)
-    T0, T1, T2, T3 = v(base + 30), v(base + 31), v(base + 32), v(base + 33)
-    W = Pl + [Ph[14]]  # w_0 .. w_15
-    L, H = W[:8], W[8:]
+    """Reduce the 512-bit value w_0..w_15 mod p into %[r0..7] (weak).
+    Entry: P_i = {w_i, w_(i+8)} for i < 8 (so P_i as a 64-bit value is
+    w_i + 2^32 w_(i+8)), and w_(i+8) also in P_(i+8).lo (i < 7) / P_14.hi.
 
-    # ---- fold: R = L + 977 H + 2^32 H ----
-    # Y_i = 977 H_i + L_i in place (< 2^43); S = Ylo + (Yhi << 32);
-    # R = S + (H << 32); R_0 = Y_0.lo stays in P_0.lo until the tail.
-    # R_8 goes to T1 with T0 = 0 so {T0, T1} = R_8 * 2^32.
+    2^256 = 2^32 + 977 (mod p), so limb i of the folded value collects
+    w_i + 977 w_(i+8) + 2^32 w_(i+8): ONE mad per limb,
+        Y_i = w_(i+8) * 977 + P_i         (65 bits: carry-out y_i, rare),
+    then one carry chain R_i = Y_i.lo + Y_(i-1).hi (+ carry), R_8 = Y_7.hi.
+    y_i (weight 2^(32(i+2)); P(set) ~ 2^-22 per limb) is added in a
+    uniform rare block entered iff some lane has one.  Then R_8 (+ c9 2^32)
+    is folded once more into limbs 0..2 and a rare tail propagates."""
+    T0, T1, T2, T3 = v(base + 30), v(base + 31), v(base + 32), v(base + 33)
+    K977 = T2
+    YC = [f"%[c{i}]" for i in range(8)]
+    CANY, cR = "%[c8]", "%[c9]"
+    H = [Pl[i + 8] for i in range(7)] + [Ph[14]]
+
+    # logical order interleaves the chain with the mads and the SALU ORs,
+    # so each chain link's carry hazard is covered without s_nop
     g.mov(K977, 977)
-    cyD = CY[3]
-    for i in range(8):
-        g.mad(PP[i], cyD, H[i], K977, PP[i])
-    # K977 is needed again in the tail: keep a copy in T2
-    g.mov(T2, K977)
-    cS, cR = CY[0], CY[1]
-    Ylo = [Pl[i] for i in range(8)]
-    Yhi = [Ph[i] for i in range(8)]
-    g.add_co(Ylo[1], cS, Ylo[1], Yhi[0])
-    g.add_co(R[1], cR, Ylo[1], H[0])
+    g.mad(PP[0], YC[0], H[0], K977, PP[0])
+    g.mad(PP[1], YC[1], H[1], K977, PP[1])
+    g.sor(CANY, YC[0], YC[1])
+    g.add_co(R[1], cR, Pl[1], Ph[0])
     for i in range(2, 8):
-        g.addc(Ylo[i], cS, Ylo[i], Yhi[i - 1], cS)
-        g.addc(R[i], cR, Ylo[i], H[i - 1], cR)
-    g.addc(Yhi[7], cS, Yhi[7], 0, cS)       # S_8
-    g.mov(T0, 0)
-    g.addc(T1, cR, Yhi[7], H[7], cR)        # R_8; cR = c9 (weight 2^288)
+        g.mad(PP[i], YC[i], H[i], K977, PP[i])
+        g.sor(CANY, CANY, YC[i])
+        g.addc(R[i], cR, Pl[i], Ph[i - 1], cR)
+    g.addc(T1, cR, Ph[7], 0, cR)            # R_8; cR = c9 (weight 2^288)
+
+    # ---- rare: y_i -> limb i + 2 (limb 8 = R_8 in T1); the carry out of
+    # limb 8 and y_7 both have weight 2^288: at most one of c9, y_7 and that
+    # carry is set (each forces R_8 small), so c9 |= y_7 | carry.
+    s = Prog(g.name + "_ycarry")
+    cS = CANY
+    limbs = [R[2], R[3], R[4], R[5], R[6], R[7], T1]
+    XT = [Ph[8], Ph[9]]                     # free since the product phase
+    for i in range(7):
+        x = XT[i % 2]
+        s.cnd(x, 0, 1, YC[i])
+        if i == 0:
+            s.add_co(limbs[0], cS, limbs[0], x)
+        else:
+            s.addc(limbs[i], cS, limbs[i], x, cS)
+    s.sor(cR, cR, YC[7])
+    s.sor(cR, cR, cS)
+    g.slow_block(CANY, s)
 
     # ---- fold 1: add (R_8 + c9 2^32)(2^32 + 977) ----
     TT = pair(T0)
-    cE = CY[2]
+    cE = CY[0]
+    g.mov(T0, 0)
     g.mad(TT, cE, T1, T2, TT)               # E = 977 R_8 + 2^32 R_8 (+ cE 2^64)
     g.cnd(T3, 0, T2, cR)                    # 977 c9 -> limb 1
     g.add(T1, T1, T3)
     g.cnd(T3, 0, 1, cE)                     # limb 2: cE | c9 (exclusive)
     g.cnd(T3, T3, 1, cR)
-    cF = CY[0]
-    g.add_co(R[0], cF, Ylo[0], T0)
+    cF = CY[1]
+    g.add_co(R[0], cF, Pl[0], T0)
     g.addc(R[1], cF, R[1], T1, cF)
     g.addc(R[2], cF, R[2], T3, cF)
     # ---- rare tail (uniform branch, taken iff some lane carried out of
     # limb 2): propagate into limbs 3..7; if that wraps past 2^256 (value is
     # then < 2^66) add 2^32 + 977 once more.  A no-op for lanes without the
     # carry, so the whole wave may run it.
-    s = Prog("fe_mul_tail")
+    t = Prog(g.name + "_tail")
     for i in range(3, 8):
-        s.addc(R[i], cF, R[i], 0, cF)
-    s.cnd(T3, 0, T2, cF)
-    s.cnd(T1, 0, 1, cF)
-    cG = CY[1]
-    s.add_co(R[0], cG, R[0], T3)
-    s.addc(R[1], cG, R[1], T1, cG)
-    s.addc(R[2], cG, R[2], 0, cG)
-    g.slow = (cF, s)
+        t.addc(R[i], cF, R[i], 0, cF)
+    t.cnd(T3, 0, T2, cF)
+    t.cnd(T1, 0, 1, cF)
+    cG = CY[2]
+    t.add_co(R[0], cG, R[0], T3)
+    t.addc(R[1], cG, R[1], T1, cG)
+    t.addc(R[2], cG, R[2], 0, cG)
+    g.slow = (cF, t)
     return g
 
 
@@ -432,8 +524,6 @@ def gen_sqr(base: int = MUL_BASE) -> Prog:
         if not counted:
             g.mov(c2, 0)
         g.mov(Pl[k + 1], Ph[k])
-        if k < 8:
-            g.mov(Ph[k], 0)  # {L_k, 0} pair for the fold
     # D: d_0 = 0, d_m = P_m.lo (1 <= m <= 14), d_15 = P_14.hi
     Dw = [None] + [Pl[m] for m in range(1, 15)] + [Ph[14]]
 
@@ -448,13 +538,14 @@ def gen_sqr(base: int = MUL_BASE) -> Prog:
     cQ = CY[1]
     g.mad(PP[0], CY[3], A[0], A[0], 0)           # w_0, and a_0^2 hi -> w_1
     g.add_co(Dw[1], cQ, Dw[1], Ph[0])
-    g.mov(Ph[0], 0)
     for i in range(1, 8):
         tp = T01 if i % 2 else T23
         tl, th = halves(tp)
         g.mad(tp, CY[2] if i % 2 else CY[3], A[i], A[i], 0)
         g.addc(Dw[2 * i], cQ, Dw[2 * i], tl, cQ)
         g.addc(Dw[2 * i + 1], cQ, Dw[2 * i + 1], th, cQ)
+    for i in range(8):
+        g.mov(Ph[i], Dw[i + 8])  # P_i = {w_i, w_(i+8)} for the fold
     return _fold(g, base, R, Pl, Ph, PP)
 
 
@@ -621,12 +712,21 @@ def asm_line(x) -> str:
         return f"v_mul_lo_u32 {x[1]}, {fmt(x[2])}, {fmt(x[3])}"
     if op == "alignbit":
         return f"v_alignbit_b32 {x[1]}, {fmt(x[2])}, {fmt(x[3])}, {x[4]}"
+    if op == "sor":
+        return f"s_or_b64 {x[1]}, {x[2]}, {x[3]}"
     raise ValueError(op)
 
 
 def asm_body(g: Prog) -> str:
     lines = []
-    for x in g.ins:
+    for k, x in enumerate(g.ins):
+        if x[0] == "slow":
+            lbl = f"BV_{g.name.upper()}_S{k}_%="
+            lines.append(f'      "s_cmp_lg_u64 {x[1]}, 0\\n"')
+            lines.append(f'      "s_cbranch_scc0 {lbl}\\n"')
+            lines.append(asm_body(x[2]))
+            lines.append(f'      "{lbl}:\\n"')
+            continue
         lines.append(f'      "{asm_line(x)}\\n"')
     if g.slow is not None:
         mask, blk = g.slow
@@ -640,8 +740,11 @@ def asm_body(g: Prog) -> str:
 def stats(g: Prog) -> dict:
     from collections import Counter
 
-    c = Counter(x[0] for x in g.ins)
+    c = Counter(x[0] for x in g.ins if x[0] != "slow")
     out = dict(c)
+    mids = [len(x[2].ins) for x in g.ins if x[0] == "slow"]
+    if mids:
+        out["rare_mid"] = mids
     if g.slow is not None:
         out["rare_tail"] = len(g.slow[1].ins)
     return out
@@ -662,7 +765,7 @@ def header() -> str:
     b_in = ", ".join(f'[b{i}] "v"(b.v[{i}])' for i in range(8))
     r_out = ", ".join(f'[r{i}] "=&v"(r.v[{i}])' for i in range(8))
     t_out = ", ".join(f'[t{i}] "=&v"(t[{i}])' for i in range(8))
-    c_out = ", ".join(f'[c{i}] "=&s"(c{i})' for i in range(4))
+    c_out = ", ".join(f'[c{i}] "=&s"(c{i})' for i in range(NCARRY))
     c3_out = ", ".join(f'[c{i}] "=&s"(c{i})' for i in range(3))
     return f"""// field_asm.h — GENERATED by tools/gen_field_asm.py; do not edit.
 //
@@ -683,7 +786,7 @@ def header() -> str:
 
 // r = a * b mod p (weak).  Temporaries: v{MUL_BASE}..v{MUL_BASE + MUL_NREGS - 1} (clobbered).
 __device__ __forceinline__ void fe_mul_asm(fe &r, const fe &a, const fe &b) {{
-  uint64_t c0, c1, c2, c3;
+  uint64_t {", ".join(f"c{i}" for i in range(NCARRY))};
   asm volatile(
 {asm_body(mul)}
       : {r_out}, {c_out}
@@ -693,7 +796,7 @@ __device__ __forceinline__ void fe_mul_asm(fe &r, const fe &a, const fe &b) {{
 
 // r = a^2 mod p (weak), Comba squaring.  Temporaries as fe_mul.
 __device__ __forceinline__ void fe_sqr_asm(fe &r, const fe &a) {{
-  uint64_t c0, c1, c2, c3;
+  uint64_t {", ".join(f"c{i}" for i in range(NCARRY))};
   asm volatile(
 {asm_body(sqr)}
       : {r_out}, {c_out}
