@@ -252,7 +252,7 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
                     &ctx->key_sub,   &ctx->key_pscr, &ctx->key_table, &ctx->scratch, &ctx->u12,
                     &ctx->rg,        &ctx->status,   &ctx->bits,     &ctx->kc_tabs, &ctx->kc_kst,
                     &ctx->kc_kxy,    &ctx->kc_btabs, &ctx->ev_lens,  &ctx->ev_ppos,  &ctx->ev_offs,
-                    &ctx->ev_bodies, &ctx->ev_tmp,   &ctx->ev_iota};
+                    &ctx->ev_bodies, &ctx->ev_tmp,   &ctx->ev_iota, &ctx->ev_mid};
   for (auto *b : bufs) b->release();
   for (auto &s : ctx->kc_slots)
     if (s.table) (void)hipFree(s.table);

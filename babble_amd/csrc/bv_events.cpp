@@ -13,6 +13,7 @@
 #include <cstring>
 
 #include "bv_internal.h"
+#include "evjson.h"  // EV_MID_U32
 
 #define HIPCHK(expr, code, what)                               \
   do {                                                         \
@@ -23,6 +24,7 @@
 namespace {
 
 constexpr uint32_t kNarrowLevel = 1024;  // events per level run by k_ev_hash_chain
+constexpr uint32_t kChainCap = 1024;     // events per k_ev_hash_chain launch (EVC_CAP)
 constexpr size_t kChunk = 16ull << 20;
 
 int validate(bv_ctx *ctx, const bv_event_batch *b) {
@@ -92,7 +94,7 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   if (n == 0) return BV_OK;
 
   // DAG levels over in-batch parents (refs point backwards: one pass)
-  std::vector<uint32_t> level, order, level_off;
+  std::vector<uint32_t> level, order, level_off, posin;
   const bool dag = memchr(eb->parent_kind, BV_PARENT_EVENT, 2 * n) != nullptr;
   if (dag) {
     level.assign(n, 0);
@@ -110,6 +112,8 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
     order.resize(n);
     std::vector<uint32_t> fill(level_off.begin(), level_off.end() - 1);
     for (uint64_t e = 0; e < n; e++) order[fill[level[e]]++] = (uint32_t)e;
+    posin.resize(n);
+    for (uint64_t i = 0; i < n; i++) posin[order[i]] = (uint32_t)i;
   }
 
   // staging layout (pinned host and HBM): the compact wire arrays
@@ -151,6 +155,7 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   const size_t o_pre = add(eb->pre, eb->pre ? n : 0);
   const size_t o_ord = add(dag ? order.data() : nullptr, dag ? n * 4 : 0);
   const size_t o_lof = add(dag ? level_off.data() : nullptr, dag ? level_off.size() * 4 : 0);
+  const size_t o_pin = add(dag ? posin.data() : nullptr, dag ? n * 4 : 0);
 
   if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
   HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
@@ -217,7 +222,12 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
     HIPCHK(bvk::ev_hash(st, n, nullptr, d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
   } else {
     const uint32_t *dord = (const uint32_t *)(dev + o_ord), *dlof = (const uint32_t *)(dev + o_lof);
+    const uint32_t *dpin = (const uint32_t *)(dev + o_pin);
     const uint32_t nl = (uint32_t)level_off.size() - 1;
+    // midstates of every event above level 0, in one wide launch
+    HIPCHK(ctx->ev_mid.ensure((size_t)n * EV_MID_U32 * 4), BV_E_OOM, "alloc midstates");
+    uint32_t *mid = ctx->ev_mid.as<uint32_t>();
+    HIPCHK(bvk::ev_mid(st, n - level_off[1], dord + level_off[1], bodies, offs, ppos, mid), BV_E_LAUNCH, "k_ev_mid");
     uint32_t L = 0;
     while (L < nl) {
       const uint32_t w = level_off[L + 1] - level_off[L];
@@ -226,9 +236,13 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
         L++;
         continue;
       }
+      // a run of narrow levels, at most kChainCap events per launch (the
+      // chain kernel keeps the launch's descriptors and digests in LDS)
       uint32_t L1 = L;
-      while (L1 < nl && level_off[L1 + 1] - level_off[L1] <= kNarrowLevel) L1++;
-      HIPCHK(bvk::ev_hash_chain(st, L, L1, dlof, dord, d, ppos, bodies, offs, dig), BV_E_LAUNCH,
+      while (L1 < nl && level_off[L1 + 1] - level_off[L1] <= kNarrowLevel &&
+             level_off[L1 + 1] - level_off[L] <= kChainCap)
+        L1++;
+      HIPCHK(bvk::ev_hash_chain(st, L, L1, dlof, dord, dpin, d, ppos, bodies, offs, mid, dig), BV_E_LAUNCH,
              "k_ev_hash_chain");
       L = L1;
     }

@@ -28,8 +28,11 @@ hipError_t ev_build(hipStream_t, const bv_event_batch &, uint64_t *, uint32_t *,
                     size_t *);
 hipError_t ev_hash(hipStream_t, uint64_t, const uint32_t *, const bv_event_batch &, const uint32_t *, uint8_t *,
                    const uint64_t *, uint32_t *);
-hipError_t ev_hash_chain(hipStream_t, uint32_t, uint32_t, const uint32_t *, const uint32_t *, const bv_event_batch &,
-                         const uint32_t *, uint8_t *, const uint64_t *, uint32_t *);
+hipError_t ev_mid(hipStream_t, uint64_t, const uint32_t *, const uint8_t *, const uint64_t *, const uint32_t *,
+                  uint32_t *);
+hipError_t ev_hash_chain(hipStream_t, uint32_t, uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
+                         const bv_event_batch &, const uint32_t *, uint8_t *, const uint64_t *, const uint32_t *,
+                         uint32_t *);
 hipError_t iota(hipStream_t, uint64_t, uint32_t *);
 hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
                         uint32_t *, uint32_t *);
@@ -193,7 +196,7 @@ struct bv_ctx {
   uint64_t kc_clock = 0, kc_bytes = 0, kc_budget = 0;
   DevBuf kc_tabs, kc_kst, kc_kxy, kc_btabs;
   // bv_verify_events: body lengths, parent-hex positions, offsets, bodies
-  DevBuf ev_lens, ev_ppos, ev_offs, ev_bodies, ev_tmp, ev_iota;
+  DevBuf ev_lens, ev_ppos, ev_offs, ev_bodies, ev_tmp, ev_iota, ev_mid;
 };
 
 // one in-flight host-entry call (bv_host_launch -> bv_host_finish)

@@ -22,6 +22,7 @@
 #include "verify_core.h"
 
 #include <hipcub/hipcub.hpp>
+#include <cstdlib>
 
 __global__ void __launch_bounds__(256) k_sha256(uint64_t n_msgs, const uint8_t *__restrict__ bytes,
                                                 const uint64_t *__restrict__ off,
@@ -131,21 +132,223 @@ __global__ void __launch_bounds__(256) k_ev_hash(uint64_t count, const uint32_t 
   if (i < count) ev_splice_hash(list ? list[i] : i, b, ppos, bodies, offs, dig, false);
 }
 
-// Consecutive NARROW levels [l0, l1) in one launch of one workgroup: level
-// L's events (order[level_off[L] .. level_off[L+1])) hash in parallel, then
-// a fence + barrier before level L+1 reads their digests.  core.sync's
-// SyncResponse is ~SyncLimit events, a few per level (one per creator).
-__global__ void __launch_bounds__(1024) k_ev_hash_chain(uint32_t l0, uint32_t l1,
-                                                        const uint32_t *__restrict__ level_off,
-                                                        const uint32_t *__restrict__ order, bv_event_batch b,
-                                                        const uint32_t *__restrict__ ppos, uint8_t *__restrict__ bodies,
-                                                        const uint64_t *__restrict__ offs, uint32_t *__restrict__ dig) {
-  for (uint32_t L = l0; L < l1; L++) {
-    for (uint32_t i = level_off[L] + threadIdx.x; i < level_off[L + 1]; i += blockDim.x)
-      ev_splice_hash(order[i], b, ppos, bodies, offs, dig, true);
-    __threadfence();
-    __syncthreads();
+// Midstates (evjson.h: ev_midstate) of `count` events (list[i]): the
+// blocks before each body's first in-batch parent, all events in parallel.
+__global__ void __launch_bounds__(256) k_ev_mid(uint64_t count, const uint32_t *__restrict__ list,
+                                                const uint8_t *__restrict__ bodies, const uint64_t *__restrict__ offs,
+                                                const uint32_t *__restrict__ ppos, uint32_t *__restrict__ mid) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) ev_midstate(list[i], bodies, offs, ppos, mid);
+}
+
+// Consecutive NARROW levels [l0, l1) in one launch of one workgroup
+// (core.sync's SyncResponse: ~SyncLimit events, a few per level, hundreds
+// of levels).  The DAG makes this a serial chain of SHA-256 compressions: a
+// lane can only start an event once its parents' digests exist.  A single
+// wave issues about one VALU per 6 cycles (tools/ubench_sha.hip), so the
+// design keeps everything but the rounds off the hashing lanes, and keeps
+// wave 0 (the hashing lanes) free of global memory operations, so no
+// s_waitcnt on HBM traffic ever lands on the chain:
+//  * prologue: the launch's events (<= EVC_CAP, host-guaranteed) get an LDS
+//    descriptor (tail location, hex positions, parents as LDS digest slots),
+//    built by the whole workgroup in parallel;
+//  * per level L:
+//    A  waves 1-3 move level L's body tails and midstates (k_ev_mid), loaded
+//       into their registers during level L-1, to LDS, then issue the loads
+//       for level L+1;
+//    B  lane i splices the i-th event's parents' hex into its LDS tail from
+//       the LDS digest cache (parents hashed by an earlier launch: HBM);
+//    C  one lane per (event, block) expands the block's W+K schedule into LDS;
+//    D  lane i runs the 64 rounds per block from its midstate; the digest
+//       goes to the LDS cache;
+//  * epilogue: the launch's digests go to HBM (coalesced).
+// Events past EVC_SLOTS / EVC_WEV in a level, or with tails longer than
+// EVC_SLOT_DW or more than EVC_WBLK blocks, take the same steps with the
+// schedule inline (and from HBM when not in LDS).
+#define EVC_SLOTS 64
+#define EVC_SLOT_DW 128
+#define EVC_CAP 1024
+#define EVC_WEV 8    // events per level with precomputed schedules
+#define EVC_WBLK 8   //   x blocks per event
+#define EVC_NT 256   // one wave per SIMD: the hashing lanes get the full register file (no spills)
+#define EVC_LT (EVC_NT - 64)                                     // loader lanes: waves 1-3
+#define EVC_PF ((EVC_SLOTS * EVC_SLOT_DW + EVC_LT - 1) / EVC_LT)  // tail dwords per loader lane
+#define EVC_PM ((EVC_SLOTS * 8 + EVC_LT - 1) / EVC_LT)            // midstate words per loader lane
+static_assert(EVC_PF + EVC_PM <= 64, "prefetch masks are 64 bits");
+// descriptor words: e | a0 lo | a0 hi | tail dwords (<= 2^24 - 1) + sh << 24 | nb | len |
+// hex pos 0, 1 (within the tail) | parent 0, 1 LDS slot | parent 0, 1 event
+#define EVC_DESC 12
+// loader lane u = t - 64 of waves 1-3: level L's tails and midstates into
+// registers; bit r of the result = register r holds a word to store
+__device__ __forceinline__ uint64_t evc_load(uint32_t L, uint32_t nl, uint32_t u, const uint32_t *sLof,
+                                             const uint32_t *sDesc, const uint32_t *bw, const uint32_t *mid,
+                                             uint32_t pf[EVC_PF + EVC_PM]) {
+  uint64_t got = 0;
+  if (L >= nl) return got;
+  const uint32_t lo = sLof[L], w = sLof[L + 1] - lo, ws = w < EVC_SLOTS ? w : EVC_SLOTS;
+#pragma unroll
+  for (int r = 0; r < EVC_PF; r++) {
+    const uint32_t x = u + EVC_LT * r, i = x / EVC_SLOT_DW, k = x % EVC_SLOT_DW;
+    if (i < ws) {
+      const uint32_t *d = sDesc + EVC_DESC * (lo + i);
+      const uint64_t a0 = (uint64_t)d[1] | ((uint64_t)d[2] << 32);
+      const uint32_t nd = d[3] & 0xFFFFFFu;
+      if (nd <= EVC_SLOT_DW && k < nd) {
+        pf[r] = bw[a0 + k];
+        got |= 1ull << r;
+      }
+    }
   }
+#pragma unroll
+  for (int r = 0; r < EVC_PM; r++) {
+    const uint32_t x = u + EVC_LT * r, i = x / 8, k = x % 8;
+    if (i < ws) {
+      pf[EVC_PF + r] = mid[(uint64_t)EV_MID_U32 * sDesc[EVC_DESC * (lo + i)] + k];
+      got |= 1ull << (EVC_PF + r);
+    }
+  }
+  return got;
+}
+__device__ __noinline__ void evc_hash_inline(uint32_t h[8], const uint32_t *src, uint32_t sh, uint32_t len,
+                                             uint32_t nb, uint32_t nblk) {
+  sha256_blocks(h, src, sh, len, nb, nblk);
+}
+__global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t l1,
+                                                        const uint32_t *__restrict__ level_off,
+                                                        const uint32_t *__restrict__ order,
+                                                        const uint32_t *__restrict__ posin, bv_event_batch b,
+                                                        const uint32_t *__restrict__ ppos, uint8_t *__restrict__ bodies,
+                                                        const uint64_t *__restrict__ offs,
+                                                        const uint32_t *__restrict__ mid, uint32_t *__restrict__ dig,
+                                                        uint64_t *__restrict__ prof) {
+  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = __builtin_readcyclecounter(), tq;
+#define EVC_STAMP(k) do { if (prof) { tq = __builtin_readcyclecounter(); acc[k] += tq - tp; tp = tq; } } while (0)
+  __shared__ uint32_t sBody[EVC_SLOTS * EVC_SLOT_DW];  // 32 KB: the level's body tails
+  __shared__ uint32_t sMid[EVC_SLOTS * 8];             //  2 KB: the level's midstates
+  __shared__ uint32_t sDig[EVC_CAP * 8];               // 32 KB: digests hashed in this launch
+  __shared__ uint32_t sDesc[EVC_CAP * EVC_DESC];       // 48 KB: per-event descriptors
+  __shared__ uint32_t sWK[EVC_WEV * EVC_WBLK * 64];    // 16 KB: W+K schedules of the level
+  __shared__ uint32_t sLof[EVC_CAP + 1];               // level offsets, relative to the launch
+  const uint32_t t = threadIdx.x;
+  const uint32_t E0 = level_off[l0], E1 = level_off[l1], nl = l1 - l0;
+  const uint32_t *bw = (const uint32_t *)bodies;
+  // ---- prologue: level offsets and descriptors, all lanes in parallel
+  for (uint32_t x = t; x <= nl; x += EVC_NT) sLof[x] = level_off[l0 + x] - E0;
+  for (uint32_t s = t; s < E1 - E0; s += EVC_NT) {
+    const uint32_t e = order[E0 + s];
+    const uint64_t o = offs[e], len = offs[e + 1] - o;
+    const uint32_t nb = mid[(uint64_t)EV_MID_U32 * e + 8];
+    const uint64_t a0 = (o + 64ull * nb) >> 2, nd = ((o + len + 8 + 3) >> 2) - a0;  // + the 8-byte over-read pad
+    uint32_t *d = sDesc + EVC_DESC * s;
+    d[0] = e;
+    d[1] = (uint32_t)a0;
+    d[2] = (uint32_t)(a0 >> 32);
+    d[3] = (uint32_t)(nd < 0xFFFFFFu ? nd : 0xFFFFFFu) | (uint32_t)(o & 3) << 24;
+    d[4] = nb;
+    d[5] = (uint32_t)len;
+    for (int p = 0; p < 2; p++) {
+      const uint32_t pos = ppos[2 * e + p];
+      const uint32_t q = pos == EVJ_NOPOS ? 0u : (uint32_t)b.parent_ref[2 * e + p];
+      const uint32_t sq = pos == EVJ_NOPOS ? 0u : posin[q];
+      d[6 + p] = pos == EVJ_NOPOS ? EVJ_NOPOS : (uint32_t)(o + pos - 4 * a0);
+      d[8 + p] = (pos != EVJ_NOPOS && sq >= E0 && sq < E1) ? sq - E0 : EVJ_NOPOS;
+      d[10 + p] = q;
+    }
+  }
+  __syncthreads();
+  uint32_t pf[EVC_PF + EVC_PM];
+  uint64_t got = t >= 64 ? evc_load(0, nl, t - 64, sLof, sDesc, bw, mid, pf) : 0;
+  EVC_STAMP(0);
+  for (uint32_t L = 0; L < nl; L++) {
+    const uint32_t lo = sLof[L], w = sLof[L + 1] - lo;
+    // ---- A: level L's tails and midstates -> LDS; loads for level L+1
+    if (t >= 64) {
+#pragma unroll
+      for (int r = 0; r < EVC_PF; r++)
+        if ((got >> r) & 1u) sBody[(t - 64) + EVC_LT * r] = pf[r];
+#pragma unroll
+      for (int r = 0; r < EVC_PM; r++)
+        if ((got >> (EVC_PF + r)) & 1u) sMid[(t - 64) + EVC_LT * r] = pf[EVC_PF + r];
+    }
+    __syncthreads();
+    if (t >= 64) got = evc_load(L + 1, nl, t - 64, sLof, sDesc, bw, mid, pf);
+    EVC_STAMP(1);
+    // ---- B: parents' hex into the tails
+    for (uint32_t i = t; i < w; i += EVC_NT) {
+      const uint32_t *d = sDesc + EVC_DESC * (lo + i);
+      const uint32_t nd = d[3] & 0xFFFFFFu;
+      const uint64_t a0 = (uint64_t)d[1] | ((uint64_t)d[2] << 32);
+      const bool in_lds = i < EVC_SLOTS && nd <= EVC_SLOT_DW;
+      for (int p = 0; p < 2; p++) {
+        const uint32_t rel = d[6 + p];
+        if (rel == EVJ_NOPOS) continue;
+        const uint32_t ps = d[8 + p], q = d[10 + p];
+        uint32_t wd[8], hx[16];
+        if (ps != EVJ_NOPOS) {  // separate loads: a selected pointer would be a FLAT access
+          for (int k = 0; k < 8; k++) wd[k] = sDig[8 * ps + k];
+        } else {
+          for (int k = 0; k < 8; k++) wd[k] = dig[8 * (uint64_t)q + k];
+        }
+        if (in_lds) {
+          evj_hex32_words(hx, wd);
+          evj_put64(sBody + i * EVC_SLOT_DW, rel, hx);
+        } else {
+          uint8_t dd[32];
+          for (int k = 0; k < 8; k++)
+            for (int c = 0; c < 4; c++) dd[4 * k + c] = (uint8_t)(wd[k] >> (8 * c));  // words hold BE digest bytes
+          evj_hex32(bodies + 4 * a0 + rel, dd);  // hashed from HBM in D
+        }
+      }
+    }
+    __syncthreads();
+    EVC_STAMP(2);
+    // ---- C: message schedules, one lane per (event, block)
+    {
+      const uint32_t wv = w < EVC_WEV ? w : EVC_WEV;
+      for (uint32_t x = t; x < wv * EVC_WBLK; x += EVC_NT) {
+        const uint32_t i = x / EVC_WBLK, jj = x % EVC_WBLK;
+        const uint32_t *d = sDesc + EVC_DESC * (lo + i);
+        const uint32_t nd = d[3] & 0xFFFFFFu, sh = d[3] >> 24, nb = d[4], len = d[5];
+        const uint32_t nblk = (uint32_t)sha256_nblocks(len), j = nb + jj;
+        if (nd > EVC_SLOT_DW || nblk - nb > EVC_WBLK || j >= nblk) continue;
+        uint32_t w16[16];
+        sha256_block_words(w16, sBody + i * EVC_SLOT_DW, sh, len, nb, j);
+        sha256_schedule_wk(sWK + x * 64, w16);
+      }
+    }
+    __syncthreads();
+    EVC_STAMP(3);
+    // ---- D: the rounds (the serial part)
+    for (uint32_t i = t; i < w; i += EVC_NT) {
+      const uint32_t *d = sDesc + EVC_DESC * (lo + i);
+      const uint32_t nd = d[3] & 0xFFFFFFu, sh = d[3] >> 24, nb = d[4], len = d[5];
+      const uint32_t nblk = (uint32_t)sha256_nblocks(len);
+      uint32_t h[8];
+      if (i < EVC_SLOTS) {
+        for (int k = 0; k < 8; k++) h[k] = sMid[8 * i + k];
+      } else {
+        for (int k = 0; k < 8; k++) h[k] = mid[(uint64_t)EV_MID_U32 * d[0] + k];
+      }
+      const bool in_lds = i < EVC_SLOTS && nd <= EVC_SLOT_DW;
+      if (in_lds && i < EVC_WEV && nblk - nb <= EVC_WBLK) {
+        for (uint32_t jj = 0; jj < nblk - nb; jj++) sha256_rounds_wk(h, sWK + (i * EVC_WBLK + jj) * 64);
+      } else {
+        const uint64_t a0 = (uint64_t)d[1] | ((uint64_t)d[2] << 32);
+        evc_hash_inline(h, in_lds ? sBody + i * EVC_SLOT_DW : bw + a0, sh, len, nb, nblk);
+      }
+      uint32_t wd[8];
+      ev_digest_words(wd, h);
+      for (int k = 0; k < 8; k++) sDig[8 * (lo + i) + k] = wd[k];
+    }
+    EVC_STAMP(4);
+    __syncthreads();
+    EVC_STAMP(5);
+  }
+  // ---- epilogue: the digests to HBM
+  for (uint32_t x = t; x < (E1 - E0) * 8; x += EVC_NT) dig[8 * (uint64_t)sDesc[EVC_DESC * (x / 8)] + x % 8] = sDig[x];
+  if (prof && t == 0)
+    for (int k = 0; k < 8; k++) prof[k] = acc[k];
+#undef EVC_STAMP
 }
 
 __global__ void __launch_bounds__(256) k_iota(uint64_t n, uint32_t *__restrict__ out) {
@@ -545,12 +748,30 @@ hipError_t ev_hash(hipStream_t st, uint64_t count, const uint32_t *list, const b
   return hipGetLastError();
 }
 
+static uint64_t *evc_prof_buf() {
+  static uint64_t *p = nullptr;
+  if (!p) (void)hipMallocManaged(&p, 64);
+  return p;
+}
+extern "C" void bv_debug_evc_prof(uint64_t out[8]) {
+  (void)hipDeviceSynchronize();
+  uint64_t *p = evc_prof_buf();
+  for (int k = 0; k < 8; k++) out[k] = p ? p[k] : 0;
+}
+
+hipError_t ev_mid(hipStream_t st, uint64_t count, const uint32_t *list, const uint8_t *bodies, const uint64_t *offs,
+                  const uint32_t *ppos, uint32_t *mid) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ev_mid, grid1(count, 256), dim3(256), 0, st, count, list, bodies, offs, ppos, mid);
+  return hipGetLastError();
+}
+
 hipError_t ev_hash_chain(hipStream_t st, uint32_t l0, uint32_t l1, const uint32_t *level_off, const uint32_t *order,
-                         const bv_event_batch &b, const uint32_t *ppos, uint8_t *bodies, const uint64_t *offs,
-                         uint32_t *dig) {
+                         const uint32_t *posin, const bv_event_batch &b, const uint32_t *ppos, uint8_t *bodies,
+                         const uint64_t *offs, const uint32_t *mid, uint32_t *dig) {
   if (l1 <= l0) return hipSuccess;
-  hipLaunchKernelGGL(k_ev_hash_chain, dim3(1), dim3(1024), 0, st, l0, l1, level_off, order, b, ppos, bodies, offs,
-                     dig);
+  hipLaunchKernelGGL(k_ev_hash_chain, dim3(1), dim3(EVC_NT), 0, st, l0, l1, level_off, order, posin, b, ppos, bodies,
+                     offs, mid, dig, getenv("BV_EVC_PROF") ? evc_prof_buf() : nullptr);
   return hipGetLastError();
 }
 

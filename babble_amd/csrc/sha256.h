@@ -73,67 +73,147 @@ DEV void sha256_compress(uint32_t h[8], uint32_t w[16]) {
   h[7] += hh;
 }
 
+DEV void sha256_init(uint32_t h[8]) {
+  h[0] = 0x6a09e667u; h[1] = 0xbb67ae85u; h[2] = 0x3c6ef372u; h[3] = 0xa54ff53au;
+  h[4] = 0x510e527fu; h[5] = 0x9b05688cu; h[6] = 0x1f83d9abu; h[7] = 0x5be0cd19u;
+}
+
+DEV uint64_t sha256_nblocks(uint64_t len) { return (len + 9 + 63) / 64; }
+
+// The 16 big-endian message words of block `blk` of a len-byte message
+// (FIPS padding and length included).  `src0` is the 4-byte aligned dword
+// holding message byte 64 blk0, `sh` that byte's offset within it; the
+// buffer is padded by >= 8 bytes past the message end (the realignment
+// over-reads one dword).
+DEV void sha256_block_words(uint32_t w[16], const uint32_t *src0, uint32_t sh, uint64_t len, uint64_t blk0,
+                            uint64_t blk) {
+  const uint64_t p0 = blk * 64;  // byte position of this block in the message
+  if (p0 + 64 <= len) {
+    // full data block: 17 aligned dwords, realigned
+    const uint32_t *src = src0 + (blk - blk0) * 16;
+    uint32_t d[17];
+#if defined(__HIP_DEVICE_COMPILE__)
+    // 4 dwordx4 loads at dword alignment (gfx950 global loads need not be
+    // 16-byte aligned): a quarter of the load instructions, and each lane
+    // touches a cache line once per load instead of four times
+    typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+    const u32x4a4 *v = (const u32x4a4 *)src;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const u32x4a4 x = v[i];
+      d[4 * i] = x.x;
+      d[4 * i + 1] = x.y;
+      d[4 * i + 2] = x.z;
+      d[4 * i + 3] = x.w;
+    }
+    d[16] = src[16];
+#else
+#pragma unroll
+    for (int i = 0; i < 17; i++) d[i] = src[i];
+#endif
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = bswap32(alignbyte(d[i + 1], d[i], sh));
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint64_t p = p0 + 4 * i;
+    uint32_t x = 0;
+    if (p < len) {
+      const uint32_t *src = src0 + ((p - blk0 * 64) >> 2);
+      x = alignbyte(src[1], src[0], sh);  // LE word of bytes p..p+3
+      const uint64_t rem = len - p;        // bytes of message left
+      if (rem < 4) {
+        const uint32_t keep = (uint32_t)rem * 8u;
+        x = (x & ((1u << keep) - 1u)) | (0x80u << keep);
+      }
+    } else if (p == len) {
+      x = 0x80u;
+    }
+    w[i] = bswap32(x);
+  }
+  if (blk == sha256_nblocks(len) - 1) {
+    const uint64_t bitlen = len * 8;
+    w[14] = (uint32_t)(bitlen >> 32);
+    w[15] = (uint32_t)bitlen;
+  }
+}
+
+// Compress blocks [blk0, blk1) of a len-byte message into h (see
+// sha256_block_words for src0 / sh).  Lets a caller hash a message in
+// pieces: a midstate over leading blocks, then the rest from another buffer
+// (k_ev_hash_chain).
+DEV void sha256_blocks(uint32_t h[8], const uint32_t *src0, uint32_t sh, uint64_t len, uint64_t blk0,
+                       uint64_t blk1) {
+  for (uint64_t blk = blk0; blk < blk1; blk++) {
+    uint32_t w[16];
+    sha256_block_words(w, src0, sh, len, blk0, blk);
+    sha256_compress(h, w);
+  }
+}
+
+// The message schedule with the round constants folded in: wk[i] = W_i + K_i.
+// Independent of the chaining state, so another lane can compute it while
+// the previous block's rounds run (k_ev_hash_chain).
+// `wk` may live in LDS: the 48 expansion steps run as a 3-trip loop of 16
+// (the ring indices stay static), which keeps the chain kernel's code small.
+DEV void sha256_schedule_wk(uint32_t *wk, const uint32_t w[16]) {
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    x[i] = w[i];
+    wk[i] = w[i] + SHA_K[i];
+  }
+#pragma unroll 1
+  for (int r = 16; r < 64; r += 16) {
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const uint32_t w15 = x[(u + 1) & 15], w2 = x[(u + 14) & 15];
+      const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+      x[u] = x[u] + s0 + x[(u + 9) & 15] + s1;
+      wk[r + u] = x[u] + SHA_K[r + u];
+    }
+  }
+}
+
+// The 64 rounds of one block from a precomputed W + K schedule.
+// An 8-trip loop of 8 rounds (the state rotation maps onto itself every 8
+// rounds, so no register moves): small code for a latency-bound single
+// wave, whose instruction cache is shared with the rest of its kernel.
+DEV void sha256_rounds_wk(uint32_t h[8], const uint32_t *wk) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll 1
+  for (int r = 0; r < 64; r += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t t1 = hh + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g)) + wk[r + u];
+      const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+      hh = g;
+      g = f;
+      f = e;
+      e = d + t1;
+      d = c;
+      c = b;
+      b = a;
+      a = t1 + t2;
+    }
+  }
+  h[0] += a;
+  h[1] += b;
+  h[2] += c;
+  h[3] += d;
+  h[4] += e;
+  h[5] += f;
+  h[6] += g;
+  h[7] += hh;
+}
+
 // SHA-256 of bytes [off, off+len) of `base` (a 4-byte aligned buffer padded
 // by >= 8 bytes past its end).  Output: the 8 state words h[0..7] (digest =
 // big-endian serialisation of h).
 DEV void sha256_msg(uint32_t h[8], const uint8_t *base, uint64_t off, uint64_t len) {
-  h[0] = 0x6a09e667u; h[1] = 0xbb67ae85u; h[2] = 0x3c6ef372u; h[3] = 0xa54ff53au;
-  h[4] = 0x510e527fu; h[5] = 0x9b05688cu; h[6] = 0x1f83d9abu; h[7] = 0x5be0cd19u;
-  const uint64_t nblocks = (len + 9 + 63) / 64;
-  const uint32_t *wbase = (const uint32_t *)(base + (off & ~(uint64_t)3));
-  const uint32_t sh = (uint32_t)(off & 3);
-  const uint64_t bitlen = len * 8;
-  for (uint64_t blk = 0; blk < nblocks; blk++) {
-    uint32_t w[16];
-    const uint64_t p0 = blk * 64;  // byte position of this block in the message
-    if (p0 + 64 <= len) {
-      // full data block: 17 aligned dwords, realigned
-      const uint32_t *src = wbase + blk * 16;
-      uint32_t d[17];
-#if defined(__HIP_DEVICE_COMPILE__)
-      // 4 dwordx4 loads at dword alignment (gfx950 global loads need not be
-      // 16-byte aligned): a quarter of the load instructions, and each lane
-      // touches a cache line once per load instead of four times
-      typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-      const u32x4a4 *v = (const u32x4a4 *)src;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const u32x4a4 x = v[i];
-        d[4 * i] = x.x;
-        d[4 * i + 1] = x.y;
-        d[4 * i + 2] = x.z;
-        d[4 * i + 3] = x.w;
-      }
-      d[16] = src[16];
-#else
-#pragma unroll
-      for (int i = 0; i < 17; i++) d[i] = src[i];
-#endif
-#pragma unroll
-      for (int i = 0; i < 16; i++) w[i] = bswap32(alignbyte(d[i + 1], d[i], sh));
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const uint64_t p = p0 + 4 * i;
-        uint32_t x = 0;
-        if (p < len) {
-          const uint32_t *src = wbase + (p >> 2);
-          x = alignbyte(src[1], src[0], sh);  // LE word of bytes p..p+3
-          const uint64_t rem = len - p;                         // bytes of message left
-          if (rem < 4) {
-            const uint32_t keep = (uint32_t)rem * 8u;
-            x = (x & ((1u << keep) - 1u)) | (0x80u << keep);
-          }
-        } else if (p == len) {
-          x = 0x80u;
-        }
-        w[i] = bswap32(x);
-      }
-      if (blk == nblocks - 1) {
-        w[14] = (uint32_t)(bitlen >> 32);
-        w[15] = (uint32_t)bitlen;
-      }
-    }
-    sha256_compress(h, w);
-  }
+  sha256_init(h);
+  sha256_blocks(h, (const uint32_t *)(base + (off & ~(uint64_t)3)), (uint32_t)(off & 3), len, 0,
+                sha256_nblocks(len));
 }
