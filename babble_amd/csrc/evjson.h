@@ -284,3 +284,24 @@ DEV void evj_put64(uint32_t *buf, uint32_t rel, const uint32_t v[16]) {
   for (int k = 1; k < 16; k++) buf[q + k] = (v[k - 1] >> (32 - sh)) | (v[k] << sh);
   buf[q + 16] = (buf[q + 16] & ~keep) | (v[15] >> (32 - sh));
 }
+
+// Dword q of a buffer holding a message tail whose bytes end at E, padded
+// per FIPS 180-4 up to F (the end of the final block): bytes < E keep `v`,
+// byte E is 0x80, the last 8 bytes before F hold the big-endian bit length,
+// the rest are zero.
+DEV uint32_t evj_pad_word(uint32_t v, uint32_t q, uint32_t E, uint32_t F, uint64_t bitlen) {
+  if (4 * q + 4 <= E) return v;
+  uint32_t out = 0;
+  for (uint32_t c = 0; c < 4; c++) {
+    const uint32_t b = 4 * q + c;
+    uint32_t byte = 0;
+    if (b < E)
+      byte = (v >> (8 * c)) & 0xFFu;
+    else if (b == E)
+      byte = 0x80u;
+    else if (b + 8 >= F && b < F)
+      byte = (uint32_t)(bitlen >> (8 * (F - 1 - b))) & 0xFFu;
+    out |= byte << (8 * c);
+  }
+  return out;
+}

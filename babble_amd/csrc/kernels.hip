@@ -22,7 +22,6 @@
 #include "verify_core.h"
 
 #include <hipcub/hipcub.hpp>
-#include <cstdlib>
 
 __global__ void __launch_bounds__(256) k_sha256(uint64_t n_msgs, const uint8_t *__restrict__ bytes,
                                                 const uint64_t *__restrict__ off,
@@ -153,14 +152,17 @@ __global__ void __launch_bounds__(256) k_ev_mid(uint64_t count, const uint32_t *
 //    descriptor (tail location, hex positions, parents as LDS digest slots),
 //    built by the whole workgroup in parallel;
 //  * per level L:
-//    A  waves 1-3 move level L's body tails and midstates (k_ev_mid), loaded
-//       into their registers during level L-1, to LDS, then issue the loads
-//       for level L+1;
+//    A  waves 1-3 move level L's body tails (padded to whole SHA-256
+//       blocks) and midstates (k_ev_mid), loaded into their registers during
+//       level L-1, to LDS, then issue the loads for level L+1;
 //    B  lane i splices the i-th event's parents' hex into its LDS tail from
 //       the LDS digest cache (parents hashed by an earlier launch: HBM);
-//    C  one lane per (event, block) expands the block's W+K schedule into LDS;
+//    C  one lane per (event, block) expands the block's W+K schedule into LDS
+//       (interleaved across events, so the round lanes read distinct banks);
 //    D  lane i runs the 64 rounds per block from its midstate; the digest
 //       goes to the LDS cache;
+//  Measured (1000 events, 4 creators, 249 levels of 6 tail blocks): ~22 us
+//  per level, ~17 of it the rounds (about 3 us per block on one wave).
 //  * epilogue: the launch's digests go to HBM (coalesced).
 // Events past EVC_SLOTS / EVC_WEV in a level, or with tails longer than
 // EVC_SLOT_DW or more than EVC_WBLK blocks, take the same steps with the
@@ -168,50 +170,80 @@ __global__ void __launch_bounds__(256) k_ev_mid(uint64_t count, const uint32_t *
 #define EVC_SLOTS 64
 #define EVC_SLOT_DW 128
 #define EVC_CAP 1024
-#define EVC_WEV 8    // events per level with precomputed schedules
-#define EVC_WBLK 8   //   x blocks per event
+#define EVC_WEV 8    // events per level with LDS schedules
+#define EVC_WBLK 7   // tail blocks of an LDS event: 7 x 16 + 1 dwords fit a slot
 #define EVC_NT 256   // one wave per SIMD: the hashing lanes get the full register file (no spills)
 #define EVC_LT (EVC_NT - 64)                                     // loader lanes: waves 1-3
 #define EVC_PF ((EVC_SLOTS * EVC_SLOT_DW + EVC_LT - 1) / EVC_LT)  // tail dwords per loader lane
 #define EVC_PM ((EVC_SLOTS * 8 + EVC_LT - 1) / EVC_LT)            // midstate words per loader lane
-static_assert(EVC_PF + EVC_PM <= 64, "prefetch masks are 64 bits");
-// descriptor words: e | a0 lo | a0 hi | tail dwords (<= 2^24 - 1) + sh << 24 | nb | len |
+// descriptor words: e | a0 lo | a0 hi | tail dwords in HBM (<= 2^24 - 1) + sh << 24 | nb | len |
 // hex pos 0, 1 (within the tail) | parent 0, 1 LDS slot | parent 0, 1 event
 #define EVC_DESC 12
-// loader lane u = t - 64 of waves 1-3: level L's tails and midstates into
-// registers; bit r of the result = register r holds a word to store
-__device__ __forceinline__ uint64_t evc_load(uint32_t L, uint32_t nl, uint32_t u, const uint32_t *sLof,
-                                             const uint32_t *sDesc, const uint32_t *bw, const uint32_t *mid,
-                                             uint32_t pf[EVC_PF + EVC_PM]) {
-  uint64_t got = 0;
-  if (L >= nl) return got;
+// An event is hashed from LDS when its tail, padded to whole blocks, fits a
+// slot: nblk - nb <= EVC_WBLK.
+DEV bool evc_lds_event(uint32_t i, uint32_t nb, uint32_t len) {
+  return i < EVC_SLOTS && (uint32_t)sha256_nblocks(len) - nb <= EVC_WBLK;
+}
+// loader lane u of waves 1-3: level L's tails and midstates into registers
+// (only the dwords the LDS events need)
+__device__ __forceinline__ void evc_load(uint32_t L, uint32_t nl, uint32_t u, const uint32_t *sLof,
+                                         const uint32_t *sDesc, const uint32_t *bw, const uint32_t *mid,
+                                         uint32_t pf[EVC_PF + EVC_PM]) {
+  if (L >= nl) return;
   const uint32_t lo = sLof[L], w = sLof[L + 1] - lo, ws = w < EVC_SLOTS ? w : EVC_SLOTS;
 #pragma unroll
   for (int r = 0; r < EVC_PF; r++) {
     const uint32_t x = u + EVC_LT * r, i = x / EVC_SLOT_DW, k = x % EVC_SLOT_DW;
-    if (i < ws) {
-      const uint32_t *d = sDesc + EVC_DESC * (lo + i);
-      const uint64_t a0 = (uint64_t)d[1] | ((uint64_t)d[2] << 32);
-      const uint32_t nd = d[3] & 0xFFFFFFu;
-      if (nd <= EVC_SLOT_DW && k < nd) {
-        pf[r] = bw[a0 + k];
-        got |= 1ull << r;
-      }
-    }
+    if (i >= ws) break;
+    const uint32_t *d = sDesc + EVC_DESC * (lo + i);
+    if (k < (d[3] & 0xFFFFFFu) && evc_lds_event(i, d[4], d[5])) pf[r] = bw[((uint64_t)d[1] | ((uint64_t)d[2] << 32)) + k];
   }
 #pragma unroll
   for (int r = 0; r < EVC_PM; r++) {
     const uint32_t x = u + EVC_LT * r, i = x / 8, k = x % 8;
-    if (i < ws) {
-      pf[EVC_PF + r] = mid[(uint64_t)EV_MID_U32 * sDesc[EVC_DESC * (lo + i)] + k];
-      got |= 1ull << (EVC_PF + r);
-    }
+    if (i >= ws) break;
+    pf[EVC_PF + r] = mid[(uint64_t)EV_MID_U32 * sDesc[EVC_DESC * (lo + i)] + k];
   }
-  return got;
 }
+__device__ __noinline__ uint32_t evc_pad(uint32_t v, uint32_t q, uint32_t E, uint32_t F, uint64_t bitlen) {
+  return evj_pad_word(v, q, E, F, bitlen);
+}
+// ... and into LDS, each tail padded to whole blocks (FIPS 180-4: 0x80,
+// zeros, the 64-bit bit length) so C reads whole blocks only
+__device__ __forceinline__ void evc_stage(uint32_t L, uint32_t u, const uint32_t *sLof, const uint32_t *sDesc,
+                                          const uint32_t pf[EVC_PF + EVC_PM], uint32_t *sBody, uint32_t *sMid) {
+  const uint32_t lo = sLof[L], w = sLof[L + 1] - lo, ws = w < EVC_SLOTS ? w : EVC_SLOTS;
+#pragma unroll
+  for (int r = 0; r < EVC_PF; r++) {
+    const uint32_t x = u + EVC_LT * r, i = x / EVC_SLOT_DW, k = x % EVC_SLOT_DW;
+    if (i >= ws) break;
+    const uint32_t *d = sDesc + EVC_DESC * (lo + i);
+    const uint32_t nb = d[4], len = d[5], sh = d[3] >> 24;
+    if (!evc_lds_event(i, nb, len)) continue;
+    const uint32_t nt = (uint32_t)sha256_nblocks(len) - nb, E = len - 64 * nb + sh;
+    if (k > 16 * nt) continue;  // 16 nt + 1 dwords: the realignment reads one past the last block
+    uint32_t v = k < (d[3] & 0xFFFFFFu) ? pf[r] : 0u;
+    if (4 * k + 4 > E) v = evc_pad(v, k, E, 64 * nt + sh, 8ull * len);
+    sBody[x] = v;
+  }
+#pragma unroll
+  for (int r = 0; r < EVC_PM; r++) {
+    const uint32_t x = u + EVC_LT * r;
+    if (x / 8 >= ws) break;
+    sMid[x] = pf[EVC_PF + r];
+  }
+}
+// the slower paths of phase D, out of line (keeps the chain's code small)
 __device__ __noinline__ void evc_hash_inline(uint32_t h[8], const uint32_t *src, uint32_t sh, uint32_t len,
                                              uint32_t nb, uint32_t nblk) {
   sha256_blocks(h, src, sh, len, nb, nblk);
+}
+__device__ __noinline__ void evc_hash_padded(uint32_t h[8], const uint32_t *slot, uint32_t sh, uint32_t nt) {
+  for (uint32_t j = 0; j < nt; j++) {
+    uint32_t w16[16];
+    sha256_block_words_padded(w16, slot + 16 * j, sh);
+    sha256_compress(h, w16);
+  }
 }
 __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t l1,
                                                         const uint32_t *__restrict__ level_off,
@@ -219,15 +251,14 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
                                                         const uint32_t *__restrict__ posin, bv_event_batch b,
                                                         const uint32_t *__restrict__ ppos, uint8_t *__restrict__ bodies,
                                                         const uint64_t *__restrict__ offs,
-                                                        const uint32_t *__restrict__ mid, uint32_t *__restrict__ dig,
-                                                        uint64_t *__restrict__ prof) {
-  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = __builtin_readcyclecounter(), tq;
-#define EVC_STAMP(k) do { if (prof) { tq = __builtin_readcyclecounter(); acc[k] += tq - tp; tp = tq; } } while (0)
+                                                        const uint32_t *__restrict__ mid, uint32_t *__restrict__ dig) {
   __shared__ uint32_t sBody[EVC_SLOTS * EVC_SLOT_DW];  // 32 KB: the level's body tails
   __shared__ uint32_t sMid[EVC_SLOTS * 8];             //  2 KB: the level's midstates
   __shared__ uint32_t sDig[EVC_CAP * 8];               // 32 KB: digests hashed in this launch
   __shared__ uint32_t sDesc[EVC_CAP * EVC_DESC];       // 48 KB: per-event descriptors
-  __shared__ uint32_t sWK[EVC_WEV * EVC_WBLK * 64];    // 16 KB: W+K schedules of the level
+  // 14 KB: W+K schedules of the level, [block][16-byte chunk][event][4]
+  // (lanes in lockstep read distinct banks)
+  __shared__ uint32_t sWK[EVC_WEV * EVC_WBLK * 64];
   __shared__ uint32_t sLof[EVC_CAP + 1];               // level offsets, relative to the launch
   const uint32_t t = threadIdx.x;
   const uint32_t E0 = level_off[l0], E1 = level_off[l1], nl = l1 - l0;
@@ -257,71 +288,57 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
   }
   __syncthreads();
   uint32_t pf[EVC_PF + EVC_PM];
-  uint64_t got = t >= 64 ? evc_load(0, nl, t - 64, sLof, sDesc, bw, mid, pf) : 0;
-  EVC_STAMP(0);
+  if (t >= 64) evc_load(0, nl, t - 64, sLof, sDesc, bw, mid, pf);
   for (uint32_t L = 0; L < nl; L++) {
     const uint32_t lo = sLof[L], w = sLof[L + 1] - lo;
-    // ---- A: level L's tails and midstates -> LDS; loads for level L+1
-    if (t >= 64) {
-#pragma unroll
-      for (int r = 0; r < EVC_PF; r++)
-        if ((got >> r) & 1u) sBody[(t - 64) + EVC_LT * r] = pf[r];
-#pragma unroll
-      for (int r = 0; r < EVC_PM; r++)
-        if ((got >> (EVC_PF + r)) & 1u) sMid[(t - 64) + EVC_LT * r] = pf[EVC_PF + r];
-    }
+    // ---- A: level L's padded tails and midstates -> LDS; loads for level L+1
+    if (t >= 64) evc_stage(L, t - 64, sLof, sDesc, pf, sBody, sMid);
     __syncthreads();
-    if (t >= 64) got = evc_load(L + 1, nl, t - 64, sLof, sDesc, bw, mid, pf);
-    EVC_STAMP(1);
-    // ---- B: parents' hex into the tails
-    for (uint32_t i = t; i < w; i += EVC_NT) {
+    if (t >= 64) evc_load(L + 1, nl, t - 64, sLof, sDesc, bw, mid, pf);
+    // ---- B: parents' hex into the tails, one lane per (event, parent)
+    for (uint32_t x = t; x < 2 * w; x += EVC_NT) {
+      const uint32_t i = x >> 1, p = x & 1;
       const uint32_t *d = sDesc + EVC_DESC * (lo + i);
-      const uint32_t nd = d[3] & 0xFFFFFFu;
-      const uint64_t a0 = (uint64_t)d[1] | ((uint64_t)d[2] << 32);
-      const bool in_lds = i < EVC_SLOTS && nd <= EVC_SLOT_DW;
-      for (int p = 0; p < 2; p++) {
-        const uint32_t rel = d[6 + p];
-        if (rel == EVJ_NOPOS) continue;
-        const uint32_t ps = d[8 + p], q = d[10 + p];
-        uint32_t wd[8], hx[16];
-        if (ps != EVJ_NOPOS) {  // separate loads: a selected pointer would be a FLAT access
-          for (int k = 0; k < 8; k++) wd[k] = sDig[8 * ps + k];
-        } else {
-          for (int k = 0; k < 8; k++) wd[k] = dig[8 * (uint64_t)q + k];
-        }
-        if (in_lds) {
-          evj_hex32_words(hx, wd);
-          evj_put64(sBody + i * EVC_SLOT_DW, rel, hx);
-        } else {
-          uint8_t dd[32];
-          for (int k = 0; k < 8; k++)
-            for (int c = 0; c < 4; c++) dd[4 * k + c] = (uint8_t)(wd[k] >> (8 * c));  // words hold BE digest bytes
-          evj_hex32(bodies + 4 * a0 + rel, dd);  // hashed from HBM in D
-        }
+      const uint32_t rel = d[6 + p];
+      if (rel == EVJ_NOPOS) continue;
+      const uint32_t ps = d[8 + p], q = d[10 + p];
+      uint32_t wd[8];
+      if (ps != EVJ_NOPOS) {  // separate loads: a selected pointer would be a FLAT access
+        for (int k = 0; k < 8; k++) wd[k] = sDig[8 * ps + k];
+      } else {
+        for (int k = 0; k < 8; k++) wd[k] = dig[8 * (uint64_t)q + k];
+      }
+      if (evc_lds_event(i, d[4], d[5])) {
+        uint32_t hx[16];
+        evj_hex32_words(hx, wd);
+        evj_put64(sBody + i * EVC_SLOT_DW, rel, hx);
+      } else {
+        const uint64_t a0 = (uint64_t)d[1] | ((uint64_t)d[2] << 32);
+        uint8_t dd[32];
+        for (int k = 0; k < 8; k++)
+          for (int c = 0; c < 4; c++) dd[4 * k + c] = (uint8_t)(wd[k] >> (8 * c));  // words hold BE digest bytes
+        evj_hex32(bodies + 4 * a0 + rel, dd);  // hashed from HBM in D
       }
     }
     __syncthreads();
-    EVC_STAMP(2);
     // ---- C: message schedules, one lane per (event, block)
     {
       const uint32_t wv = w < EVC_WEV ? w : EVC_WEV;
       for (uint32_t x = t; x < wv * EVC_WBLK; x += EVC_NT) {
-        const uint32_t i = x / EVC_WBLK, jj = x % EVC_WBLK;
+        const uint32_t i = x / EVC_WBLK, j = x % EVC_WBLK;
         const uint32_t *d = sDesc + EVC_DESC * (lo + i);
-        const uint32_t nd = d[3] & 0xFFFFFFu, sh = d[3] >> 24, nb = d[4], len = d[5];
-        const uint32_t nblk = (uint32_t)sha256_nblocks(len), j = nb + jj;
-        if (nd > EVC_SLOT_DW || nblk - nb > EVC_WBLK || j >= nblk) continue;
+        const uint32_t nb = d[4], len = d[5];
+        if (!evc_lds_event(i, nb, len) || j >= (uint32_t)sha256_nblocks(len) - nb) continue;
         uint32_t w16[16];
-        sha256_block_words(w16, sBody + i * EVC_SLOT_DW, sh, len, nb, j);
-        sha256_schedule_wk(sWK + x * 64, w16);
+        sha256_block_words_padded(w16, sBody + i * EVC_SLOT_DW + 16 * j, d[3] >> 24);
+        sha256_schedule_wk(sWK + (j * 16 * EVC_WEV + i) * 4, w16, 4 * EVC_WEV);
       }
     }
     __syncthreads();
-    EVC_STAMP(3);
     // ---- D: the rounds (the serial part)
     for (uint32_t i = t; i < w; i += EVC_NT) {
       const uint32_t *d = sDesc + EVC_DESC * (lo + i);
-      const uint32_t nd = d[3] & 0xFFFFFFu, sh = d[3] >> 24, nb = d[4], len = d[5];
+      const uint32_t sh = d[3] >> 24, nb = d[4], len = d[5];
       const uint32_t nblk = (uint32_t)sha256_nblocks(len);
       uint32_t h[8];
       if (i < EVC_SLOTS) {
@@ -329,26 +346,21 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
       } else {
         for (int k = 0; k < 8; k++) h[k] = mid[(uint64_t)EV_MID_U32 * d[0] + k];
       }
-      const bool in_lds = i < EVC_SLOTS && nd <= EVC_SLOT_DW;
-      if (in_lds && i < EVC_WEV && nblk - nb <= EVC_WBLK) {
-        for (uint32_t jj = 0; jj < nblk - nb; jj++) sha256_rounds_wk(h, sWK + (i * EVC_WBLK + jj) * 64);
+      if (i < EVC_WEV && evc_lds_event(i, nb, len)) {
+        for (uint32_t j = 0; j < nblk - nb; j++) sha256_rounds_wk(h, sWK + (j * 16 * EVC_WEV + i) * 4, 4 * EVC_WEV);
+      } else if (evc_lds_event(i, nb, len)) {  // in LDS, schedule inline (padded: whole blocks)
+        evc_hash_padded(h, sBody + i * EVC_SLOT_DW, sh, nblk - nb);
       } else {
-        const uint64_t a0 = (uint64_t)d[1] | ((uint64_t)d[2] << 32);
-        evc_hash_inline(h, in_lds ? sBody + i * EVC_SLOT_DW : bw + a0, sh, len, nb, nblk);
+        evc_hash_inline(h, bw + ((uint64_t)d[1] | ((uint64_t)d[2] << 32)), sh, len, nb, nblk);
       }
       uint32_t wd[8];
       ev_digest_words(wd, h);
       for (int k = 0; k < 8; k++) sDig[8 * (lo + i) + k] = wd[k];
     }
-    EVC_STAMP(4);
     __syncthreads();
-    EVC_STAMP(5);
   }
   // ---- epilogue: the digests to HBM
   for (uint32_t x = t; x < (E1 - E0) * 8; x += EVC_NT) dig[8 * (uint64_t)sDesc[EVC_DESC * (x / 8)] + x % 8] = sDig[x];
-  if (prof && t == 0)
-    for (int k = 0; k < 8; k++) prof[k] = acc[k];
-#undef EVC_STAMP
 }
 
 __global__ void __launch_bounds__(256) k_iota(uint64_t n, uint32_t *__restrict__ out) {
@@ -748,17 +760,6 @@ hipError_t ev_hash(hipStream_t st, uint64_t count, const uint32_t *list, const b
   return hipGetLastError();
 }
 
-static uint64_t *evc_prof_buf() {
-  static uint64_t *p = nullptr;
-  if (!p) (void)hipMallocManaged(&p, 64);
-  return p;
-}
-extern "C" void bv_debug_evc_prof(uint64_t out[8]) {
-  (void)hipDeviceSynchronize();
-  uint64_t *p = evc_prof_buf();
-  for (int k = 0; k < 8; k++) out[k] = p ? p[k] : 0;
-}
-
 hipError_t ev_mid(hipStream_t st, uint64_t count, const uint32_t *list, const uint8_t *bodies, const uint64_t *offs,
                   const uint32_t *ppos, uint32_t *mid) {
   if (count == 0) return hipSuccess;
@@ -771,7 +772,7 @@ hipError_t ev_hash_chain(hipStream_t st, uint32_t l0, uint32_t l1, const uint32_
                          const uint64_t *offs, const uint32_t *mid, uint32_t *dig) {
   if (l1 <= l0) return hipSuccess;
   hipLaunchKernelGGL(k_ev_hash_chain, dim3(1), dim3(EVC_NT), 0, st, l0, l1, level_off, order, posin, b, ppos, bodies,
-                     offs, mid, dig, getenv("BV_EVC_PROF") ? evc_prof_buf() : nullptr);
+                     offs, mid, dig);
   return hipGetLastError();
 }
 

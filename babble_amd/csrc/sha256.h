@@ -139,6 +139,16 @@ DEV void sha256_block_words(uint32_t w[16], const uint32_t *src0, uint32_t sh, u
   }
 }
 
+// The 16 message words of a block whose padding (if any) is already in
+// the buffer: 17 aligned dwords at `src`, realigned by `sh` bytes.
+DEV void sha256_block_words_padded(uint32_t w[16], const uint32_t *src, uint32_t sh) {
+  uint32_t d[17];
+#pragma unroll
+  for (int i = 0; i < 17; i++) d[i] = src[i];
+#pragma unroll
+  for (int i = 0; i < 16; i++) w[i] = bswap32(alignbyte(d[i + 1], d[i], sh));
+}
+
 // Compress blocks [blk0, blk1) of a len-byte message into h (see
 // sha256_block_words for src0 / sh).  Lets a caller hash a message in
 // pieces: a midstate over leading blocks, then the rest from another buffer
@@ -152,17 +162,20 @@ DEV void sha256_blocks(uint32_t h[8], const uint32_t *src0, uint32_t sh, uint64_
   }
 }
 
-// The message schedule with the round constants folded in: wk[i] = W_i + K_i.
+// The message schedule with the round constants folded in: wk[i] = W_i + K_i,
+// element i stored at wk[(i / 4) * stride + i % 4] (stride 4: contiguous; a
+// wider stride interleaves several lanes' schedules in 16-byte chunks, so
+// lanes reading their own schedule in lockstep hit distinct LDS banks).
 // Independent of the chaining state, so another lane can compute it while
 // the previous block's rounds run (k_ev_hash_chain).
 // `wk` may live in LDS: the 48 expansion steps run as a 3-trip loop of 16
 // (the ring indices stay static), which keeps the chain kernel's code small.
-DEV void sha256_schedule_wk(uint32_t *wk, const uint32_t w[16]) {
+DEV void sha256_schedule_wk(uint32_t *wk, const uint32_t w[16], uint32_t stride = 4) {
   uint32_t x[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) {
     x[i] = w[i];
-    wk[i] = w[i] + SHA_K[i];
+    wk[(i >> 2) * stride + (i & 3)] = w[i] + SHA_K[i];
   }
 #pragma unroll 1
   for (int r = 16; r < 64; r += 16) {
@@ -172,7 +185,7 @@ DEV void sha256_schedule_wk(uint32_t *wk, const uint32_t w[16]) {
       const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
       const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
       x[u] = x[u] + s0 + x[(u + 9) & 15] + s1;
-      wk[r + u] = x[u] + SHA_K[r + u];
+      wk[((r + u) >> 2) * stride + (u & 3)] = x[u] + SHA_K[r + u];
     }
   }
 }
@@ -181,13 +194,15 @@ DEV void sha256_schedule_wk(uint32_t *wk, const uint32_t w[16]) {
 // An 8-trip loop of 8 rounds (the state rotation maps onto itself every 8
 // rounds, so no register moves): small code for a latency-bound single
 // wave, whose instruction cache is shared with the rest of its kernel.
-DEV void sha256_rounds_wk(uint32_t h[8], const uint32_t *wk) {
+DEV void sha256_rounds_wk(uint32_t h[8], const uint32_t *wk, uint32_t stride = 4) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
 #pragma unroll 1
   for (int r = 0; r < 64; r += 8) {
+    const uint32_t *q = wk + (r >> 2) * stride;
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      const uint32_t t1 = hh + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g)) + wk[r + u];
+      const uint32_t t1 = hh + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g)) +
+                          q[(u >> 2) * stride + (u & 3)];
       const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
       hh = g;
       g = f;

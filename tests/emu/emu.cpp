@@ -286,10 +286,10 @@ uint64_t emu_ev_bodies(const bv_event_batch *b, uint8_t *bodies, uint64_t cap, u
     for (int k = 0; k < 8; k++) h[k] = mid[(size_t)EV_MID_U32 * e + k];
     // as the device: per block the W+K schedule, then the rounds
     for (uint64_t j = nb; j < sha256_nblocks(len); j++) {
-      uint32_t w[16], wk[64];
+      uint32_t w[16], wk[64 * 3];  // interleaved layout as the device's (stride 12 here)
       sha256_block_words(w, slot.data(), (uint32_t)(o & 3), len, nb, j);
-      sha256_schedule_wk(wk, w);
-      sha256_rounds_wk(h, wk);
+      sha256_schedule_wk(wk + 4, w, 12);
+      sha256_rounds_wk(h, wk + 4, 12);
     }
     ev_digest_words(&dig[8 * e], h);
   }
