@@ -718,8 +718,20 @@ def asm_line(x) -> str:
 
 
 def asm_body(g: Prog) -> str:
+    """Consecutive wait states are merged into one s_nop N (N + 1 states):
+    one issue slot instead of N + 1."""
     lines = []
-    for k, x in enumerate(g.ins):
+    run = 0
+    for k, x in enumerate(g.ins + [("end",)]):
+        if x[0] == "nop":
+            run += 1
+            continue
+        while run:
+            m = min(run, 8)  # s_nop takes 0..7 (1..8 wait states)
+            lines.append(f'      "s_nop {m - 1}\\n"')
+            run -= m
+        if x[0] == "end":
+            break
         if x[0] == "slow":
             lbl = f"BV_{g.name.upper()}_S{k}_%="
             lines.append(f'      "s_cmp_lg_u64 {x[1]}, 0\\n"')
