@@ -49,7 +49,7 @@ sys.path.insert(0, ROOT)
 #          + 2 products) and the projective check X == r Z^2 (1S + 1M)
 #                                                           ~   8
 #   = 349 modmuls = 27,920 IMUL32 per item.
-# `achieved` = items x 28,800 / (k_verify_g + k_verify_q time); `peak` = the
+# `achieved` = items x 27,920 / (k_verify_g + k_verify_q time); `peak` = the
 # v_mad_u64_u32 rate measured on MI355X (tools/ubench_int.hip,
 # profiles/r01_ubench_int.txt).  SURVEY §8d's canonical Strauss schedule
 # (4,050 modmuls per verify) is reported only as `speedup_vs_canonical`.

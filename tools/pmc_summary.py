@@ -101,7 +101,7 @@ def kverify(summary: dict, items: int, source: str) -> dict:
     cnt = lambda c: sum(summary[k]["counters"].get(c, 0.0) for k in ks)  # noqa: E731
     return {"source": source, "kernels": ks, "items_per_launch": items,
             "hbm_bytes_per_launch": tot("hbm_bytes"), "hbm_read_bytes_uncorrected": cnt("FETCH_SIZE") * 1024,
-            "algorithmic_table_bytes": items * 33 * 64,
+            "algorithmic_table_bytes": items * (10 + 22) * 64,  # 10 G (26-bit) + 22 K12 table entries per item
             "valu_wave_insts": cnt("SQ_INSTS_VALU"), "valu_int64_wave_insts": cnt("SQ_INSTS_VALU_INT64"),
             "valu_issue_util": {k: summary[k].get("valu_issue_util") for k in ks}}
 

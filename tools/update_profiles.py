@@ -26,11 +26,11 @@ out = {
     "items_per_launch": items,
     "hbm_bytes_per_launch": g["hbm_bytes"] + q["hbm_bytes"],
     "hbm_read_bytes_uncorrected": (g["counters"]["FETCH_SIZE"] + q["counters"]["FETCH_SIZE"]) * 1024,
-    "algorithmic_table_bytes": items * (11 + 22) * 64,
+    "algorithmic_table_bytes": items * (10 + 22) * 64,  # 10 G windows (26-bit) + 22 K12 windows
     "valu_wave_insts_per_launch": g["valu_wave_insts"] + q["valu_wave_insts"],
     "note": "hbm_bytes applies the guide's x2 FETCH_SIZE correction (calibrated for 16-B/lane streaming reads); "
             "the verify kernels read 64-B table entries by random gather, an uncalibrated width: uncorrected "
-            "FETCH_SIZE equals the algorithmic table bytes (33 entries x 64 B per item).",
+            "FETCH_SIZE equals the algorithmic table bytes (32 entries x 64 B per item).",
 }
 json.dump(out, open(os.path.join(P, "kverify_traffic.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
