@@ -36,14 +36,14 @@ constexpr uint64_t kKTableBytes = BV_KTABLE_U32 * 4;
 constexpr uint64_t kK12TableBytes = BV_K12TABLE_U32 * 4;
 constexpr uint64_t kK12SubBytes = BV_K12SUB_U32 * 4;
 constexpr uint64_t kK12PrefixBytes = (uint64_t)BV_K12NWIN * BV_K12ENT * 32;  // one fe per entry
-constexpr uint64_t kKcTableBytes = BV_KCTABLE_U32 * 4;                      // 470 MB per cached key
+constexpr uint64_t kKcTableBytes = BV_KCTABLE_U32 * 4;                      // 805 MB per cached key
 constexpr uint64_t kKcSubBytes = BV_KCSUB_U32 * 4;
 constexpr uint32_t kBasesPerKey = 22;       // max(K8 16, K12 22, KC 14) bases per key
 constexpr uint64_t kK12MinItemsPerKey = 2048;  // K12 pays for its 11x larger build above this
 constexpr uint32_t kMaxTableKeys = 8192;       // K8: 4 GiB of key tables
 constexpr uint32_t kMaxK12Keys = 1024;         // K12: 2.8 GiB
 constexpr uint32_t kKcMaxBatchKeys = 4096;     // key cache: batches with more keys use per-batch tables
-constexpr uint32_t kKcBuildGroup = 16;         // keys per KC build launch (pscr: 117 MB per key)
+constexpr uint32_t kKcBuildGroup = 8;          // keys per KC build launch (pscr: 403 MB per key)
 constexpr uint32_t kPrepM = 16;                // items per s^-1 batch
 constexpr uint32_t kRgWords = 25;              // R_G words per item
 constexpr size_t kChunk = 16ull << 20;         // host-entry staging / PCIe chunk
@@ -210,7 +210,7 @@ static int create_impl(bv_ctx *ctx) {
   const unsigned hw = std::thread::hardware_concurrency();
   ctx->pool = new CopyPool((int)std::min<unsigned>(hw ? hw - 1 : 0, 7));
   if (ctx->flags & BV_F_KEY_CACHE) {
-    double gb = 64.0;
+    double gb = 96.0;  // 119 KC tables: C5's 100 validators fit
     if (const char *s = getenv("BV_KEY_CACHE_GB")) gb = atof(s);
     ctx->kc_budget = (uint64_t)(std::max(gb, 0.0) * 1e9);
   }

@@ -53,18 +53,21 @@
 #define BV_K12SUB_U32 ((uint64_t)BV_K12NSUB * (1ull << BV_K12L) * BV_ENTRY_U32)
 // KC: the key-cache geometry (BV_F_KEY_CACHE).  Validator sets are stable
 // (peers/peer_set.go), so a key's table is built once and kept in HBM across
-// calls; the build cost is amortised and the windows can be wide: 20-bit
-// signed-digit windows x 7 (140 bits >= 129) = 14 adds per item for u2 Q
-// (K12: 22), 470 MB per key (64 keys: 30 GB, 100 validators: 47 GB of the
-// GPU's 288 GB).  Entries are chord sums of two 10-bit sub-table points
-// S_k[x] = x 2^(10 k) Q, k < 14, same scheme as the generator table.
-#define BV_KCW 20
-#define BV_KCNWIN 7
-#define BV_KCL 10
-#define BV_KCNSUB 14
+// calls; the build cost is amortised and the windows can be wide: 22-bit
+// signed-digit windows x 6 (132 bits >= 129) = 12 adds per item for u2 Q
+// (K12: 22).  Only the k1 half is stored; the k2 half's entries are
+// phi(T) = (beta x, y), formed in k_verify_q with one multiply per lookup
+// (12 adds + 6 multiplies instead of the 14 adds of 20-bit windows with a
+// stored phi half): 805 MB per key (64 keys: 52 GB, 100 validators: 81 GB
+// of the GPU's 288 GB).  Entries are chord sums of two 11-bit sub-table
+// points S_k[x] = x 2^(11 k) Q, k < 12, same scheme as the generator table.
+#define BV_KCW 22
+#define BV_KCNWIN 6
+#define BV_KCL 11
+#define BV_KCNSUB 12
 #define BV_KCENT (1u << (BV_KCW - 1))
 #define BV_KCHALF_U32 (((uint64_t)BV_KCNWIN * BV_KCENT + 1) * BV_ENTRY_U32)
-#define BV_KCTABLE_U32 (2 * BV_KCHALF_U32)
+#define BV_KCTABLE_U32 BV_KCHALF_U32  // no stored phi half
 #define BV_KCSUB_U32 ((uint64_t)BV_KCNSUB * (1ull << BV_KCL) * BV_ENTRY_U32)
 #define BV_KCPAIR_ENT 4096  // entries per k_table_pair_kc block (16 per thread)
 // per-item GLV halves of u2 (k_verify_g -> k_verify_q): k1[4] | k2[4] | signs | pad

@@ -629,21 +629,21 @@ __global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, const uint32
   write_status(i, n_items, st, status, bits);
 }
 
-// Key-cache (KC) table windows from the 10-bit sub-tables: block (c, key)
+// Key-cache (KC) table windows from the 11-bit sub-tables: block (c, key)
 // holds slots s = BV_KCPAIR_ENT c' + 256 e + t (e < 16) of window
 // j = c / (ENT / BV_KCPAIR_ENT), c' = c mod that; digit k12_digit(s) (signed
 // windows: slot 0 builds digit ENT, stored in window j+1's slot 0).  A wave
 // reads 64 consecutive S_lo points and one S_hi point from L2 (the key's
-// sub-tables are 0.9 MB).  One field inversion per block (Montgomery's trick
+// sub-tables are 1.5 MB).  One field inversion per block (Montgomery's trick
 // over 4096 chord denominators, prefix products in `pscr`), then each entry
-// and its phi image are stored.  Blocks beyond the top window's live digits
-// (<= 2^(128 - W j) + 1) return at once.  `tabs[b]` is key b's table.
+// is stored (no phi half: k_verify_q forms phi(T) = (beta x, y)).  Blocks
+// beyond the top window's live digits (<= 2^(128 - W j) + 1) return at once.
+// `tabs[b]` is key b's table.
 template <int W, int L, int NWIN>
 __global__ void __launch_bounds__(256) k_table_pair_kc(const uint32_t *__restrict__ sub,
                                                        const uint8_t *__restrict__ bstatus,
                                                        const uint64_t *__restrict__ tabs, uint4 *__restrict__ pscr) {
   constexpr uint32_t ENT = 1u << (W - 1), NS = 1u << L, E = BV_KCPAIR_ENT / 256u, CH = ENT / BV_KCPAIR_ENT;
-  constexpr uint64_t half_u32 = ((uint64_t)NWIN * ENT + 1) * BV_ENTRY_U32;
   const uint32_t b = blockIdx.y, j = blockIdx.x / CH, c = blockIdx.x % CH, t = threadIdx.x;
   if (bstatus && bstatus[b] != KS_OK) return;
   const int live_bits = 128 - W * (int)j;
@@ -698,8 +698,7 @@ __global__ void __launch_bounds__(256) k_table_pair_kc(const uint32_t *__restric
     pre.v[4] = p1.x; pre.v[5] = p1.y; pre.v[6] = p1.z; pre.v[7] = p1.w;
     fe_mul(Hinv, q, pre);
     fe_mul(q, q, H);
-    uint32_t *entry = base + (uint64_t)d * BV_ENTRY_U32;
-    pair_store(entry, entry + half_u32, kind, x1, y1, x2, y2, Hinv);
+    pair_store(base + (uint64_t)d * BV_ENTRY_U32, nullptr, kind, x1, y1, x2, y2, Hinv);  // no phi half (geometry.h)
   }
 }
 
@@ -856,7 +855,7 @@ hipError_t verify_g(hipStream_t st, uint64_t n, const uint32_t *item_key, const 
   return hipGetLastError();
 }
 
-// kw = 8 / 12: contiguous per-batch tables in key_table; kw = 20: the key
+// kw = 8 / 12: contiguous per-batch tables in key_table; kw = 22: the key
 // cache (KC), table base address per batch key in key_tabs.
 hipError_t verify_q(hipStream_t st, int kw, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
                     const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst, const uint32_t *u12,
@@ -876,9 +875,10 @@ hipError_t verify_q(hipStream_t st, int kw, uint64_t n, const uint32_t *item_key
 }
 
 // Key-cache tables for n keys (decoded affine points kxy, statuses kst):
-// bases 2^(10 k) Q (k < 14), the 10-bit sub-tables into `sub`
-// (n * BV_KCSUB_U32 words), then every window's chord sums + phi half into
-// tabs[b] (BV_KCTABLE_U32 words each).  `pscr`: n * kc_pscr_bytes() bytes.
+// bases 2^(11 k) Q (k < 12), the 11-bit sub-tables into `sub`
+// (n * BV_KCSUB_U32 words), then every window's chord sums into
+// tabs[b] (BV_KCTABLE_U32 words each; k_verify_q forms the phi half).
+// `pscr`: n * kc_pscr_bytes() bytes.
 size_t kc_pscr_bytes() {
   return (size_t)BV_KCNWIN * (BV_KCENT / BV_KCPAIR_ENT) * BV_KCPAIR_ENT * 32;
 }

@@ -521,8 +521,10 @@ DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const u
 // SIGNED (K12): digits in (-2^(W-1), 2^(W-1)] by carry recoding, T[j][|d|]
 // with y negated for d < 0; a window holds ENT = 2^(W-1) slots.  k < 2^128
 // and W NWIN >= 129 bits, so no carry is left after the top window.
+// `phi`: the table holds T (the k1 half) and this half needs phi(T) =
+// (beta x, y): one multiply per lookup instead of a stored phi half (KC).
 template <int W, int NWIN, bool SIGNED>
-DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bool neg) {
+DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bool neg, bool phi = false) {
   constexpr uint32_t ENT = SIGNED ? (1u << (W - 1)) : (1u << W);
   static_assert(!SIGNED || W * NWIN >= 129, "signed windows must absorb the last carry");
   if (neg) fe_neg(R.Y, R.Y);
@@ -546,6 +548,11 @@ DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bo
       fe x, y;
       fe_load4(x, e);
       fe_load4(y, e + 8);
+      if (phi) {
+        fe beta;
+        fe_load(beta, FE_BETA);
+        fe_mul(x, x, beta);
+      }
       if (dneg) fe_neg(y, y);
       gej_add_ge(R, inf, x, y);
     }
@@ -562,10 +569,11 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
                           const uint32_t *s_be, const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12,
                           const uint32_t *key_table, const uint64_t *key_tabs, const uint32_t *rg) {
   constexpr bool SIGNED = W != BV_KW;
+  constexpr bool KC = W == BV_KCW;  // one stored half, phi(T) formed per lookup
   constexpr uint64_t half =
       SIGNED ? ((uint64_t)NWIN * (1ull << (W - 1)) + 1) * BV_ENTRY_U32 : (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
   static_assert(W != BV_K12W || half == BV_K12HALF_U32, "K12 geometry");
-  static_assert(W != BV_KCW || half == BV_KCHALF_U32, "KC geometry");
+  static_assert(!KC || half == BV_KCHALF_U32, "KC geometry");
   fe r;
   const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
   if (st != 0xFF) return st;
@@ -575,7 +583,7 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
   bool inf;
   rg_load(rg, n, i, R, inf);
   const uint32_t *tab = key_tabs ? (const uint32_t *)key_tabs[item_key[i]]
-                                 : key_table + (uint64_t)item_key[i] * 2 * half;
+                                 : key_table + (uint64_t)item_key[i] * (KC ? 1 : 2) * half;
   // One loop body for both GLV halves (one inlined copy of the point
   // addition: smaller code, fewer live registers than two calls).
 #pragma unroll 1
@@ -583,7 +591,7 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
     uint32_t kk[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) kk[c] = h ? k2[c] : k1[c];
-    key_table_add<W, NWIN, SIGNED>(R, inf, tab + (h ? half : 0), kk, (signs >> h) & 1u);
+    key_table_add<W, NWIN, SIGNED>(R, inf, tab + (h && !KC ? half : 0), kk, (signs >> h) & 1u, KC && h);
   }
   fe_load_be_words(r, r_be + 8 * i);  // reloaded: not kept live through the loop
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;

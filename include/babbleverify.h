@@ -64,10 +64,10 @@ extern "C" {
 #define BV_F_DEFAULT 0u
 #define BV_F_KEY_CACHE 1u /* keep per-key tables in HBM across calls, keyed by
                              the raw pubkey bytes (validator sets are stable,
-                             peers/peer_set.go): 20-bit signed-window GLV
-                             tables, 470 MB per valid key, built on first use,
+                             peers/peer_set.go): 22-bit signed-window GLV
+                             tables, 805 MB per valid key, built on first use,
                              LRU-evicted past the cache budget (env
-                             BV_KEY_CACHE_GB, default 64).  Malformed keys are
+                             BV_KEY_CACHE_GB, default 96).  Malformed keys are
                              never given a table.  Off by default: tables are
                              then rebuilt for every batch.                     */
 #define BV_F_K8 2u        /* per-batch tables: never use the 12-bit tables

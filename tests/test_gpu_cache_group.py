@@ -49,14 +49,14 @@ def test_key_cache_cold_then_warm(cached):
     b = synth.adversarial(30_000, seed=41, n_creators=6, scale_per_million=MIX)
     st = oracle_check(cached.verify(b), b)
     t = cached.timing()
-    assert t["key_path"] == 20
+    assert t["key_path"] == 22
     n_valid = sum(1 for k in range(b.n_keys) if gs.Unmarshal(b.key(k)) is not None)
     assert 0 < n_valid < b.n_keys  # the mix carries malformed keys
     assert t["kc_builds"] == n_valid and t["kc_hits"] == 0
     assert set(np.unique(st)) == {0, 1, 2, 3}
     oracle_check(cached.verify(b), b)
     t = cached.timing()
-    assert t["kc_builds"] == 0 and t["kc_hits"] == b.n_keys and t["key_path"] == 20
+    assert t["kc_builds"] == 0 and t["kc_hits"] == b.n_keys and t["key_path"] == 22
 
 
 def test_key_cache_small_batches(cached):
@@ -65,7 +65,7 @@ def test_key_cache_small_batches(cached):
     for n in (1, 100, 1000):
         b = synth.events(n, n_creators=4, seed=100 + n)
         oracle_check(cached.verify(b), b)
-        assert cached.timing()["key_path"] == 20
+        assert cached.timing()["key_path"] == 22
 
 
 def test_key_cache_device_entry(cached):
@@ -73,15 +73,15 @@ def test_key_cache_device_entry(cached):
     d = cached.to_device(b)
     cached.verify_device(d)
     oracle_check(d.result(), b)
-    assert cached.timing()["key_path"] == 20
+    assert cached.timing()["key_path"] == 22
 
 
 def test_key_cache_eviction(monkeypatch):
-    """A 1.5 GB budget holds 3 tables: a batch with 2 new keys after a batch
+    """A 2.5 GB budget holds 3 tables (805 MB each): a batch with 2 new keys after a batch
     with 2 others evicts the least recently used; results stay exact."""
     from babble_amd.verifier import Verifier
 
-    monkeypatch.setenv("BV_KEY_CACHE_GB", "1.5")
+    monkeypatch.setenv("BV_KEY_CACHE_GB", "2.5")
     v = Verifier(device=0, flags=native.F_KEY_CACHE)
     try:
         a = synth.events(3000, n_creators=2, seed=51)
@@ -174,7 +174,7 @@ def test_c5_full_size_check_block(cached, verifier_default, key_cache):
     b.s_be[bad, 7] ^= 0x40
     v = cached if key_cache else verifier_default
     res = v.verify(b)
-    assert v.timing()["key_path"] == (20 if key_cache else 12)
+    assert v.timing()["key_path"] == (22 if key_cache else 12)
     st = oracle_check(res, b)
     valid = (st == 1).reshape(wb.n_blocks, wb.n_validators).sum(axis=1)
     got = (res.status == 1).reshape(wb.n_blocks, wb.n_validators).sum(axis=1)
