@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--events", type=int, default=1_000_000, help="events per GPU per step")
     ap.add_argument("--creators", type=int, default=64)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration (each leg)")
+    ap.add_argument("--cpu-seconds", type=float, default=9.0, help="target CPU-baseline sample duration (each leg)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="headline only (profiler passes)")
     return ap.parse_args()
@@ -117,13 +117,17 @@ def cpu_baseline(batch, target_s: float) -> dict:
         return {"value": n / dt, "n": n, "seconds": dt, "accepted": acc}
 
     legs = {
-        "port": timed(lambda s, t: int(np.count_nonzero(coracle.verify_batch(s, n_threads=t)[1] == 1)), "port"),
+        "port": timed(lambda s, t: int(np.count_nonzero(coracle.port_verify_batch(s, n_threads=t) == 1)), "port"),
+        "oracle": timed(lambda s, t: int(np.count_nonzero(coracle.verify_batch(s, n_threads=t)[1] == 1)), "oracle"),
         "openssl": timed(lambda s, t: int(np.count_nonzero(coracle.ossl_verify_batch(s, n_threads=t) == 1)),
                          "openssl"),
     }
     best = max(legs, key=lambda k: legs[k]["value"])
-    what = {"port": "oracle/oracle.c (C restatement of Event.Verify: btcec-style byte tables for u1 G, "
-                    "double-and-add u2 Q)",
+    what = {"port": "oracle/oracle.c port_verify_batch (C port of the reference stack's algorithms: Go 1.13 "
+                    "ecdsa.Verify over btcec, i.e. byte-table ScalarBaseMult, GLV + NAF ScalarMult, mixed "
+                    "additions, 3 affine conversions)",
+            "oracle": "oracle/oracle.c oracle_verify_batch (the checker: byte tables for u1 G, 4-bit fixed "
+                      "window for u2 Q)",
             "openssl": "oracle/openssl_ref.c (OpenSSL libcrypto SHA256 + o2i_ECPublicKey + ECDSA_do_verify, "
                        "the SURVEY §8d proxy)"}
     L = legs[best]

@@ -65,6 +65,8 @@ def lib():
         L.oracle_unmarshal.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         L.oracle_scalar_base_mult.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_init.argtypes = []
+        L.port_verify_batch.argtypes = [ctypes.POINTER(_Batch), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.port_verify_batch.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -172,3 +174,15 @@ def verify_batch(arrs: dict, n_threads: int = 0):
     bits = np.zeros(max((n_items + 63) // 64, 1), np.uint64)
     L.oracle_verify_batch(ctypes.byref(b), h.ctypes.data, st.ctypes.data, bits.ctypes.data, n_threads)
     return h[:n_msgs], st[:n_items], bits[: (n_items + 63) // 64]
+
+
+def port_verify_batch(arrs: dict, n_threads: int = 0) -> np.ndarray:
+    """The btcec-algorithm CPU port (oracle.c: GLV + NAF ScalarMult, byte-table
+    ScalarBaseMult, mixed additions) over a packed batch: statuses.  Timed as
+    bench.py's cpu_baseline "port" leg; checked against the oracle in tests."""
+    keep: list = []
+    b = _cbatch(arrs, keep)
+    h = np.zeros((max(b.n_msgs, 1), 32), np.uint8)
+    st = np.zeros(max(b.n_items, 1), np.uint8)
+    lib().port_verify_batch(ctypes.byref(b), h.ctypes.data, st.ctypes.data, n_threads or default_threads())
+    return st[: b.n_items]

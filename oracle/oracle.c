@@ -442,9 +442,10 @@ static int ecdsa_math(const uint8_t *pub65, const uint8_t digest[32], const uint
   return memcmp(x, r, sizeof x) == 0;
 }
 
-/* One item, SURVEY §8a-9 ordering. */
-int oracle_item_status(const uint8_t *pub, uint64_t publen, const uint8_t digest[32], uint8_t pre,
-                       const uint8_t r_be[32], const uint8_t s_be[32]) {
+/* Steps (1)-(6) of SURVEY §8a-9: the final status, or -1 when the item
+ * reaches the ECDSA math. */
+static int oracle_item_status_pre(const uint8_t *pub, uint64_t publen, uint8_t pre, const uint8_t r_be[32],
+                                  const uint8_t s_be[32]) {
   if (pre & BV_PRE_PARTS_BAD) return BV_REJECT_ERR;
   if (publen == 0) return BV_REF_PANIC;
   int rc = pre & 3, sc = (pre >> 2) & 3;
@@ -461,6 +462,14 @@ int oracle_item_status(const uint8_t *pub, uint64_t publen, const uint8_t digest
   if (sc == BV_SC_NONPOS) return BV_REJECT;
   if (rc == BV_SC_GE_N || sc == BV_SC_GE_N) return BV_REJECT;
   if (!oracle_unmarshal(pub, publen, NULL)) return BV_REF_PANIC;
+  return -1;
+}
+
+/* One item, SURVEY §8a-9 ordering. */
+int oracle_item_status(const uint8_t *pub, uint64_t publen, const uint8_t digest[32], uint8_t pre,
+                       const uint8_t r_be[32], const uint8_t s_be[32]) {
+  const int st = oracle_item_status_pre(pub, publen, pre, r_be, s_be);
+  if (st >= 0) return st;
   return ecdsa_math(pub, digest, r_be, s_be) ? BV_ACCEPT : BV_REJECT;
 }
 
@@ -481,6 +490,9 @@ int oracle_scalar_base_mult(const uint8_t k_be[32], uint8_t xy_out[64]) {
 /* ------------------------------------------------------------------------ */
 /* Batch driver (pthreads)                                                   */
 /* ------------------------------------------------------------------------ */
+int port_item_status(const uint8_t *pub, uint64_t publen, const uint8_t digest[32], uint8_t pre,
+                     const uint8_t r_be[32], const uint8_t s_be[32]);
+
 typedef struct {
   const bv_batch *b;
   uint8_t *hash;
@@ -501,8 +513,9 @@ static void *worker(void *arg) {
       const uint8_t *pub = b->key_bytes + b->key_off[k];
       uint64_t publen = b->key_off[k + 1] - b->key_off[k];
       uint8_t pre = b->pre ? b->pre[i] : 0;
-      j->status[i] = (uint8_t)oracle_item_status(pub, publen, j->hash + 32 * (uint64_t)b->item_msg[i], pre,
-                                                  b->r_be + 32 * i, b->s_be + 32 * i);
+      const uint8_t *dg = j->hash + 32 * (uint64_t)b->item_msg[i];
+      j->status[i] = (uint8_t)(j->phase == 2 ? port_item_status(pub, publen, dg, pre, b->r_be + 32 * i, b->s_be + 32 * i)
+                                              : oracle_item_status(pub, publen, dg, pre, b->r_be + 32 * i, b->s_be + 32 * i));
     }
   }
   return NULL;
@@ -538,4 +551,192 @@ int oracle_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, u
   return 0;
 }
 
+/* The same batch through the btcec-algorithm port (cpu_baseline timing). */
+int port_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, int n_threads) {
+  pthread_once(&g_once, init_tables);
+  run_phase(b, msg_hash, status, b->n_msgs, 0, n_threads);
+  run_phase(b, msg_hash, status, b->n_items, 2, n_threads);
+  return 0;
+}
+
 void oracle_init(void) { pthread_once(&g_once, init_tables); }
+
+/* ------------------------------------------------------------------------ */
+/* btcec-algorithm PORT — the cpu_baseline "port" leg (timing only; the     */
+/* checker above stays the simple restatement).  Same decisions as          */
+/* oracle_item_status; the two scalar multiplications follow the reference  */
+/* stack's own algorithms (btcec v0.0.0-20190523000118-16327141da8c, called  */
+/* by Go 1.13 ecdsa.Verify, src/crypto/keys/signature.go:20-22):            */
+/*   ScalarBaseMult: the 32 x 256 byte-point tables, mixed additions;       */
+/*   ScalarMult:     GLV split k = k1 + k2 lambda (|k1|, |k2| < 2^128), NAF */
+/*                   of both halves, one joint double-and-add over Q and    */
+/*                   phi(Q) = (beta x, y) with mixed additions;             */
+/*   Add:            affine in, Jacobian sum, affine out (3 inversions in   */
+/*                   all, as fieldJacobianToBigAffine does).                */
+/* ------------------------------------------------------------------------ */
+static const uint64_t GLV_G1[4] = {0xE893209A45DBB031ULL, 0x3DAA8A1471E8CA7FULL, 0xE86C90E49284EB15ULL, 0x3086D221A7D46BCDULL};
+static const uint64_t GLV_G2[4] = {0x1571B4AE8AC47F71ULL, 0x221208AC9DF506C6ULL, 0x6F547FA90ABFE4C4ULL, 0xE4437ED6010E8828ULL};
+static const uint64_t GLV_MB1[4] = {0x6F547FA90ABFE4C3ULL, 0xE4437ED6010E8828ULL, 0, 0};
+static const uint64_t GLV_MB2[4] = {0xD765CDA83DB1562CULL, 0x8A280AC50774346DULL, 0xFFFFFFFFFFFFFFFEULL, 0xFFFFFFFFFFFFFFFFULL};
+static const uint64_t GLV_LAM[4] = {0xDF02967C1B23BD72ULL, 0x122E22EA20816678ULL, 0xA5261C028812645AULL, 0x5363AD4CC05C30E0ULL};
+static const fe FE_BETA64 = {{0xC1396C28719501EEULL, 0x9CF0497512F58995ULL, 0x6E64479EAC3434E9ULL, 0x7AE96A2B657C0710ULL}};
+
+/* round(k g / 2^384) */
+static void glv_mulshift(uint64_t c[4], const uint64_t k[4], const uint64_t g[4]) {
+  uint64_t w[8];
+  mul256(w, k, g);
+  const uint64_t rnd = (w[5] >> 63) & 1; /* bit 383 */
+  u128 s = (u128)w[6] + rnd;
+  c[0] = (uint64_t)s; s >>= 64;
+  s += w[7];
+  c[1] = (uint64_t)s;
+  c[2] = c[3] = 0;
+}
+
+/* k = k1 + k2 lambda (mod N): magnitudes < 2^128 and signs (1 = negative) */
+static void glv_split(const uint64_t k[4], uint64_t m1[2], int *neg1, uint64_t m2[2], int *neg2) {
+  uint64_t c1[4], c2[4], t1[4], t2[4], k1[4], k2[4], half[4];
+  glv_mulshift(c1, k, GLV_G1);
+  glv_mulshift(c2, k, GLV_G2);
+  sc_mul(t1, c1, GLV_MB1);
+  sc_mul(t2, c2, GLV_MB2);
+  if (u256_add(k2, t1, t2) || u256_ge(k2, SC_N)) u256_sub(k2, k2, SC_N);
+  sc_mul(t1, k2, GLV_LAM);
+  if (u256_sub(k1, k, t1)) u256_add(k1, k1, SC_N);
+  /* N/2 rounded up: values above it are negative */
+  memcpy(half, SC_N, sizeof half);
+  for (int i = 0; i < 3; i++) half[i] = (half[i] >> 1) | (half[i + 1] << 63);
+  half[3] >>= 1;
+  uint64_t *ks[2] = {k1, k2}, *ms[2] = {m1, m2};
+  int *ns[2] = {neg1, neg2};
+  for (int h = 0; h < 2; h++) {
+    uint64_t v[4];
+    memcpy(v, ks[h], sizeof v);
+    *ns[h] = u256_ge(v, half) && !(v[0] == half[0] && v[1] == half[1] && v[2] == half[2] && v[3] == half[3]);
+    if (*ns[h]) u256_sub(v, SC_N, v);
+    ms[h][0] = v[0];
+    ms[h][1] = v[1];
+  }
+}
+
+/* width-2 NAF of a < 2^128 magnitude: digits in {-1, 0, 1}, LSB first; returns the length */
+static int naf128(int8_t d[130], const uint64_t m[2]) {
+  u128 k = ((u128)m[1] << 64) | m[0];
+  uint64_t top = 0; /* k may become 2^128 after a -1 digit */
+  int n = 0;
+  while (k || top) {
+    int8_t z = 0;
+    if (k & 1) {
+      z = (k & 3) == 3 ? -1 : 1;
+      if (z == 1) k -= 1;
+      else { u128 k2 = k + 1; if (k2 == 0) top = 1; k = k2; }
+    }
+    d[n++] = z;
+    k = (k >> 1) | ((u128)top << 127);
+    top = 0;
+  }
+  return n;
+}
+
+/* r += b (affine, not the identity): btcec's addZ2EqualsOne, 8M + 3S, with
+ * its doubling and P + (-P) cases */
+static void gej_add_ge(gej *r, const ge *b) {
+  if (gej_is_inf(r)) { ge_to_gej(r, b); return; }
+  fe Z1Z1, U2, S2, H, R, HH, HHH, V, t;
+  fe_sqr(&Z1Z1, &r->Z);
+  fe_mul(&U2, &b->x, &Z1Z1);
+  fe_mul(&t, &r->Z, &Z1Z1);
+  fe_mul(&S2, &b->y, &t);
+  fe_sub(&H, &U2, &r->X);
+  fe_sub(&R, &S2, &r->Y);
+  if (fe_is_zero(&H)) {
+    if (fe_is_zero(&R)) gej_double(r, r);
+    else gej_set_inf(r);
+    return;
+  }
+  fe_sqr(&HH, &H);
+  fe_mul(&HHH, &H, &HH);
+  fe_mul(&V, &r->X, &HH);
+  fe_mul(&r->Z, &r->Z, &H);
+  fe X3;
+  fe_sqr(&X3, &R); fe_sub(&X3, &X3, &HHH); fe_sub(&X3, &X3, &V); fe_sub(&X3, &X3, &V);
+  fe_sub(&t, &V, &X3); fe_mul(&t, &R, &t);
+  fe_mul(&HHH, &r->Y, &HHH);
+  fe_sub(&r->Y, &t, &HHH);
+  r->X = X3;
+}
+
+static void port_scalar_base_mult(gej *r, const uint8_t k[32]) {
+  gej_set_inf(r);
+  for (int i = 0; i < 32; i++)
+    if (k[i]) gej_add_ge(r, &BYTEPTS[i][k[i]]);
+}
+
+static void port_scalar_mult(gej *r, const ge *q, const uint64_t k[4]) {
+  uint64_t m1[2], m2[2];
+  int n1, n2;
+  glv_split(k, m1, &n1, m2, &n2);
+  ge p1 = *q, p2 = *q, p1n, p2n;
+  fe_mul(&p2.x, &q->x, &FE_BETA64); /* phi(Q) = (beta x, y) */
+  const fe zero = {{0, 0, 0, 0}};
+  if (n1) fe_sub(&p1.y, &zero, &p1.y);
+  if (n2) fe_sub(&p2.y, &zero, &p2.y);
+  p1n = p1; fe_sub(&p1n.y, &zero, &p1.y);
+  p2n = p2; fe_sub(&p2n.y, &zero, &p2.y);
+  int8_t d1[130] = {0}, d2[130] = {0};
+  const int l1 = naf128(d1, m1), l2 = naf128(d2, m2);
+  gej_set_inf(r);
+  for (int i = (l1 > l2 ? l1 : l2) - 1; i >= 0; i--) {
+    if (!gej_is_inf(r)) gej_double(r, r);
+    if (d1[i] == 1) gej_add_ge(r, &p1);
+    else if (d1[i] == -1) gej_add_ge(r, &p1n);
+    if (d2[i] == 1) gej_add_ge(r, &p2);
+    else if (d2[i] == -1) gej_add_ge(r, &p2n);
+  }
+}
+
+static int port_ecdsa_math(const uint8_t *pub65, const uint8_t digest[32], const uint8_t r_be[32],
+                           const uint8_t s_be[32]) {
+  uint64_t e[4], r[4], s[4], w[4], u1[4], u2[4];
+  u256_from_be(e, digest);
+  u256_from_be(r, r_be);
+  u256_from_be(s, s_be);
+  sc_inv(w, s);
+  sc_mul(u1, e, w);
+  sc_mul(u2, r, w);
+  uint8_t u1b[32];
+  u256_to_be(u1b, u1);
+  ge q;
+  fe_from_be(&q.x, pub65 + 1);
+  fe_from_be(&q.y, pub65 + 33);
+  q.inf = 0;
+  gej j1, j2, jr;
+  ge a1, a2, ar;
+  port_scalar_base_mult(&j1, u1b);
+  gej_to_ge(&a1, &j1);
+  port_scalar_mult(&j2, &q, u2);
+  gej_to_ge(&a2, &j2);
+  if (a1.inf) ar = a2;
+  else if (a2.inf) ar = a1;
+  else {
+    gej p1;
+    ge_to_gej(&p1, &a1);
+    jr = p1;
+    gej_add_ge(&jr, &a2);
+    gej_to_ge(&ar, &jr);
+  }
+  if (ar.inf) return 0;
+  uint64_t x[4];
+  memcpy(x, ar.x.v, sizeof x);
+  if (u256_ge(x, SC_N)) u256_sub(x, x, SC_N);
+  return memcmp(x, r, sizeof x) == 0;
+}
+
+/* One item through the port: the oracle's decision order, btcec's algorithms. */
+int port_item_status(const uint8_t *pub, uint64_t publen, const uint8_t digest[32], uint8_t pre,
+                     const uint8_t r_be[32], const uint8_t s_be[32]) {
+  pthread_once(&g_once, init_tables);
+  const int st = oracle_item_status_pre(pub, publen, pre, r_be, s_be);
+  if (st >= 0) return st;
+  return port_ecdsa_math(pub, digest, r_be, s_be) ? BV_ACCEPT : BV_REJECT;
+}

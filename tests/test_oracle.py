@@ -101,3 +101,20 @@ def test_golden_events_and_blocks():
     peers = [gs.Peer(PubKeyHex=gs.EncodeToString(bytes.fromhex(v))) for v in bl["validators"]]
     assert gs.peer_set_hash(peers).hex() == bl["blocks"][0]["peers_hash"]
     assert gs.trust_count(len(peers)) == bl["blocks"][0]["trust_count"] == 4
+
+
+def test_btcec_port_equals_oracle():
+    """The cpu_baseline port (oracle.c: btcec's GLV + NAF ScalarMult, byte-table
+    ScalarBaseMult, mixed additions) decides every item as the checker does:
+    the golden items (all classes, incl. R = infinity / doubling tags) and an
+    adversarial mix."""
+    from babble_amd import synth
+
+    batch, expected, _ = golden_items_batch()
+    assert np.array_equal(coracle.port_verify_batch(batch.as_dict(), n_threads=4), expected)
+    b = synth.adversarial(3000, seed=77, scale_per_million=dict(
+        rflip=50000, sflip=50000, body=20000, highs=50000, range=20000, fmt=20000, key=30000))
+    d = b.as_dict()
+    _, st, _ = coracle.verify_batch(d, n_threads=4)
+    assert np.array_equal(coracle.port_verify_batch(d, n_threads=4), st)
+    assert len(set(st.tolist())) == 4
