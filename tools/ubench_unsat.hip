@@ -100,6 +100,12 @@ __global__ void __launch_bounds__(256) k(uint32_t seed, int iters, uint32_t *out
     for (int it = 0; it < iters; it++) fe_mul(x, x, y);
     fe_canon(x);
     for (int i = 0; i < 8; i++) out[8 * t + i] = x.v[i];
+  } else if (MODE == 2) {  // variable-time inversion (modinv.h), the batched-affine cost model's unknown
+    for (int it = 0; it < iters / 16; it++) {
+      fe_inv_var(x, x);
+      x.v[0] ^= it;
+    }
+    for (int i = 0; i < 8; i++) out[8 * t + i] ^= x.v[i];
   } else if (MODE == 1) {
     uint32_t a[9], b[9];
     to9(a, x);
@@ -136,6 +142,12 @@ int main() {
     hipEventSynchronize(e1);
     hipEventElapsedTime(&ms[1], e0, e1);
   }
+  float msi;
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(k<2>, dim3(blocks), dim3(threads), 0, 0, 1u, iters, out, bad);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  hipEventElapsedTime(&msi, e0, e1);
   uint32_t nb = 0;
   hipMemcpy(&nb, bad, 4, hipMemcpyDeviceToHost);
   const double ops = (double)blocks * threads * iters;
@@ -143,5 +155,7 @@ int main() {
   printf("unsaturated 9x29 fe9_mul (prototype)  %7.3f ms  %7.1f G mul/s  (%.2fx)\n", ms[1], ops / ms[1] / 1e6,
          ms[1] / ms[0]);
   printf("cross-check: %u mismatching words (unsaturated vs saturated results)\n", nb);
+  printf("fe_inv_var (divsteps)                 %7.3f ms  %7.1f G inv/s  = %.1f fe_mul-equivalents\n", msi,
+         ops / 16 / msi / 1e6, (msi / (ops / 16)) / (ms[0] / ops));
   return nb != 0;
 }
