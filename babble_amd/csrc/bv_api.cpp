@@ -46,6 +46,10 @@ constexpr uint32_t kKcMaxBatchKeys = 4096;     // key cache: batches with more k
 constexpr uint32_t kKcBuildGroup = 8;          // keys per KC build launch (pscr: 403 MB per key)
 constexpr uint32_t kPrepM = 16;                // items per s^-1 batch
 constexpr uint32_t kRgWords = 25;              // R_G words per item
+#ifndef BV_FUSED_KC
+#define BV_FUSED_KC 1
+#endif
+constexpr bool kFusedKc = BV_FUSED_KC;         // key cache: one fused verify kernel (k_verify_gq)
 constexpr size_t kChunk = 16ull << 20;         // host-entry staging / PCIe chunk
 
 }  // namespace
@@ -514,7 +518,13 @@ int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
   HIPCHK(hipEventRecord(ev[E_SHA], st), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamWaitEvent(st, ev[E_SINV], 0), BV_E_LAUNCH, "join");
   HIPCHK(hipEventRecord(ev[E_SCALAR], st), BV_E_LAUNCH, "event");
-  if (table_mode) {
+  if (kc && kFusedKc) {  // key cache: G and Q parts in one kernel (R_G stays in registers)
+    HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
+    HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
+    HIPCHK(bvk::verify_gq(st, n_items, b->item_key, r32, s32, b->pre, kst, b->item_msg, dig, w, ctx->g_table,
+                          ctx->kc_tabs.as<uint64_t>(), status, bits),
+           BV_E_LAUNCH, "k_verify_gq");
+  } else if (table_mode) {
     HIPCHK(bvk::verify_g(st, n_items, b->item_key, r32, s32, b->pre, kst, b->item_msg, dig, w, u12, ctx->g_table,
                          ctx->rg.as<uint32_t>()),
            BV_E_LAUNCH, "k_verify_g");

@@ -40,6 +40,9 @@ hipError_t build_kc(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, ui
                     const uint64_t *);
 size_t kc_pscr_bytes();
 hipError_t sinv(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *);
+hipError_t verify_gq(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
+                     const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *,
+                     const uint64_t *, uint8_t *, uint64_t *);
 hipError_t verify_g(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
                     const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
                     const uint32_t *, uint32_t *);

@@ -629,6 +629,23 @@ __global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, const uint32
   write_status(i, n_items, st, status, bits);
 }
 
+// Key-cache path, G and Q parts fused (verify_core.h: verify_item_gq_kc).
+__global__ void __launch_bounds__(256) k_verify_gq(uint64_t n_items, const uint32_t *__restrict__ item_key,
+                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
+                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
+                                                   const uint32_t *__restrict__ item_msg,
+                                                   const uint32_t *__restrict__ digest_words,
+                                                   const uint32_t *__restrict__ w_in,
+                                                   const uint32_t *__restrict__ g_table,
+                                                   const uint64_t *__restrict__ key_tabs, uint8_t *__restrict__ status,
+                                                   uint64_t *__restrict__ bits) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint8_t st = BV_REJECT;
+  if (i < n_items)
+    st = verify_item_gq_kc(i, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, g_table, key_tabs);
+  write_status(i, n_items, st, status, bits);
+}
+
 // Key-cache (KC) table windows from the 11-bit sub-tables: block (c, key)
 // holds slots s = BV_KCPAIR_ENT c' + 256 e + t (e < 16) of window
 // j = c / (ENT / BV_KCPAIR_ENT), c' = c mod that; digit k12_digit(s) (signed
@@ -871,6 +888,16 @@ hipError_t verify_q(hipStream_t st, int kw, uint64_t n, const uint32_t *item_key
   else
     hipLaunchKernelGGL((k_verify_q<BV_KCW, BV_KCNWIN>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be,
                        pre, kst, u12, nullptr, key_tabs, rg, status, bits);
+  return hipGetLastError();
+}
+
+hipError_t verify_gq(hipStream_t st, uint64_t n, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
+                     const uint8_t *pre, const uint8_t *kst, const uint32_t *item_msg, const uint32_t *dig,
+                     const uint32_t *w, const uint32_t *g_table, const uint64_t *key_tabs, uint8_t *status,
+                     uint64_t *bits) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_verify_gq, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, item_msg, dig,
+                     w, g_table, key_tabs, status, bits);
   return hipGetLastError();
 }
 

@@ -597,6 +597,37 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
 }
 
+// Key-cache path in ONE pass (k_verify_gq): R = u1 G + k1 T + k2 phi(T) with
+// the G table and the key's cached table, R_G kept in registers (no HBM
+// round trip of R_G / u12 between two kernels, no kernel boundary).  Same
+// decisions as verify_item_g followed by verify_item_q.
+DEV uint8_t verify_item_gq_kc(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
+                              const uint8_t *pre, const uint8_t *kstatus, const uint32_t *item_msg,
+                              const uint32_t *digest_words, const uint32_t *w_in, const uint32_t *g_table,
+                              const uint64_t *key_tabs) {
+  fe r;
+  const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
+  if (st != 0xFF) return st;
+  uint32_t u[8], k1[4], k2[4], signs;
+  item_scalars(i, r_be, item_msg, digest_words, w_in, u, k1, k2, signs);
+  gej R;
+  bool inf = true;
+  fe_set(R.X, 0);
+  fe_set(R.Y, 0);
+  fe_set(R.Z, 0);
+  g_table_add<BV_GW, BV_GNWIN>(R, inf, g_table, u);
+  const uint32_t *tab = (const uint32_t *)key_tabs[item_key[i]];
+#pragma unroll 1
+  for (int h = 0; h < 2; h++) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) kk[c] = h ? k2[c] : k1[c];
+    key_table_add<BV_KCW, BV_KCNWIN, true>(R, inf, tab, kk, (signs >> h) & 1u, h != 0);
+  }
+  fe_load_be_words(r, r_be + 8 * i);
+  return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
+}
+
 // One signature item without a key table: k1 Q + k2 phi(Q) by a joint
 // (Strauss-Shamir) per-lane double-and-add over the 128-bit GLV halves.
 DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
