@@ -38,7 +38,12 @@ __global__ void __launch_bounds__(256) kop(uint32_t *out, uint32_t seed, int ite
   if constexpr (OP == 4) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(w[c]) : "v"(w[(c + 1) & 15])); \
   if constexpr (OP == 5) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[c]) : "v"(b));              \
   if constexpr (OP == 6) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[c]) : "v"(b));              \
-  if constexpr (OP == 7) asm volatile("v_fma_f64 %0, %0, %1, %0" : "+v"(w[c]) : "v"(w[(c + 3) & 15]));
+  if constexpr (OP == 7) asm volatile("v_fma_f64 %0, %0, %1, %0" : "+v"(w[c]) : "v"(w[(c + 3) & 15]));   \
+  if constexpr (OP == 8) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(a[c]));                  \
+  if constexpr (OP == 9) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[c]) : "v"(b), "v"(a[(c + 1) & 15])); \
+  if constexpr (OP == 10) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[c]) : "v"(b), "v"(a[(c + 1) & 15])); \
+  if constexpr (OP == 11) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[c]) : "v"(b));                 \
+  if constexpr (OP == 12) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a[c]));
     REP16(BODY)
 #undef BODY
   }
@@ -84,5 +89,10 @@ int main() {
   run<5>("v_mul_lo_u32", out, blocks);
   run<6>("v_mul_hi_u32", out, blocks);
   run<7>("v_fma_f64", out, blocks);
+  run<8>("v_alignbit_b32", out, blocks);
+  run<9>("v_bitop3_b32", out, blocks);
+  run<10>("v_add3_u32", out, blocks);
+  run<11>("v_xor_b32", out, blocks);
+  run<12>("v_lshrrev_b32", out, blocks);
   return 0;
 }
