@@ -432,33 +432,20 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
 // arrays prepared by kc_prepare.  Every call starts after the previous call
 // on this ctx has finished on the device (ev_done), whatever its stream:
 // work buffers are shared between calls.
-int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
-                  hipStream_t st, bool hashed, bool kc) {
-  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
+// Phase A of a verify (needs only the keys, s and pre in HBM): batched s^-1
+// on the s^-1 stream, key decode + per-batch key tables on the keys stream,
+// both after `ready` (an event recorded once those arrays are in HBM).  The
+// host entry points call it as soon as the small arrays have landed, so the
+// key tables build while the message bytes still cross PCIe.
+int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t ready, bool kc) {
+  const uint64_t n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
   if (n_items > 0 && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be))
     return bv_fail(ctx, BV_E_ARGS, "null item arrays");
-  if (n_msgs > 0 && !b->msg_off) return bv_fail(ctx, BV_E_ARGS, "null msg_off");
   if (n_items > 0 && n_keys == 0) return bv_fail(ctx, BV_E_ARGS, "items without keys");
   if (n_keys > 0 && !b->key_off) return bv_fail(ctx, BV_E_ARGS, "null key_off");
   if (((uintptr_t)b->r_be | (uintptr_t)b->s_be) & 15)
     return bv_fail(ctx, BV_E_ARGS, "r_be/s_be must be 16-byte aligned");
-
-  uint32_t *dig = (uint32_t *)d_msg_hash;
-  if (hashed || !dig || ((uintptr_t)dig & 15)) {
-    HIPCHK(ctx->digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
-    dig = ctx->digests.as<uint32_t>();
-  }
-  uint8_t *status = d_status;
-  if (!status) {
-    HIPCHK(ctx->status.ensure(std::max<uint64_t>(n_items, 1)), BV_E_OOM, "alloc status");
-    status = ctx->status.as<uint8_t>();
-  }
-  uint64_t *bits = d_bits;
-  if (!bits) {
-    HIPCHK(ctx->bits.ensure(std::max<uint64_t>((n_items + 63) / 64, 1) * 8), BV_E_OOM, "alloc bits");
-    bits = ctx->bits.as<uint64_t>();
-  }
   HIPCHK(ctx->kstatus.ensure(std::max<uint32_t>(n_keys, 1)), BV_E_OOM, "alloc kstatus");
   HIPCHK(ctx->kxy.ensure(std::max<uint32_t>(n_keys, 1) * 64ull), BV_E_OOM, "alloc kxy");
   HIPCHK(ctx->scratch.ensure(std::max<uint64_t>(n_items, 1) * 32), BV_E_OOM, "alloc scratch");
@@ -488,45 +475,75 @@ int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
              "alloc key tables");
     }
   }
-  const uint8_t *kst = kc ? ctx->kc_kst.as<uint8_t>() : ctx->kstatus.as<uint8_t>();
+  hipEvent_t *ev = ctx->ev;
+  // s^-1 needs only s: concurrent with everything up to k_verify_g
+  HIPCHK(hipStreamWaitEvent(ctx->sstream, ready, 0), BV_E_LAUNCH, "fork");
+  HIPCHK(hipEventRecord(ev[E_START], ctx->sstream), BV_E_LAUNCH, "event");
+  // items per lane: kPrepM amortises the inversion in large batches; a small
+  // batch spreads over ~64k lanes instead, since there the serial chain of
+  // one lane (M products, the inversion, 2M products) is the latency
+  const uint32_t M = (uint32_t)std::min<uint64_t>(kPrepM, std::max<uint64_t>(1, (n_items + 65535) / 65536));
+  HIPCHK(bvk::sinv(ctx->sstream, n_items, M, (const uint32_t *)b->s_be, b->pre, ctx->scratch.as<uint32_t>()),
+         BV_E_LAUNCH, "k_sinv");
+  HIPCHK(hipEventRecord(ev[E_SINV], ctx->sstream), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(ctx->kstream, ready, 0), BV_E_LAUNCH, "fork");
+  if (!kc) {
+    HIPCHK(bvk::key_decode(ctx->kstream, n_keys, b->key_bytes, b->key_off, ctx->kstatus.as<uint8_t>(),
+                           ctx->kxy.as<uint32_t>()),
+           BV_E_LAUNCH, "k_key_decode");
+    if (table_mode)
+      HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
+                               ctx->bases_jac.as<uint32_t>(), ctx->key_sub.as<uint32_t>(),
+                               ctx->key_pscr.as<uint32_t>(), ctx->key_table.as<uint32_t>()),
+             BV_E_LAUNCH, "key tables");
+  }
+  HIPCHK(hipEventRecord(ev[E_KEYS], ctx->kstream), BV_E_LAUNCH, "event");
+  return BV_OK;
+}
 
+// Phase B on `st` (after bv_run_keys): SHA-256 of the messages (unless
+// `hashed`: digests already in ctx->digests), then the verify kernels once
+// s^-1 and the key tables are ready; statuses and bits.
+int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
+                  hipStream_t st, bool hashed, bool kc) {
+  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
+  if (n_msgs > 0 && !b->msg_off) return bv_fail(ctx, BV_E_ARGS, "null msg_off");
+  uint32_t *dig = (uint32_t *)d_msg_hash;
+  if (hashed || !dig || ((uintptr_t)dig & 15)) {
+    HIPCHK(ctx->digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
+    dig = ctx->digests.as<uint32_t>();
+  }
+  uint8_t *status = d_status;
+  if (!status) {
+    HIPCHK(ctx->status.ensure(std::max<uint64_t>(n_items, 1)), BV_E_OOM, "alloc status");
+    status = ctx->status.as<uint8_t>();
+  }
+  uint64_t *bits = d_bits;
+  if (!bits) {
+    HIPCHK(ctx->bits.ensure(std::max<uint64_t>((n_items + 63) / 64, 1) * 8), BV_E_OOM, "alloc bits");
+    bits = ctx->bits.as<uint64_t>();
+  }
+  const bool table_mode = ctx->table_mode;
+  const int key_w = ctx->key_w;
+  const uint8_t *kst = kc ? ctx->kc_kst.as<uint8_t>() : ctx->kstatus.as<uint8_t>();
   hipEvent_t *ev = ctx->ev;
   const uint32_t *r32 = (const uint32_t *)b->r_be, *s32 = (const uint32_t *)b->s_be;
   uint32_t *w = ctx->scratch.as<uint32_t>(), *u12 = ctx->u12.as<uint32_t>();
-  if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order after previous call");
-  HIPCHK(hipEventRecord(ev[E_START], st), BV_E_LAUNCH, "event");
-  // s^-1 needs only s: its own stream, concurrent with everything up to k_verify_g
-  HIPCHK(hipStreamWaitEvent(ctx->sstream, ev[E_START], 0), BV_E_LAUNCH, "fork");
-  HIPCHK(bvk::sinv(ctx->sstream, n_items, kPrepM, s32, b->pre, w), BV_E_LAUNCH, "k_sinv");
-  HIPCHK(hipEventRecord(ev[E_SINV], ctx->sstream), BV_E_LAUNCH, "event");
-  if (!kc)
-    HIPCHK(bvk::key_decode(st, n_keys, b->key_bytes, b->key_off, ctx->kstatus.as<uint8_t>(),
-                           ctx->kxy.as<uint32_t>()),
-           BV_E_LAUNCH, "k_key_decode");
   HIPCHK(hipEventRecord(ev[E_FORK], st), BV_E_LAUNCH, "event");
-  if (table_mode && !kc) {  // key tables on the keys stream, concurrent with the main stream below
-    HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_FORK], 0), BV_E_LAUNCH, "fork");
-    HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
-                             ctx->bases_jac.as<uint32_t>(), ctx->key_sub.as<uint32_t>(),
-                             ctx->key_pscr.as<uint32_t>(), ctx->key_table.as<uint32_t>()),
-           BV_E_LAUNCH, "key tables");
-    HIPCHK(hipEventRecord(ev[E_KEYS], ctx->kstream), BV_E_LAUNCH, "event");
-  } else {
-    HIPCHK(hipEventRecord(ev[E_KEYS], st), BV_E_LAUNCH, "event");
-  }
   if (!hashed) HIPCHK(bvk::sha256(st, n_msgs, b->msg_bytes, b->msg_off, dig), BV_E_LAUNCH, "k_sha256");
   HIPCHK(hipEventRecord(ev[E_SHA], st), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamWaitEvent(st, ev[E_SINV], 0), BV_E_LAUNCH, "join");
   HIPCHK(hipEventRecord(ev[E_SCALAR], st), BV_E_LAUNCH, "event");
   if (kc && kFusedKc) {  // key cache: G and Q parts in one kernel (R_G stays in registers)
+    HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
     HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
     HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
     HIPCHK(bvk::verify_gq(st, n_items, b->item_key, r32, s32, b->pre, kst, b->item_msg, dig, w, ctx->g_table,
                           ctx->kc_tabs.as<uint64_t>(), status, bits),
            BV_E_LAUNCH, "k_verify_gq");
   } else if (table_mode) {
-    HIPCHK(bvk::verify_g(st, n_items, b->item_key, r32, s32, b->pre, kst, b->item_msg, dig, w, u12, ctx->g_table,
-                         ctx->rg.as<uint32_t>()),
+    HIPCHK(bvk::verify_g(st, n_items, 0, n_items, b->item_key, r32, s32, b->pre, kst, b->item_msg, dig, w, u12,
+                         ctx->g_table, ctx->rg.as<uint32_t>()),
            BV_E_LAUNCH, "k_verify_g");
     HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
@@ -535,6 +552,7 @@ int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
                          kc ? ctx->kc_tabs.as<uint64_t>() : nullptr, ctx->rg.as<uint32_t>(), status, bits),
            BV_E_LAUNCH, "k_verify_q");
   } else {
+    HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
     HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
     HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
     HIPCHK(bvk::verify_generic(st, n_items, b->item_key, r32, s32, b->pre, kst, ctx->kxy.as<uint32_t>(), b->item_msg,
@@ -549,6 +567,16 @@ int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
   return BV_OK;
 }
 
+// The whole verify of a batch already in HBM on `st`.
+int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
+                  hipStream_t st, bool hashed, bool kc) {
+  if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order after previous call");
+  HIPCHK(hipEventRecord(ctx->ev[E_READY], st), BV_E_LAUNCH, "event");
+  int rc = bv_run_keys(ctx, b, ctx->ev[E_READY], kc);
+  if (rc != BV_OK) return rc;
+  return bv_run_verify(ctx, b, d_msg_hash, d_status, d_bits, st, hashed, kc);
+}
+
 static float elapsed(hipEvent_t a, hipEvent_t b) {
   float t;
   return hipEventElapsedTime(&t, a, b) == hipSuccess ? t : -1.f;
@@ -559,7 +587,7 @@ void bv_read_timing(bv_ctx *ctx) {
   bv_timing &t = ctx->timing;
   t.ms_sha256 = elapsed(ev[E_FORK], ev[E_SHA]);
   t.key_path = (uint32_t)ctx->key_w;
-  t.ms_keyprep = ctx->table_mode ? elapsed(ev[E_START], ev[E_KEYS]) : elapsed(ev[E_START], ev[E_FORK]);
+  t.ms_keyprep = elapsed(ev[E_START], ev[E_KEYS]);
   t.ms_scalar = elapsed(ev[E_START], ev[E_SINV]);
   t.ms_verify_g = elapsed(ev[E_SCALAR], ev[E_G]);
   t.ms_verify = elapsed(ev[E_JOINED], ev[E_END]);
@@ -740,6 +768,10 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
     rc = bv_kc_prepare(ctx, n_keys, b->key_bytes, b->key_off, d.key_bytes, d.key_off, st, &kc);
     if (rc != BV_OK) return rc;
   }
+  // s^-1 and the key tables need only the small arrays: they run while the
+  // message bytes below still cross PCIe
+  rc = bv_run_keys(ctx, &d, ctx->ev[E_SMALL], kc);
+  if (rc != BV_OK) return rc;
 
   // message bytes: chunks on message boundaries, each hashed once it lands
   HIPCHK(ctx->digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
@@ -768,7 +800,7 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
   call->ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_STAGED], 0), BV_E_LAUNCH, "join staging");
   HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
-  rc = bv_run_device(ctx, &d, nullptr, nullptr, nullptr, st, true, kc);
+  rc = bv_run_verify(ctx, &d, nullptr, nullptr, nullptr, st, true, kc);
   if (rc != BV_OK) return rc;
 
   // results into pinned memory: digests as soon as hashing ended (overlaps

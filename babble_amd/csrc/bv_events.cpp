@@ -7,8 +7,9 @@
 // bodies never cross PCIe.  Device: k_ev_len -> inclusive scan (hipcub) ->
 // k_ev_write -> level 0 in one grid launch -> the remaining levels, wide ones
 // as grid launches and runs of narrow ones (<= 1024 events) as ONE
-// single-workgroup launch each (k_ev_hash_chain) -> bv_run_device on the
-// hashed bodies.
+// single-workgroup launch each (k_ev_hash_chain) -> bv_run_verify on the
+// hashed bodies.  s^-1 and the key tables (bv_run_keys) start as soon as the
+// keys, r, s and pre (staged first) have landed.
 #include <algorithm>
 #include <cstring>
 
@@ -133,9 +134,15 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
     total += align256(bytes + pad);
     return o;
   };
+  // keys, r, s, pre and creators first: s^-1 and the key tables start once
+  // they have landed, while the rest of the batch still crosses PCIe
   const size_t o_koff = add(eb->key_off, (eb->n_keys + 1) * 8ull);
   const size_t o_kb = add(eb->key_bytes, key_len, 64);
+  const size_t o_r = add(eb->r_be, n * 32);
+  const size_t o_s = add(eb->s_be, n * 32);
+  const size_t o_pre = add(eb->pre, eb->pre ? n : 0);
   const size_t o_cr = add(eb->creator, n * 4);
+  const size_t small_end = total;
   const size_t o_ix = add(eb->index, n * 8);
   const size_t o_ts = add(eb->timestamp, n * 8);
   const size_t o_pk = add(eb->parent_kind, n * 2);
@@ -150,9 +157,6 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   const size_t o_ij = add(eb->itx_json, itx_len);
   const size_t o_bo = add(eb->bsig_off, eb->bsig_off ? (n + 1) * 8 : 0);
   const size_t o_bj = add(eb->bsig_json, bsig_len);
-  const size_t o_r = add(eb->r_be, n * 32);
-  const size_t o_s = add(eb->s_be, n * 32);
-  const size_t o_pre = add(eb->pre, eb->pre ? n : 0);
   const size_t o_ord = add(dag ? order.data() : nullptr, dag ? n * 4 : 0);
   const size_t o_lof = add(dag ? level_off.data() : nullptr, dag ? level_off.size() * 4 : 0);
   const size_t o_pin = add(dag ? posin.data() : nullptr, dag ? n * 4 : 0);
@@ -160,18 +164,8 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
   HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
   HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
+  HIPCHK(ctx->ev_iota.ensure(n * 4), BV_E_OOM, "alloc item index");
   uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
-  HIPCHK(hipEventRecord(ctx->ev[E_CALL], st), BV_E_LAUNCH, "event");
-  for (size_t a = 0; a < total; a += kChunk) {
-    const size_t z = std::min(total, a + kChunk);
-    for (const Seg &s : segs) {
-      const size_t lo = std::max(a, s.off), hi = std::min(z, s.off + s.n);
-      if (s.src && lo < hi) ctx->pool->copy(pin + lo, (const uint8_t *)s.src + (lo - s.off), hi - lo);
-    }
-    HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
-  }
-  HIPCHK(hipEventRecord(ctx->ev[E_STAGED], st), BV_E_LAUNCH, "event");
-  call.ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call.t0).count();
 
   // the same batch over device pointers
   bv_event_batch d = *eb;
@@ -196,6 +190,42 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   d.s_be = dev + o_s;
   d.pre = eb->pre ? dev + o_pre : nullptr;
 
+  // verification items: item e = (body e, creator key, r, s)
+  bv_batch vb = {};
+  vb.n_msgs = n;
+  vb.n_keys = eb->n_keys;
+  vb.key_bytes = d.key_bytes;
+  vb.key_off = d.key_off;
+  vb.n_items = n;
+  vb.item_msg = ctx->ev_iota.as<uint32_t>();
+  vb.item_key = d.creator;
+  vb.r_be = d.r_be;
+  vb.s_be = d.s_be;
+  vb.pre = d.pre;
+
+  HIPCHK(hipEventRecord(ctx->ev[E_CALL], st), BV_E_LAUNCH, "event");
+  bool kc = false, launched = false;
+  for (size_t a = 0; a < total; a += kChunk) {
+    const size_t z = std::min(total, a + kChunk);
+    for (const Seg &s : segs) {
+      const size_t lo = std::max(a, s.off), hi = std::min(z, s.off + s.n);
+      if (s.src && lo < hi) ctx->pool->copy(pin + lo, (const uint8_t *)s.src + (lo - s.off), hi - lo);
+    }
+    HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
+    if (!launched && z >= small_end) {  // keys, r, s, pre, creators are queued: phase A
+      launched = true;
+      HIPCHK(hipEventRecord(ctx->ev[E_SMALL], st), BV_E_LAUNCH, "event");
+      if (ctx->flags & BV_F_KEY_CACHE) {
+        rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, d.key_bytes, d.key_off, st, &kc);
+        if (rc != BV_OK) return rc;
+      }
+      rc = bv_run_keys(ctx, &vb, ctx->ev[E_SMALL], kc);
+      if (rc != BV_OK) return rc;
+    }
+  }
+  HIPCHK(hipEventRecord(ctx->ev[E_STAGED], st), BV_E_LAUNCH, "event");
+  call.ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call.t0).count();
+
   // bodies: an upper bound on their size (exact lengths are on the device)
   uint64_t kmax = 0;
   for (uint32_t k = 0; k < eb->n_keys; k++) kmax = std::max<uint64_t>(kmax, eb->key_off[k + 1] - eb->key_off[k]);
@@ -208,9 +238,7 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   HIPCHK(ctx->ev_offs.ensure((n + 1) * 8), BV_E_OOM, "alloc offs");
   HIPCHK(ctx->ev_bodies.ensure(bound), BV_E_OOM, "alloc bodies");
   HIPCHK(ctx->ev_tmp.ensure(std::max<size_t>(tmp_bytes, 256)), BV_E_OOM, "alloc scan scratch");
-  HIPCHK(ctx->ev_iota.ensure(n * 4), BV_E_OOM, "alloc item index");
   HIPCHK(ctx->digests.ensure(n * 32), BV_E_OOM, "alloc digests");
-  if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order");
   uint64_t *offs = ctx->ev_offs.as<uint64_t>();
   uint32_t *ppos = ctx->ev_ppos.as<uint32_t>(), *dig = ctx->digests.as<uint32_t>();
   uint8_t *bodies = ctx->ev_bodies.as<uint8_t>();
@@ -250,39 +278,28 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   HIPCHK(bvk::iota(st, n, ctx->ev_iota.as<uint32_t>()), BV_E_LAUNCH, "k_iota");
   HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
 
-  // verification: item e = (body e, creator key, r, s)
-  bv_batch vb = {};
-  vb.n_msgs = n;
-  vb.msg_bytes = bodies;
-  vb.msg_off = offs;
-  vb.n_keys = eb->n_keys;
-  vb.key_bytes = d.key_bytes;
-  vb.key_off = d.key_off;
-  vb.n_items = n;
-  vb.item_msg = ctx->ev_iota.as<uint32_t>();
-  vb.item_key = d.creator;
-  vb.r_be = d.r_be;
-  vb.s_be = d.s_be;
-  vb.pre = d.pre;
-  bool kc = false;
-  if (ctx->flags & BV_F_KEY_CACHE) {
-    rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, d.key_bytes, d.key_off, st, &kc);
-    if (rc != BV_OK) return rc;
-  }
-  rc = bv_run_device(ctx, &vb, nullptr, nullptr, nullptr, st, true, kc);
-  if (rc != BV_OK) return rc;
-
+  // the digests go back on the copy stream while the verify kernels run
   const size_t o_st = align256(n * 32), o_bits = o_st + align256(n);
   HIPCHK(ctx->pin_out.ensure(o_bits + align256((n + 63) / 64 * 8) + 256), BV_E_OOM, "alloc pinned results");
   uint8_t *pout = (uint8_t *)ctx->pin_out.p;
   call.pout = pout;
   call.o_st = o_st;
   call.o_bits = o_bits;
-  HIPCHK(hipMemcpyAsync(pout, ctx->digests.p, n * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h digests");
+  HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev[E_HASHED], 0), BV_E_LAUNCH, "join");
+  HIPCHK(hipMemcpyAsync(pout, ctx->digests.p, n * 32, hipMemcpyDeviceToHost, ctx->cstream), BV_E_LAUNCH,
+         "d2h digests");
+  HIPCHK(hipEventRecord(ctx->ev[E_CSDONE], ctx->cstream), BV_E_LAUNCH, "event");
+
+  // verification of the hashed bodies (phase A is already under way)
+  vb.msg_bytes = bodies;
+  vb.msg_off = offs;
+  rc = bv_run_verify(ctx, &vb, nullptr, nullptr, nullptr, st, true, kc);
+  if (rc != BV_OK) return rc;
   HIPCHK(hipMemcpyAsync(pout + o_st, ctx->status.p, n, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
   HIPCHK(hipMemcpyAsync(pout + o_bits, ctx->bits.p, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
          "d2h bits");
   HIPCHK(hipEventRecord(ctx->ev[E_OUT], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_CSDONE], 0), BV_E_LAUNCH, "join");  // digests out before ev_done
   HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
   bv_batch sizes = {};
   sizes.n_msgs = n;

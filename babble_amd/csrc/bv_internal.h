@@ -43,8 +43,8 @@ hipError_t sinv(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint8_t
 hipError_t verify_gq(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
                      const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *,
                      const uint64_t *, uint8_t *, uint64_t *);
-hipError_t verify_g(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
-                    const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
+hipError_t verify_g(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
+                    const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
                     const uint32_t *, uint32_t *);
 hipError_t verify_q(hipStream_t, int, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
                     const uint8_t *, const uint32_t *, const uint32_t *, const uint64_t *, const uint32_t *,
@@ -159,7 +159,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // timing / ordering events (see bv_read_timing)
 enum {
   E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_SINV,
-  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_COUNT
+  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_COUNT
 };
 
 struct KcSlot {
@@ -213,6 +213,9 @@ struct bv_host_call {
 int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess);
 int bv_validate_host_batch(bv_ctx *ctx, const bv_batch *b);
 int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
+                  hipStream_t st, bool hashed, bool kc);
+int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t ready, bool kc);
+int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc);
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
                   const uint64_t *dko, hipStream_t st, bool *use);

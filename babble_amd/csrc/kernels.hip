@@ -401,19 +401,21 @@ __global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict
   if (bstatus && bstatus[b] != KS_OK) return;  // uniform per block
   __shared__ fe sPre[BLOCK];
   __shared__ fe sSuf[BLOCK];
-  __shared__ fe sBx, sBy, sInvTotal;
-  if (t == 0) {
-    fe x, y;
-    jac_to_affine(x, y, bases_jac + ((uint64_t)b * NWIN + j) * 24);
-    sBx = x;
-    sBy = y;
-  }
-  __syncthreads();
-  const fe bx = sBx, by = sBy;
+  __shared__ fe sInvTotal;
+  // The base B = (X, Y, Z) stays Jacobian: (X, Y) is an affine point of the
+  // isomorphic curve y^2 = x^3 + 7 Z^6, and the a = 0 doubling / mixed-add
+  // formulas never use b, so d (X, Y) computed there as (X', Y', Z') is
+  // d B = (X', Y', Z' Z) on secp256k1.  No inversion before the entries.
+  const uint32_t *bj = bases_jac + ((uint64_t)b * NWIN + j) * 24;
+  fe bx, by, bz;
+  fe_load(bx, bj);
+  fe_load(by, bj + 8);
+  fe_load(bz, bj + 16);
   gej R;
   bool inf;
   fe Z;
   table_point(R, inf, Z, bx, by, d, W);
+  if (!inf) fe_mul(Z, Z, bz);
   sPre[t] = Z;
   sSuf[t] = Z;
   __syncthreads();
@@ -601,19 +603,20 @@ __device__ __forceinline__ void write_status(uint64_t i, uint64_t n_items, uint8
   if ((threadIdx.x & 63) == 0 && i < n_items) bits[i >> 6] = mask;
 }
 
-__global__ void __launch_bounds__(256) k_verify_g(uint64_t n_items, const uint32_t *__restrict__ item_key,
+template <bool LAT>
+__global__ void __launch_bounds__(256) k_verify_g(uint64_t n_items, uint64_t lo, uint64_t hi, const uint32_t *__restrict__ item_key,
                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
                                                   const uint32_t *__restrict__ item_msg,
                                                   const uint32_t *__restrict__ digest_words,
                                                   const uint32_t *__restrict__ w_in, uint32_t *__restrict__ u12,
                                                   const uint32_t *__restrict__ g_table, uint32_t *__restrict__ rg) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_items)
-    verify_item_g(i, n_items, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, u12, g_table, rg);
+  const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < hi)
+    verify_item_g<LAT>(i, n_items, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, u12, g_table, rg);
 }
 
-template <int W, int NWIN>
+template <int W, int NWIN, bool LAT>
 __global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, const uint32_t *__restrict__ item_key,
                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
@@ -625,11 +628,12 @@ __global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, const uint32
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t st = BV_REJECT;
   if (i < n_items)
-    st = verify_item_q<W, NWIN>(i, n_items, item_key, r_be, s_be, pre, kstatus, u12, key_table, key_tabs, rg);
+    st = verify_item_q<W, NWIN, LAT>(i, n_items, item_key, r_be, s_be, pre, kstatus, u12, key_table, key_tabs, rg);
   write_status(i, n_items, st, status, bits);
 }
 
 // Key-cache path, G and Q parts fused (verify_core.h: verify_item_gq_kc).
+template <bool LAT>
 __global__ void __launch_bounds__(256) k_verify_gq(uint64_t n_items, const uint32_t *__restrict__ item_key,
                                                    const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                    const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
@@ -642,7 +646,7 @@ __global__ void __launch_bounds__(256) k_verify_gq(uint64_t n_items, const uint3
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t st = BV_REJECT;
   if (i < n_items)
-    st = verify_item_gq_kc(i, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, g_table, key_tabs);
+    st = verify_item_gq_kc<LAT>(i, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, g_table, key_tabs);
   write_status(i, n_items, st, status, bits);
 }
 
@@ -719,6 +723,7 @@ __global__ void __launch_bounds__(256) k_table_pair_kc(const uint32_t *__restric
   }
 }
 
+template <bool LAT>
 __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, const uint32_t *__restrict__ item_key,
                                                         const uint32_t *__restrict__ r_be,
                                                         const uint32_t *__restrict__ s_be,
@@ -733,7 +738,7 @@ __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, const 
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t st = BV_REJECT;
   if (i < n_items)
-    st = verify_item_generic(i, item_key, r_be, s_be, pre, kstatus, kxy, item_msg, digest_words, w_in, g_table);
+    st = verify_item_generic<LAT>(i, item_key, r_be, s_be, pre, kstatus, kxy, item_msg, digest_words, w_in, g_table);
   write_status(i, n_items, st, status, bits);
 }
 
@@ -743,6 +748,15 @@ __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, const 
 namespace bvk {
 
 static inline dim3 grid1(uint64_t n, uint32_t block) { return dim3((uint32_t)((n + block - 1) / block)); }
+
+// Verify kernels come in two variants: the throughput one (one multiply at a
+// time, few VGPRs, 4+ waves per SIMD hide the latency) and the latency one
+// (gej_*_lat: independent multiplies interleaved in one asm program) for
+// batches too small to put more than ~2 waves on each of the 1024 SIMDs.
+#ifndef BV_LAT_MAX_ITEMS
+#define BV_LAT_MAX_ITEMS 131072
+#endif
+static inline bool lat_variant(uint64_t n) { return n <= BV_LAT_MAX_ITEMS; }
 
 hipError_t sha256(hipStream_t st, uint64_t n, const uint8_t *bytes, const uint64_t *off, uint32_t *dig) {
   if (n == 0) return hipSuccess;
@@ -863,12 +877,18 @@ hipError_t sinv(hipStream_t st, uint64_t n, uint32_t M, const uint32_t *s_be, co
   return hipGetLastError();
 }
 
-hipError_t verify_g(hipStream_t st, uint64_t n, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
-                    const uint8_t *pre, const uint8_t *kst, const uint32_t *item_msg, const uint32_t *dig,
-                    const uint32_t *w, uint32_t *u12, const uint32_t *g_table, uint32_t *rg) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_verify_g, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, item_msg, dig, w,
-                     u12, g_table, rg);
+// Items [lo, hi) of an n-item batch (R_G is stored SoA with stride n).
+hipError_t verify_g(hipStream_t st, uint64_t n, uint64_t lo, uint64_t hi, const uint32_t *item_key,
+                    const uint32_t *r_be, const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst,
+                    const uint32_t *item_msg, const uint32_t *dig, const uint32_t *w, uint32_t *u12,
+                    const uint32_t *g_table, uint32_t *rg) {
+  if (hi <= lo) return hipSuccess;
+  if (lat_variant(n))
+    hipLaunchKernelGGL(k_verify_g<true>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be, pre,
+                       kst, item_msg, dig, w, u12, g_table, rg);
+  else
+    hipLaunchKernelGGL(k_verify_g<false>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be, pre,
+                       kst, item_msg, dig, w, u12, g_table, rg);
   return hipGetLastError();
 }
 
@@ -879,15 +899,22 @@ hipError_t verify_q(hipStream_t st, int kw, uint64_t n, const uint32_t *item_key
                     const uint32_t *key_table, const uint64_t *key_tabs, const uint32_t *rg, uint8_t *status,
                     uint64_t *bits) {
   if (n == 0) return hipSuccess;
-  if (kw == 8)
-    hipLaunchKernelGGL((k_verify_q<BV_KW, BV_KNWIN>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre,
-                       kst, u12, key_table, nullptr, rg, status, bits);
-  else if (kw == 12)
-    hipLaunchKernelGGL((k_verify_q<BV_K12W, BV_K12NWIN>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be,
-                       pre, kst, u12, key_table, nullptr, rg, status, bits);
-  else
-    hipLaunchKernelGGL((k_verify_q<BV_KCW, BV_KCNWIN>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be,
-                       pre, kst, u12, nullptr, key_tabs, rg, status, bits);
+  const bool lat = lat_variant(n);
+#define BV_LAUNCH_Q(W, NWIN, KT, KTABS)                                                                             \
+  if (lat)                                                                                                       \
+    hipLaunchKernelGGL((k_verify_q<W, NWIN, true>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, \
+                       kst, u12, KT, KTABS, rg, status, bits);                                                   \
+  else                                                                                                           \
+    hipLaunchKernelGGL((k_verify_q<W, NWIN, false>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be,     \
+                       pre, kst, u12, KT, KTABS, rg, status, bits);
+  if (kw == 8) {
+    BV_LAUNCH_Q(BV_KW, BV_KNWIN, key_table, nullptr)
+  } else if (kw == 12) {
+    BV_LAUNCH_Q(BV_K12W, BV_K12NWIN, key_table, nullptr)
+  } else {
+    BV_LAUNCH_Q(BV_KCW, BV_KCNWIN, nullptr, key_tabs)
+  }
+#undef BV_LAUNCH_Q
   return hipGetLastError();
 }
 
@@ -896,8 +923,12 @@ hipError_t verify_gq(hipStream_t st, uint64_t n, const uint32_t *item_key, const
                      const uint32_t *w, const uint32_t *g_table, const uint64_t *key_tabs, uint8_t *status,
                      uint64_t *bits) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_verify_gq, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, item_msg, dig,
-                     w, g_table, key_tabs, status, bits);
+  if (lat_variant(n))
+    hipLaunchKernelGGL(k_verify_gq<true>, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, item_msg,
+                       dig, w, g_table, key_tabs, status, bits);
+  else
+    hipLaunchKernelGGL(k_verify_gq<false>, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst,
+                       item_msg, dig, w, g_table, key_tabs, status, bits);
   return hipGetLastError();
 }
 
@@ -929,8 +960,12 @@ hipError_t verify_generic(hipStream_t st, uint64_t n, const uint32_t *item_key, 
                           const uint32_t *item_msg, const uint32_t *dig, const uint32_t *w, const uint32_t *g_table,
                           uint8_t *status, uint64_t *bits) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_verify_generic, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, kxy,
-                     item_msg, dig, w, g_table, status, bits);
+  if (lat_variant(n))
+    hipLaunchKernelGGL(k_verify_generic<true>, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst,
+                       kxy, item_msg, dig, w, g_table, status, bits);
+  else
+    hipLaunchKernelGGL(k_verify_generic<false>, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst,
+                       kxy, item_msg, dig, w, g_table, status, bits);
   return hipGetLastError();
 }
 

@@ -41,6 +41,37 @@ DEV void gej_double(gej &r, const gej &a) {
   fe_sub(r.Y, r.Y, t);
 }
 
+// The same doubling for latency-bound single-wave chains (k_table_bases):
+// dbl-2009-l's seven multiplies form three dependent levels,
+// {X^2, Y^2, Y Z} -> {B^2, (X + B)^2, E^2} -> E (D - X3), and each of the
+// first two runs as ONE interleaved asm program (field_asm.h, gen_zip), so
+// a lone wave issues from three independent streams instead of stalling on
+// every dependent instruction.  Same values as gej_double; r may alias a.
+DEV void gej_double_lat(gej &r, const gej &a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe A, B, YZ, C, t, E, F, D;
+  fe_sqr_sqr_mul_zip_asm(A, a.X, B, a.Y, YZ, a.Y, a.Z);
+  fe_add(t, a.X, B);
+  fe_dbl(E, A);
+  fe_add(E, E, A);
+  fe_sqr_sqr_sqr_zip_asm(C, B, t, t, F, E);
+  fe_sub(t, t, A);
+  fe_sub(t, t, C);
+  fe_dbl(D, t);
+  fe_dbl(r.Z, YZ);
+  fe_dbl(t, D);
+  fe_sub(r.X, F, t);
+  fe_sub(t, D, r.X);
+  fe_mul(r.Y, E, t);
+  fe_dbl(t, C);
+  fe_dbl(t, t);
+  fe_dbl(t, t);
+  fe_sub(r.Y, r.Y, t);
+#else
+  gej_double(r, a);
+#endif
+}
+
 // r += (x2, y2) (affine): 8M + 3S + 7 add/sub (madd with Z3 = Z1 H; fewer
 // additions and live temporaries than madd-2007-bl's 7M + 4S + 11, and on
 // gfx950 a multiply costs the same as a square).  `inf` is r's identity flag.
@@ -84,6 +115,62 @@ DEV void gej_add_ge(gej &r, bool &inf, const fe &x2, const fe &y2) {
   fe_mul(t, R, t);
   fe_mul(HHH, r.Y, HHH);
   fe_sub(r.Y, t, HHH);
+}
+
+// The same mixed addition for latency-bound launches (one or two waves per
+// SIMD: small batches, the table fills): its multiplies run as five levels
+// {Z1^2} -> {x2 Z1Z1, Z1 Z1Z1} -> {y2 t, H^2} -> {H HH, X1 HH, Z1 H, R^2} ->
+// {R (V - X3), Y1 HHH}, each level one interleaved asm program (field_asm.h
+// gen_zip).  Same values and exceptional cases as gej_add_ge.
+DEV void gej_add_ge_lat(gej &r, bool &inf, const fe &x2, const fe &y2) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (inf) {
+    r.X = x2;
+    r.Y = y2;
+    fe_set(r.Z, 1);
+    inf = false;
+    return;
+  }
+  fe Z1Z1, U2, S2, H, R, t, HH, HHH, V, Z3, RR;
+  fe_sqr(Z1Z1, r.Z);
+  fe_mul_mul_zip_asm(U2, x2, Z1Z1, t, r.Z, Z1Z1);
+  fe_sub(H, U2, r.X);
+  fe_mul_sqr_zip_asm(S2, y2, t, HH, H);
+  fe_sub(R, S2, r.Y);
+  if (fe_is_zero(H)) {
+    if (fe_is_zero(R)) {
+      gej d;
+      gej_double_lat(d, r);
+      r = d;
+    } else {
+      inf = true;
+    }
+    return;
+  }
+  fe_mul_mul_mul_sqr_zip_asm(HHH, H, HH, V, r.X, HH, Z3, r.Z, H, RR, R);
+  r.Z = Z3;
+  // X3 = R^2 - HHH - 2V;  Y3 = R (V - X3) - Y1 HHH
+  fe_sub(t, RR, HHH);
+  fe_sub(t, t, V);
+  fe_sub(r.X, t, V);
+  fe_sub(t, V, r.X);
+  fe_mul_mul_zip_asm(t, R, t, HHH, r.Y, HHH);
+  fe_sub(r.Y, t, HHH);
+#else
+  gej_add_ge(r, inf, x2, y2);
+#endif
+}
+
+// Point-op selection for kernels with a latency variant (LAT: zipped).
+template <bool LAT>
+DEV void gej_add_ge_sel(gej &r, bool &inf, const fe &x2, const fe &y2) {
+  if (LAT) gej_add_ge_lat(r, inf, x2, y2);
+  else gej_add_ge(r, inf, x2, y2);
+}
+template <bool LAT>
+DEV void gej_double_sel(gej &r, const gej &a) {
+  if (LAT) gej_double_lat(r, a);
+  else gej_double(r, a);
 }
 
 // r += b (both Jacobian), add-2007-bl with exceptional cases: 11M + 5S.

@@ -136,21 +136,9 @@ DEV void table_bases_one(uint32_t b, const uint32_t *bxy, uint32_t *bases_jac, i
     fe_store(out + 24 * j + 8, P.Y);
     fe_store(out + 24 * j + 16, P.Z);
     if (j + 1 < nwin) {
-      for (int k = 0; k < w; k++) gej_double(P, P);
+      for (int k = 0; k < w; k++) gej_double_lat(P, P);  // one wave per 64 keys: latency bound
     }
   }
-}
-
-DEV void jac_to_affine(fe &x, fe &y, const uint32_t *jac) {
-  fe X, Y, Z, zi, zi2, zi3;
-  fe_load(X, jac);
-  fe_load(Y, jac + 8);
-  fe_load(Z, jac + 16);
-  fe_inv_var(zi, Z);
-  fe_sqr(zi2, zi);
-  fe_mul(zi3, zi2, zi);
-  fe_mul(x, X, zi2);
-  fe_mul(y, Y, zi3);
 }
 
 // d * B (B affine), MSB-first double-and-add over `bits` bits of d.  The
@@ -161,8 +149,8 @@ DEV void table_point(gej &R, bool &inf, fe &Z, const fe &bx, const fe &by, uint3
   fe_set(R.Y, 0);
   fe_set(R.Z, 0);
   for (int bit = bits - 1; bit >= 0; bit--) {
-    if (!inf) gej_double(R, R);
-    if ((d >> bit) & 1) gej_add_ge(R, inf, bx, by);
+    if (!inf) gej_double_lat(R, R);  // few waves per SIMD in the fill kernels
+    if ((d >> bit) & 1) gej_add_ge_lat(R, inf, bx, by);
   }
   if (inf) fe_set(Z, 1);
   else Z = R.Z;
@@ -438,7 +426,7 @@ DEV bool final_check(const gej &R, bool inf, const fe &r) {
 // SIGNED digits in (-2^(W-1), 2^(W-1)] by carry recoding: T[j][|d|], y
 // negated for d < 0 (geometry.h).  u < N < 2^256 and W NWIN >= 257, so no
 // carry is left after the top window.
-template <int W, int NWIN>
+template <int W, int NWIN, bool LAT = false>
 DEV void g_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t u[8]) {
   constexpr uint32_t ENT = 1u << (W - 1);
   static_assert(W * NWIN >= 257 && W < 32, "signed G windows must absorb the last carry");
@@ -457,7 +445,7 @@ DEV void g_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t u[8]) {
       fe_load4(x, e);
       fe_load4(y, e + 8);
       if (dneg) fe_neg(y, y);
-      gej_add_ge(R, inf, x, y);
+      gej_add_ge_sel<LAT>(R, inf, x, y);
     }
   }
 }
@@ -495,6 +483,7 @@ DEV void rg_load(const uint32_t *rg, uint64_t n, uint64_t i, gej &R, bool &inf) 
 
 // Phase 1 (overlaps the key-table build): R_G = u1 G for items that reach
 // the math.
+template <bool LAT = false>
 DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
                        const uint8_t *pre, const uint8_t *kstatus, const uint32_t *item_msg,
                        const uint32_t *digest_words, const uint32_t *w_in, uint32_t *u12, const uint32_t *g_table,
@@ -512,7 +501,7 @@ DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const u
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
   fe_set(R.Z, 0);
-  g_table_add<BV_GW, BV_GNWIN>(R, inf, g_table, u);
+  g_table_add<BV_GW, BV_GNWIN, LAT>(R, inf, g_table, u);
   rg_store(rg, n, i, R, inf);
 }
 
@@ -523,7 +512,7 @@ DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const u
 // and W NWIN >= 129 bits, so no carry is left after the top window.
 // `phi`: the table holds T (the k1 half) and this half needs phi(T) =
 // (beta x, y): one multiply per lookup instead of a stored phi half (KC).
-template <int W, int NWIN, bool SIGNED>
+template <int W, int NWIN, bool SIGNED, bool LAT = false>
 DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bool neg, bool phi = false) {
   constexpr uint32_t ENT = SIGNED ? (1u << (W - 1)) : (1u << W);
   static_assert(!SIGNED || W * NWIN >= 129, "signed windows must absorb the last carry");
@@ -554,7 +543,7 @@ DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bo
         fe_mul(x, x, beta);
       }
       if (dneg) fe_neg(y, y);
-      gej_add_ge(R, inf, x, y);
+      gej_add_ge_sel<LAT>(R, inf, x, y);
     }
   }
   if (neg) fe_neg(R.Y, R.Y);
@@ -564,7 +553,7 @@ DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bo
 // final check -> status.
 // key_tabs != null (key cache): per-batch-key table base addresses, else
 // the tables are contiguous in key_table (per-batch K8 / K12 build).
-template <int W, int NWIN>
+template <int W, int NWIN, bool LAT = false>
 DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
                           const uint32_t *s_be, const uint8_t *pre, const uint8_t *kstatus, const uint32_t *u12,
                           const uint32_t *key_table, const uint64_t *key_tabs, const uint32_t *rg) {
@@ -591,7 +580,7 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
     uint32_t kk[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) kk[c] = h ? k2[c] : k1[c];
-    key_table_add<W, NWIN, SIGNED>(R, inf, tab + (h && !KC ? half : 0), kk, (signs >> h) & 1u, KC && h);
+    key_table_add<W, NWIN, SIGNED, LAT>(R, inf, tab + (h && !KC ? half : 0), kk, (signs >> h) & 1u, KC && h);
   }
   fe_load_be_words(r, r_be + 8 * i);  // reloaded: not kept live through the loop
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
@@ -601,6 +590,7 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
 // the G table and the key's cached table, R_G kept in registers (no HBM
 // round trip of R_G / u12 between two kernels, no kernel boundary).  Same
 // decisions as verify_item_g followed by verify_item_q.
+template <bool LAT = false>
 DEV uint8_t verify_item_gq_kc(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
                               const uint8_t *pre, const uint8_t *kstatus, const uint32_t *item_msg,
                               const uint32_t *digest_words, const uint32_t *w_in, const uint32_t *g_table,
@@ -615,14 +605,14 @@ DEV uint8_t verify_item_gq_kc(uint64_t i, const uint32_t *item_key, const uint32
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
   fe_set(R.Z, 0);
-  g_table_add<BV_GW, BV_GNWIN>(R, inf, g_table, u);
+  g_table_add<BV_GW, BV_GNWIN, LAT>(R, inf, g_table, u);
   const uint32_t *tab = (const uint32_t *)key_tabs[item_key[i]];
 #pragma unroll 1
   for (int h = 0; h < 2; h++) {
     uint32_t kk[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) kk[c] = h ? k2[c] : k1[c];
-    key_table_add<BV_KCW, BV_KCNWIN, true>(R, inf, tab, kk, (signs >> h) & 1u, h != 0);
+    key_table_add<BV_KCW, BV_KCNWIN, true, LAT>(R, inf, tab, kk, (signs >> h) & 1u, h != 0);
   }
   fe_load_be_words(r, r_be + 8 * i);
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
@@ -630,6 +620,7 @@ DEV uint8_t verify_item_gq_kc(uint64_t i, const uint32_t *item_key, const uint32
 
 // One signature item without a key table: k1 Q + k2 phi(Q) by a joint
 // (Strauss-Shamir) per-lane double-and-add over the 128-bit GLV halves.
+template <bool LAT = false>
 DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
                                 const uint8_t *pre, const uint8_t *kstatus, const uint32_t *kxy,
                                 const uint32_t *item_msg, const uint32_t *digest_words, const uint32_t *w_in,
@@ -654,10 +645,10 @@ DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint
   fe_set(R.Y, 0);
   fe_set(R.Z, 0);
   for (int bit = 127; bit >= 0; bit--) {
-    if (!inf) gej_double(R, R);
-    if ((k1[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge(R, inf, q1x, q1y);
-    if ((k2[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge(R, inf, q2x, q2y);
+    if (!inf) gej_double_sel<LAT>(R, R);
+    if ((k1[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge_sel<LAT>(R, inf, q1x, q1y);
+    if ((k2[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge_sel<LAT>(R, inf, q2x, q2y);
   }
-  g_table_add<BV_GW, BV_GNWIN>(R, inf, g_table, u1);
+  g_table_add<BV_GW, BV_GNWIN, LAT>(R, inf, g_table, u1);
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
 }

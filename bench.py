@@ -21,7 +21,7 @@ Rank 0 prints one JSON line.  `value` is the headline above.  Beside it:
   * `host_entry` — bv_verify_batch from host (pageable) buffers, what a cgo
     caller sees: pinned staging, PCIe, kernels and copy-out in the timing;
   * `latency_ms` — bv_verify_batch at 1 / 100 / 1000 (SyncLimit,
-    config.go:44) / 10^4 events, cold (no cache) and warm (key cache);
+    config.go:44) / 10^4 / 10^5 events, cold (no cache) and warm (key cache);
   * `cpu_baseline` — the faster of two CPU legs on this host's cores, each on
     a bounded sample of the same batch: the C oracle (oracle/oracle.c, a
     restatement of the Go path) and the OpenSSL libcrypto proxy of SURVEY
@@ -347,6 +347,15 @@ def warm_leg(args, dev, world, dist, local, step_with):
     return out
 
 
+def host_breakdown(ts):
+    """Where a host-entry call's time goes (bv_timing): the library call's
+    wall clock, its host prep (validation + staging copies until the last
+    H2D is queued), the device span of the kernels, the result copy-out."""
+    return {"lib_call": mean(ts, "ms_host"), "host_prep": mean(ts, "ms_host_prep"),
+            "device_kernels": mean(ts, "ms_total"), "d2h_tail": mean(ts, "ms_d2h"),
+            "host_out": mean(ts, "ms_host_out")}
+
+
 def host_entry_leg(args, v, batch):
     """bv_verify_batch from pageable host buffers (the cgo entry point)."""
     msgs = batch.msg_bytes.nbytes
@@ -361,7 +370,8 @@ def host_entry_leg(args, v, batch):
     elapsed = time.perf_counter() - t0
     h2d = mean(ts, "ms_h2d")
     return {"value": args.events * reps / elapsed, "unit": "verifies/s", "ms_per_call": elapsed / reps * 1e3,
-            "ms_h2d": h2d, "ms_d2h_tail": mean(ts, "ms_d2h"), "bytes_staged": staged,
+            "ms_h2d": h2d, "ms_d2h_tail": mean(ts, "ms_d2h"), "host_breakdown_ms": host_breakdown(ts),
+            "bytes_staged": staged,
             "pcie_gb_s": staged / (h2d * 1e-3) / 1e9 if h2d > 0 else None,
             "note": "inputs in pageable host memory; staged through pinned chunks, hashing overlaps the transfer; "
                     "PCIe-bound (~520 B per event crosses the link)"}
@@ -396,6 +406,7 @@ def events_entry_leg(args):
     tm = v.timing()
     wb = E.wire_bytes(wire)
     out["bulk"] = {"value": args.events / el, "unit": "verifies/s", "ms_per_call": el * 1e3, "ms_h2d": tm["ms_h2d"],
+                   "host_breakdown_ms": host_breakdown([tm]),
                    "bytes_staged": wb, "bytes_per_event": wb / args.events,
                    "pcie_gb_s": wb / (tm["ms_h2d"] * 1e-3) / 1e9 if tm["ms_h2d"] > 0 else None}
     v.close()
@@ -424,7 +435,7 @@ def latency_leg(args):
     out = {}
     vc = Verifier(device=int(os.environ.get("LOCAL_RANK", "0")), flags=native.F_KEY_CACHE)
     v0 = Verifier(device=int(os.environ.get("LOCAL_RANK", "0")))
-    for n in (1, 100, 1000, 10_000):
+    for n in (1, 100, 1000, 10_000, 100_000):
         b = synth.events(n, n_creators=min(4, n), seed=900 + n)
         row = {}
         for name, ver in (("cold", v0), ("warm_key_cache", vc)):

@@ -38,14 +38,20 @@ void emu_fill(uint32_t n_bases, const uint8_t *bstatus, const uint32_t *bases, i
     const uint32_t jc = (uint32_t)(task % ((uint64_t)nwin * chunks));
     const uint32_t j = jc / chunks, c = jc % chunks;
     if (bstatus && bstatus[b] != KS_OK) return;
-    fe bx, by;
-    jac_to_affine(bx, by, bases + ((uint64_t)b * nwin + j) * 24);
+    // as the kernel: the Jacobian base's (X, Y) on the isomorphic curve
+    // y^2 = x^3 + 7 Z^6, entries' Z scaled by the base's Z
+    fe bx, by, bz;
+    const uint32_t *bj = bases + ((uint64_t)b * nwin + j) * 24;
+    fe_load(bx, bj);
+    fe_load(by, bj + 8);
+    fe_load(bz, bj + 16);
     std::vector<gej> R(block);
     std::vector<fe> Z(block), pre(block), suf(block);
     std::vector<char> inf(block);
     for (uint32_t t = 0; t < block; t++) {
       bool f;
       table_point(R[t], f, Z[t], bx, by, c * block + t, w);
+      if (!f) fe_mul(Z[t], Z[t], bz);
       inf[t] = f;
     }
     pre[0] = Z[0];

@@ -9,7 +9,10 @@
 #include <stdint.h>
 #include "../../babble_amd/csrc/field.h"
 
-enum { OP_MUL = 0, OP_SQR = 1, OP_ADD = 2, OP_SUB = 3, OP_MONT = 4, OP_INV = 5 };
+// OP_ZSSM + k: component k of the zipped (x^2, y^2, x y) program;
+// OP_ZSSS + k: component k of the zipped (x^2, y^2, (x ^ y)^2) program
+// (field_asm.h gen_zip, used by the key-table doubling chain).
+enum { OP_MUL = 0, OP_SQR = 1, OP_ADD = 2, OP_SUB = 3, OP_MONT = 4, OP_INV = 5, OP_ZSSM = 6, OP_ZSSS = 9, OP_LAST = 11 };
 
 __global__ void __launch_bounds__(256) k_field(int op, uint32_t n, const uint32_t *__restrict__ a,
                                                const uint32_t *__restrict__ b, uint32_t *__restrict__ r) {
@@ -35,7 +38,18 @@ __global__ void __launch_bounds__(256) k_field(int op, uint32_t n, const uint32_
       for (int k = 0; k < 8; k++) z.v[k] = s.v[k];
       break;
     }
-    default: fe_inv_var(z, x); break;
+    case OP_INV: fe_inv_var(z, x); break;
+    default: {
+      fe w, o[3];
+#pragma unroll
+      for (int k = 0; k < 8; k++) w.v[k] = x.v[k] ^ y.v[k];
+#if defined(__HIP_DEVICE_COMPILE__)
+      if (op < OP_ZSSS) fe_sqr_sqr_mul_zip_asm(o[0], x, o[1], y, o[2], x, y);
+      else fe_sqr_sqr_sqr_zip_asm(o[0], x, o[1], y, o[2], w);
+#endif
+      z = o[(op - OP_ZSSM) % 3];
+      break;
+    }
   }
 #pragma unroll
   for (int k = 0; k < 8; k++) r[8 * (uint64_t)i + k] = z.v[k];
@@ -44,7 +58,7 @@ __global__ void __launch_bounds__(256) k_field(int op, uint32_t n, const uint32_
 // Host entry: n operand pairs (8 little-endian u32 limbs each).  Returns 0,
 // or a negative HIP error code.  Synchronous.
 extern "C" int fc_run(int op, uint32_t n, const uint32_t *a, const uint32_t *b, uint32_t *r) {
-  if (op < OP_MUL || op > OP_INV) return -1000;
+  if (op < OP_MUL || op > OP_LAST) return -1000;
   uint32_t *da = nullptr, *db = nullptr, *dr = nullptr;
   const size_t bytes = (size_t)n * 32;
   hipError_t e = hipMalloc(&da, bytes ? bytes : 32);

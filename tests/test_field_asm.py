@@ -78,3 +78,32 @@ def test_header_is_fresh():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_field_asm.py"), "--check"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.parametrize("kinds", G.ZIP_COMBOS, ids=lambda k: "_".join(k))
+@pytest.mark.parametrize("force_slow", [False, True])
+def test_zipped_programs_match_python_ints(kinds, force_slow):
+    """The interleaved multi-product programs (gen_zip) of the key-table
+    doubling chain: every component equals its own product mod p."""
+    g = G.build(G.zip_name(kinds))
+    G.check_hazards(g)
+    rng = random.Random(7)
+    for trial in range(150):
+        m = G.Machine()
+        want = []
+        for k, kind in enumerate(kinds):
+            a, b = rng.getrandbits(256), rng.getrandbits(256)
+            if trial < 50:
+                a = 2**256 - 1 - rng.getrandbits(rng.choice([1, 8, 64]))
+                b = 2**256 - 1 - rng.getrandbits(rng.choice([1, 3, 40]))
+            if kind == "sqr":
+                b = a
+            for i in range(8):
+                m.r[f"%[z{k}a{i}]"] = (a >> (32 * i)) & G.M32
+                if kind == "mul":
+                    m.r[f"%[z{k}b{i}]"] = (b >> (32 * i)) & G.M32
+            want.append(a * b)
+        m.run(g, force_slow)
+        for k in range(len(kinds)):
+            r = sum(m.r[f"%[z{k}r{i}]"] << (32 * i) for i in range(8))
+            assert r < 2**256 and (r - want[k]) % P == 0, (kinds, k)

@@ -17,7 +17,8 @@ LIB = os.path.join(ROOT, "tests", "fieldcheck", "libfieldcheck.so")
 P = 2**256 - 2**32 - 977
 N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 M32 = 2**32 - 1
-OPS = {"mul": 0, "sqr": 1, "add": 2, "sub": 3, "mont": 4, "inv": 5}
+OPS = {"mul": 0, "sqr": 1, "add": 2, "sub": 3, "mont": 4, "inv": 5,
+       "zssm0": 6, "zssm1": 7, "zssm2": 8, "zsss0": 9, "zsss1": 10, "zsss2": 11}
 
 pytestmark = pytest.mark.gpu
 
@@ -25,6 +26,8 @@ pytestmark = pytest.mark.gpu
 def _lib():
     if not os.path.exists(LIB):
         pytest.fail("tests/fieldcheck/libfieldcheck.so missing: run __graft_entry__.build()")
+    import torch  # noqa: F401  (bind the same HIP runtime torch uses, as babble_amd.native does)
+
     L = ctypes.CDLL(LIB)
     L.fc_run.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     L.fc_run.restype = ctypes.c_int
@@ -115,3 +118,21 @@ def test_fe_inv_var_matches_python_ints():
     r = _run("inv", a, a)
     bad = [(hex(x), hex(z)) for x, z in zip(a, r) if (z * x - 1) % P]
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("combo", ["zssm", "zsss"])
+def test_zipped_programs_match_python_ints(combo):
+    """The interleaved multi-product programs of the key-table doubling chain
+    (gen_zip: fe_sqr_sqr_mul_zip / fe_sqr_sqr_sqr_zip), every component, on
+    operands that also drive each program's rare blocks."""
+    a, b = _pairs(3000, 41)
+    rng = random.Random(43)
+    for _ in range(1500):  # near-2^256 limbs: fold carry-outs in all three programs at once
+        a.append(2**256 - 1 - rng.getrandbits(rng.choice([1, 4, 12, 33, 70])))
+        b.append(2**256 - 1 - rng.getrandbits(rng.choice([1, 4, 12, 33, 70])))
+    want = {"zssm": [lambda x, y: x * x, lambda x, y: y * y, lambda x, y: x * y],
+            "zsss": [lambda x, y: x * x, lambda x, y: y * y, lambda x, y: (x ^ y) ** 2]}[combo]
+    for k in range(3):
+        r = _run(f"{combo}{k}", a, b)
+        bad = [(hex(x), hex(y), hex(z)) for x, y, z in zip(a, b, r) if z >= 2**256 or (z - want[k](x, y)) % P]
+        assert not bad, (k, bad[:5])

@@ -33,6 +33,7 @@ inserted only when nothing else can issue.  The scheduled list is both
 from __future__ import annotations
 
 import os
+import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -153,7 +154,8 @@ def halves(x) -> list[str]:
 
 
 def is_sgpr(x) -> bool:
-    return isinstance(x, str) and x.startswith("%[c")
+    """SGPR lane masks: %[cN] (and %[zKcN] in zipped programs)."""
+    return isinstance(x, str) and re.fullmatch(r"%\[(z\d+)?c\d+\]", x) is not None
 
 
 def reads(ins) -> list[str]:
@@ -671,7 +673,90 @@ def gen_mont(base: int = MONT_BASE) -> Prog:
 PROGRAMS = {"fe_mul": gen_mul, "fe_sqr": gen_sqr, "fe_add": gen_add, "fe_sub": gen_sub, "sc_mont": gen_mont}
 
 
+# ---------------------------------------------------------------------------
+# zipped programs: K independent multiplies in one asm block (latency-bound
+# single-wave chains: the per-key doubling chain of k_table_bases)
+# ---------------------------------------------------------------------------
+# A lone wave issues a dependent VALU instruction only every ~2x its issue
+# cost (tools/ubench_lat.hip); the serial doubling chain of the key-table
+# bases runs one wave per 64 keys, so it is latency bound.  Interleaving the
+# independent multiplies of one doubling (dbl-2009-l: {X^2, Y^2, Y Z} then
+# {B^2, (X+B)^2, E^2}) fills those slots: each program keeps its own
+# physical temporaries (v[34 k, 34 k + 34)) and carry SGPRs.  The mixed
+# addition's eleven multiplies form five levels the same way
+# ({Z^2} -> {x Z1Z1, Z Z1Z1} -> {y t, H^2} -> {H HH, X HH, Z H, R^2} ->
+# {R (V - X3), Y HHH}): the verify kernels' latency variant (small batches,
+# one or two waves per SIMD) uses them.
+ZIP_KINDS = {"mul": gen_mul, "sqr": gen_sqr}
+ZIP_COMBOS = [("sqr", "sqr", "mul"), ("sqr", "sqr", "sqr"),      # gej_double_lat
+              ("mul", "mul"), ("mul", "sqr"), ("mul", "mul", "mul", "sqr")]  # gej_add_ge_lat
+
+
+def _rename(g: Prog, f) -> Prog:
+    """Copy of g with every asm operand name passed through f; the tail
+    block becomes a trailing mid-program slow block (same semantics: run iff
+    some lane's mask bit is set, a no-op for the other lanes)."""
+    def op(x):
+        return f(x) if isinstance(x, str) and x.startswith("%[") else x
+
+    out = Prog(g.name)
+    for x in g.ins:
+        if x[0] == "slow":
+            out.ins.append(("slow", op(x[1]), _rename(x[2], f)))
+        else:
+            out.ins.append(tuple([x[0]] + [op(y) for y in x[1:]]))
+    if g.slow is not None:
+        out.ins.append(("slow", op(g.slow[0]), _rename(g.slow[1], f)))
+    return out
+
+
+def _segments(g: Prog) -> list[tuple[list, tuple | None]]:
+    segs, cur = [], []
+    for x in g.ins:
+        if x[0] == "slow":
+            segs.append((cur, (x[1], x[2])))
+            cur = []
+        else:
+            cur.append(x)
+    segs.append((cur, None))
+    return segs
+
+
+def zip_name(kinds) -> str:
+    return "fe_" + "_".join(kinds) + "_zip"
+
+
+def gen_zip(kinds) -> Prog:
+    """Programs kinds[k] over operands %[z{k}a*], %[z{k}b*] -> %[z{k}r*],
+    carries %[z{k}c*], temporaries v[34 k, 34 k + 34); the instruction
+    streams are merged segment by segment in proportion to their lengths
+    (the list scheduler keeps that order where dependences allow) and each
+    program's rare blocks follow its segment."""
+    progs = []
+    for k, kind in enumerate(kinds):
+        g = ZIP_KINDS[kind](base=MUL_NREGS * k)
+        progs.append(_rename(g, lambda x, k=k: f"%[z{k}{x[2:]}"))
+    segs = [_segments(p) for p in progs]
+    out = Prog(zip_name(kinds))
+    for si in range(max(len(s) for s in segs)):
+        keyed = []
+        for k, s in enumerate(segs):
+            part = s[si][0] if si < len(s) else []
+            keyed += [((j + 0.5) / len(part), k, x) for j, x in enumerate(part)]
+        keyed.sort(key=lambda t: (t[0], t[1]))
+        out.ins += [x for _, _, x in keyed]
+        for s in segs:
+            if si < len(s) and s[si][1] is not None:
+                out.ins.append(("slow",) + s[si][1])
+    return out
+
+
 def build(name: str) -> Prog:
+    for kinds in ZIP_COMBOS:
+        if name == zip_name(kinds):
+            g = schedule(gen_zip(kinds))
+            check_hazards(g)
+            return g
     g = schedule(PROGRAMS[name]())
     check_hazards(g)
     return g
@@ -762,6 +847,31 @@ def stats(g: Prog) -> dict:
     return out
 
 
+def zip_wrapper(kinds) -> str:
+    """C++ wrapper of a zipped program: fe_<kinds>_zip_asm(r0, a0[, b0], r1, ...)."""
+    g = build(zip_name(kinds))
+    params, outs, ins, cys = [], [], [], []
+    for k, kind in enumerate(kinds):
+        params.append(f"fe &r{k}, const fe &a{k}" + (f", const fe &b{k}" if kind == "mul" else ""))
+        outs += [f'[z{k}r{i}] "=&v"(r{k}.v[{i}])' for i in range(8)]
+        outs += [f'[z{k}c{i}] "=&s"(c{k}_{i})' for i in range(NCARRY)]
+        cys += [f"c{k}_{i}" for i in range(NCARRY)]
+        ins += [f'[z{k}a{i}] "v"(a{k}.v[{i}])' for i in range(8)]
+        if kind == "mul":
+            ins += [f'[z{k}b{i}] "v"(b{k}.v[{i}])' for i in range(8)]
+    clob = ", ".join(f'"v{i}"' for i in range(MUL_NREGS * len(kinds)))
+    return f"""// {", ".join(kinds)} interleaved (independent operands): {stats(g)}
+__device__ __forceinline__ void {zip_name(kinds)}_asm({", ".join(params)}) {{
+  uint64_t {", ".join(cys)};
+  asm volatile(
+{asm_body(g)}
+      : {", ".join(outs)}
+      : {", ".join(ins)}
+      : {clob}, "scc");
+}}
+"""
+
+
 def header() -> str:
     mul = build("fe_mul")
     sqr = build("fe_sqr")
@@ -848,7 +958,10 @@ __device__ __forceinline__ void sc_mont_asm(sc &r, const sc &a, const sc &b) {{
       : {a_in}, {b_in}, {n_in}, {nc_in}, [ninv] "v"({hex(NINV)}u)
       : {clob_m});
 }}
-"""
+
+// ---- zipped multiplies for latency-bound single-wave chains (gen_zip) ----
+// Temporaries: v0..v{MUL_NREGS}*K - 1 (clobbered).
+{"".join(zip_wrapper(k) for k in ZIP_COMBOS)}"""
 
 
 def main():
