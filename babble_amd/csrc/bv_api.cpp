@@ -432,12 +432,12 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
 // arrays prepared by kc_prepare.  Every call starts after the previous call
 // on this ctx has finished on the device (ev_done), whatever its stream:
 // work buffers are shared between calls.
-// Phase A of a verify (needs only the keys, s and pre in HBM): batched s^-1
-// on the s^-1 stream, key decode + per-batch key tables on the keys stream,
-// both after `ready` (an event recorded once those arrays are in HBM).  The
-// host entry points call it as soon as the small arrays have landed, so the
-// key tables build while the message bytes still cross PCIe.
-int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t ready, bool kc) {
+// Phase A of a verify: batched s^-1 on the s^-1 stream after `s_ready` (s
+// and pre in HBM), key decode + per-batch key tables on the keys stream after
+// `keys_ready` (the keys in HBM).  The host entry points stage the keys
+// first, then s and pre, so the key tables build while the rest of the batch
+// still crosses PCIe.
+int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_t s_ready, bool kc) {
   const uint64_t n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
   if (n_items > 0 && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be))
@@ -477,7 +477,7 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t ready, bool kc) {
   }
   hipEvent_t *ev = ctx->ev;
   // s^-1 needs only s: concurrent with everything up to k_verify_g
-  HIPCHK(hipStreamWaitEvent(ctx->sstream, ready, 0), BV_E_LAUNCH, "fork");
+  HIPCHK(hipStreamWaitEvent(ctx->sstream, s_ready, 0), BV_E_LAUNCH, "fork");
   HIPCHK(hipEventRecord(ev[E_START], ctx->sstream), BV_E_LAUNCH, "event");
   // items per lane: kPrepM amortises the inversion in large batches; a small
   // batch spreads over ~64k lanes instead, since there the serial chain of
@@ -486,7 +486,7 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t ready, bool kc) {
   HIPCHK(bvk::sinv(ctx->sstream, n_items, M, (const uint32_t *)b->s_be, b->pre, ctx->scratch.as<uint32_t>()),
          BV_E_LAUNCH, "k_sinv");
   HIPCHK(hipEventRecord(ev[E_SINV], ctx->sstream), BV_E_LAUNCH, "event");
-  HIPCHK(hipStreamWaitEvent(ctx->kstream, ready, 0), BV_E_LAUNCH, "fork");
+  HIPCHK(hipStreamWaitEvent(ctx->kstream, keys_ready, 0), BV_E_LAUNCH, "fork");
   if (!kc) {
     HIPCHK(bvk::key_decode(ctx->kstream, n_keys, b->key_bytes, b->key_off, ctx->kstatus.as<uint8_t>(),
                            ctx->kxy.as<uint32_t>()),
@@ -501,67 +501,123 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t ready, bool kc) {
   return BV_OK;
 }
 
+// Output buffers of a verify: the caller's device buffers when given (and
+// usable), else the ctx's own.
+int bv_out_bufs(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
+                bool hashed, bv_out *o) {
+  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
+  o->dig = (uint32_t *)d_msg_hash;
+  if (hashed || !o->dig || ((uintptr_t)o->dig & 15)) {
+    HIPCHK(ctx->digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
+    o->dig = ctx->digests.as<uint32_t>();
+  }
+  o->status = d_status;
+  if (!o->status) {
+    HIPCHK(ctx->status.ensure(std::max<uint64_t>(n_items, 1)), BV_E_OOM, "alloc status");
+    o->status = ctx->status.as<uint8_t>();
+  }
+  o->bits = d_bits;
+  if (!o->bits) {
+    HIPCHK(ctx->bits.ensure(std::max<uint64_t>((n_items + 63) / 64, 1) * 8), BV_E_OOM, "alloc bits");
+    o->bits = ctx->bits.as<uint64_t>();
+  }
+  return BV_OK;
+}
+
+// The verify kernels for items [lo, hi) (lo a multiple of 64) on `st`, after
+// bv_run_keys; the caller orders `st` after s^-1 (E_SINV) and, for part 2,
+// the key tables (E_KEYS).  part 1: k_verify_g (per-batch tables only: it
+// needs no key table); part 2: the rest (k_verify_q, the fused key-cache
+// kernel or the generic path) with statuses and bits.
+int bv_launch_items(bv_ctx *ctx, const bv_batch *b, const bv_out &o, hipStream_t st, bool kc, uint64_t lo,
+                    uint64_t hi, int part) {
+  const uint64_t n = b->n_items;
+  const uint8_t *kst = kc ? ctx->kc_kst.as<uint8_t>() : ctx->kstatus.as<uint8_t>();
+  const uint32_t *r32 = (const uint32_t *)b->r_be, *s32 = (const uint32_t *)b->s_be;
+  uint32_t *w = ctx->scratch.as<uint32_t>(), *u12 = ctx->u12.as<uint32_t>();
+  const bool fused = kc && kFusedKc;  // key cache: G and Q parts in one kernel (R_G stays in registers)
+  if (part == 1) {
+    if (ctx->table_mode && !fused)
+      HIPCHK(bvk::verify_g(st, n, lo, hi, b->item_key, r32, s32, b->pre, kst, b->item_msg, o.dig, w, u12,
+                           ctx->g_table, ctx->rg.as<uint32_t>()),
+             BV_E_LAUNCH, "k_verify_g");
+    return BV_OK;
+  }
+  if (fused)
+    HIPCHK(bvk::verify_gq(st, n, lo, hi, b->item_key, r32, s32, b->pre, kst, b->item_msg, o.dig, w, ctx->g_table,
+                          ctx->kc_tabs.as<uint64_t>(), o.status, o.bits),
+           BV_E_LAUNCH, "k_verify_gq");
+  else if (ctx->table_mode)
+    HIPCHK(bvk::verify_q(st, ctx->key_w, n, lo, hi, b->item_key, r32, s32, b->pre, kst, u12,
+                         ctx->key_table.as<uint32_t>(), kc ? ctx->kc_tabs.as<uint64_t>() : nullptr,
+                         ctx->rg.as<uint32_t>(), o.status, o.bits),
+           BV_E_LAUNCH, "k_verify_q");
+  else
+    HIPCHK(bvk::verify_generic(st, n, lo, hi, b->item_key, r32, s32, b->pre, kst, ctx->kxy.as<uint32_t>(),
+                               b->item_msg, o.dig, w, ctx->g_table, o.status, o.bits),
+           BV_E_LAUNCH, "k_verify_generic");
+  return BV_OK;
+}
+
+int bv_item_pipe::upto(uint64_t end) {
+  if (end <= done) return BV_OK;
+  if (done == 0) {
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SINV], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipEventRecord(ctx->ev[E_SCALAR], st), BV_E_LAUNCH, "event");
+    HIPCHK(hipEventRecord(ctx->ev[E_G], st), BV_E_LAUNCH, "event");
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_KEYS], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipEventRecord(ctx->ev[E_JOINED], st), BV_E_LAUNCH, "event");
+  }
+  for (int part = 1; part <= 2; part++) {
+    const int r = bv_launch_items(ctx, b, o, st, kc, done, end, part);
+    if (r != BV_OK) return r;
+  }
+  done = end;
+  return BV_OK;
+}
+
+int bv_item_pipe::finish() {
+  const uint64_t n = b->n_items;
+  if (n == 0) {
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SINV], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_KEYS], 0), BV_E_LAUNCH, "join");
+    for (int e : {E_SCALAR, E_G, E_JOINED}) HIPCHK(hipEventRecord(ctx->ev[e], st), BV_E_LAUNCH, "event");
+  }
+  const int r = upto(n);
+  if (r != BV_OK) return r;
+  HIPCHK(hipEventRecord(ctx->ev[E_END], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
+  ctx->has_done = true;
+  return BV_OK;
+}
+
 // Phase B on `st` (after bv_run_keys): SHA-256 of the messages (unless
 // `hashed`: digests already in ctx->digests), then the verify kernels once
-// s^-1 and the key tables are ready; statuses and bits.
+// s^-1 and the key tables are ready; statuses and bits.  k_verify_g needs
+// no key table, so it runs while the keys stream still builds them.
 int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc) {
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   if (n_msgs > 0 && !b->msg_off) return bv_fail(ctx, BV_E_ARGS, "null msg_off");
-  uint32_t *dig = (uint32_t *)d_msg_hash;
-  if (hashed || !dig || ((uintptr_t)dig & 15)) {
-    HIPCHK(ctx->digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
-    dig = ctx->digests.as<uint32_t>();
-  }
-  uint8_t *status = d_status;
-  if (!status) {
-    HIPCHK(ctx->status.ensure(std::max<uint64_t>(n_items, 1)), BV_E_OOM, "alloc status");
-    status = ctx->status.as<uint8_t>();
-  }
-  uint64_t *bits = d_bits;
-  if (!bits) {
-    HIPCHK(ctx->bits.ensure(std::max<uint64_t>((n_items + 63) / 64, 1) * 8), BV_E_OOM, "alloc bits");
-    bits = ctx->bits.as<uint64_t>();
-  }
-  const bool table_mode = ctx->table_mode;
-  const int key_w = ctx->key_w;
-  const uint8_t *kst = kc ? ctx->kc_kst.as<uint8_t>() : ctx->kstatus.as<uint8_t>();
+  bv_out o;
+  int rc = bv_out_bufs(ctx, b, d_msg_hash, d_status, d_bits, hashed, &o);
+  if (rc != BV_OK) return rc;
   hipEvent_t *ev = ctx->ev;
-  const uint32_t *r32 = (const uint32_t *)b->r_be, *s32 = (const uint32_t *)b->s_be;
-  uint32_t *w = ctx->scratch.as<uint32_t>(), *u12 = ctx->u12.as<uint32_t>();
   HIPCHK(hipEventRecord(ev[E_FORK], st), BV_E_LAUNCH, "event");
-  if (!hashed) HIPCHK(bvk::sha256(st, n_msgs, b->msg_bytes, b->msg_off, dig), BV_E_LAUNCH, "k_sha256");
+  if (!hashed) HIPCHK(bvk::sha256(st, n_msgs, b->msg_bytes, b->msg_off, o.dig), BV_E_LAUNCH, "k_sha256");
   HIPCHK(hipEventRecord(ev[E_SHA], st), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamWaitEvent(st, ev[E_SINV], 0), BV_E_LAUNCH, "join");
   HIPCHK(hipEventRecord(ev[E_SCALAR], st), BV_E_LAUNCH, "event");
-  if (kc && kFusedKc) {  // key cache: G and Q parts in one kernel (R_G stays in registers)
-    HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
-    HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
-    HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
-    HIPCHK(bvk::verify_gq(st, n_items, b->item_key, r32, s32, b->pre, kst, b->item_msg, dig, w, ctx->g_table,
-                          ctx->kc_tabs.as<uint64_t>(), status, bits),
-           BV_E_LAUNCH, "k_verify_gq");
-  } else if (table_mode) {
-    HIPCHK(bvk::verify_g(st, n_items, 0, n_items, b->item_key, r32, s32, b->pre, kst, b->item_msg, dig, w, u12,
-                         ctx->g_table, ctx->rg.as<uint32_t>()),
-           BV_E_LAUNCH, "k_verify_g");
-    HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
-    HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
-    HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
-    HIPCHK(bvk::verify_q(st, key_w, n_items, b->item_key, r32, s32, b->pre, kst, u12, ctx->key_table.as<uint32_t>(),
-                         kc ? ctx->kc_tabs.as<uint64_t>() : nullptr, ctx->rg.as<uint32_t>(), status, bits),
-           BV_E_LAUNCH, "k_verify_q");
-  } else {
-    HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
-    HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
-    HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
-    HIPCHK(bvk::verify_generic(st, n_items, b->item_key, r32, s32, b->pre, kst, ctx->kxy.as<uint32_t>(), b->item_msg,
-                               dig, w, ctx->g_table, status, bits),
-           BV_E_LAUNCH, "k_verify_generic");
-  }
+  rc = bv_launch_items(ctx, b, o, st, kc, 0, n_items, 1);
+  if (rc != BV_OK) return rc;
+  HIPCHK(hipEventRecord(ev[E_G], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
+  HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
+  rc = bv_launch_items(ctx, b, o, st, kc, 0, n_items, 2);
+  if (rc != BV_OK) return rc;
   HIPCHK(hipEventRecord(ev[E_END], st), BV_E_LAUNCH, "event");
-  if (d_msg_hash && (uint8_t *)dig != d_msg_hash)
-    HIPCHK(hipMemcpyAsync(d_msg_hash, dig, n_msgs * 32, hipMemcpyDeviceToDevice, st), BV_E_LAUNCH, "copy digests");
+  if (d_msg_hash && (uint8_t *)o.dig != d_msg_hash)
+    HIPCHK(hipMemcpyAsync(d_msg_hash, o.dig, n_msgs * 32, hipMemcpyDeviceToDevice, st), BV_E_LAUNCH, "copy digests");
   HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
   ctx->has_done = true;
   return BV_OK;
@@ -572,7 +628,7 @@ int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
                   hipStream_t st, bool hashed, bool kc) {
   if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order after previous call");
   HIPCHK(hipEventRecord(ctx->ev[E_READY], st), BV_E_LAUNCH, "event");
-  int rc = bv_run_keys(ctx, b, ctx->ev[E_READY], kc);
+  int rc = bv_run_keys(ctx, b, ctx->ev[E_READY], ctx->ev[E_READY], kc);
   if (rc != BV_OK) return rc;
   return bv_run_verify(ctx, b, d_msg_hash, d_status, d_bits, st, hashed, kc);
 }
@@ -708,14 +764,16 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
     segs[i] = {src, n, total};
     total += align256(n + pad);
   };
-  add(0, b->msg_off, n_msgs ? (n_msgs + 1) * 8 : 0, 0);
+  // staging order: the keys (the key tables start once they land), s and
+  // pre (s^-1), the other item arrays, then the message bytes
   add(1, b->key_off, n_keys ? (n_keys + 1) * 8ull : 0, 0);
   add(2, b->key_bytes, key_len, 64);
+  add(6, b->s_be, n_items * 32, 0);
+  add(7, b->pre, b->pre ? n_items : 0, 0);
+  add(0, b->msg_off, n_msgs ? (n_msgs + 1) * 8 : 0, 0);
   add(3, b->item_msg, n_items * 4, 0);
   add(4, b->item_key, n_items * 4, 0);
   add(5, b->r_be, n_items * 32, 0);
-  add(6, b->s_be, n_items * 32, 0);
-  add(7, b->pre, b->pre ? n_items : 0, 0);
   add(8, b->msg_bytes, msg_len, 64);
   // previous work on this ctx must be done before its staging is reused
   if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
@@ -732,16 +790,30 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
     ev_i++;
     return e;
   };
-  const size_t small_end = segs[8].off;
-  for (size_t a = 0; a < small_end; a += kChunk) {
-    const size_t z = std::min(small_end, a + kChunk);
-    for (int i = 0; i < 8; i++) {  // the parts of segments 0-7 inside [a, z)
-      const Seg &s = segs[i];
-      const size_t lo = std::max(a, s.off), hi = std::min(z, s.off + s.n);
-      if (lo < hi) ctx->pool->copy(pin + lo, (const uint8_t *)s.src + (lo - s.off), hi - lo);
+  // layout bytes [a0, a1) of segments 0-7, in kChunk pieces: the pool fills
+  // piece c+1 while the DMA engine moves piece c
+  auto stage = [&](size_t a0, size_t a1) -> int {
+    for (size_t a = a0; a < a1; a += kChunk) {
+      const size_t z = std::min(a1, a + kChunk);
+      std::vector<CopyPool::Piece> pieces;
+      for (int i = 0; i < 8; i++) {
+        const Seg &s = segs[i];
+        const size_t lo = std::max(a, s.off), hi = std::min(z, s.off + s.n);
+        if (lo < hi) pieces.push_back({pin + lo, (const uint8_t *)s.src + (lo - s.off), hi - lo});
+      }
+      ctx->pool->copy_many(pieces);
+      HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
     }
-    HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
-  }
+    return BV_OK;
+  };
+  rc = stage(0, segs[6].off);  // the keys
+  if (rc != BV_OK) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[E_KREADY], cs), BV_E_LAUNCH, "event");
+  rc = stage(segs[6].off, segs[0].off);  // s, pre
+  if (rc != BV_OK) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[E_SREADY], cs), BV_E_LAUNCH, "event");
+  rc = stage(segs[0].off, segs[8].off);  // msg_off, item_msg, item_key, r
+  if (rc != BV_OK) return rc;
   // zero the message-bytes pad in the staging (the SHA kernel over-reads
   // the last dword of a message into it)
   if (msg_len) memset(pin + segs[8].off + msg_len, 0, 64);
@@ -764,19 +836,31 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
   // key cache resolution needs the keys on the device (decode of misses)
   bool kc = false;
   if ((ctx->flags & BV_F_KEY_CACHE) && n_keys && n_keys <= kKcMaxBatchKeys) {
-    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SMALL], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_KREADY], 0), BV_E_LAUNCH, "join");
     rc = bv_kc_prepare(ctx, n_keys, b->key_bytes, b->key_off, d.key_bytes, d.key_off, st, &kc);
     if (rc != BV_OK) return rc;
   }
-  // s^-1 and the key tables need only the small arrays: they run while the
-  // message bytes below still cross PCIe
-  rc = bv_run_keys(ctx, &d, ctx->ev[E_SMALL], kc);
+  // the key tables need only the keys and s^-1 only s: they run while the
+  // rest of the batch still crosses PCIe
+  rc = bv_run_keys(ctx, &d, ctx->ev[E_KREADY], ctx->ev[E_SREADY], kc);
+  if (rc != BV_OK) return rc;
+
+  // Items in message order (item_msg non-decreasing: events, blocks) are
+  // verified chunk by chunk as their messages are hashed, so the verify
+  // kernels also run under the PCIe transfer; otherwise after the last chunk.
+  const bool in_order = ctx->pool->parallel_for(n_items > 0 ? n_items - 1 : 0, 1 << 17, [b](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; i++)
+      if (b->item_msg[i] > b->item_msg[i + 1]) return false;
+    return true;
+  });
+  bv_item_pipe pipe{ctx, &d, {}, st, kc};
+  rc = bv_out_bufs(ctx, &d, nullptr, nullptr, nullptr, true, &pipe.o);
   if (rc != BV_OK) return rc;
 
   // message bytes: chunks on message boundaries, each hashed once it lands
-  HIPCHK(ctx->digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
   if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order");
   HIPCHK(hipEventRecord(ctx->ev[E_HASH0], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->ev[E_FORK], st), BV_E_LAUNCH, "event");
   uint64_t m0 = 0;
   while (m0 < n_msgs) {
     // messages [m0, m1) holding about kChunk bytes (at least one message)
@@ -792,15 +876,23 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
     HIPCHK(hipEventRecord(e, cs), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, e, 0), BV_E_LAUNCH, "join chunk");
     if (m0 == 0) HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SMALL], 0), BV_E_LAUNCH, "join offsets");
-    HIPCHK(bvk::sha256(st, m1 - m0, d.msg_bytes, d.msg_off + m0, ctx->digests.as<uint32_t>() + 8 * m0), BV_E_LAUNCH,
-           "k_sha256");
+    HIPCHK(bvk::sha256(st, m1 - m0, d.msg_bytes, d.msg_off + m0, pipe.o.dig + 8 * m0), BV_E_LAUNCH, "k_sha256");
+    HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is the one used
+    if (in_order) {  // items up to the first one of a message >= m1, in whole 64-item words
+      const uint64_t i_end = m1 == n_msgs ? n_items
+                                          : (uint64_t)(std::lower_bound(b->item_msg, b->item_msg + n_items, m1) -
+                                                       b->item_msg) / 64 * 64;
+      rc = pipe.upto(i_end);
+      if (rc != BV_OK) return rc;
+    }
     m0 = m1;
   }
   HIPCHK(hipEventRecord(ctx->ev[E_STAGED], cs), BV_E_LAUNCH, "event");
   call->ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_STAGED], 0), BV_E_LAUNCH, "join staging");
-  HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
-  rc = bv_run_verify(ctx, &d, nullptr, nullptr, nullptr, st, true, kc);
+  HIPCHK(hipEventRecord(ctx->ev[E_SHA], st), BV_E_LAUNCH, "event");
+  if (n_msgs == 0) HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
+  rc = pipe.finish();
   if (rc != BV_OK) return rc;
 
   // results into pinned memory: digests as soon as hashing ended (overlaps

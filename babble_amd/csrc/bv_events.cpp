@@ -11,6 +11,7 @@
 // hashed bodies.  s^-1 and the key tables (bv_run_keys) start as soon as the
 // keys, r, s and pre (staged first) have landed.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "bv_internal.h"
@@ -26,7 +27,7 @@ namespace {
 
 constexpr uint32_t kNarrowLevel = 1024;  // events per level run by k_ev_hash_chain
 constexpr uint32_t kChainCap = 1024;     // events per k_ev_hash_chain launch (EVC_CAP)
-constexpr size_t kChunk = 16ull << 20;
+constexpr size_t kChunk = 16ull << 20;  // staged bytes per PCIe piece / event chunk
 
 int validate(bv_ctx *ctx, const bv_event_batch *b) {
   const uint64_t n = b->n_events;
@@ -122,44 +123,86 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   const uint64_t tx_len = n_tx ? eb->tx_off[n_tx] : 0;
   const uint64_t key_len = eb->key_off[eb->n_keys];
   const uint64_t itx_len = eb->itx_off ? eb->itx_off[n] : 0, bsig_len = eb->bsig_off ? eb->bsig_off[n] : 0;
+  // How a segment splits over an event chunk [e0, e1): ALL = whole, in the
+  // first part; EV = `unit` bytes per event; EV1 = an n + 1 offset array
+  // (elements e0 ..= e1); TX / TX1 = the same per transaction of the chunk's
+  // events; TXB / ITX / BSIG = the chunk's bytes of tx_bytes / itx_json /
+  // bsig_json.
+  enum Kind { ALL, EV, EV1, TX, TX1, TXB, ITX, BSIG };
   struct Seg {
     const void *src;
     size_t n, off;
+    Kind kind;
+    size_t unit;
   };
   std::vector<Seg> segs;
   size_t total = 0;
-  auto add = [&](const void *src, size_t bytes, size_t pad = 0) -> size_t {
-    segs.push_back({src, bytes, total});
+  auto add = [&](const void *src, size_t bytes, Kind kind, size_t unit = 1, size_t pad = 0) -> size_t {
+    segs.push_back({src, bytes, total, kind, unit});
     const size_t o = total;
     total += align256(bytes + pad);
     return o;
   };
-  // keys, r, s, pre and creators first: s^-1 and the key tables start once
-  // they have landed, while the rest of the batch still crosses PCIe
-  const size_t o_koff = add(eb->key_off, (eb->n_keys + 1) * 8ull);
-  const size_t o_kb = add(eb->key_bytes, key_len, 64);
-  const size_t o_r = add(eb->r_be, n * 32);
-  const size_t o_s = add(eb->s_be, n * 32);
-  const size_t o_pre = add(eb->pre, eb->pre ? n : 0);
-  const size_t o_cr = add(eb->creator, n * 4);
+  // keys first (the key tables start once they land), then s and pre (s^-1),
+  // r, creators and the parent hashes; the per-event fields follow chunk by
+  // chunk (each chunk's bodies are built, hashed and verified while the next
+  // one crosses PCIe)
+  const size_t o_koff = add(eb->key_off, (eb->n_keys + 1) * 8ull, ALL);
+  const size_t o_kb = add(eb->key_bytes, key_len, ALL, 1, 64);
+  const size_t keys_end = total;
+  const size_t o_s = add(eb->s_be, n * 32, ALL);
+  const size_t o_pre = add(eb->pre, eb->pre ? n : 0, ALL);
+  const size_t s_end = total;
+  const size_t o_r = add(eb->r_be, n * 32, ALL);
+  const size_t o_cr = add(eb->creator, n * 4, ALL);
+  const size_t o_ph = add(eb->parent_hashes, eb->parent_hashes ? eb->n_parent_hashes * 32 : 0, ALL);
+  const size_t o_ord = add(dag ? order.data() : nullptr, dag ? n * 4 : 0, ALL);
+  const size_t o_lof = add(dag ? level_off.data() : nullptr, dag ? level_off.size() * 4 : 0, ALL);
+  const size_t o_pin = add(dag ? posin.data() : nullptr, dag ? n * 4 : 0, ALL);
   const size_t small_end = total;
-  const size_t o_ix = add(eb->index, n * 8);
-  const size_t o_ts = add(eb->timestamp, n * 8);
-  const size_t o_pk = add(eb->parent_kind, n * 2);
-  const size_t o_pr = add(eb->parent_ref, n * 16);
-  const size_t o_ph = add(eb->parent_hashes, eb->parent_hashes ? eb->n_parent_hashes * 32 : 0);
-  const size_t o_txs = add(eb->tx_start, (n + 1) * 8);
-  const size_t o_txo = add(eb->tx_off, n_tx ? (n_tx + 1) * 8 : 0);
-  const size_t o_txb = add(eb->tx_bytes, tx_len);
-  const size_t o_tln = add(eb->tx_list_nil, eb->tx_list_nil ? n : 0);
-  const size_t o_txn = add(eb->tx_nil, eb->tx_nil ? n_tx : 0);
-  const size_t o_io = add(eb->itx_off, eb->itx_off ? (n + 1) * 8 : 0);
-  const size_t o_ij = add(eb->itx_json, itx_len);
-  const size_t o_bo = add(eb->bsig_off, eb->bsig_off ? (n + 1) * 8 : 0);
-  const size_t o_bj = add(eb->bsig_json, bsig_len);
-  const size_t o_ord = add(dag ? order.data() : nullptr, dag ? n * 4 : 0);
-  const size_t o_lof = add(dag ? level_off.data() : nullptr, dag ? level_off.size() * 4 : 0);
-  const size_t o_pin = add(dag ? posin.data() : nullptr, dag ? n * 4 : 0);
+  const size_t o_ix = add(eb->index, n * 8, EV, 8);
+  const size_t o_ts = add(eb->timestamp, n * 8, EV, 8);
+  const size_t o_pk = add(eb->parent_kind, n * 2, EV, 2);
+  const size_t o_pr = add(eb->parent_ref, n * 16, EV, 16);
+  const size_t o_txs = add(eb->tx_start, (n + 1) * 8, EV1, 8);
+  const size_t o_txo = add(eb->tx_off, n_tx ? (n_tx + 1) * 8 : 0, TX1, 8);
+  const size_t o_txb = add(eb->tx_bytes, tx_len, TXB, 1, 64);
+  const size_t o_tln = add(eb->tx_list_nil, eb->tx_list_nil ? n : 0, EV, 1);
+  const size_t o_txn = add(eb->tx_nil, eb->tx_nil ? n_tx : 0, TX, 1);
+  const size_t o_io = add(eb->itx_off, eb->itx_off ? (n + 1) * 8 : 0, EV1, 8);
+  const size_t o_ij = add(eb->itx_json, itx_len, ITX);
+  const size_t o_bo = add(eb->bsig_off, eb->bsig_off ? (n + 1) * 8 : 0, EV1, 8);
+  const size_t o_bj = add(eb->bsig_json, bsig_len, BSIG);
+  auto seg_range = [&](const Seg &g, uint64_t e0, uint64_t e1, size_t *lo, size_t *hi) {
+    const uint64_t t0 = eb->tx_start[e0], t1 = eb->tx_start[e1];
+    switch (g.kind) {
+      case ALL: *lo = 0; *hi = g.n; break;
+      case EV: *lo = e0 * g.unit; *hi = e1 * g.unit; break;
+      case EV1: *lo = e0 * g.unit; *hi = (e1 + 1) * g.unit; break;
+      case TX: *lo = t0 * g.unit; *hi = t1 * g.unit; break;
+      case TX1: *lo = t0 * g.unit; *hi = (t1 + 1) * g.unit; break;
+      case TXB: *lo = n_tx ? eb->tx_off[t0] : 0; *hi = n_tx ? eb->tx_off[t1] : 0; break;
+      case ITX: *lo = eb->itx_off[e0]; *hi = eb->itx_off[e1]; break;
+      case BSIG: *lo = eb->bsig_off[e0]; *hi = eb->bsig_off[e1]; break;
+    }
+    *hi = std::min(*hi, g.n);
+    *lo = std::min(*lo, *hi);
+  };
+
+  // event chunks of ~kChunk staged bytes (whole 256-event groups, so each
+  // chunk's items fill whole words of the accept bitmask); a DAG batch is
+  // hashed level by level across all its events: one chunk
+  std::vector<uint64_t> cb{0};
+  const char *env_chunk = getenv("BV_EV_CHUNK_MB");  // A/B knob: 0 = one chunk
+  const uint64_t chunk_bytes = env_chunk ? (uint64_t)(atof(env_chunk) * (1 << 20)) : kChunk;
+  if (!dag && chunk_bytes > 0) {
+    const uint64_t per_ev = std::max<uint64_t>(1, (total - small_end) / n);
+    const uint64_t per = std::max<uint64_t>(256, chunk_bytes / per_ev / 256 * 256);
+    for (uint64_t e = per; e < n; e += per) cb.push_back(e);
+  }
+  cb.push_back(n);
+  uint64_t max_chunk = 0;
+  for (size_t c = 0; c + 1 < cb.size(); c++) max_chunk = std::max(max_chunk, cb[c + 1] - cb[c]);
 
   if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
   HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
@@ -190,9 +233,29 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   d.s_be = dev + o_s;
   d.pre = eb->pre ? dev + o_pre : nullptr;
 
+  // bodies: an upper bound on their size (exact lengths are on the device)
+  uint64_t kmax = 0;
+  for (uint32_t k = 0; k < eb->n_keys; k++) kmax = std::max<uint64_t>(kmax, eb->key_off[k + 1] - eb->key_off[k]);
+  const uint64_t bound = n * (160 + 2 * 68 + 2 * 20 + 4 * (kmax / 3 + 1) + 16) + 4 * (tx_len / 3 + n_tx) +
+                         8 * n_tx + itx_len + bsig_len + 64;
+  size_t tmp_bytes = 0;
+  HIPCHK(bvk::ev_build(st, d, 0, max_chunk, nullptr, nullptr, nullptr, nullptr, nullptr, &tmp_bytes), BV_E_LAUNCH,
+         "scan size");
+  HIPCHK(ctx->ev_lens.ensure(n * 8), BV_E_OOM, "alloc lens");
+  HIPCHK(ctx->ev_ppos.ensure(n * 8), BV_E_OOM, "alloc ppos");
+  HIPCHK(ctx->ev_offs.ensure((n + 1) * 8), BV_E_OOM, "alloc offs");
+  HIPCHK(ctx->ev_bodies.ensure(bound), BV_E_OOM, "alloc bodies");
+  HIPCHK(ctx->ev_tmp.ensure(std::max<size_t>(tmp_bytes, 256)), BV_E_OOM, "alloc scan scratch");
+  if (dag) HIPCHK(ctx->ev_mid.ensure((size_t)n * EV_MID_U32 * 4), BV_E_OOM, "alloc midstates");
+  uint64_t *offs = ctx->ev_offs.as<uint64_t>();
+  uint32_t *ppos = ctx->ev_ppos.as<uint32_t>();
+  uint8_t *bodies = ctx->ev_bodies.as<uint8_t>();
+
   // verification items: item e = (body e, creator key, r, s)
   bv_batch vb = {};
   vb.n_msgs = n;
+  vb.msg_bytes = bodies;
+  vb.msg_off = offs;
   vb.n_keys = eb->n_keys;
   vb.key_bytes = d.key_bytes;
   vb.key_off = d.key_off;
@@ -202,65 +265,93 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   vb.r_be = d.r_be;
   vb.s_be = d.s_be;
   vb.pre = d.pre;
+  bool kc = false;
+  bv_item_pipe pipe{ctx, &vb, {}, st, false};
+  rc = bv_out_bufs(ctx, &vb, nullptr, nullptr, nullptr, true, &pipe.o);
+  if (rc != BV_OK) return rc;
+  uint32_t *dig = pipe.o.dig;
 
-  HIPCHK(hipEventRecord(ctx->ev[E_CALL], st), BV_E_LAUNCH, "event");
-  bool kc = false, launched = false;
-  for (size_t a = 0; a < total; a += kChunk) {
-    const size_t z = std::min(total, a + kChunk);
-    for (const Seg &s : segs) {
-      const size_t lo = std::max(a, s.off), hi = std::min(z, s.off + s.n);
-      if (s.src && lo < hi) ctx->pool->copy(pin + lo, (const uint8_t *)s.src + (lo - s.off), hi - lo);
-    }
-    HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
-    if (!launched && z >= small_end) {  // keys, r, s, pre, creators are queued: phase A
-      launched = true;
-      HIPCHK(hipEventRecord(ctx->ev[E_SMALL], st), BV_E_LAUNCH, "event");
-      if (ctx->flags & BV_F_KEY_CACHE) {
-        rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, d.key_bytes, d.key_off, st, &kc);
-        if (rc != BV_OK) return rc;
+  // the first part: pinned copies by the pool, H2D on the copy stream
+  hipStream_t cs = ctx->cstream;
+  HIPCHK(hipEventRecord(ctx->ev[E_CALL], cs), BV_E_LAUNCH, "event");
+  auto stage = [&](size_t a0, size_t a1) -> int {
+    for (size_t a = a0; a < a1; a += kChunk) {
+      const size_t z = std::min(a1, a + kChunk);
+      std::vector<CopyPool::Piece> pieces;
+      for (const Seg &g : segs) {
+        const size_t lo = std::max(a, g.off), hi = std::min(z, g.off + g.n);
+        if (g.kind == ALL && g.src && lo < hi)
+          pieces.push_back({pin + lo, (const uint8_t *)g.src + (lo - g.off), hi - lo});
       }
-      rc = bv_run_keys(ctx, &vb, ctx->ev[E_SMALL], kc);
+      ctx->pool->copy_many(pieces);
+      HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
+    }
+    return BV_OK;
+  };
+  rc = stage(0, keys_end);  // the keys: the key tables start once they land
+  if (rc != BV_OK) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[E_KREADY], cs), BV_E_LAUNCH, "event");
+  if (ctx->flags & BV_F_KEY_CACHE) {
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_KREADY], 0), BV_E_LAUNCH, "join");
+    rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, d.key_bytes, d.key_off, st, &kc);
+    if (rc != BV_OK) return rc;
+  }
+  rc = stage(keys_end, s_end);  // s, pre: s^-1
+  if (rc != BV_OK) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[E_SREADY], cs), BV_E_LAUNCH, "event");
+  pipe.kc = kc;
+  rc = bv_run_keys(ctx, &vb, ctx->ev[E_KREADY], ctx->ev[E_SREADY], kc);
+  if (rc != BV_OK) return rc;
+  rc = stage(s_end, small_end);  // r, creators, parent hashes (, the DAG order)
+  if (rc != BV_OK) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[E_SMALL], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SMALL], 0), BV_E_LAUNCH, "join");
+  HIPCHK(bvk::iota(st, n, ctx->ev_iota.as<uint32_t>()), BV_E_LAUNCH, "k_iota");
+  HIPCHK(hipEventRecord(ctx->ev[E_FORK], st), BV_E_LAUNCH, "event");
+
+  // per chunk: its fields cross PCIe on the copy stream; on the main stream
+  // the chunk's bodies are built and (bulk) hashed and its items verified
+  for (size_t c = 0; c + 1 < cb.size(); c++) {
+    const uint64_t e0 = cb[c], e1 = cb[c + 1];
+    std::vector<CopyPool::Piece> pieces;
+    for (const Seg &g : segs) {
+      if (g.kind == ALL || !g.src) continue;
+      size_t lo, hi;
+      seg_range(g, e0, e1, &lo, &hi);
+      if (lo < hi) pieces.push_back({pin + g.off + lo, (const uint8_t *)g.src + lo, hi - lo});
+    }
+    ctx->pool->copy_many(pieces);  // the whole chunk into pinned memory, then its DMA
+    for (const CopyPool::Piece &q : pieces) {
+      const size_t o = (uint8_t *)q.dst - pin;
+      HIPCHK(hipMemcpyAsync(dev + o, pin + o, q.n, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
+    }
+    hipEvent_t landed = ctx->chunk_ev[c % ctx->chunk_ev.size()];
+    HIPCHK(hipEventRecord(landed, cs), BV_E_LAUNCH, "event");
+    HIPCHK(hipStreamWaitEvent(st, landed, 0), BV_E_LAUNCH, "join chunk");
+    HIPCHK(bvk::ev_build(st, d, e0, e1, ctx->ev_lens.as<uint64_t>(), ppos, offs, bodies, ctx->ev_tmp.p, &tmp_bytes),
+           BV_E_LAUNCH, "event bodies");
+    if (!dag) {
+      HIPCHK(bvk::ev_hash(st, e1 - e0, nullptr, e0, d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
+      HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is used
+      rc = pipe.upto(e1);
       if (rc != BV_OK) return rc;
     }
   }
-  HIPCHK(hipEventRecord(ctx->ev[E_STAGED], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->ev[E_STAGED], cs), BV_E_LAUNCH, "event");
   call.ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call.t0).count();
 
-  // bodies: an upper bound on their size (exact lengths are on the device)
-  uint64_t kmax = 0;
-  for (uint32_t k = 0; k < eb->n_keys; k++) kmax = std::max<uint64_t>(kmax, eb->key_off[k + 1] - eb->key_off[k]);
-  const uint64_t bound = n * (160 + 2 * 68 + 2 * 20 + 4 * (kmax / 3 + 1) + 16) + 4 * (tx_len / 3 + n_tx) +
-                         8 * n_tx + itx_len + bsig_len + 64;
-  size_t tmp_bytes = 0;
-  HIPCHK(bvk::ev_build(st, d, nullptr, nullptr, nullptr, nullptr, nullptr, &tmp_bytes), BV_E_LAUNCH, "scan size");
-  HIPCHK(ctx->ev_lens.ensure(n * 8), BV_E_OOM, "alloc lens");
-  HIPCHK(ctx->ev_ppos.ensure(n * 8), BV_E_OOM, "alloc ppos");
-  HIPCHK(ctx->ev_offs.ensure((n + 1) * 8), BV_E_OOM, "alloc offs");
-  HIPCHK(ctx->ev_bodies.ensure(bound), BV_E_OOM, "alloc bodies");
-  HIPCHK(ctx->ev_tmp.ensure(std::max<size_t>(tmp_bytes, 256)), BV_E_OOM, "alloc scan scratch");
-  HIPCHK(ctx->digests.ensure(n * 32), BV_E_OOM, "alloc digests");
-  uint64_t *offs = ctx->ev_offs.as<uint64_t>();
-  uint32_t *ppos = ctx->ev_ppos.as<uint32_t>(), *dig = ctx->digests.as<uint32_t>();
-  uint8_t *bodies = ctx->ev_bodies.as<uint8_t>();
-  HIPCHK(bvk::ev_build(st, d, ctx->ev_lens.as<uint64_t>(), ppos, offs, bodies, ctx->ev_tmp.p, &tmp_bytes),
-         BV_E_LAUNCH, "event bodies");
-
-  // hashing: all at once, or level by level over the in-batch DAG
-  if (!dag) {
-    HIPCHK(bvk::ev_hash(st, n, nullptr, d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
-  } else {
+  if (dag) {  // level by level over the in-batch DAG
     const uint32_t *dord = (const uint32_t *)(dev + o_ord), *dlof = (const uint32_t *)(dev + o_lof);
     const uint32_t *dpin = (const uint32_t *)(dev + o_pin);
     const uint32_t nl = (uint32_t)level_off.size() - 1;
     // midstates of every event above level 0, in one wide launch
-    HIPCHK(ctx->ev_mid.ensure((size_t)n * EV_MID_U32 * 4), BV_E_OOM, "alloc midstates");
     uint32_t *mid = ctx->ev_mid.as<uint32_t>();
     HIPCHK(bvk::ev_mid(st, n - level_off[1], dord + level_off[1], bodies, offs, ppos, mid), BV_E_LAUNCH, "k_ev_mid");
     uint32_t L = 0;
     while (L < nl) {
       const uint32_t w = level_off[L + 1] - level_off[L];
       if (w > kNarrowLevel || L == 0) {
-        HIPCHK(bvk::ev_hash(st, w, dord + level_off[L], d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
+        HIPCHK(bvk::ev_hash(st, w, dord + level_off[L], 0, d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
         L++;
         continue;
       }
@@ -274,32 +365,29 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
              "k_ev_hash_chain");
       L = L1;
     }
+    HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
   }
-  HIPCHK(bvk::iota(st, n, ctx->ev_iota.as<uint32_t>()), BV_E_LAUNCH, "k_iota");
-  HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->ev[E_SHA], st), BV_E_LAUNCH, "event");
 
-  // the digests go back on the copy stream while the verify kernels run
+  // the digests go back on the copy stream while the last verify kernels run
   const size_t o_st = align256(n * 32), o_bits = o_st + align256(n);
   HIPCHK(ctx->pin_out.ensure(o_bits + align256((n + 63) / 64 * 8) + 256), BV_E_OOM, "alloc pinned results");
   uint8_t *pout = (uint8_t *)ctx->pin_out.p;
   call.pout = pout;
   call.o_st = o_st;
   call.o_bits = o_bits;
-  HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev[E_HASHED], 0), BV_E_LAUNCH, "join");
-  HIPCHK(hipMemcpyAsync(pout, ctx->digests.p, n * 32, hipMemcpyDeviceToHost, ctx->cstream), BV_E_LAUNCH,
-         "d2h digests");
-  HIPCHK(hipEventRecord(ctx->ev[E_CSDONE], ctx->cstream), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(cs, ctx->ev[E_HASHED], 0), BV_E_LAUNCH, "join");
+  HIPCHK(hipMemcpyAsync(pout, dig, n * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH, "d2h digests");
+  HIPCHK(hipEventRecord(ctx->ev[E_CSDONE], cs), BV_E_LAUNCH, "event");
 
-  // verification of the hashed bodies (phase A is already under way)
-  vb.msg_bytes = bodies;
-  vb.msg_off = offs;
-  rc = bv_run_verify(ctx, &vb, nullptr, nullptr, nullptr, st, true, kc);
+  rc = pipe.finish();  // bulk: the last chunk's items; DAG: all of them
   if (rc != BV_OK) return rc;
-  HIPCHK(hipMemcpyAsync(pout + o_st, ctx->status.p, n, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
-  HIPCHK(hipMemcpyAsync(pout + o_bits, ctx->bits.p, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
+  HIPCHK(hipMemcpyAsync(pout + o_st, pipe.o.status, n, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
+  HIPCHK(hipMemcpyAsync(pout + o_bits, pipe.o.bits, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
          "d2h bits");
   HIPCHK(hipEventRecord(ctx->ev[E_OUT], st), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_CSDONE], 0), BV_E_LAUNCH, "join");  // digests out before ev_done
+  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_STAGED], 0), BV_E_LAUNCH, "join");  // staging free after ev_done
   HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
   bv_batch sizes = {};
   sizes.n_msgs = n;

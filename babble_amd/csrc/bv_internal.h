@@ -24,10 +24,10 @@ namespace bvk {
 hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
 hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
 hipError_t sha256_chain(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
-hipError_t ev_build(hipStream_t, const bv_event_batch &, uint64_t *, uint32_t *, uint64_t *, uint8_t *, void *,
-                    size_t *);
-hipError_t ev_hash(hipStream_t, uint64_t, const uint32_t *, const bv_event_batch &, const uint32_t *, uint8_t *,
-                   const uint64_t *, uint32_t *);
+hipError_t ev_build(hipStream_t, const bv_event_batch &, uint64_t, uint64_t, uint64_t *, uint32_t *, uint64_t *,
+                    uint8_t *, void *, size_t *);
+hipError_t ev_hash(hipStream_t, uint64_t, const uint32_t *, uint64_t, const bv_event_batch &, const uint32_t *,
+                   uint8_t *, const uint64_t *, uint32_t *);
 hipError_t ev_mid(hipStream_t, uint64_t, const uint32_t *, const uint8_t *, const uint64_t *, const uint32_t *,
                   uint32_t *);
 hipError_t ev_hash_chain(hipStream_t, uint32_t, uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
@@ -40,18 +40,19 @@ hipError_t build_kc(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, ui
                     const uint64_t *);
 size_t kc_pscr_bytes();
 hipError_t sinv(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *);
-hipError_t verify_gq(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
-                     const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *,
-                     const uint64_t *, uint8_t *, uint64_t *);
+// verify kernels over items [lo, hi) of an n-item batch (lo a multiple of 64)
+hipError_t verify_gq(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
+                     const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
+                     const uint32_t *, const uint64_t *, uint8_t *, uint64_t *);
 hipError_t verify_g(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
                     const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
                     const uint32_t *, uint32_t *);
-hipError_t verify_q(hipStream_t, int, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *, const uint8_t *,
-                    const uint8_t *, const uint32_t *, const uint32_t *, const uint64_t *, const uint32_t *,
-                    uint8_t *, uint64_t *);
-hipError_t verify_generic(hipStream_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
-                          const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
-                          const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
+hipError_t verify_q(hipStream_t, int, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
+                    const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
+                    const uint64_t *, const uint32_t *, uint8_t *, uint64_t *);
+hipError_t verify_generic(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
+                          const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
+                          const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
 }  // namespace bvk
 
 struct DevBuf {
@@ -151,6 +152,36 @@ struct CopyPool {
     std::unique_lock<std::mutex> lk(mu);
     done_cv.wait(lk, [this]() { return pending == 0; });
   }
+  // several copies at once (the pieces of one staging chunk), split into
+  // 1 MB parts spread over the pool; returns when all are done
+  struct Piece {
+    void *dst;
+    const void *src;
+    size_t n;
+  };
+  void copy_many(const std::vector<Piece> &v) {
+    constexpr size_t kPart = 1ull << 20;
+    std::vector<Piece> parts;
+    for (const Piece &p : v)
+      for (size_t o = 0; o < p.n; o += kPart)
+        parts.push_back({(uint8_t *)p.dst + o, (const uint8_t *)p.src + o, std::min(kPart, p.n - o)});
+    if (parts.size() <= 1 || th.empty()) {
+      for (const Piece &p : parts) memcpy(p.dst, p.src, p.n);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (size_t i = 1; i < parts.size(); i++) {
+        const Piece p = parts[i];
+        q.push_back([p]() { memcpy(p.dst, p.src, p.n); });
+        pending++;
+      }
+    }
+    cv.notify_all();
+    memcpy(parts[0].dst, parts[0].src, parts[0].n);
+    std::unique_lock<std::mutex> lk(mu);
+    done_cv.wait(lk, [this]() { return pending == 0; });
+  }
 };
 
 
@@ -159,7 +190,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // timing / ordering events (see bv_read_timing)
 enum {
   E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_SINV,
-  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_COUNT
+  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_COUNT
 };
 
 struct KcSlot {
@@ -214,7 +245,30 @@ int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess);
 int bv_validate_host_batch(bv_ctx *ctx, const bv_batch *b);
 int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc);
-int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t ready, bool kc);
+int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_t s_ready, bool kc);
+struct bv_out {  // device outputs of one verify
+  uint32_t *dig = nullptr;
+  uint8_t *status = nullptr;
+  uint64_t *bits = nullptr;
+};
+int bv_out_bufs(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
+                bool hashed, bv_out *o);
+int bv_launch_items(bv_ctx *ctx, const bv_batch *b, const bv_out &o, hipStream_t st, bool kc, uint64_t lo,
+                    uint64_t hi, int part);
+// Host entry points: items verified in order on `st` as their messages get
+// hashed (after bv_run_keys); upto(end) launches items [done, end), end a
+// multiple of 64 or n_items.  The first launch orders `st` after s^-1 and
+// the key tables.
+struct bv_item_pipe {
+  bv_ctx *ctx;
+  const bv_batch *b;
+  bv_out o;
+  hipStream_t st;
+  bool kc;
+  uint64_t done = 0;
+  int upto(uint64_t end);
+  int finish();  // the rest, and the timing events even when there are no items
+};
 int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc);
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,

@@ -58,10 +58,11 @@ __global__ void __launch_bounds__(64) k_sha256_chain(uint32_t n, const uint8_t *
 // ---------------------------------------------------------------------------
 // Events from wire fields (evjson.h): body lengths, bodies, level hashing
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_ev_len(bv_event_batch b, uint64_t *__restrict__ lens,
-                                                uint32_t *__restrict__ ppos) {
-  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= b.n_events) return;
+// Events [e0, e1) of the batch in every kernel below (a staging chunk).
+__global__ void __launch_bounds__(256) k_ev_len(bv_event_batch b, uint64_t e0, uint64_t e1,
+                                                uint64_t *__restrict__ lens, uint32_t *__restrict__ ppos) {
+  const uint64_t e = e0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= e1) return;
   uint32_t pp[2];
   lens[e] = evj_len(b, e, pp);
   ppos[2 * e] = pp[0];
@@ -75,11 +76,12 @@ __global__ void __launch_bounds__(256) k_ev_len(bv_event_batch b, uint64_t *__re
 // whose bodies exceed the LDS buffer write straight to global memory.
 #define EV_WRITE_NT 64
 #define EV_WRITE_CAP (32 * 1024)
-__global__ void __launch_bounds__(EV_WRITE_NT) k_ev_write(bv_event_batch b, const uint64_t *__restrict__ offs,
+__global__ void __launch_bounds__(EV_WRITE_NT) k_ev_write(bv_event_batch b, uint64_t c0, uint64_t c1,
+                                                          const uint64_t *__restrict__ offs,
                                                           uint8_t *__restrict__ bodies) {
   __shared__ uint32_t lds[EV_WRITE_CAP / 4 + 4];
-  const uint64_t n = b.n_events;
-  const uint64_t e0 = (uint64_t)blockIdx.x * EV_WRITE_NT, e = e0 + threadIdx.x;
+  const uint64_t n = c1;
+  const uint64_t e0 = c0 + (uint64_t)blockIdx.x * EV_WRITE_NT, e = e0 + threadIdx.x;
   const uint64_t e1 = e0 + EV_WRITE_NT < n ? e0 + EV_WRITE_NT : n;
   const uint64_t base = offs[e0], end = offs[e1], a0 = base & ~(uint64_t)3;
   if (end - a0 > EV_WRITE_CAP) {  // uniform per block
@@ -123,12 +125,21 @@ __device__ __forceinline__ void ev_splice_hash(uint64_t e, const bv_event_batch 
   sha256_one(e, bodies, offs, dig);
 }
 
-// One DAG level (or all events when list == null): a grid over its events.
-__global__ void __launch_bounds__(256) k_ev_hash(uint64_t count, const uint32_t *__restrict__ list, bv_event_batch b,
-                                                 const uint32_t *__restrict__ ppos, uint8_t *__restrict__ bodies,
-                                                 const uint64_t *__restrict__ offs, uint32_t *__restrict__ dig) {
+// One DAG level (or events e0 .. e0 + count - 1 when list == null): a grid
+// over its events.
+__global__ void __launch_bounds__(256) k_ev_hash(uint64_t count, const uint32_t *__restrict__ list, uint64_t e0,
+                                                 bv_event_batch b, const uint32_t *__restrict__ ppos,
+                                                 uint8_t *__restrict__ bodies, const uint64_t *__restrict__ offs,
+                                                 uint32_t *__restrict__ dig) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) ev_splice_hash(list ? list[i] : i, b, ppos, bodies, offs, dig, false);
+  if (i < count) ev_splice_hash(list ? list[i] : e0 + i, b, ppos, bodies, offs, dig, false);
+}
+
+// offs[0, count) += *base (the end of the previous chunk's bodies)
+__global__ void __launch_bounds__(256) k_add_base(uint64_t count, uint64_t *__restrict__ offs,
+                                                  const uint64_t *__restrict__ base) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) offs[i] += *base;
 }
 
 // Midstates (evjson.h: ev_midstate) of `count` events (list[i]): the
@@ -596,15 +607,17 @@ __global__ void __launch_bounds__(256) k_sinv(uint64_t n_items, uint32_t M, cons
   sinv_thread(t, T, n_items, M, s_be, pre, w_out);
 }
 
-__device__ __forceinline__ void write_status(uint64_t i, uint64_t n_items, uint8_t st, uint8_t *status,
-                                             uint64_t *bits) {
-  if (i < n_items) status[i] = st;
-  const uint64_t mask = __ballot(i < n_items && st == BV_ACCEPT);
-  if ((threadIdx.x & 63) == 0 && i < n_items) bits[i >> 6] = mask;
+// Items [lo, hi) of a launch, lo a multiple of 64: each wave owns whole
+// 64-bit words of the accept bitmask (hi is a multiple of 64 or the end).
+__device__ __forceinline__ void write_status(uint64_t i, uint64_t hi, uint8_t st, uint8_t *status, uint64_t *bits) {
+  if (i < hi) status[i] = st;
+  const uint64_t mask = __ballot(i < hi && st == BV_ACCEPT);
+  if ((threadIdx.x & 63) == 0 && i < hi) bits[i >> 6] = mask;
 }
 
 template <bool LAT>
-__global__ void __launch_bounds__(256) k_verify_g(uint64_t n_items, uint64_t lo, uint64_t hi, const uint32_t *__restrict__ item_key,
+__global__ void __launch_bounds__(256) k_verify_g(uint64_t n_items, uint64_t lo, uint64_t hi,
+                                                  const uint32_t *__restrict__ item_key,
                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
                                                   const uint32_t *__restrict__ item_msg,
@@ -617,7 +630,8 @@ __global__ void __launch_bounds__(256) k_verify_g(uint64_t n_items, uint64_t lo,
 }
 
 template <int W, int NWIN, bool LAT>
-__global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, const uint32_t *__restrict__ item_key,
+__global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, uint64_t lo, uint64_t hi,
+                                                  const uint32_t *__restrict__ item_key,
                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
                                                   const uint32_t *__restrict__ u12,
@@ -625,16 +639,17 @@ __global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, const uint32
                                                   const uint64_t *__restrict__ key_tabs,
                                                   const uint32_t *__restrict__ rg, uint8_t *__restrict__ status,
                                                   uint64_t *__restrict__ bits) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t st = BV_REJECT;
-  if (i < n_items)
+  if (i < hi)
     st = verify_item_q<W, NWIN, LAT>(i, n_items, item_key, r_be, s_be, pre, kstatus, u12, key_table, key_tabs, rg);
-  write_status(i, n_items, st, status, bits);
+  write_status(i, hi, st, status, bits);
 }
 
 // Key-cache path, G and Q parts fused (verify_core.h: verify_item_gq_kc).
 template <bool LAT>
-__global__ void __launch_bounds__(256) k_verify_gq(uint64_t n_items, const uint32_t *__restrict__ item_key,
+__global__ void __launch_bounds__(256) k_verify_gq(uint64_t n_items, uint64_t lo, uint64_t hi,
+                                                   const uint32_t *__restrict__ item_key,
                                                    const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                    const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
                                                    const uint32_t *__restrict__ item_msg,
@@ -643,11 +658,11 @@ __global__ void __launch_bounds__(256) k_verify_gq(uint64_t n_items, const uint3
                                                    const uint32_t *__restrict__ g_table,
                                                    const uint64_t *__restrict__ key_tabs, uint8_t *__restrict__ status,
                                                    uint64_t *__restrict__ bits) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t st = BV_REJECT;
-  if (i < n_items)
+  if (i < hi)
     st = verify_item_gq_kc<LAT>(i, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, g_table, key_tabs);
-  write_status(i, n_items, st, status, bits);
+  write_status(i, hi, st, status, bits);
 }
 
 // Key-cache (KC) table windows from the 11-bit sub-tables: block (c, key)
@@ -724,7 +739,8 @@ __global__ void __launch_bounds__(256) k_table_pair_kc(const uint32_t *__restric
 }
 
 template <bool LAT>
-__global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, const uint32_t *__restrict__ item_key,
+__global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, uint64_t lo, uint64_t hi,
+                                                        const uint32_t *__restrict__ item_key,
                                                         const uint32_t *__restrict__ r_be,
                                                         const uint32_t *__restrict__ s_be,
                                                         const uint8_t *__restrict__ pre,
@@ -735,11 +751,11 @@ __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, const 
                                                         const uint32_t *__restrict__ w_in,
                                                         const uint32_t *__restrict__ g_table,
                                                         uint8_t *__restrict__ status, uint64_t *__restrict__ bits) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t st = BV_REJECT;
-  if (i < n_items)
+  if (i < hi)
     st = verify_item_generic<LAT>(i, item_key, r_be, s_be, pre, kstatus, kxy, item_msg, digest_words, w_in, g_table);
-  write_status(i, n_items, st, status, bits);
+  write_status(i, hi, st, status, bits);
 }
 
 // ---------------------------------------------------------------------------
@@ -764,29 +780,38 @@ hipError_t sha256(hipStream_t st, uint64_t n, const uint8_t *bytes, const uint64
   return hipGetLastError();
 }
 
-// Bodies of the events of `b` (device pointers): lengths, offsets (offs:
-// n + 1, inclusive scan into offs + 1), then the JSON.  `tmp` / `tmp_bytes`:
-// scan scratch (query with tmp == null).
-hipError_t ev_build(hipStream_t st, const bv_event_batch &b, uint64_t *lens, uint32_t *ppos, uint64_t *offs,
-                    uint8_t *bodies, void *tmp, size_t *tmp_bytes) {
-  const uint64_t n = b.n_events;
-  if (!tmp) return hipcub::DeviceScan::InclusiveSum(nullptr, *tmp_bytes, lens, offs + 1, (int)n, st);
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ev_len, grid1(n, 256), dim3(256), 0, st, b, lens, ppos);
+// Bodies of events [e0, e1) of `b` (device pointers): lengths, offsets
+// (offs: n + 1; an inclusive scan of the chunk's lengths into
+// offs + e0 + 1, shifted by offs[e0], the end of the previous chunk's bodies;
+// offs[0] = 0), then the JSON.  `tmp` / `tmp_bytes`: scan scratch (query with
+// tmp == null for chunks of up to e1 - e0 events).
+hipError_t ev_build(hipStream_t st, const bv_event_batch &b, uint64_t e0, uint64_t e1, uint64_t *lens,
+                    uint32_t *ppos, uint64_t *offs, uint8_t *bodies, void *tmp, size_t *tmp_bytes) {
+  const uint64_t m = e1 - e0;
+  if (!tmp) return hipcub::DeviceScan::InclusiveSum(nullptr, *tmp_bytes, lens, offs + 1, (int)m, st);
+  if (m == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ev_len, grid1(m, 256), dim3(256), 0, st, b, e0, e1, lens, ppos);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(offs, 0, 8, st);
+  if (e0 == 0) {
+    e = hipMemsetAsync(offs, 0, 8, st);
+    if (e != hipSuccess) return e;
+  }
+  e = hipcub::DeviceScan::InclusiveSum(tmp, *tmp_bytes, lens + e0, offs + e0 + 1, (int)m, st);
   if (e != hipSuccess) return e;
-  e = hipcub::DeviceScan::InclusiveSum(tmp, *tmp_bytes, lens, offs + 1, (int)n, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_ev_write, grid1(n, EV_WRITE_NT), dim3(EV_WRITE_NT), 0, st, b, offs, bodies);
+  if (e0 > 0) {
+    hipLaunchKernelGGL(k_add_base, grid1(m, 256), dim3(256), 0, st, m, offs + e0 + 1, offs + e0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_ev_write, grid1(m, EV_WRITE_NT), dim3(EV_WRITE_NT), 0, st, b, e0, e1, offs, bodies);
   return hipGetLastError();
 }
 
-hipError_t ev_hash(hipStream_t st, uint64_t count, const uint32_t *list, const bv_event_batch &b, const uint32_t *ppos,
-                   uint8_t *bodies, const uint64_t *offs, uint32_t *dig) {
+hipError_t ev_hash(hipStream_t st, uint64_t count, const uint32_t *list, uint64_t e0, const bv_event_batch &b,
+                   const uint32_t *ppos, uint8_t *bodies, const uint64_t *offs, uint32_t *dig) {
   if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ev_hash, grid1(count, 256), dim3(256), 0, st, count, list, b, ppos, bodies, offs, dig);
+  hipLaunchKernelGGL(k_ev_hash, grid1(count, 256), dim3(256), 0, st, count, list, e0, b, ppos, bodies, offs, dig);
   return hipGetLastError();
 }
 
@@ -894,19 +919,19 @@ hipError_t verify_g(hipStream_t st, uint64_t n, uint64_t lo, uint64_t hi, const 
 
 // kw = 8 / 12: contiguous per-batch tables in key_table; kw = 22: the key
 // cache (KC), table base address per batch key in key_tabs.
-hipError_t verify_q(hipStream_t st, int kw, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
-                    const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst, const uint32_t *u12,
-                    const uint32_t *key_table, const uint64_t *key_tabs, const uint32_t *rg, uint8_t *status,
-                    uint64_t *bits) {
-  if (n == 0) return hipSuccess;
+hipError_t verify_q(hipStream_t st, int kw, uint64_t n, uint64_t lo, uint64_t hi, const uint32_t *item_key,
+                    const uint32_t *r_be, const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst,
+                    const uint32_t *u12, const uint32_t *key_table, const uint64_t *key_tabs, const uint32_t *rg,
+                    uint8_t *status, uint64_t *bits) {
+  if (hi <= lo) return hipSuccess;
   const bool lat = lat_variant(n);
 #define BV_LAUNCH_Q(W, NWIN, KT, KTABS)                                                                             \
   if (lat)                                                                                                       \
-    hipLaunchKernelGGL((k_verify_q<W, NWIN, true>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, \
-                       kst, u12, KT, KTABS, rg, status, bits);                                                   \
+    hipLaunchKernelGGL((k_verify_q<W, NWIN, true>), grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key,  \
+                       r_be, s_be, pre, kst, u12, KT, KTABS, rg, status, bits);                                  \
   else                                                                                                           \
-    hipLaunchKernelGGL((k_verify_q<W, NWIN, false>), grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be,     \
-                       pre, kst, u12, KT, KTABS, rg, status, bits);
+    hipLaunchKernelGGL((k_verify_q<W, NWIN, false>), grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key,   \
+                       r_be, s_be, pre, kst, u12, KT, KTABS, rg, status, bits);
   if (kw == 8) {
     BV_LAUNCH_Q(BV_KW, BV_KNWIN, key_table, nullptr)
   } else if (kw == 12) {
@@ -918,17 +943,17 @@ hipError_t verify_q(hipStream_t st, int kw, uint64_t n, const uint32_t *item_key
   return hipGetLastError();
 }
 
-hipError_t verify_gq(hipStream_t st, uint64_t n, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
-                     const uint8_t *pre, const uint8_t *kst, const uint32_t *item_msg, const uint32_t *dig,
-                     const uint32_t *w, const uint32_t *g_table, const uint64_t *key_tabs, uint8_t *status,
-                     uint64_t *bits) {
-  if (n == 0) return hipSuccess;
+hipError_t verify_gq(hipStream_t st, uint64_t n, uint64_t lo, uint64_t hi, const uint32_t *item_key,
+                     const uint32_t *r_be, const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst,
+                     const uint32_t *item_msg, const uint32_t *dig, const uint32_t *w, const uint32_t *g_table,
+                     const uint64_t *key_tabs, uint8_t *status, uint64_t *bits) {
+  if (hi <= lo) return hipSuccess;
   if (lat_variant(n))
-    hipLaunchKernelGGL(k_verify_gq<true>, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst, item_msg,
-                       dig, w, g_table, key_tabs, status, bits);
+    hipLaunchKernelGGL(k_verify_gq<true>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be, pre,
+                       kst, item_msg, dig, w, g_table, key_tabs, status, bits);
   else
-    hipLaunchKernelGGL(k_verify_gq<false>, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst,
-                       item_msg, dig, w, g_table, key_tabs, status, bits);
+    hipLaunchKernelGGL(k_verify_gq<false>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be, pre,
+                       kst, item_msg, dig, w, g_table, key_tabs, status, bits);
   return hipGetLastError();
 }
 
@@ -955,17 +980,17 @@ hipError_t build_kc(hipStream_t st, uint32_t n, const uint32_t *kxy, const uint8
   return hipGetLastError();
 }
 
-hipError_t verify_generic(hipStream_t st, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
-                          const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst, const uint32_t *kxy,
-                          const uint32_t *item_msg, const uint32_t *dig, const uint32_t *w, const uint32_t *g_table,
-                          uint8_t *status, uint64_t *bits) {
-  if (n == 0) return hipSuccess;
+hipError_t verify_generic(hipStream_t st, uint64_t n, uint64_t lo, uint64_t hi, const uint32_t *item_key,
+                          const uint32_t *r_be, const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst,
+                          const uint32_t *kxy, const uint32_t *item_msg, const uint32_t *dig, const uint32_t *w,
+                          const uint32_t *g_table, uint8_t *status, uint64_t *bits) {
+  if (hi <= lo) return hipSuccess;
   if (lat_variant(n))
-    hipLaunchKernelGGL(k_verify_generic<true>, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst,
-                       kxy, item_msg, dig, w, g_table, status, bits);
+    hipLaunchKernelGGL(k_verify_generic<true>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be,
+                       pre, kst, kxy, item_msg, dig, w, g_table, status, bits);
   else
-    hipLaunchKernelGGL(k_verify_generic<false>, grid1(n, 256), dim3(256), 0, st, n, item_key, r_be, s_be, pre, kst,
-                       kxy, item_msg, dig, w, g_table, status, bits);
+    hipLaunchKernelGGL(k_verify_generic<false>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be,
+                       s_be, pre, kst, kxy, item_msg, dig, w, g_table, status, bits);
   return hipGetLastError();
 }
 

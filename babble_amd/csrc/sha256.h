@@ -32,6 +32,15 @@ DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return a ^ b ^ c;
 #endif
 }
+// Maj(a, b, c) in one v_bitop3_b32 (truth table 0xE8); left to itself the
+// compiler emits xor + and + bitop3 (three VALU) per round.
+DEV uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+#else
+  return (a & b) ^ (a & c) ^ (b & c);
+#endif
+}
 DEV uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 // bytes sh..sh+3 of the little-endian pair (lo, hi) (v_alignbyte_b32 on gfx950)
 DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
@@ -53,7 +62,7 @@ DEV void sha256_compress(uint32_t h[8], uint32_t w[16]) {
       w[i & 15] = wi;
     }
     uint32_t t1 = hh + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g)) + SHA_K[i] + wi;
-    uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, b, c);
     hh = g;
     g = f;
     f = e;
@@ -203,7 +212,7 @@ DEV void sha256_rounds_wk(uint32_t h[8], const uint32_t *wk, uint32_t stride = 4
     for (int u = 0; u < 8; u++) {
       const uint32_t t1 = hh + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g)) +
                           q[(u >> 2) * stride + (u & 3)];
-      const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+      const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, b, c);
       hh = g;
       g = f;
       f = e;

@@ -124,6 +124,28 @@ def test_k12_tables_adversarial(verifier):
     assert verifier.timing()["key_path"] == 12
 
 
+def test_host_entry_item_order(verifier):
+    """bv_verify_batch verifies items chunk by chunk as their messages land
+    when item_msg is non-decreasing, and after the whole transfer otherwise:
+    the same batch (several 16 MB staging chunks, K12 tables, the C4 mix) in
+    message order, shuffled, and with a run of 63 items re-hitting an early
+    message: every status equal to the oracle's."""
+    import dataclasses
+
+    b = synth.adversarial(120_000, seed=13, n_creators=16, scale_per_million=MIX)
+    assert np.all(np.diff(b.item_msg.astype(np.int64)) >= 0)
+    check_against_oracle(verifier, b)
+    rng = np.random.default_rng(13)
+    perm = rng.permutation(b.n_items)
+    pre = None if b.pre is None else b.pre[perm]
+    shuffled = dataclasses.replace(b, item_msg=b.item_msg[perm], item_key=b.item_key[perm], r_be=b.r_be[perm],
+                                   s_be=b.s_be[perm], pre=pre)
+    check_against_oracle(verifier, shuffled)
+    late = b.item_msg.copy()
+    late[-63:] = 0  # the last word's items point back at message 0: out of order
+    check_against_oracle(verifier, dataclasses.replace(b, item_msg=late))
+
+
 def test_k8_tables_forced_by_flag():
     """BV_F_K8 keeps the 8-bit key tables on a batch that would take K12."""
     from babble_amd.verifier import Verifier
