@@ -254,7 +254,7 @@ def main():
         achieved = args.events * MODMUL_PER_ITEM_EXEC * IMUL32_PER_MODMUL / kv_s
         roof = {
             "bound": "valu-int",
-            "kernel": "k_verify_g + k_verify_q<12,11>",
+            "kernel": "k_verify_g<false> + k_verify_q<12, 11, false>",
             "achieved": achieved / 1e12,
             "peak": PEAK_IMUL32_PER_S / 1e12,
             "unit": "T IMUL32/s (executed schedule: 349 modmuls x 80 IMUL32 per item; bench.py ROOFLINE)",

@@ -16,13 +16,13 @@ for src, dst in [("bench.json", f"{tag}_bench.json"), ("prof/run_kernel_stats.cs
                  ("pmc_summary.json", f"{tag}_pmc_summary.json")]:
     shutil.copy(os.path.join(G, src), os.path.join(P, dst))
 d = json.load(open(os.path.join(P, f"{tag}_pmc_summary.json")))
-g = d["k_verify_g"]
+g = next(v for k, v in d.items() if k.startswith("k_verify_g"))
 q = next(v for k, v in d.items() if k.startswith("k_verify_q"))
 items = 1_000_000
 out = {
     "source": f"profiles/{tag}_pmc_summary.json (tools/gpu_pmc.sh: separate rocprofv3 --pmc passes "
               "FETCH_SIZE / WRITE_SIZE / SQ_*, bench.py --events 1000000)",
-    "kernels": "k_verify_g + k_verify_q<12,11>",
+    "kernels": "k_verify_g + k_verify_q<12,11> (throughput variants)",
     "items_per_launch": items,
     "hbm_bytes_per_launch": g["hbm_bytes"] + q["hbm_bytes"],
     "hbm_read_bytes_uncorrected": (g["counters"]["FETCH_SIZE"] + q["counters"]["FETCH_SIZE"]) * 1024,
