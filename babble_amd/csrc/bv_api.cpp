@@ -171,7 +171,7 @@ static const uint32_t *gtable_acquire(int device, hipStream_t st) {
       }
     ok = hipMemcpyAsync(xy, gxy, sizeof gxy, hipMemcpyHostToDevice, st) == hipSuccess &&
          bvk::build_tables(st, 0, 1, (const uint32_t *)xy, nullptr, (uint32_t *)bases, (uint32_t *)sub,
-                           (uint32_t *)pscr, (uint32_t *)table) == hipSuccess &&
+                           (uint32_t *)pscr, (uint32_t *)table, 0) == hipSuccess &&
          hipStreamSynchronize(st) == hipSuccess;
   }
   for (void *p : {xy, bases, sub, pscr})
@@ -494,7 +494,7 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
     if (table_mode)
       HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
                                ctx->bases_jac.as<uint32_t>(), ctx->key_sub.as<uint32_t>(),
-                               ctx->key_pscr.as<uint32_t>(), ctx->key_table.as<uint32_t>()),
+                               ctx->key_pscr.as<uint32_t>(), ctx->key_table.as<uint32_t>(), n_items),
              BV_E_LAUNCH, "key tables");
   }
   HIPCHK(hipEventRecord(ev[E_KEYS], ctx->kstream), BV_E_LAUNCH, "event");

@@ -35,7 +35,7 @@ hipError_t ev_hash_chain(hipStream_t, uint32_t, uint32_t, const uint32_t *, cons
                          uint32_t *);
 hipError_t iota(hipStream_t, uint64_t, uint32_t *);
 hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
-                        uint32_t *, uint32_t *);
+                        uint32_t *, uint32_t *, uint64_t n_items);
 hipError_t build_kc(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *, uint32_t *,
                     const uint64_t *);
 size_t kc_pscr_bytes();

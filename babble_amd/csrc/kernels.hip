@@ -18,7 +18,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "evjson.h"
+
 #include "verify_core.h"
 
 #include <hipcub/hipcub.hpp>
@@ -386,20 +389,21 @@ __global__ void __launch_bounds__(64) k_key_decode(uint32_t n_keys, const uint8_
   if (k < n_keys) key_decode_one(k, kbytes, koff, kstatus, kxy);
 }
 
+template <bool LAT>
 __global__ void __launch_bounds__(64) k_table_bases(uint32_t n_bases, const uint32_t *__restrict__ bxy,
                                                     const uint8_t *__restrict__ bstatus,
                                                     uint32_t *__restrict__ bases_jac, int w, int nwin) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n_bases) return;
   if (bstatus && bstatus[b] != KS_OK) return;
-  table_bases_one(b, bxy, bases_jac, w, nwin);
+  table_bases_one<LAT>(b, bxy, bases_jac, w, nwin);
 }
 
 // blockDim = BLOCK (<= 2^W), grid (NWIN * 2^W/BLOCK, n_bases).  Block (j, c)
 // computes entries d = BLOCK c + t of window j and normalises them to
 // affine with one field inversion (prefix/suffix products in LDS).  PHI:
 // also write the phi(T) half of a GLV key table.
-template <int W, int NWIN, bool PHI, int BLOCK = 256>
+template <int W, int NWIN, bool PHI, int BLOCK = 256, bool LAT = true>
 __global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict__ bases_jac,
                                                       const uint8_t *__restrict__ bstatus,
                                                       uint32_t *__restrict__ table) {
@@ -425,7 +429,7 @@ __global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict
   gej R;
   bool inf;
   fe Z;
-  table_point(R, inf, Z, bx, by, d, W);
+  table_point<LAT>(R, inf, Z, bx, by, d, W);
   if (!inf) fe_mul(Z, Z, bz);
   sPre[t] = Z;
   sSuf[t] = Z;
@@ -849,17 +853,40 @@ hipError_t key_decode(hipStream_t st, uint32_t n, const uint8_t *kb, const uint6
   return hipGetLastError();
 }
 
+// Point-op variant of the K12 table build (bit 0: base chains, bit 1:
+// sub-table fills; 1 = zipped).  Beside a large batch's bulk kernels (`busy`)
+// the fills take the throughput ops: with 4 bulk waves on a SIMD a wave needs
+// a small VGPR footprint to be placed at all (same-box A/B: 415 -> 424 M
+// verifies/s), while the lone-wave base chain keeps its zipped doubling.
+// BV_K12_LAT overrides for A/B runs.
+static int k12_lat_mask(bool busy) {
+  static const int env = [] {
+    const char *s = getenv("BV_K12_LAT");
+    return s ? atoi(s) : -1;
+  }();
+  return env >= 0 ? env : busy ? 1 : 3;
+}
+
 // kw = 0: the generator table (BV_GW-bit windows over 256 bits from
 // BV_GL-bit sub-tables, built once per process and device); kw = 8 / 12: the K8 / K12
 // GLV key tables (verify_core.h).  `sub`
 // is the K12 sub-table scratch (n_bases * BV_K12SUB_U32 words), `pscr` the
 // K12 prefix-product scratch (n_bases * BV_K12HALF_U32 / 2 words).
 hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
-                        uint32_t *bases_jac, uint32_t *sub, uint32_t *pscr, uint32_t *table) {
+                        uint32_t *bases_jac, uint32_t *sub, uint32_t *pscr, uint32_t *table, uint64_t n_items) {
   if (n_bases == 0) return hipSuccess;
   const int w = kw == 0 ? BV_GL : kw == 8 ? BV_KW : BV_K12L;
   const int nwin = kw == 0 ? BV_GNSUB : kw == 8 ? BV_KNWIN : BV_K12NSUB;
-  hipLaunchKernelGGL(k_table_bases, grid1(n_bases, 64), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w, nwin);
+  // K12 (large batches) builds beside the bulk kernels on a busy chip, where
+  // a kernel's VGPR footprint decides when its waves get a SIMD: there the
+  // throughput point ops (fewer VGPRs) win; elsewhere the zipped ones.
+  const int lat = kw == 12 ? k12_lat_mask(!lat_variant(n_items)) : 3;
+  if (lat & 1)
+    hipLaunchKernelGGL(k_table_bases<true>, grid1(n_bases, 64), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w,
+                       nwin);
+  else
+    hipLaunchKernelGGL(k_table_bases<false>, grid1(n_bases, 64), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w,
+                       nwin);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (kw == 0) {  // n_bases == 1 (G); `pscr` holds BV_GPAIR_BLOCKS blocks x 4096 fe
@@ -885,8 +912,12 @@ hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t
     hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
                        dim3(256), 0, st, bases_jac, bstatus, table);
   } else {
-    hipLaunchKernelGGL((k_table_fill<BV_K12L, BV_K12NSUB, false, 1 << BV_K12L>), dim3(BV_K12NSUB, n_bases),
-                       dim3(1 << BV_K12L), 0, st, bases_jac, bstatus, sub);
+    if (lat & 2)
+      hipLaunchKernelGGL((k_table_fill<BV_K12L, BV_K12NSUB, false, 1 << BV_K12L, true>), dim3(BV_K12NSUB, n_bases),
+                         dim3(1 << BV_K12L), 0, st, bases_jac, bstatus, sub);
+    else
+      hipLaunchKernelGGL((k_table_fill<BV_K12L, BV_K12NSUB, false, 1 << BV_K12L, false>), dim3(BV_K12NSUB, n_bases),
+                         dim3(1 << BV_K12L), 0, st, bases_jac, bstatus, sub);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_table_pair<BV_K12W, BV_K12L, BV_K12NWIN>), dim3(BV_K12NWIN, n_bases), dim3(256), 0, st, sub,
@@ -968,7 +999,7 @@ size_t kc_pscr_bytes() {
 hipError_t build_kc(hipStream_t st, uint32_t n, const uint32_t *kxy, const uint8_t *kst, uint32_t *bases_jac,
                     uint32_t *sub, uint32_t *pscr, const uint64_t *tabs) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_table_bases, grid1(n, 64), dim3(64), 0, st, n, kxy, kst, bases_jac, BV_KCL, BV_KCNSUB);
+  hipLaunchKernelGGL(k_table_bases<true>, grid1(n, 64), dim3(64), 0, st, n, kxy, kst, bases_jac, BV_KCL, BV_KCNSUB);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_table_fill<BV_KCL, BV_KCNSUB, false>), dim3(BV_KCNSUB * ((1u << BV_KCL) / 256u), n),

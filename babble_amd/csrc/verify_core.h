@@ -125,6 +125,7 @@ DEV void key_decode_one(uint32_t k, const uint8_t *kbytes, const uint64_t *koff,
 // ---------------------------------------------------------------------------
 // B_j = 2^(w j) P_b (Jacobian, 24 words each), j < nwin: a serial doubling
 // chain per base.
+template <bool LAT = false>
 DEV void table_bases_one(uint32_t b, const uint32_t *bxy, uint32_t *bases_jac, int w, int nwin) {
   gej P;
   fe_load(P.X, bxy + 16 * b);
@@ -136,21 +137,22 @@ DEV void table_bases_one(uint32_t b, const uint32_t *bxy, uint32_t *bases_jac, i
     fe_store(out + 24 * j + 8, P.Y);
     fe_store(out + 24 * j + 16, P.Z);
     if (j + 1 < nwin) {
-      for (int k = 0; k < w; k++) gej_double_lat(P, P);  // one wave per 64 keys: latency bound
+      for (int k = 0; k < w; k++) gej_double_sel<LAT>(P, P);  // one wave per 64 keys: latency bound
     }
   }
 }
 
 // d * B (B affine), MSB-first double-and-add over `bits` bits of d.  The
 // returned Z is 1 for d == 0 so it can join a batch inversion.
+template <bool LAT = false>
 DEV void table_point(gej &R, bool &inf, fe &Z, const fe &bx, const fe &by, uint32_t d, int bits) {
   inf = true;
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
   fe_set(R.Z, 0);
   for (int bit = bits - 1; bit >= 0; bit--) {
-    if (!inf) gej_double_lat(R, R);  // few waves per SIMD in the fill kernels
-    if ((d >> bit) & 1) gej_add_ge_lat(R, inf, bx, by);
+    if (!inf) gej_double_sel<LAT>(R, R);
+    if ((d >> bit) & 1) gej_add_ge_sel<LAT>(R, inf, bx, by);
   }
   if (inf) fe_set(Z, 1);
   else Z = R.Z;
