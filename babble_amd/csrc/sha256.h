@@ -199,29 +199,28 @@ DEV void sha256_schedule_wk(uint32_t *wk, const uint32_t w[16], uint32_t stride 
   }
 }
 
-// The 64 rounds of one block from a precomputed W + K schedule.
-// An 8-trip loop of 8 rounds (the state rotation maps onto itself every 8
-// rounds, so no register moves): small code for a latency-bound single
-// wave, whose instruction cache is shared with the rest of its kernel.
+// The 64 rounds of one block from a precomputed W + K schedule, for a
+// latency-bound single wave (k_ev_hash_chain).  Fully unrolled, and round
+// i + 1's h + K + W (its h is round i's g) is formed during round i, off the
+// e -> e' chain: e' = d + (hkw + S1(e) + Ch(e, f, g)).  One wave, 4 lanes:
+// 1.66 us per block against 2.51 us for an 8-trip loop of 8 rounds
+// (tools/ubench_sha.hip, profiles/r02_ubench_sha_lat.txt).
 DEV void sha256_rounds_wk(uint32_t h[8], const uint32_t *wk, uint32_t stride = 4) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#pragma unroll 1
-  for (int r = 0; r < 64; r += 8) {
-    const uint32_t *q = wk + (r >> 2) * stride;
+  uint32_t hkw = hh + wk[0];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const uint32_t t1 = hh + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g)) +
-                          q[(u >> 2) * stride + (u & 3)];
-      const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, b, c);
-      hh = g;
-      g = f;
-      f = e;
-      e = d + t1;
-      d = c;
-      c = b;
-      b = a;
-      a = t1 + t2;
-    }
+  for (int i = 0; i < 64; i++) {
+    const uint32_t t1 = hkw + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g));
+    if (i < 63) hkw = g + wk[((i + 1) >> 2) * stride + ((i + 1) & 3)];
+    const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, b, c);
+    hh = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
   }
   h[0] += a;
   h[1] += b;
