@@ -25,8 +25,8 @@
 
 namespace {
 
-constexpr uint32_t kNarrowLevel = 1024;  // events per level run by k_ev_hash_chain
-constexpr uint32_t kChainCap = 1024;     // events per k_ev_hash_chain launch (EVC_CAP)
+constexpr uint32_t kNarrowLevel = 768;   // events per level run by k_ev_hash_chain (<= kChainCap)
+constexpr uint32_t kChainCap = 768;      // events per k_ev_hash_chain launch (EVC_CAP)
 constexpr size_t kChunk = 16ull << 20;  // staged bytes per PCIe piece / event chunk
 
 int validate(bv_ctx *ctx, const bv_event_batch *b) {
@@ -182,8 +182,8 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
       case TX: *lo = t0 * g.unit; *hi = t1 * g.unit; break;
       case TX1: *lo = t0 * g.unit; *hi = (t1 + 1) * g.unit; break;
       case TXB: *lo = n_tx ? eb->tx_off[t0] : 0; *hi = n_tx ? eb->tx_off[t1] : 0; break;
-      case ITX: *lo = eb->itx_off[e0]; *hi = eb->itx_off[e1]; break;
-      case BSIG: *lo = eb->bsig_off[e0]; *hi = eb->bsig_off[e1]; break;
+      case ITX: *lo = eb->itx_off ? eb->itx_off[e0] : 0; *hi = eb->itx_off ? eb->itx_off[e1] : 0; break;
+      case BSIG: *lo = eb->bsig_off ? eb->bsig_off[e0] : 0; *hi = eb->bsig_off ? eb->bsig_off[e1] : 0; break;
     }
     *hi = std::min(*hi, g.n);
     *lo = std::min(*lo, *hi);

@@ -240,6 +240,7 @@ DEV void ev_midstate(uint64_t e, const uint8_t *bodies, const uint64_t *offs, co
 
 // digest words as stored by sha256_one: the 32 big-endian digest bytes
 DEV void ev_digest_words(uint32_t out[8], const uint32_t h[8]) {
+#pragma unroll
   for (int k = 0; k < 8; k++) out[k] = bswap32(h[k]);
 }
 
@@ -264,6 +265,7 @@ DEV uint32_t evj_hexnib4(uint32_t n) {
 // evj_hex32 over digest words (byte c of wd[k] = digest byte 4k+c): the 64
 // hex characters as 16 little-endian words (memory order)
 DEV void evj_hex32_words(uint32_t out[16], const uint32_t wd[8]) {
+#pragma unroll
   for (int k = 0; k < 8; k++) {
     const uint32_t hi = evj_hexnib4((wd[k] >> 4) & 0x0F0F0F0Fu), lo = evj_hexnib4(wd[k] & 0x0F0F0F0Fu);
     out[2 * k] = evj_perm(lo, hi, 0x05010400u);      // hi0 lo0 hi1 lo1
@@ -276,11 +278,13 @@ DEV void evj_hex32_words(uint32_t out[16], const uint32_t wd[8]) {
 DEV void evj_put64(uint32_t *buf, uint32_t rel, const uint32_t v[16]) {
   const uint32_t q = rel >> 2, sh = (rel & 3) * 8;
   if (sh == 0) {
+#pragma unroll
     for (int k = 0; k < 16; k++) buf[q + k] = v[k];
     return;
   }
   const uint32_t keep = (1u << sh) - 1u;
   buf[q] = (buf[q] & keep) | (v[0] << sh);
+#pragma unroll
   for (int k = 1; k < 16; k++) buf[q + k] = (v[k - 1] >> (32 - sh)) | (v[k] << sh);
   buf[q + 16] = (buf[q + 16] & ~keep) | (v[15] >> (32 - sh));
 }

@@ -165,25 +165,25 @@ __global__ void __launch_bounds__(256) k_ev_mid(uint64_t count, const uint32_t *
 //  * prologue: the launch's events (<= EVC_CAP, host-guaranteed) get an LDS
 //    descriptor (tail location, hex positions, parents as LDS digest slots),
 //    built by the whole workgroup in parallel;
-//  * per level L:
-//    A  waves 1-3 move level L's body tails (padded to whole SHA-256
-//       blocks) and midstates (k_ev_mid), loaded into their registers during
-//       level L-1, to LDS, then issue the loads for level L+1;
+//  * per level L (tails and midstates double-buffered: level L in buffer L & 1):
 //    B  lane i splices the i-th event's parents' hex into its LDS tail from
 //       the LDS digest cache (parents hashed by an earlier launch: HBM);
 //    C  one lane per (event, block) expands the block's W+K schedule into LDS
 //       (interleaved across events, so the round lanes read distinct banks);
-//    D  lane i runs the 64 rounds per block from its midstate; the digest
+//    D  lane i runs the 64 rounds per block from its midstate (registers
+//       only: sha256_rounds_wk, 1.66 us per block on one wave); the digest
 //       goes to the LDS cache;
-//  Measured (1000 events, 4 creators, 249 levels of 6 tail blocks): ~22 us
-//  per level, ~17 of it the rounds (about 3 us per block on one wave).
+//    A  beside D, waves 1-3 move level L+1's body tails (padded to whole
+//       SHA-256 blocks) and midstates (k_ev_mid), loaded into their
+//       registers during level L, into the other buffer, then issue the
+//       loads for level L+2;
 //  * epilogue: the launch's digests go to HBM (coalesced).
 // Events past EVC_SLOTS / EVC_WEV in a level, or with tails longer than
 // EVC_SLOT_DW or more than EVC_WBLK blocks, take the same steps with the
 // schedule inline (and from HBM when not in LDS).
 #define EVC_SLOTS 64
 #define EVC_SLOT_DW 128
-#define EVC_CAP 1024
+#define EVC_CAP 768
 #define EVC_WEV 8    // events per level with LDS schedules
 #define EVC_WBLK 7   // tail blocks of an LDS event: 7 x 16 + 1 dwords fit a slot
 #define EVC_NT 256   // one wave per SIMD: the hashing lanes get the full register file (no spills)
@@ -266,10 +266,12 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
                                                         const uint32_t *__restrict__ ppos, uint8_t *__restrict__ bodies,
                                                         const uint64_t *__restrict__ offs,
                                                         const uint32_t *__restrict__ mid, uint32_t *__restrict__ dig) {
-  __shared__ uint32_t sBody[EVC_SLOTS * EVC_SLOT_DW];  // 32 KB: the level's body tails
-  __shared__ uint32_t sMid[EVC_SLOTS * 8];             //  2 KB: the level's midstates
-  __shared__ uint32_t sDig[EVC_CAP * 8];               // 32 KB: digests hashed in this launch
-  __shared__ uint32_t sDesc[EVC_CAP * EVC_DESC];       // 48 KB: per-event descriptors
+  // double-buffered (level L in buffer L & 1): waves 1-3 stage level L+1
+  // while wave 0 runs level L's rounds
+  __shared__ uint32_t sBodyB[2 * EVC_SLOTS * EVC_SLOT_DW];  // 64 KB: body tails
+  __shared__ uint32_t sMidB[2 * EVC_SLOTS * 8];             //  4 KB: midstates
+  __shared__ uint32_t sDig[EVC_CAP * 8];                    // 24 KB: digests hashed in this launch
+  __shared__ uint32_t sDesc[EVC_CAP * EVC_DESC];            // 36 KB: per-event descriptors
   // 14 KB: W+K schedules of the level, [block][16-byte chunk][event][4]
   // (lanes in lockstep read distinct banks)
   __shared__ uint32_t sWK[EVC_WEV * EVC_WBLK * 64];
@@ -302,13 +304,15 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
   }
   __syncthreads();
   uint32_t pf[EVC_PF + EVC_PM];
-  if (t >= 64) evc_load(0, nl, t - 64, sLof, sDesc, bw, mid, pf);
+  if (t >= 64) {  // level 0 staged up front, level 1's loads issued
+    evc_load(0, nl, t - 64, sLof, sDesc, bw, mid, pf);
+    evc_stage(0, t - 64, sLof, sDesc, pf, sBodyB, sMidB);
+    evc_load(1, nl, t - 64, sLof, sDesc, bw, mid, pf);
+  }
+  __syncthreads();
   for (uint32_t L = 0; L < nl; L++) {
     const uint32_t lo = sLof[L], w = sLof[L + 1] - lo;
-    // ---- A: level L's padded tails and midstates -> LDS; loads for level L+1
-    if (t >= 64) evc_stage(L, t - 64, sLof, sDesc, pf, sBody, sMid);
-    __syncthreads();
-    if (t >= 64) evc_load(L + 1, nl, t - 64, sLof, sDesc, bw, mid, pf);
+    uint32_t *sBody = sBodyB + (L & 1) * EVC_SLOTS * EVC_SLOT_DW, *sMid = sMidB + (L & 1) * EVC_SLOTS * 8;
     // ---- B: parents' hex into the tails, one lane per (event, parent)
     for (uint32_t x = t; x < 2 * w; x += EVC_NT) {
       const uint32_t i = x >> 1, p = x & 1;
@@ -316,10 +320,12 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
       const uint32_t rel = d[6 + p];
       if (rel == EVJ_NOPOS) continue;
       const uint32_t ps = d[8 + p], q = d[10 + p];
-      uint32_t wd[8];
+      uint32_t wd[8];  // unrolled: a dynamically indexed array would live in scratch
       if (ps != EVJ_NOPOS) {  // separate loads: a selected pointer would be a FLAT access
+#pragma unroll
         for (int k = 0; k < 8; k++) wd[k] = sDig[8 * ps + k];
       } else {
+#pragma unroll
         for (int k = 0; k < 8; k++) wd[k] = dig[8 * (uint64_t)q + k];
       }
       if (evc_lds_event(i, d[4], d[5])) {
@@ -329,7 +335,9 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
       } else {
         const uint64_t a0 = (uint64_t)d[1] | ((uint64_t)d[2] << 32);
         uint8_t dd[32];
+#pragma unroll
         for (int k = 0; k < 8; k++)
+#pragma unroll
           for (int c = 0; c < 4; c++) dd[4 * k + c] = (uint8_t)(wd[k] >> (8 * c));  // words hold BE digest bytes
         evj_hex32(bodies + 4 * a0 + rel, dd);  // hashed from HBM in D
       }
@@ -349,27 +357,55 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
       }
     }
     __syncthreads();
+    // ---- A (waves 1-3, beside D): level L+1's tails and midstates into the
+    // other buffer (its loads were issued during level L-1), then the loads
+    // for level L+2.  Only when level L has <= 64 events: then D runs on
+    // wave 0 alone and waves 1-3 are free.
+    const bool beside = w <= 64;
+    if (beside && t >= 64 && L + 1 < nl) {
+      evc_stage(L + 1, t - 64, sLof, sDesc, pf, sBodyB + ((L + 1) & 1) * EVC_SLOTS * EVC_SLOT_DW,
+                sMidB + ((L + 1) & 1) * EVC_SLOTS * 8);
+      evc_load(L + 2, nl, t - 64, sLof, sDesc, bw, mid, pf);
+    }
     // ---- D: the rounds (the serial part)
     for (uint32_t i = t; i < w; i += EVC_NT) {
       const uint32_t *d = sDesc + EVC_DESC * (lo + i);
       const uint32_t sh = d[3] >> 24, nb = d[4], len = d[5];
       const uint32_t nblk = (uint32_t)sha256_nblocks(len);
-      uint32_t h[8];
-      if (i < EVC_SLOTS) {
-        for (int k = 0; k < 8; k++) h[k] = sMid[8 * i + k];
-      } else {
-        for (int k = 0; k < 8; k++) h[k] = mid[(uint64_t)EV_MID_U32 * d[0] + k];
-      }
-      if (i < EVC_WEV && evc_lds_event(i, nb, len)) {
-        for (uint32_t j = 0; j < nblk - nb; j++) sha256_rounds_wk(h, sWK + (j * 16 * EVC_WEV + i) * 4, 4 * EVC_WEV);
-      } else if (evc_lds_event(i, nb, len)) {  // in LDS, schedule inline (padded: whole blocks)
-        evc_hash_padded(h, sBody + i * EVC_SLOT_DW, sh, nblk - nb);
-      } else {
-        evc_hash_inline(h, bw + ((uint64_t)d[1] | ((uint64_t)d[2] << 32)), sh, len, nb, nblk);
-      }
       uint32_t wd[8];
-      ev_digest_words(wd, h);
+      if (i < EVC_WEV && evc_lds_event(i, nb, len)) {
+        // the common path stays in registers (the out-of-line paths below
+        // take their state by pointer, which would put it in scratch)
+        uint32_t h[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) h[k] = sMid[8 * i + k];
+        for (uint32_t j = 0; j < nblk - nb; j++) sha256_rounds_wk(h, sWK + (j * 16 * EVC_WEV + i) * 4, 4 * EVC_WEV);
+        ev_digest_words(wd, h);
+      } else {
+        uint32_t hm[8];
+        if (i < EVC_SLOTS) {
+#pragma unroll
+          for (int k = 0; k < 8; k++) hm[k] = sMid[8 * i + k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; k++) hm[k] = mid[(uint64_t)EV_MID_U32 * d[0] + k];
+        }
+        if (evc_lds_event(i, nb, len))  // in LDS, schedule inline (padded: whole blocks)
+          evc_hash_padded(hm, sBody + i * EVC_SLOT_DW, sh, nblk - nb);
+        else
+          evc_hash_inline(hm, bw + ((uint64_t)d[1] | ((uint64_t)d[2] << 32)), sh, len, nb, nblk);
+        ev_digest_words(wd, hm);
+      }
+#pragma unroll
       for (int k = 0; k < 8; k++) sDig[8 * (lo + i) + k] = wd[k];
+    }
+    if (!beside && L + 1 < nl) {  // a wide level: stage the next one after its rounds
+      __syncthreads();
+      if (t >= 64) {
+        evc_stage(L + 1, t - 64, sLof, sDesc, pf, sBodyB + ((L + 1) & 1) * EVC_SLOTS * EVC_SLOT_DW,
+                  sMidB + ((L + 1) & 1) * EVC_SLOTS * 8);
+        evc_load(L + 2, nl, t - 64, sLof, sDesc, bw, mid, pf);
+      }
     }
     __syncthreads();
   }

@@ -21,9 +21,10 @@ from oracle import gosemantics as gs
 from tests.emu import emu
 
 
-def random_wire(seed, n=300):
+def random_wire(seed, n=300, in_batch=True):
     """(EventWireBatch, oracle EventBodies, signatures as (pre, r, s)):
-    parents reference earlier events of the batch or known hashes."""
+    parents reference earlier events of the batch (unless not `in_batch`)
+    or known hashes."""
     rng = random.Random(seed)
     b = E.EventBatchBuilder()
     keys = [bytes(rng.getrandbits(8) for _ in range(rng.choice([65, 65, 65, 33, 0, 70]))) for _ in range(5)]
@@ -37,7 +38,7 @@ def random_wire(seed, n=300):
             if r < 0.2 or e == 0:
                 parents.append(None)
                 pstr.append("")
-            elif r < 0.5:
+            elif r < 0.5 or not in_batch:
                 h = bytes(rng.getrandbits(8) for _ in range(32))
                 parents.append(("hash", h))
                 pstr.append(gs.EncodeToString(h))
@@ -134,6 +135,29 @@ def test_verify_events_edge_cases_digests():
             wire, want, wd = random_wire(seed, n=500)
             res = v.verify_events(wire)
             assert [d.tobytes() for d in res.msg_hash] == wd
+    finally:
+        v.close()
+
+
+@pytest.mark.gpu
+def test_verify_events_chunk_boundaries(monkeypatch):
+    """Bulk batches (no in-batch parents) stage their per-event fields in
+    event chunks (bv_events.cpp); a tiny chunk size puts chunk boundaries
+    through nil / empty transaction lists, nil transactions and ITX /
+    BlockSignature fragments: digests equal the oracle's, statuses and bits
+    equal the single-chunk run's."""
+    from babble_amd.verifier import Verifier
+
+    v = Verifier(0)
+    try:
+        for seed in (6, 7):
+            wire, want, wd = random_wire(seed, n=1100, in_batch=False)
+            monkeypatch.setenv("BV_EV_CHUNK_MB", "0")
+            one = v.verify_events(wire)
+            monkeypatch.setenv("BV_EV_CHUNK_MB", "0.001")  # 256-event chunks
+            many = v.verify_events(wire)
+            assert [d.tobytes() for d in many.msg_hash] == wd
+            assert np.array_equal(many.status, one.status) and np.array_equal(many.accept_bits, one.accept_bits)
     finally:
         v.close()
 
