@@ -10,11 +10,15 @@ producing status bytes and the accept bitmask (the SURVEY §8d C2 workload:
 1M Events, 64 creators, one 64-byte transaction each).  With N > 1 ranks
 (torch.distributed.run, one process per GPU) every rank verifies its own
 1M-event shard (weak scaling) and the per-rank accept bitmasks are
-all-gathered over RCCL inside the timed step.
+all-gathered over RCCL inside the timed step.  Steps are issued back to
+back (asynchronous calls; the library starts a ctx's call when its previous
+one is done), so the host's per-call work overlaps the device's, as in a
+service that streams batches; the timed region is closed by synchronize.
 
 Rank 0 prints one JSON line.  `value` is the headline above.  Beside it:
   * `roofline` — the two verify kernels (k_verify_g + k_verify_q), timed with
-    the library's HIP events on the stream they run on; see ROOFLINE below;
+    the library's HIP events on the stream they run on (the last timed
+    step); see ROOFLINE below;
   * `warm` — the same batches with BV_F_KEY_CACHE (validator tables kept in
     HBM across calls; Babble's validator set is stable), every other piece of
     work still done per step;
@@ -168,7 +172,12 @@ def expected_words(rank: int, n: int):
     return np.concatenate([packed, np.zeros(words * 8 - len(packed), np.uint8)]).view(np.uint64)
 
 
-def timed_steps(step, steps: int, warmup: int, world: int, dist, local: int):
+def timed_steps(step, steps: int, warmup: int, world: int, dist, local: int, ver):
+    """K steps issued back to back (each a full asynchronous VerifyBatch; the
+    library orders a ctx's calls on the device, so step k+1 starts when step
+    k is done and the host's launch work overlaps the device's), bracketed
+    by barrier + synchronize.  The per-kernel breakdown is the library's HIP
+    events of the last timed step, read after the closing synchronize."""
     import torch
 
     for _ in range(warmup):
@@ -178,12 +187,15 @@ def timed_steps(step, steps: int, warmup: int, world: int, dist, local: int):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tms = [step() for _ in range(steps)]
+    for _ in range(steps):
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    ver.sync()
+    tms = [ver.timing()]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -228,13 +240,12 @@ def main():
 
     def step_with(ver):
         def step():
-            ver.verify_device(dev)  # synchronous
-            if world > 1:
+            ver.verify_device(dev, sync=False)  # on torch's current stream
+            if world > 1:  # ordered after the verify on the same stream
                 dist.all_gather_into_tensor(gathered, dev.accept_bits)
-            return ver.timing()
         return step
 
-    elapsed, tms = timed_steps(step_with(v), args.steps, args.warmup, world, dist, local)
+    elapsed, tms = timed_steps(step_with(v), args.steps, args.warmup, world, dist, local, v)
     res = dev.result()
     want = expected_words(rank, args.events)
     if not np.array_equal(res.accept_bits, want):
@@ -334,7 +345,7 @@ def warm_leg(args, dev, world, dist, local, step_with):
     vc.verify_device(dev)
     cold_ms = (time.perf_counter() - t0) * 1e3
     builds = vc.timing()["kc_builds"]
-    elapsed, tms = timed_steps(step_with(vc), args.steps, 1, 1, None, local)
+    elapsed, tms = timed_steps(step_with(vc), args.steps, 1, 1, None, local, vc)
     res = dev.result()
     assert np.array_equal(res.accept_bits, expected_words(0, args.events))
     out = {"value": args.events * args.steps / elapsed, "unit": "verifies/s",

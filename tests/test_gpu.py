@@ -146,6 +146,15 @@ def test_host_entry_item_order(verifier):
     check_against_oracle(verifier, dataclasses.replace(b, item_msg=late))
 
 
+def test_throughput_variants_above_latency_threshold(verifier):
+    """Batches of <= 128k items take the verify kernels' latency variants
+    (zipped point ops), larger ones the throughput variants: just above the
+    threshold (a ragged last word), the C4 mix, K12 tables, bit-exact."""
+    b = synth.adversarial(131_072 + 64 + 5, seed=14, n_creators=16, scale_per_million=MIX)
+    check_against_oracle(verifier, b)
+    assert verifier.timing()["key_path"] == 12
+
+
 def test_k8_tables_forced_by_flag():
     """BV_F_K8 keeps the 8-bit key tables on a batch that would take K12."""
     from babble_amd.verifier import Verifier
