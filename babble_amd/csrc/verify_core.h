@@ -103,8 +103,25 @@ DEV void key_decode_one(uint32_t k, const uint8_t *kbytes, const uint64_t *koff,
   if (len == 0) {
     st = KS_EMPTY;
   } else if (len == 65 && kbytes[o] == 4) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // 17 aligned dword loads issued together (bytewise loads of an unaligned
+    // key serialise on memory latency: 80 us for one wave of 64 keys); the
+    // last dword may extend <= 7 bytes past the key (key_bytes is padded)
+    const uint32_t *w = (const uint32_t *)(kbytes + (o & ~(uint64_t)3));
+    const uint32_t sh = (uint32_t)(o & 3);
+    uint32_t d[18];
+#pragma unroll
+    for (int i = 0; i < 18; i++) d[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {  // big-endian bytes 1 + 4 (7 - i) .. and 33 + 4 (7 - i) ..
+      const uint32_t bx = 1 + 4 * (7 - i) + sh, by = 33 + 4 * (7 - i) + sh;
+      x.v[i] = bswap32(alignbyte(d[bx / 4 + 1], d[bx / 4], bx % 4));
+      y.v[i] = bswap32(alignbyte(d[by / 4 + 1], d[by / 4], by % 4));
+    }
+#else
     fe_load_be(x, kbytes + o + 1);
     fe_load_be(y, kbytes + o + 33);
+#endif
     if (!fe_ge_p(x) && !fe_ge_p(y)) {
       fe y2, x3, seven;
       fe_sqr(y2, y);

@@ -137,7 +137,9 @@ int bv_verify_batch(bv_ctx *ctx, const bv_batch *batch, bv_result *result);
 /* Same, with every bv_batch / bv_result pointer in device memory of the ctx's
  * device (inputs already resident in HBM).  `stream` is a hipStream_t (NULL =
  * the ctx stream); the call returns after the work is enqueued when
- * `async` != 0, else after it completes. */
+ * `async` != 0, else after it completes.  msg_bytes and key_bytes must stay
+ * readable for 64 bytes past their last byte (the kernels read them with
+ * aligned vector loads; the host entry points pad their staging copies). */
 int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresult,
                            void *stream, int async);
 /* Calls on one ctx are ordered on the device whatever their streams: a call's
