@@ -127,6 +127,46 @@ int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e) {
     if (_e != hipSuccess) return bv_fail(ctx, code, what, _e); \
   } while (0)
 
+int bv_wait_all(bv_ctx *ctx) {
+  for (auto &sl : ctx->slot)
+    if (sl.has_done) HIPCHK(hipEventSynchronize(sl.done), BV_E_LAUNCH, "sync previous calls");
+  for (auto &sl : ctx->slot) sl.uncovered.clear();
+  return BV_OK;
+}
+
+int bv_slot_begin(bv_ctx *ctx, hipStream_t st, const bv_batch *b, const bv_result *res) {
+  bv_ctx::Slot &other = ctx->S();
+  ctx->cur ^= 1;
+  bv_ctx::Slot &sl = ctx->S();
+  if (sl.has_done) HIPCHK(hipStreamWaitEvent(st, sl.done, 0), BV_E_LAUNCH, "order after the slot's last call");
+  // The caller's result buffers: a call writing buffers that a call still in
+  // flight on the other slot writes (e.g. the same DeviceBatch issued on two
+  // streams) is ordered after that slot's last call, as if serial.
+  const void *p[3] = {res->msg_hash, res->status, res->accept_bits};
+  const uint64_t n[3] = {b->n_msgs * 32, b->n_items, (b->n_items + 63) / 64 * 8};
+  std::array<uintptr_t, 6> r{};
+  for (int i = 0; i < 3; i++)
+    if (p[i] && n[i]) r[2 * i] = (uintptr_t)p[i], r[2 * i + 1] = (uintptr_t)p[i] + n[i];
+  bool overlap = other.uncovered.size() >= 8;
+  for (const auto &u : other.uncovered)
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) overlap |= u[2 * j] < r[2 * i + 1] && r[2 * i] < u[2 * j + 1];
+  if (overlap) {
+    HIPCHK(hipStreamWaitEvent(st, other.done, 0), BV_E_LAUNCH, "order after an overlapping call");
+    other.uncovered.clear();
+  }
+  if (std::find(sl.uncovered.begin(), sl.uncovered.end(), r) == sl.uncovered.end()) sl.uncovered.push_back(r);
+  return BV_OK;
+}
+
+int bv_mark_done(bv_ctx *ctx, hipStream_t st) {
+  HIPCHK(hipEventRecord(ctx->S().done, st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
+  ctx->S().has_done = true;
+  ctx->has_done = true;
+  return BV_OK;
+}
+
 static const uint8_t kGenerator[64] = {
     0x79, 0xBE, 0x66, 0x7E, 0xF9, 0xDC, 0xBB, 0xAC, 0x55, 0xA0, 0x62, 0x95, 0xCE, 0x87, 0x0B, 0x07,
     0x02, 0x9B, 0xFC, 0xDB, 0x2D, 0xCE, 0x28, 0xD9, 0x59, 0xF2, 0x81, 0x5B, 0x16, 0xF8, 0x17, 0x98,
@@ -205,8 +245,11 @@ static int create_impl(bv_ctx *ctx) {
   HIPCHK(hipStreamCreateWithPriority(&ctx->kstream, hipStreamNonBlocking, hi), BV_E_NODEVICE, "hipStreamCreate");
   HIPCHK(hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
   HIPCHK(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
-  for (auto &e : ctx->ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
+  for (auto &sl : ctx->slot)
+    for (auto &e : sl.ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
   HIPCHK(hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming), BV_E_NODEVICE, "hipEventCreate");
+  for (auto &sl : ctx->slot)
+    HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), BV_E_NODEVICE, "hipEventCreate");
   ctx->chunk_ev.resize(64);
   for (auto &e : ctx->chunk_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming), BV_E_NODEVICE, "event");
   ctx->g_table = gtable_acquire(ctx->device, ctx->stream);
@@ -252,19 +295,24 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   for (hipStream_t s : {ctx->stream, ctx->kstream, ctx->sstream, ctx->cstream})
     if (s) (void)hipStreamSynchronize(s);
   if (ctx->g_table) gtable_release(ctx->device);
-  DevBuf *bufs[] = {&ctx->d_in,      &ctx->digests,  &ctx->kstatus,  &ctx->kxy,     &ctx->bases_jac,
-                    &ctx->key_sub,   &ctx->key_pscr, &ctx->key_table, &ctx->scratch, &ctx->u12,
-                    &ctx->rg,        &ctx->status,   &ctx->bits,     &ctx->kc_tabs, &ctx->kc_kst,
-                    &ctx->kc_kxy,    &ctx->kc_btabs, &ctx->ev_lens,  &ctx->ev_ppos,  &ctx->ev_offs,
-                    &ctx->ev_bodies, &ctx->ev_tmp,   &ctx->ev_iota, &ctx->ev_mid};
+  DevBuf *bufs[] = {&ctx->d_in, &ctx->kc_kxy,  &ctx->kc_btabs, &ctx->ev_lens,
+                    &ctx->ev_ppos,   &ctx->ev_offs, &ctx->ev_bodies, &ctx->ev_tmp, &ctx->ev_iota, &ctx->ev_mid};
   for (auto *b : bufs) b->release();
+  for (auto &sl : ctx->slot) {
+    DevBuf *sb[] = {&sl.digests,   &sl.kstatus, &sl.kxy, &sl.bases_jac, &sl.key_sub, &sl.key_pscr,
+                    &sl.key_table, &sl.scratch, &sl.u12, &sl.rg,        &sl.status,  &sl.bits,
+                    &sl.kc_tabs,   &sl.kc_kst};
+    for (auto *b : sb) b->release();
+    sl.pin_small.release();
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
   for (auto &s : ctx->kc_slots)
     if (s.table) (void)hipFree(s.table);
   ctx->pin_in.release();
   ctx->pin_out.release();
-  ctx->pin_small.release();
-  for (auto &e : ctx->ev)
-    if (e) (void)hipEventDestroy(e);
+  for (auto &sl : ctx->slot)
+    for (auto &e : sl.ev)
+      if (e) (void)hipEventDestroy(e);
   for (auto &e : ctx->chunk_ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
@@ -285,7 +333,7 @@ extern "C" int bv_get_timing(const bv_ctx *ctx, bv_timing *out) {
 // ---------------------------------------------------------------------------
 // Resolves the batch's keys against the cache: hits need nothing; valid
 // misses get a KC table built now (cold); malformed keys are remembered with
-// their status and no table.  On success fills ctx->kc_tabs / kc_kst (device,
+// their status and no table.  On success fills ctx->S().kc_tabs / kc_kst (device,
 // per batch key) and returns BV_OK with *use = true; *use = false when the
 // batch cannot use the cache (too many keys, budget) and must take the
 // per-batch path.  hkb/hko: host copies of the key bytes; dkb/dko: device.
@@ -293,6 +341,8 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
                       const uint64_t *dko, hipStream_t st, bool *use) {
   *use = false;
   if (n_keys == 0 || n_keys > kKcMaxBatchKeys) return BV_OK;
+  if (ctx->S().has_done)  // the slot's pin_small may still feed its previous (async) call
+    HIPCHK(hipEventSynchronize(ctx->S().done), BV_E_LAUNCH, "sync slot");
   ctx->kc_clock++;
   std::vector<int> slot_of(n_keys, -1);
   std::vector<uint32_t> miss;
@@ -312,12 +362,12 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
   if (!miss.empty()) {
     // statuses of the missing keys: k_key_decode on the device (the product
     // path for elliptic.Unmarshal), then one small synchronous copy back
-    HIPCHK(ctx->kstatus.ensure(n_keys), BV_E_OOM, "alloc kstatus");
-    HIPCHK(ctx->kxy.ensure((uint64_t)n_keys * 64), BV_E_OOM, "alloc kxy");
-    HIPCHK(bvk::key_decode(st, n_keys, dkb, dko, ctx->kstatus.as<uint8_t>(), ctx->kxy.as<uint32_t>()), BV_E_LAUNCH,
+    HIPCHK(ctx->S().kstatus.ensure(n_keys), BV_E_OOM, "alloc kstatus");
+    HIPCHK(ctx->S().kxy.ensure((uint64_t)n_keys * 64), BV_E_OOM, "alloc kxy");
+    HIPCHK(bvk::key_decode(st, n_keys, dkb, dko, ctx->S().kstatus.as<uint8_t>(), ctx->S().kxy.as<uint32_t>()), BV_E_LAUNCH,
            "k_key_decode");
     std::vector<uint8_t> kst(n_keys);
-    HIPCHK(hipMemcpyAsync(kst.data(), ctx->kstatus.p, n_keys, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h kst");
+    HIPCHK(hipMemcpyAsync(kst.data(), ctx->S().kstatus.p, n_keys, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h kst");
     HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
     std::vector<uint32_t> build;  // valid misses
     for (uint32_t k : miss)
@@ -333,7 +383,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
           victim = (int)i;
       }
       if (victim < 0) return BV_OK;
-      HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync before eviction");
+      if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // sync before eviction
       auto &s = ctx->kc_slots[victim];
       HIPCHK(hipFree(s.table), BV_E_LAUNCH, "free cached table");
       s.table = nullptr;
@@ -378,43 +428,42 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
     const uint32_t G = std::min<uint32_t>(kKcBuildGroup, (uint32_t)std::max<size_t>(build.size(), 1));
     HIPCHK(ctx->kc_kxy.ensure((uint64_t)G * 64), BV_E_OOM, "alloc kc kxy");
     HIPCHK(ctx->kc_btabs.ensure((uint64_t)G * 8), BV_E_OOM, "alloc kc tabs");
-    HIPCHK(ctx->bases_jac.ensure((uint64_t)G * kBasesPerKey * 96), BV_E_OOM, "alloc bases");
-    HIPCHK(ctx->key_sub.ensure((uint64_t)G * kKcSubBytes), BV_E_OOM, "alloc kc sub-tables");
-    HIPCHK(ctx->key_pscr.ensure((uint64_t)G * bvk::kc_pscr_bytes()), BV_E_OOM, "alloc kc prefix scratch");
-    HIPCHK(ctx->pin_small.ensure(4096), BV_E_OOM, "alloc pinned");
+    HIPCHK(ctx->S().bases_jac.ensure((uint64_t)G * kBasesPerKey * 96), BV_E_OOM, "alloc bases");
+    HIPCHK(ctx->S().key_sub.ensure((uint64_t)G * kKcSubBytes), BV_E_OOM, "alloc kc sub-tables");
+    HIPCHK(ctx->S().key_pscr.ensure((uint64_t)G * bvk::kc_pscr_bytes()), BV_E_OOM, "alloc kc prefix scratch");
+    HIPCHK(ctx->S().pin_small.ensure(4096), BV_E_OOM, "alloc pinned");
     for (size_t g0 = 0; g0 < build.size(); g0 += G) {
       const uint32_t n = (uint32_t)std::min<size_t>(G, build.size() - g0);
-      uint64_t *tabs = (uint64_t *)ctx->pin_small.p;
+      uint64_t *tabs = (uint64_t *)ctx->S().pin_small.p;
       HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");  // pin_small reuse
       for (uint32_t i = 0; i < n; i++) {
         const uint32_t k = build[g0 + i];
-        HIPCHK(hipMemcpyAsync(ctx->kc_kxy.as<uint8_t>() + 64ull * i, ctx->kxy.as<uint8_t>() + 64ull * k, 64,
+        HIPCHK(hipMemcpyAsync(ctx->kc_kxy.as<uint8_t>() + 64ull * i, ctx->S().kxy.as<uint8_t>() + 64ull * k, 64,
                               hipMemcpyDeviceToDevice, st),
                BV_E_LAUNCH, "gather kxy");
         tabs[i] = (uint64_t)(uintptr_t)ctx->kc_slots[slot_of[k]].table;
       }
       HIPCHK(hipMemcpyAsync(ctx->kc_btabs.p, tabs, n * 8ull, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d tabs");
-      HIPCHK(bvk::build_kc(st, n, ctx->kc_kxy.as<uint32_t>(), nullptr, ctx->bases_jac.as<uint32_t>(),
-                           ctx->key_sub.as<uint32_t>(), ctx->key_pscr.as<uint32_t>(), ctx->kc_btabs.as<uint64_t>()),
+      HIPCHK(bvk::build_kc(st, n, ctx->kc_kxy.as<uint32_t>(), nullptr, ctx->S().bases_jac.as<uint32_t>(),
+                           ctx->S().key_sub.as<uint32_t>(), ctx->S().key_pscr.as<uint32_t>(), ctx->kc_btabs.as<uint64_t>()),
              BV_E_LAUNCH, "KC key tables");
       builds += n;
     }
     HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
   }
   // per-batch arrays: table address and status of every batch key
-  HIPCHK(ctx->pin_small.ensure((uint64_t)n_keys * 9 + 64), BV_E_OOM, "alloc pinned");
-  HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync");  // pin_small may feed an earlier async call
-  uint64_t *tabs = (uint64_t *)ctx->pin_small.p;
+  HIPCHK(ctx->S().pin_small.ensure((uint64_t)n_keys * 9 + 64), BV_E_OOM, "alloc pinned");
+  uint64_t *tabs = (uint64_t *)ctx->S().pin_small.p;
   uint8_t *kst = (uint8_t *)(tabs + n_keys);
   for (uint32_t k = 0; k < n_keys; k++) {
     const auto &s = ctx->kc_slots[slot_of[k]];
     tabs[k] = (uint64_t)(uintptr_t)s.table;
     kst[k] = s.status;
   }
-  HIPCHK(ctx->kc_tabs.ensure((uint64_t)n_keys * 8), BV_E_OOM, "alloc kc tabs");
-  HIPCHK(ctx->kc_kst.ensure(n_keys), BV_E_OOM, "alloc kc kst");
-  HIPCHK(hipMemcpyAsync(ctx->kc_tabs.p, tabs, n_keys * 8ull, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d tabs");
-  HIPCHK(hipMemcpyAsync(ctx->kc_kst.p, kst, n_keys, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d kst");
+  HIPCHK(ctx->S().kc_tabs.ensure((uint64_t)n_keys * 8), BV_E_OOM, "alloc kc tabs");
+  HIPCHK(ctx->S().kc_kst.ensure(n_keys), BV_E_OOM, "alloc kc kst");
+  HIPCHK(hipMemcpyAsync(ctx->S().kc_tabs.p, tabs, n_keys * 8ull, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d tabs");
+  HIPCHK(hipMemcpyAsync(ctx->S().kc_kst.p, kst, n_keys, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d kst");
   ctx->timing.kc_hits = hits;
   ctx->timing.kc_builds = builds;
   ctx->timing.kc_keys = (uint32_t)ctx->kc_index.size();
@@ -427,11 +476,11 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
 // ---------------------------------------------------------------------------
 // Over device-resident inputs.  msg_hash/status/bits may be null (ctx
 // buffers are used).  Caller holds ctx->mu and has set the device.
-// `hashed`: the digests are already in ctx->digests (host entry point,
+// `hashed`: the digests are already in ctx->S().digests (host entry point,
 // hashed chunk by chunk as the bytes landed).  `kc`: use the key cache
 // arrays prepared by kc_prepare.  Every call starts after the previous call
-// on this ctx has finished on the device (ev_done), whatever its stream:
-// work buffers are shared between calls.
+// on this ctx that used the same work-buffer slot has finished on the device
+// (ctx->slot[].done), whatever its stream.
 // Phase A of a verify: batched s^-1 on the s^-1 stream after `s_ready` (s
 // and pre in HBM), key decode + per-batch key tables on the keys stream after
 // `keys_ready` (the keys in HBM).  The host entry points stage the keys
@@ -446,10 +495,10 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   if (n_keys > 0 && !b->key_off) return bv_fail(ctx, BV_E_ARGS, "null key_off");
   if (((uintptr_t)b->r_be | (uintptr_t)b->s_be) & 15)
     return bv_fail(ctx, BV_E_ARGS, "r_be/s_be must be 16-byte aligned");
-  HIPCHK(ctx->kstatus.ensure(std::max<uint32_t>(n_keys, 1)), BV_E_OOM, "alloc kstatus");
-  HIPCHK(ctx->kxy.ensure(std::max<uint32_t>(n_keys, 1) * 64ull), BV_E_OOM, "alloc kxy");
-  HIPCHK(ctx->scratch.ensure(std::max<uint64_t>(n_items, 1) * 32), BV_E_OOM, "alloc scratch");
-  HIPCHK(ctx->u12.ensure(std::max<uint64_t>(n_items, 1) * BV_U_STRIDE * 4), BV_E_OOM, "alloc u12");
+  HIPCHK(ctx->S().kstatus.ensure(std::max<uint32_t>(n_keys, 1)), BV_E_OOM, "alloc kstatus");
+  HIPCHK(ctx->S().kxy.ensure(std::max<uint32_t>(n_keys, 1) * 64ull), BV_E_OOM, "alloc kxy");
+  HIPCHK(ctx->S().scratch.ensure(std::max<uint64_t>(n_items, 1) * 32), BV_E_OOM, "alloc scratch");
+  HIPCHK(ctx->S().u12.ensure(std::max<uint64_t>(n_items, 1) * BV_U_STRIDE * 4), BV_E_OOM, "alloc u12");
 
   // Key path: the key cache when prepared; otherwise per-batch fixed-base
   // tables once a key signs enough items (K12 for large batches, K8 for
@@ -463,38 +512,44 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   ctx->table_mode = table_mode;
   ctx->key_w = key_w;
   if (table_mode) {
-    HIPCHK(ctx->rg.ensure(std::max<uint64_t>(n_items, 1) * kRgWords * 4), BV_E_OOM, "alloc R_G");
+    HIPCHK(ctx->S().rg.ensure(std::max<uint64_t>(n_items, 1) * kRgWords * 4), BV_E_OOM, "alloc R_G");
     if (!kc) {
       const uint64_t nk = std::max<uint32_t>(n_keys, 1);
-      HIPCHK(ctx->bases_jac.ensure(nk * kBasesPerKey * 96ull), BV_E_OOM, "alloc bases");
+      HIPCHK(ctx->S().bases_jac.ensure(nk * kBasesPerKey * 96ull), BV_E_OOM, "alloc bases");
       if (key_w == 12) {
-        HIPCHK(ctx->key_sub.ensure(nk * kK12SubBytes), BV_E_OOM, "alloc key sub-tables");
-        HIPCHK(ctx->key_pscr.ensure(nk * kK12PrefixBytes), BV_E_OOM, "alloc key prefix scratch");
+        HIPCHK(ctx->S().key_sub.ensure(nk * kK12SubBytes), BV_E_OOM, "alloc key sub-tables");
+        HIPCHK(ctx->S().key_pscr.ensure(nk * kK12PrefixBytes), BV_E_OOM, "alloc key prefix scratch");
       }
-      HIPCHK(ctx->key_table.ensure(nk * (key_w == 12 ? kK12TableBytes : kKTableBytes)), BV_E_OOM,
+      HIPCHK(ctx->S().key_table.ensure(nk * (key_w == 12 ? kK12TableBytes : kKTableBytes)), BV_E_OOM,
              "alloc key tables");
     }
   }
-  hipEvent_t *ev = ctx->ev;
+  hipEvent_t *ev = ctx->S().ev;
+  // The key statuses (k_key_decode) go on the s^-1 stream ahead of s^-1:
+  // k_verify_g reads them and is ordered after s^-1, while the key tables
+  // (kstream) may queue behind another in-flight call's build.
+  HIPCHK(hipStreamWaitEvent(ctx->sstream, keys_ready, 0), BV_E_LAUNCH, "fork");
+  HIPCHK(hipEventRecord(ev[E_START], ctx->sstream), BV_E_LAUNCH, "event");
+  if (!kc)
+    HIPCHK(bvk::key_decode(ctx->sstream, n_keys, b->key_bytes, b->key_off, ctx->S().kstatus.as<uint8_t>(),
+                           ctx->S().kxy.as<uint32_t>()),
+           BV_E_LAUNCH, "k_key_decode");
+  HIPCHK(hipEventRecord(ev[E_KDEC], ctx->sstream), BV_E_LAUNCH, "event");
   // s^-1 needs only s: concurrent with everything up to k_verify_g
   HIPCHK(hipStreamWaitEvent(ctx->sstream, s_ready, 0), BV_E_LAUNCH, "fork");
-  HIPCHK(hipEventRecord(ev[E_START], ctx->sstream), BV_E_LAUNCH, "event");
   // items per lane: kPrepM amortises the inversion in large batches; a small
   // batch spreads over ~64k lanes instead, since there the serial chain of
   // one lane (M products, the inversion, 2M products) is the latency
   const uint32_t M = (uint32_t)std::min<uint64_t>(kPrepM, std::max<uint64_t>(1, (n_items + 65535) / 65536));
-  HIPCHK(bvk::sinv(ctx->sstream, n_items, M, (const uint32_t *)b->s_be, b->pre, ctx->scratch.as<uint32_t>()),
+  HIPCHK(bvk::sinv(ctx->sstream, n_items, M, (const uint32_t *)b->s_be, b->pre, ctx->S().scratch.as<uint32_t>()),
          BV_E_LAUNCH, "k_sinv");
   HIPCHK(hipEventRecord(ev[E_SINV], ctx->sstream), BV_E_LAUNCH, "event");
-  HIPCHK(hipStreamWaitEvent(ctx->kstream, keys_ready, 0), BV_E_LAUNCH, "fork");
+  HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_KDEC], 0), BV_E_LAUNCH, "fork");
   if (!kc) {
-    HIPCHK(bvk::key_decode(ctx->kstream, n_keys, b->key_bytes, b->key_off, ctx->kstatus.as<uint8_t>(),
-                           ctx->kxy.as<uint32_t>()),
-           BV_E_LAUNCH, "k_key_decode");
     if (table_mode)
-      HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->kxy.as<uint32_t>(), ctx->kstatus.as<uint8_t>(),
-                               ctx->bases_jac.as<uint32_t>(), ctx->key_sub.as<uint32_t>(),
-                               ctx->key_pscr.as<uint32_t>(), ctx->key_table.as<uint32_t>(), n_items),
+      HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->S().kxy.as<uint32_t>(), ctx->S().kstatus.as<uint8_t>(),
+                               ctx->S().bases_jac.as<uint32_t>(), ctx->S().key_sub.as<uint32_t>(),
+                               ctx->S().key_pscr.as<uint32_t>(), ctx->S().key_table.as<uint32_t>(), n_items),
              BV_E_LAUNCH, "key tables");
   }
   HIPCHK(hipEventRecord(ev[E_KEYS], ctx->kstream), BV_E_LAUNCH, "event");
@@ -508,18 +563,18 @@ int bv_out_bufs(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   o->dig = (uint32_t *)d_msg_hash;
   if (hashed || !o->dig || ((uintptr_t)o->dig & 15)) {
-    HIPCHK(ctx->digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
-    o->dig = ctx->digests.as<uint32_t>();
+    HIPCHK(ctx->S().digests.ensure(std::max<uint64_t>(n_msgs, 1) * 32), BV_E_OOM, "alloc digests");
+    o->dig = ctx->S().digests.as<uint32_t>();
   }
   o->status = d_status;
   if (!o->status) {
-    HIPCHK(ctx->status.ensure(std::max<uint64_t>(n_items, 1)), BV_E_OOM, "alloc status");
-    o->status = ctx->status.as<uint8_t>();
+    HIPCHK(ctx->S().status.ensure(std::max<uint64_t>(n_items, 1)), BV_E_OOM, "alloc status");
+    o->status = ctx->S().status.as<uint8_t>();
   }
   o->bits = d_bits;
   if (!o->bits) {
-    HIPCHK(ctx->bits.ensure(std::max<uint64_t>((n_items + 63) / 64, 1) * 8), BV_E_OOM, "alloc bits");
-    o->bits = ctx->bits.as<uint64_t>();
+    HIPCHK(ctx->S().bits.ensure(std::max<uint64_t>((n_items + 63) / 64, 1) * 8), BV_E_OOM, "alloc bits");
+    o->bits = ctx->S().bits.as<uint64_t>();
   }
   return BV_OK;
 }
@@ -532,28 +587,28 @@ int bv_out_bufs(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_
 int bv_launch_items(bv_ctx *ctx, const bv_batch *b, const bv_out &o, hipStream_t st, bool kc, uint64_t lo,
                     uint64_t hi, int part) {
   const uint64_t n = b->n_items;
-  const uint8_t *kst = kc ? ctx->kc_kst.as<uint8_t>() : ctx->kstatus.as<uint8_t>();
+  const uint8_t *kst = kc ? ctx->S().kc_kst.as<uint8_t>() : ctx->S().kstatus.as<uint8_t>();
   const uint32_t *r32 = (const uint32_t *)b->r_be, *s32 = (const uint32_t *)b->s_be;
-  uint32_t *w = ctx->scratch.as<uint32_t>(), *u12 = ctx->u12.as<uint32_t>();
+  uint32_t *w = ctx->S().scratch.as<uint32_t>(), *u12 = ctx->S().u12.as<uint32_t>();
   const bool fused = kc && kFusedKc;  // key cache: G and Q parts in one kernel (R_G stays in registers)
   if (part == 1) {
     if (ctx->table_mode && !fused)
       HIPCHK(bvk::verify_g(st, n, lo, hi, b->item_key, r32, s32, b->pre, kst, b->item_msg, o.dig, w, u12,
-                           ctx->g_table, ctx->rg.as<uint32_t>()),
+                           ctx->g_table, ctx->S().rg.as<uint32_t>()),
              BV_E_LAUNCH, "k_verify_g");
     return BV_OK;
   }
   if (fused)
     HIPCHK(bvk::verify_gq(st, n, lo, hi, b->item_key, r32, s32, b->pre, kst, b->item_msg, o.dig, w, ctx->g_table,
-                          ctx->kc_tabs.as<uint64_t>(), o.status, o.bits),
+                          ctx->S().kc_tabs.as<uint64_t>(), o.status, o.bits),
            BV_E_LAUNCH, "k_verify_gq");
   else if (ctx->table_mode)
     HIPCHK(bvk::verify_q(st, ctx->key_w, n, lo, hi, b->item_key, r32, s32, b->pre, kst, u12,
-                         ctx->key_table.as<uint32_t>(), kc ? ctx->kc_tabs.as<uint64_t>() : nullptr,
-                         ctx->rg.as<uint32_t>(), o.status, o.bits),
+                         ctx->S().key_table.as<uint32_t>(), kc ? ctx->S().kc_tabs.as<uint64_t>() : nullptr,
+                         ctx->S().rg.as<uint32_t>(), o.status, o.bits),
            BV_E_LAUNCH, "k_verify_q");
   else
-    HIPCHK(bvk::verify_generic(st, n, lo, hi, b->item_key, r32, s32, b->pre, kst, ctx->kxy.as<uint32_t>(),
+    HIPCHK(bvk::verify_generic(st, n, lo, hi, b->item_key, r32, s32, b->pre, kst, ctx->S().kxy.as<uint32_t>(),
                                b->item_msg, o.dig, w, ctx->g_table, o.status, o.bits),
            BV_E_LAUNCH, "k_verify_generic");
   return BV_OK;
@@ -562,11 +617,11 @@ int bv_launch_items(bv_ctx *ctx, const bv_batch *b, const bv_out &o, hipStream_t
 int bv_item_pipe::upto(uint64_t end) {
   if (end <= done) return BV_OK;
   if (done == 0) {
-    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SINV], 0), BV_E_LAUNCH, "join");
-    HIPCHK(hipEventRecord(ctx->ev[E_SCALAR], st), BV_E_LAUNCH, "event");
-    HIPCHK(hipEventRecord(ctx->ev[E_G], st), BV_E_LAUNCH, "event");
-    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_KEYS], 0), BV_E_LAUNCH, "join");
-    HIPCHK(hipEventRecord(ctx->ev[E_JOINED], st), BV_E_LAUNCH, "event");
+    HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SINV], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipEventRecord(ctx->S().ev[E_SCALAR], st), BV_E_LAUNCH, "event");
+    HIPCHK(hipEventRecord(ctx->S().ev[E_G], st), BV_E_LAUNCH, "event");
+    HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_KEYS], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipEventRecord(ctx->S().ev[E_JOINED], st), BV_E_LAUNCH, "event");
   }
   for (int part = 1; part <= 2; part++) {
     const int r = bv_launch_items(ctx, b, o, st, kc, done, end, part);
@@ -579,20 +634,18 @@ int bv_item_pipe::upto(uint64_t end) {
 int bv_item_pipe::finish() {
   const uint64_t n = b->n_items;
   if (n == 0) {
-    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SINV], 0), BV_E_LAUNCH, "join");
-    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_KEYS], 0), BV_E_LAUNCH, "join");
-    for (int e : {E_SCALAR, E_G, E_JOINED}) HIPCHK(hipEventRecord(ctx->ev[e], st), BV_E_LAUNCH, "event");
+    HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SINV], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_KEYS], 0), BV_E_LAUNCH, "join");
+    for (int e : {E_SCALAR, E_G, E_JOINED}) HIPCHK(hipEventRecord(ctx->S().ev[e], st), BV_E_LAUNCH, "event");
   }
   const int r = upto(n);
   if (r != BV_OK) return r;
-  HIPCHK(hipEventRecord(ctx->ev[E_END], st), BV_E_LAUNCH, "event");
-  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
-  ctx->has_done = true;
-  return BV_OK;
+  HIPCHK(hipEventRecord(ctx->S().ev[E_END], st), BV_E_LAUNCH, "event");
+  return bv_mark_done(ctx, st);
 }
 
 // Phase B on `st` (after bv_run_keys): SHA-256 of the messages (unless
-// `hashed`: digests already in ctx->digests), then the verify kernels once
+// `hashed`: digests already in ctx->S().digests), then the verify kernels once
 // s^-1 and the key tables are ready; statuses and bits.  k_verify_g needs
 // no key table, so it runs while the keys stream still builds them.
 int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
@@ -602,7 +655,7 @@ int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
   bv_out o;
   int rc = bv_out_bufs(ctx, b, d_msg_hash, d_status, d_bits, hashed, &o);
   if (rc != BV_OK) return rc;
-  hipEvent_t *ev = ctx->ev;
+  hipEvent_t *ev = ctx->S().ev;
   HIPCHK(hipEventRecord(ev[E_FORK], st), BV_E_LAUNCH, "event");
   if (!hashed) HIPCHK(bvk::sha256(st, n_msgs, b->msg_bytes, b->msg_off, o.dig), BV_E_LAUNCH, "k_sha256");
   HIPCHK(hipEventRecord(ev[E_SHA], st), BV_E_LAUNCH, "event");
@@ -618,17 +671,15 @@ int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
   HIPCHK(hipEventRecord(ev[E_END], st), BV_E_LAUNCH, "event");
   if (d_msg_hash && (uint8_t *)o.dig != d_msg_hash)
     HIPCHK(hipMemcpyAsync(d_msg_hash, o.dig, n_msgs * 32, hipMemcpyDeviceToDevice, st), BV_E_LAUNCH, "copy digests");
-  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
-  ctx->has_done = true;
-  return BV_OK;
+  return bv_mark_done(ctx, st);
 }
 
-// The whole verify of a batch already in HBM on `st`.
+// The whole verify of a batch already in HBM on `st` (which has waited for
+// the last call on the current work-buffer slot: bv_slot_begin).
 int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc) {
-  if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order after previous call");
-  HIPCHK(hipEventRecord(ctx->ev[E_READY], st), BV_E_LAUNCH, "event");
-  int rc = bv_run_keys(ctx, b, ctx->ev[E_READY], ctx->ev[E_READY], kc);
+  HIPCHK(hipEventRecord(ctx->S().ev[E_READY], st), BV_E_LAUNCH, "event");
+  int rc = bv_run_keys(ctx, b, ctx->S().ev[E_READY], ctx->S().ev[E_READY], kc);
   if (rc != BV_OK) return rc;
   return bv_run_verify(ctx, b, d_msg_hash, d_status, d_bits, st, hashed, kc);
 }
@@ -639,7 +690,7 @@ static float elapsed(hipEvent_t a, hipEvent_t b) {
 }
 
 void bv_read_timing(bv_ctx *ctx) {
-  hipEvent_t *ev = ctx->ev;
+  hipEvent_t *ev = ctx->S().ev;
   bv_timing &t = ctx->timing;
   t.ms_sha256 = elapsed(ev[E_FORK], ev[E_SHA]);
   t.key_path = (uint32_t)ctx->key_w;
@@ -659,10 +710,10 @@ extern "C" int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_re
   hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
   ctx->timing = bv_timing{};
   bool kc = false;
+  if (bv_slot_begin(ctx, st, dbatch, dresult) != BV_OK) return BV_E_LAUNCH;
   if ((ctx->flags & BV_F_KEY_CACHE) && dbatch->n_keys && dbatch->n_keys <= kKcMaxBatchKeys) {
     // the cache is keyed by the raw key bytes: bring them (small) to the host
     const uint32_t nk = dbatch->n_keys;
-    if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order");
     std::vector<uint64_t> hko(nk + 1);
     HIPCHK(hipMemcpyAsync(hko.data(), dbatch->key_off, (nk + 1) * 8ull, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
            "d2h key_off");
@@ -695,7 +746,8 @@ extern "C" int bv_sync(bv_ctx *ctx) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   if (!ctx->has_done) return BV_OK;
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
-  HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync");
+  const int rc = bv_wait_all(ctx);
+  if (rc != BV_OK) return rc;
   bv_read_timing(ctx);
   return BV_OK;
 }
@@ -776,11 +828,11 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
   add(5, b->r_be, n_items * 32, 0);
   add(8, b->msg_bytes, msg_len, 64);
   // previous work on this ctx must be done before its staging is reused
-  if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
+  if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // previous calls' work buffers / staging
   HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
   HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
   uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
-  HIPCHK(hipEventRecord(ctx->ev[E_CALL], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_CALL], cs), BV_E_LAUNCH, "event");
 
   // keys and item arrays first (one contiguous region of the layout), in
   // kChunk pieces: the pool fills piece c+1 while the DMA engine moves piece c
@@ -808,16 +860,16 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
   };
   rc = stage(0, segs[6].off);  // the keys
   if (rc != BV_OK) return rc;
-  HIPCHK(hipEventRecord(ctx->ev[E_KREADY], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_KREADY], cs), BV_E_LAUNCH, "event");
   rc = stage(segs[6].off, segs[0].off);  // s, pre
   if (rc != BV_OK) return rc;
-  HIPCHK(hipEventRecord(ctx->ev[E_SREADY], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_SREADY], cs), BV_E_LAUNCH, "event");
   rc = stage(segs[0].off, segs[8].off);  // msg_off, item_msg, item_key, r
   if (rc != BV_OK) return rc;
   // zero the message-bytes pad in the staging (the SHA kernel over-reads
   // the last dword of a message into it)
   if (msg_len) memset(pin + segs[8].off + msg_len, 0, 64);
-  HIPCHK(hipEventRecord(ctx->ev[E_SMALL], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_SMALL], cs), BV_E_LAUNCH, "event");
 
   bv_batch d = {};
   d.n_msgs = n_msgs;
@@ -836,13 +888,13 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
   // key cache resolution needs the keys on the device (decode of misses)
   bool kc = false;
   if ((ctx->flags & BV_F_KEY_CACHE) && n_keys && n_keys <= kKcMaxBatchKeys) {
-    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_KREADY], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_KREADY], 0), BV_E_LAUNCH, "join");
     rc = bv_kc_prepare(ctx, n_keys, b->key_bytes, b->key_off, d.key_bytes, d.key_off, st, &kc);
     if (rc != BV_OK) return rc;
   }
   // the key tables need only the keys and s^-1 only s: they run while the
   // rest of the batch still crosses PCIe
-  rc = bv_run_keys(ctx, &d, ctx->ev[E_KREADY], ctx->ev[E_SREADY], kc);
+  rc = bv_run_keys(ctx, &d, ctx->S().ev[E_KREADY], ctx->S().ev[E_SREADY], kc);
   if (rc != BV_OK) return rc;
 
   // Items in message order (item_msg non-decreasing: events, blocks) are
@@ -859,8 +911,8 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
 
   // message bytes: chunks on message boundaries, each hashed once it lands
   if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order");
-  HIPCHK(hipEventRecord(ctx->ev[E_HASH0], st), BV_E_LAUNCH, "event");
-  HIPCHK(hipEventRecord(ctx->ev[E_FORK], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_HASH0], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_FORK], st), BV_E_LAUNCH, "event");
   uint64_t m0 = 0;
   while (m0 < n_msgs) {
     // messages [m0, m1) holding about kChunk bytes (at least one message)
@@ -875,9 +927,9 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
     hipEvent_t e = chunk_event();
     HIPCHK(hipEventRecord(e, cs), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, e, 0), BV_E_LAUNCH, "join chunk");
-    if (m0 == 0) HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SMALL], 0), BV_E_LAUNCH, "join offsets");
+    if (m0 == 0) HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SMALL], 0), BV_E_LAUNCH, "join offsets");
     HIPCHK(bvk::sha256(st, m1 - m0, d.msg_bytes, d.msg_off + m0, pipe.o.dig + 8 * m0), BV_E_LAUNCH, "k_sha256");
-    HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is the one used
+    HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is the one used
     if (in_order) {  // items up to the first one of a message >= m1, in whole 64-item words
       const uint64_t i_end = m1 == n_msgs ? n_items
                                           : (uint64_t)(std::lower_bound(b->item_msg, b->item_msg + n_items, m1) -
@@ -887,11 +939,11 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
     }
     m0 = m1;
   }
-  HIPCHK(hipEventRecord(ctx->ev[E_STAGED], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_STAGED], cs), BV_E_LAUNCH, "event");
   call->ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_STAGED], 0), BV_E_LAUNCH, "join staging");
-  HIPCHK(hipEventRecord(ctx->ev[E_SHA], st), BV_E_LAUNCH, "event");
-  if (n_msgs == 0) HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_STAGED], 0), BV_E_LAUNCH, "join staging");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_SHA], st), BV_E_LAUNCH, "event");
+  if (n_msgs == 0) HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");
   rc = pipe.finish();
   if (rc != BV_OK) return rc;
 
@@ -904,22 +956,21 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
   call->o_st = o_st;
   call->o_bits = o_bits;
   if (n_msgs) {
-    HIPCHK(hipStreamWaitEvent(cs, ctx->ev[E_HASHED], 0), BV_E_LAUNCH, "join");
-    HIPCHK(hipMemcpyAsync(pout, ctx->digests.p, n_msgs * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH, "d2h digests");
+    HIPCHK(hipStreamWaitEvent(cs, ctx->S().ev[E_HASHED], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipMemcpyAsync(pout, ctx->S().digests.p, n_msgs * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH, "d2h digests");
   }
   if (n_items) {
-    HIPCHK(hipMemcpyAsync(pout + o_st, ctx->status.p, n_items, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
-    HIPCHK(hipMemcpyAsync(pout + o_bits, ctx->bits.p, (n_items + 63) / 64 * 8, hipMemcpyDeviceToHost, st),
+    HIPCHK(hipMemcpyAsync(pout + o_st, ctx->S().status.p, n_items, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
+    HIPCHK(hipMemcpyAsync(pout + o_bits, ctx->S().bits.p, (n_items + 63) / 64 * 8, hipMemcpyDeviceToHost, st),
            BV_E_LAUNCH, "d2h bits");
   }
-  HIPCHK(hipEventRecord(ctx->ev[E_OUT], st), BV_E_LAUNCH, "event");
-  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_STAGED], 0), BV_E_LAUNCH, "join");  // staging free after this point
-  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_HASHED], 0), BV_E_LAUNCH, "join");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_OUT], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_STAGED], 0), BV_E_LAUNCH, "join");  // staging free after this point
+  HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_HASHED], 0), BV_E_LAUNCH, "join");
   // the digests' d2h on the copy stream also precedes ev_done
-  HIPCHK(hipEventRecord(ctx->ev[E_CSDONE], cs), BV_E_LAUNCH, "event");
-  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_CSDONE], 0), BV_E_LAUNCH, "join");
-  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
-  return BV_OK;
+  HIPCHK(hipEventRecord(ctx->S().ev[E_CSDONE], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_CSDONE], 0), BV_E_LAUNCH, "join");
+  return bv_mark_done(ctx, st);
 }
 
 int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call *call, bool bits_out) {
@@ -931,8 +982,8 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
   if (bits_out && res->accept_bits && n_items)
     memcpy(res->accept_bits, call->pout + call->o_bits, (n_items + 63) / 64 * 8);
   bv_read_timing(ctx);
-  ctx->timing.ms_h2d = elapsed(ctx->ev[E_CALL], ctx->ev[E_STAGED]);
-  ctx->timing.ms_d2h = elapsed(ctx->ev[E_END], ctx->ev[E_OUT]);
+  ctx->timing.ms_h2d = elapsed(ctx->S().ev[E_CALL], ctx->S().ev[E_STAGED]);
+  ctx->timing.ms_d2h = elapsed(ctx->S().ev[E_END], ctx->S().ev[E_OUT]);
   const auto t_end = std::chrono::steady_clock::now();
   ctx->timing.ms_host = std::chrono::duration<float, std::milli>(t_end - call->t0).count();
   ctx->timing.ms_host_prep = call->ms_prep;
@@ -961,22 +1012,21 @@ extern "C" int bv_sha256_batch(bv_ctx *ctx, uint64_t n_msgs, const uint8_t *msg_
     if (msg_off[m] > msg_off[m + 1]) return bv_fail(ctx, BV_E_ARGS, "msg_off not monotone");
   hipStream_t st = ctx->stream;
   const uint64_t len = msg_off[n_msgs];
-  if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
+  if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // previous calls' work buffers / staging
   const size_t o_off = align256(len + 64), total = o_off + align256((n_msgs + 1) * 8);
   HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
   HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
   HIPCHK(ctx->pin_out.ensure(n_msgs * 32), BV_E_OOM, "alloc pinned results");
-  HIPCHK(ctx->digests.ensure(n_msgs * 32), BV_E_OOM, "alloc digests");
+  HIPCHK(ctx->S().digests.ensure(n_msgs * 32), BV_E_OOM, "alloc digests");
   uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
   ctx->pool->copy(pin, msg_bytes, len);
   memset(pin + len, 0, 64);
   memcpy(pin + o_off, msg_off, (n_msgs + 1) * 8);
   HIPCHK(hipMemcpyAsync(dev, pin, total, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d");
-  HIPCHK(bvk::sha256(st, n_msgs, dev, (const uint64_t *)(dev + o_off), ctx->digests.as<uint32_t>()), BV_E_LAUNCH,
+  HIPCHK(bvk::sha256(st, n_msgs, dev, (const uint64_t *)(dev + o_off), ctx->S().digests.as<uint32_t>()), BV_E_LAUNCH,
          "k_sha256");
-  HIPCHK(hipMemcpyAsync(ctx->pin_out.p, ctx->digests.p, n_msgs * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h");
-  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
-  ctx->has_done = true;
+  HIPCHK(hipMemcpyAsync(ctx->pin_out.p, ctx->S().digests.p, n_msgs * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h");
+  if (bv_mark_done(ctx, st) != BV_OK) return BV_E_LAUNCH;
   HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
   memcpy(out_hash, ctx->pin_out.p, n_msgs * 32);
   return BV_OK;
@@ -997,7 +1047,7 @@ extern "C" int bv_peer_set_hash(bv_ctx *ctx, uint32_t n_peers, const uint8_t *ke
   const uint64_t len = key_off[n_peers];
   if (len && !key_bytes) return bv_fail(ctx, BV_E_ARGS, "null key bytes");
   hipStream_t st = ctx->stream;
-  if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
+  if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // previous calls' work buffers / staging
   const size_t o_off = align256(len + 8), o_scr = o_off + align256((n_peers + 1) * 8ull);
   const size_t total = o_scr + align256(32 + maxlen + 72);
   HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
@@ -1011,8 +1061,7 @@ extern "C" int bv_peer_set_hash(bv_ctx *ctx, uint32_t n_peers, const uint8_t *ke
   HIPCHK(bvk::sha256_chain(st, n_peers, dev, (const uint64_t *)(dev + o_off), dev + o_scr, dout), BV_E_LAUNCH,
          "k_sha256_chain");
   HIPCHK(hipMemcpyAsync(ctx->pin_out.p, dout, 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h");
-  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
-  ctx->has_done = true;
+  if (bv_mark_done(ctx, st) != BV_OK) return BV_E_LAUNCH;
   HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
   memcpy(out_hash, ctx->pin_out.p, 32);
   return BV_OK;

@@ -204,7 +204,7 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   uint64_t max_chunk = 0;
   for (size_t c = 0; c + 1 < cb.size(); c++) max_chunk = std::max(max_chunk, cb[c + 1] - cb[c]);
 
-  if (ctx->has_done) HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "sync previous call");
+  if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // previous calls' work buffers / staging
   HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
   HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
   HIPCHK(ctx->ev_iota.ensure(n * 4), BV_E_OOM, "alloc item index");
@@ -273,7 +273,7 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
 
   // the first part: pinned copies by the pool, H2D on the copy stream
   hipStream_t cs = ctx->cstream;
-  HIPCHK(hipEventRecord(ctx->ev[E_CALL], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_CALL], cs), BV_E_LAUNCH, "event");
   auto stage = [&](size_t a0, size_t a1) -> int {
     for (size_t a = a0; a < a1; a += kChunk) {
       const size_t z = std::min(a1, a + kChunk);
@@ -290,24 +290,24 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   };
   rc = stage(0, keys_end);  // the keys: the key tables start once they land
   if (rc != BV_OK) return rc;
-  HIPCHK(hipEventRecord(ctx->ev[E_KREADY], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_KREADY], cs), BV_E_LAUNCH, "event");
   if (ctx->flags & BV_F_KEY_CACHE) {
-    HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_KREADY], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_KREADY], 0), BV_E_LAUNCH, "join");
     rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, d.key_bytes, d.key_off, st, &kc);
     if (rc != BV_OK) return rc;
   }
   rc = stage(keys_end, s_end);  // s, pre: s^-1
   if (rc != BV_OK) return rc;
-  HIPCHK(hipEventRecord(ctx->ev[E_SREADY], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_SREADY], cs), BV_E_LAUNCH, "event");
   pipe.kc = kc;
-  rc = bv_run_keys(ctx, &vb, ctx->ev[E_KREADY], ctx->ev[E_SREADY], kc);
+  rc = bv_run_keys(ctx, &vb, ctx->S().ev[E_KREADY], ctx->S().ev[E_SREADY], kc);
   if (rc != BV_OK) return rc;
   rc = stage(s_end, small_end);  // r, creators, parent hashes (, the DAG order)
   if (rc != BV_OK) return rc;
-  HIPCHK(hipEventRecord(ctx->ev[E_SMALL], cs), BV_E_LAUNCH, "event");
-  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_SMALL], 0), BV_E_LAUNCH, "join");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_SMALL], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SMALL], 0), BV_E_LAUNCH, "join");
   HIPCHK(bvk::iota(st, n, ctx->ev_iota.as<uint32_t>()), BV_E_LAUNCH, "k_iota");
-  HIPCHK(hipEventRecord(ctx->ev[E_FORK], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_FORK], st), BV_E_LAUNCH, "event");
 
   // per chunk: its fields cross PCIe on the copy stream; on the main stream
   // the chunk's bodies are built and (bulk) hashed and its items verified
@@ -332,12 +332,12 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
            BV_E_LAUNCH, "event bodies");
     if (!dag) {
       HIPCHK(bvk::ev_hash(st, e1 - e0, nullptr, e0, d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
-      HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is used
+      HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is used
       rc = pipe.upto(e1);
       if (rc != BV_OK) return rc;
     }
   }
-  HIPCHK(hipEventRecord(ctx->ev[E_STAGED], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_STAGED], cs), BV_E_LAUNCH, "event");
   call.ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call.t0).count();
 
   if (dag) {  // level by level over the in-batch DAG
@@ -365,9 +365,9 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
              "k_ev_hash_chain");
       L = L1;
     }
-    HIPCHK(hipEventRecord(ctx->ev[E_HASHED], st), BV_E_LAUNCH, "event");
+    HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");
   }
-  HIPCHK(hipEventRecord(ctx->ev[E_SHA], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_SHA], st), BV_E_LAUNCH, "event");
 
   // the digests go back on the copy stream while the last verify kernels run
   const size_t o_st = align256(n * 32), o_bits = o_st + align256(n);
@@ -376,19 +376,20 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   call.pout = pout;
   call.o_st = o_st;
   call.o_bits = o_bits;
-  HIPCHK(hipStreamWaitEvent(cs, ctx->ev[E_HASHED], 0), BV_E_LAUNCH, "join");
+  HIPCHK(hipStreamWaitEvent(cs, ctx->S().ev[E_HASHED], 0), BV_E_LAUNCH, "join");
   HIPCHK(hipMemcpyAsync(pout, dig, n * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH, "d2h digests");
-  HIPCHK(hipEventRecord(ctx->ev[E_CSDONE], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_CSDONE], cs), BV_E_LAUNCH, "event");
 
   rc = pipe.finish();  // bulk: the last chunk's items; DAG: all of them
   if (rc != BV_OK) return rc;
   HIPCHK(hipMemcpyAsync(pout + o_st, pipe.o.status, n, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
   HIPCHK(hipMemcpyAsync(pout + o_bits, pipe.o.bits, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
          "d2h bits");
-  HIPCHK(hipEventRecord(ctx->ev[E_OUT], st), BV_E_LAUNCH, "event");
-  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_CSDONE], 0), BV_E_LAUNCH, "join");  // digests out before ev_done
-  HIPCHK(hipStreamWaitEvent(st, ctx->ev[E_STAGED], 0), BV_E_LAUNCH, "join");  // staging free after ev_done
-  HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_OUT], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_CSDONE], 0), BV_E_LAUNCH, "join");  // digests out before ev_done
+  HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_STAGED], 0), BV_E_LAUNCH, "join");  // staging free after ev_done
+  rc = bv_mark_done(ctx, st);
+  if (rc != BV_OK) return rc;
   bv_batch sizes = {};
   sizes.n_msgs = n;
   sizes.n_items = n;

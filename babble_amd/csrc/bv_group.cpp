@@ -233,7 +233,7 @@ extern "C" int bv_group_verify_batch(bv_group *g, const bv_batch *b, bv_result *
       }
       const uint64_t sw = (sb[d].n_items + 63) / 64;
       if (hipMemsetAsync(g->send[d].p, 0, words * 8, c->stream) != hipSuccess ||
-          (sw && hipMemcpyAsync(g->send[d].p, c->bits.p, sw * 8, hipMemcpyDeviceToDevice, c->stream) != hipSuccess))
+          (sw && hipMemcpyAsync(g->send[d].p, c->S().bits.p, sw * 8, hipMemcpyDeviceToDevice, c->stream) != hipSuccess))
         rcs[d] = BV_E_LAUNCH;
     });
   for (auto &t : th) t.join();
@@ -259,7 +259,7 @@ extern "C" int bv_group_verify_batch(bv_group *g, const bv_batch *b, bv_result *
     bv_ctx *c = g->ctx[d];
     std::lock_guard<std::mutex> clk(c->mu);
     (void)hipSetDevice(c->device);
-    if (hipEventRecord(c->ev_done, c->stream) != hipSuccess) return gfail(g, BV_E_LAUNCH, "event");
+    if (bv_mark_done(c, c->stream) != BV_OK) return gfail(g, BV_E_LAUNCH, "event");
     bv_result sr = {};
     sr.msg_hash = res->msg_hash ? res->msg_hash + 32 * mlo[d] : nullptr;
     sr.status = res->status ? res->status + bounds[d] : nullptr;

@@ -13,6 +13,7 @@
 #include <thread>
 #include <string>
 #include <unordered_map>
+#include <array>
 #include <vector>
 
 #include "../../include/babbleverify.h"
@@ -190,7 +191,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // timing / ordering events (see bv_read_timing)
 enum {
   E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_SINV,
-  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_COUNT
+  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_KDEC, E_COUNT
 };
 
 struct KcSlot {
@@ -213,13 +214,29 @@ struct bv_ctx {
   const uint32_t *g_table = nullptr;  // process-wide, per device (gtable_acquire)
   CopyPool *pool = nullptr;
   // host-entry staging: one layout in pinned memory and in HBM
-  PinnedBuf pin_in, pin_out, pin_small;
+  PinnedBuf pin_in, pin_out;
   DevBuf d_in;
   // work buffers
-  DevBuf digests, kstatus, kxy, bases_jac, key_sub, key_pscr, key_table, scratch, u12, rg, status, bits;
-  hipEvent_t ev[E_COUNT] = {};
+  // Per-call work buffers in two slots: device-resident calls alternate
+  // slots, so a call waits only for the call before the previous one (the
+  // last user of its slot) and two batches can be in flight, e.g. the next
+  // batch's key tables building during this batch's k_verify_q when the
+  // caller alternates streams.
+  struct Slot {
+    DevBuf digests, kstatus, kxy, bases_jac, key_sub, key_pscr, key_table, scratch, u12, rg, status, bits;
+    DevBuf kc_tabs, kc_kst;  // key-cache table address / status per batch key
+    PinnedBuf pin_small;     // their host staging
+    // caller result ranges [lo, hi) of this slot's device calls that the
+    // other slot's calls have not yet been ordered after (deduplicated)
+    std::vector<std::array<uintptr_t, 6>> uncovered;
+    hipEvent_t ev[E_COUNT] = {};  // the slot's call's fork/join and timing events
+    hipEvent_t done = nullptr;  // end of the last call that used this slot
+    bool has_done = false;
+  } slot[2];
+  int cur = 0;
+  Slot &S() { return slot[cur]; }
   std::vector<hipEvent_t> chunk_ev;
-  hipEvent_t ev_done = nullptr;  // end of the last call's device work
+  hipEvent_t ev_done = nullptr;  // end of the last call's device work (both slots: bv_wait_all)
   bool has_done = false;
   bool table_mode = false;
   int key_w = 0;  // 8, 12 or 20 (KC) in table mode
@@ -228,7 +245,7 @@ struct bv_ctx {
   std::unordered_map<std::string, int> kc_index;
   std::vector<KcSlot> kc_slots;
   uint64_t kc_clock = 0, kc_bytes = 0, kc_budget = 0;
-  DevBuf kc_tabs, kc_kst, kc_kxy, kc_btabs;
+  DevBuf kc_kxy, kc_btabs;
   // bv_verify_events: body lengths, parent-hex positions, offsets, bodies
   DevBuf ev_lens, ev_ppos, ev_offs, ev_bodies, ev_tmp, ev_iota, ev_mid;
 };
@@ -242,6 +259,11 @@ struct bv_host_call {
 };
 
 int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess);
+int bv_wait_all(bv_ctx *ctx);              // host: every call's device work has finished
+int bv_mark_done(bv_ctx *ctx, hipStream_t st);
+// Next slot for a device call writing `res`: st waits for the slot's last
+// call, and for the other slot's last call when their result ranges overlap.
+int bv_slot_begin(bv_ctx *ctx, hipStream_t st, const bv_batch *b, const bv_result *res);  // record the end of this call (its slot and ev_done)
 int bv_validate_host_batch(bv_ctx *ctx, const bv_batch *b);
 int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc);

@@ -70,13 +70,15 @@ N_SIMD = 256 * 4
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--events", type=int, default=1_000_000, help="events per GPU per step")
     ap.add_argument("--creators", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=9.0, help="target CPU-baseline sample duration (each leg)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="headline only (profiler passes)")
+    ap.add_argument("--inflight", type=int, default=2, choices=(1, 2),
+                    help="batches in flight: consecutive steps alternate two streams and two result buffers")
     return ap.parse_args()
 
 
@@ -234,33 +236,54 @@ def main():
                          ts0=synth.TS0 + rank * args.events * 8)
     batch.r_be[corrupted(rank, args.events), 31] ^= 1
     v = Verifier(device=local)
-    dev = v.to_device(batch)
-    words = dev.accept_bits.numel()
-    gathered = torch.empty(words * world, dtype=torch.int64, device=f"cuda:{local}") if world > 1 else None
+    # Consecutive steps alternate two streams and two result buffers (the
+    # library alternates its two work-buffer slots), so one batch's key
+    # tables and hashing overlap the previous batch's k_verify_q tail — a
+    # node verifying back-to-back SyncResponses.  Every step still verifies
+    # its whole batch; the result of each buffer's last step is checked.
+    devs = [v.to_device(batch) for _ in range(args.inflight)]
+    streams = [torch.cuda.Stream(device=local) for _ in range(args.inflight)]
+    torch.cuda.synchronize()
+    words = devs[0].accept_bits.numel()
+    gathered = ([torch.empty(words * world, dtype=torch.int64, device=f"cuda:{local}") for _ in devs]
+                if world > 1 else None)
+    k = [0]
 
     def step_with(ver):
         def step():
-            ver.verify_device(dev, sync=False)  # on torch's current stream
-            if world > 1:  # ordered after the verify on the same stream
-                dist.all_gather_into_tensor(gathered, dev.accept_bits)
+            j = k[0] % len(devs)
+            k[0] += 1
+            with torch.cuda.stream(streams[j]):
+                ver.verify_device(devs[j], sync=False)  # on streams[j]
+                if world > 1:  # ordered after the verify on the same stream
+                    dist.all_gather_into_tensor(gathered[j], devs[j].accept_bits)
         return step
 
     elapsed, tms = timed_steps(step_with(v), args.steps, args.warmup, world, dist, local, v)
-    res = dev.result()
     want = expected_words(rank, args.events)
-    if not np.array_equal(res.accept_bits, want):
-        raise SystemExit(f"rank {rank}: accept bitmask differs from the expected one")
-    if world > 1:  # the all-gathered mask of the last step: every rank's shard, bit for bit
-        got = gathered.cpu().numpy().view(np.uint64).reshape(world, -1)
-        for q in range(world):
-            if not np.array_equal(got[q], expected_words(q, args.events)):
-                raise SystemExit(f"rank {rank}: gathered bitmask of rank {q} differs from the expected one")
+    for j, dev in enumerate(devs):
+        res = dev.result()
+        if not np.array_equal(res.accept_bits, want):
+            raise SystemExit(f"rank {rank}: accept bitmask (buffer {j}) differs from the expected one")
+        if world > 1:  # the all-gathered mask of the buffer's last step: every rank's shard, bit for bit
+            got = gathered[j].cpu().numpy().view(np.uint64).reshape(world, -1)
+            for q in range(world):
+                if not np.array_equal(got[q], expected_words(q, args.events)):
+                    raise SystemExit(f"rank {rank}: gathered bitmask of rank {q} differs from the expected one")
 
+    # Kernel durations for the roofline: with two batches in flight the
+    # kernels share the CUs with the other batch's, so their HIP-event spans
+    # are stretched; the per-launch figures come from a batch alone on the
+    # chip (synchronous calls, same workload), right after the timed region.
+    iso = []
+    for _ in range(5):
+        v.verify_device(devs[0], sync=True)
+        iso.append(v.timing())
     line = None
     if rank == 0:
         total_items = world * args.events * args.steps
         value = total_items / elapsed
-        kq_ms, kg_ms = mean(tms, "ms_verify"), mean(tms, "ms_verify_g")
+        kq_ms, kg_ms = mean(iso, "ms_verify"), mean(iso, "ms_verify_g")
         kv_s = (kq_ms + kg_ms) * 1e-3
         achieved = args.events * MODMUL_PER_ITEM_EXEC * IMUL32_PER_MODMUL / kv_s
         roof = {
@@ -272,6 +295,10 @@ def main():
             "frac": achieved / PEAK_IMUL32_PER_S,
             "traffic": None,
             "speedup_vs_canonical": CANONICAL_MODMUL_PER_VERIFY / MODMUL_PER_ITEM_EXEC,
+            "durations": "k_verify_g + k_verify_q HIP-event spans of a batch alone on the chip (breakdown_ms)",
+            # the whole chip over the timed region (two batches in flight):
+            # the verify kernels' executed IMUL32 at the headline rate
+            "chip_frac": value / world * MODMUL_PER_ITEM_EXEC * IMUL32_PER_MODMUL / PEAK_IMUL32_PER_S,
         }
         pmc = pmc_profile(args.events)
         if pmc:
@@ -303,21 +330,27 @@ def main():
                 "creators": args.creators,
                 "parallelism": f"shard{world}" if world > 1 else "single",
                 "collective": "RCCL all_gather of accept bitmasks" if world > 1 else None,
+                "batches_in_flight": args.inflight,
             },
-            "breakdown_ms": {
-                "k_sha256": mean(tms, "ms_sha256"),
-                "keyprep_stream": mean(tms, "ms_keyprep"),
-                "k_sinv": mean(tms, "ms_scalar"),
+            "breakdown_ms": {  # one batch alone on the chip (5 synchronous calls)
+                "k_sha256": mean(iso, "ms_sha256"),
+                "keyprep_stream": mean(iso, "ms_keyprep"),
+                "k_sinv": mean(iso, "ms_scalar"),
                 "k_verify_g": kg_ms,
                 "k_verify_q": kq_ms,
+                "device_total": mean(iso, "ms_total"),
+            },
+            "in_flight_step_ms": {  # the last timed step's spans, overlapped with its neighbour
                 "device_total": mean(tms, "ms_total"),
+                "k_verify_g": mean(tms, "ms_verify_g"),
+                "k_verify_q": mean(tms, "ms_verify"),
             },
             "roofline": roof,
             "bitmask_check": f"exact: {world} x {args.events} events, accept bits all-gathered and equal to the "
                              f"expected mask ({len(corrupted(0, args.events))} seeded r-bit flips per rank rejected)",
         }
     if rank == 0 and world == 1 and not args.no_extras:
-        line["warm"] = warm_leg(args, dev, world, dist, local, step_with)
+        line["warm"] = warm_leg(args, devs, world, dist, local, step_with)
         line["host_entry"] = host_entry_leg(args, v, batch)
         line["latency_ms"] = latency_leg(args)
         line["events_entry"] = events_entry_leg(args)
@@ -331,7 +364,7 @@ def main():
         dist.destroy_process_group()
 
 
-def warm_leg(args, dev, world, dist, local, step_with):
+def warm_leg(args, devs, world, dist, local, step_with):
     """Same device-resident batches with BV_F_KEY_CACHE: the first call
     builds the 64 creators' tables (reported as cold_ms), the timed steps
     reuse them; hashing, s^-1, u1 G, u2 Q and the decision run every step."""
@@ -342,12 +375,12 @@ def warm_leg(args, dev, world, dist, local, step_with):
 
     vc = Verifier(device=local, flags=native.F_KEY_CACHE)
     t0 = time.perf_counter()
-    vc.verify_device(dev)
+    vc.verify_device(devs[0])
     cold_ms = (time.perf_counter() - t0) * 1e3
     builds = vc.timing()["kc_builds"]
     elapsed, tms = timed_steps(step_with(vc), args.steps, 1, 1, None, local, vc)
-    res = dev.result()
-    assert np.array_equal(res.accept_bits, expected_words(0, args.events))
+    for dev in devs:
+        assert np.array_equal(dev.result().accept_bits, expected_words(0, args.events))
     out = {"value": args.events * args.steps / elapsed, "unit": "verifies/s",
            "ms_per_step": elapsed / args.steps * 1e3, "first_call_ms": cold_ms, "tables_built_first_call": builds,
            "key_path": int(tms[-1]["key_path"]),

@@ -142,10 +142,15 @@ int bv_verify_batch(bv_ctx *ctx, const bv_batch *batch, bv_result *result);
  * aligned vector loads; the host entry points pad their staging copies). */
 int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresult,
                            void *stream, int async);
-/* Calls on one ctx are ordered on the device whatever their streams: a call's
- * work starts after the previous call's work has finished (the ctx's work
- * buffers are shared).  bv_sync waits for the last call's work (after an
- * async call) and updates bv_get_timing. */
+/* The ctx holds two sets of work buffers.  Consecutive bv_verify_batch_device
+ * calls alternate them, and each waits (on the device) only for the last call
+ * that used the same set — and for the call before it when their result
+ * buffers overlap: two async calls on different streams writing different
+ * results overlap, one call's key tables building beside the other's verify
+ * (the caller orders a call whose inputs an earlier in-flight call's results
+ * write, as for any two streams).  Every other entry
+ * point first waits for all earlier calls.  bv_sync waits for every call's
+ * work and updates bv_get_timing (the last call's). */
 int bv_sync(bv_ctx *ctx);
 
 /* Events from their wire fields.  Instead of the

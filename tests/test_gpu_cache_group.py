@@ -144,6 +144,38 @@ def test_async_calls_on_two_streams_are_ordered():
         v.close()
 
 
+@pytest.mark.parametrize("flags", [0, native.F_KEY_CACHE], ids=["per_batch", "key_cache"])
+def test_async_calls_two_in_flight(flags):
+    """Two work-buffer slots: consecutive async device calls alternate them
+    and wait only for the slot's previous call, so calls on two streams
+    overlap.  Six calls over three batches of different sizes/keys (each
+    slot reused with other shapes), then a host-entry call (waits for all)
+    and one more async pair: every result exact."""
+    import torch
+
+    from babble_amd.verifier import Verifier
+
+    v = Verifier(device=0, flags=flags)
+    try:
+        bs = [synth.adversarial(n, seed=63 + i, n_creators=c, scale_per_million=MIX)
+              for i, (n, c) in enumerate([(70_000, 8), (9_000, 3), (40_000, 12)])]
+        ds = [v.to_device(b) for b in bs]
+        ss = [torch.cuda.Stream(0), torch.cuda.Stream(0)]
+        torch.cuda.synchronize()
+        for k in range(6):
+            v.verify_device(ds[k % 3], stream=ss[k % 2].cuda_stream, sync=False)
+        torch.cuda.synchronize()
+        for d, b in zip(ds, bs):
+            oracle_check(d.result(), b)
+        oracle_check(v.verify(bs[1]), bs[1])
+        v.verify_device(ds[2], stream=ss[0].cuda_stream, sync=False)
+        v.verify_device(ds[0], stream=ss[1].cuda_stream, sync=False)
+        oracle_check(ds[2].result(), bs[2])
+        oracle_check(ds[0].result(), bs[0])
+    finally:
+        v.close()
+
+
 def test_group_one_device():
     """bv_group over the box's device(s): shards, per-device staging and the
     RCCL all-gather of the bitmask; equal to the oracle."""

@@ -9,7 +9,7 @@ EV=${PMC_EVENTS:-1000000}
 run_pass() {
   name=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$name -o run --output-format csv -- \
-    python3 bench.py --no-cpu --no-extras --steps 2 --warmup 1 --events $EV > gpurun_out/pmc_$name.log 2>&1 \
+    python3 bench.py --no-cpu --no-extras --inflight 1 --steps 2 --warmup 1 --events $EV > gpurun_out/pmc_$name.log 2>&1 \
     || { echo "PMC pass $name failed"; tail -20 gpurun_out/pmc_$name.log; exit 1; }
   echo "pass $name ok"
 }
