@@ -11,14 +11,15 @@ producing status bytes and the accept bitmask (the SURVEY §8d C2 workload:
 (torch.distributed.run, one process per GPU) every rank verifies its own
 1M-event shard (weak scaling) and the per-rank accept bitmasks are
 all-gathered over RCCL inside the timed step.  Steps are issued back to
-back (asynchronous calls; the library starts a ctx's call when its previous
-one is done), so the host's per-call work overlaps the device's, as in a
-service that streams batches; the timed region is closed by synchronize.
+back as asynchronous calls on two alternating streams with two result
+buffers (the library's two work-buffer slots), so two batches are in flight
+and the host's per-call work overlaps the device's, as in a node verifying
+a stream of SyncResponses; the timed region is closed by synchronize.
 
 Rank 0 prints one JSON line.  `value` is the headline above.  Beside it:
   * `roofline` — the two verify kernels (k_verify_g + k_verify_q), timed with
-    the library's HIP events on the stream they run on (the last timed
-    step); see ROOFLINE below;
+    the library's HIP events on the stream they run on, for a batch alone on
+    the chip (five synchronous calls after the timed region); see ROOFLINE;
   * `warm` — the same batches with BV_F_KEY_CACHE (validator tables kept in
     HBM across calls; Babble's validator set is stable), every other piece of
     work still done per step;
@@ -175,11 +176,11 @@ def expected_words(rank: int, n: int):
 
 
 def timed_steps(step, steps: int, warmup: int, world: int, dist, local: int, ver):
-    """K steps issued back to back (each a full asynchronous VerifyBatch; the
-    library orders a ctx's calls on the device, so step k+1 starts when step
-    k is done and the host's launch work overlaps the device's), bracketed
-    by barrier + synchronize.  The per-kernel breakdown is the library's HIP
-    events of the last timed step, read after the closing synchronize."""
+    """K steps issued back to back (each a full asynchronous VerifyBatch;
+    the library orders a ctx's calls on the device per work-buffer slot, so
+    with steps on two streams two batches are in flight and the host's
+    launch work overlaps the device's), bracketed by barrier + synchronize.
+    The last timed step's HIP events are read after the closing synchronize."""
     import torch
 
     for _ in range(warmup):
