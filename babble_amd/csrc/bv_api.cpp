@@ -530,11 +530,12 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   // (kstream) may queue behind another in-flight call's build.
   HIPCHK(hipStreamWaitEvent(ctx->sstream, keys_ready, 0), BV_E_LAUNCH, "fork");
   HIPCHK(hipEventRecord(ev[E_START], ctx->sstream), BV_E_LAUNCH, "event");
-  if (!kc)
+  if (!kc) {
     HIPCHK(bvk::key_decode(ctx->sstream, n_keys, b->key_bytes, b->key_off, ctx->S().kstatus.as<uint8_t>(),
                            ctx->S().kxy.as<uint32_t>()),
            BV_E_LAUNCH, "k_key_decode");
-  HIPCHK(hipEventRecord(ev[E_KDEC], ctx->sstream), BV_E_LAUNCH, "event");
+    HIPCHK(hipEventRecord(ev[E_KDEC], ctx->sstream), BV_E_LAUNCH, "event");
+  }
   // s^-1 needs only s: concurrent with everything up to k_verify_g
   HIPCHK(hipStreamWaitEvent(ctx->sstream, s_ready, 0), BV_E_LAUNCH, "fork");
   // items per lane: kPrepM amortises the inversion in large batches; a small
@@ -544,7 +545,7 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   HIPCHK(bvk::sinv(ctx->sstream, n_items, M, (const uint32_t *)b->s_be, b->pre, ctx->S().scratch.as<uint32_t>()),
          BV_E_LAUNCH, "k_sinv");
   HIPCHK(hipEventRecord(ev[E_SINV], ctx->sstream), BV_E_LAUNCH, "event");
-  HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_KDEC], 0), BV_E_LAUNCH, "fork");
+  HIPCHK(hipStreamWaitEvent(ctx->kstream, kc ? keys_ready : ev[E_KDEC], 0), BV_E_LAUNCH, "fork");
   if (!kc) {
     if (table_mode)
       HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->S().kxy.as<uint32_t>(), ctx->S().kstatus.as<uint8_t>(),
