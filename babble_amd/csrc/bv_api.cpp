@@ -135,25 +135,27 @@ int bv_wait_all(bv_ctx *ctx) {
 }
 
 int bv_slot_begin(bv_ctx *ctx, hipStream_t st, const bv_batch *b, const bv_result *res) {
-  bv_ctx::Slot &other = ctx->S();
-  ctx->cur ^= 1;
+  ctx->cur = (ctx->cur + 1) % bv_ctx::kSlots;
   bv_ctx::Slot &sl = ctx->S();
   if (sl.has_done) HIPCHK(hipStreamWaitEvent(st, sl.done, 0), BV_E_LAUNCH, "order after the slot's last call");
   // The caller's result buffers: a call writing buffers that a call still in
-  // flight on the other slot writes (e.g. the same DeviceBatch issued on two
+  // flight on another slot writes (e.g. the same DeviceBatch issued on two
   // streams) is ordered after that slot's last call, as if serial.
   const void *p[3] = {res->msg_hash, res->status, res->accept_bits};
   const uint64_t n[3] = {b->n_msgs * 32, b->n_items, (b->n_items + 63) / 64 * 8};
   std::array<uintptr_t, 6> r{};
   for (int i = 0; i < 3; i++)
     if (p[i] && n[i]) r[2 * i] = (uintptr_t)p[i], r[2 * i + 1] = (uintptr_t)p[i] + n[i];
-  bool overlap = other.uncovered.size() >= 8;
-  for (const auto &u : other.uncovered)
-    for (int i = 0; i < 3; i++)
-      for (int j = 0; j < 3; j++) overlap |= u[2 * j] < r[2 * i + 1] && r[2 * i] < u[2 * j + 1];
-  if (overlap) {
-    HIPCHK(hipStreamWaitEvent(st, other.done, 0), BV_E_LAUNCH, "order after an overlapping call");
-    other.uncovered.clear();
+  for (auto &other : ctx->slot) {
+    if (&other == &sl) continue;
+    bool overlap = other.uncovered.size() >= 8;
+    for (const auto &u : other.uncovered)
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) overlap |= u[2 * j] < r[2 * i + 1] && r[2 * i] < u[2 * j + 1];
+    if (overlap) {
+      HIPCHK(hipStreamWaitEvent(st, other.done, 0), BV_E_LAUNCH, "order after an overlapping call");
+      other.uncovered.clear();
+    }
   }
   if (std::find(sl.uncovered.begin(), sl.uncovered.end(), r) == sl.uncovered.end()) sl.uncovered.push_back(r);
   return BV_OK;

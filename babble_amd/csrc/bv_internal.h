@@ -14,6 +14,10 @@
 #include <string>
 #include <unordered_map>
 #include <array>
+
+#ifndef BV_SLOTS
+#define BV_SLOTS 2  // work-buffer slots: device calls that may be in flight at once (3: -4 % in a same-box A/B)
+#endif
 #include <vector>
 
 #include "../../include/babbleverify.h"
@@ -217,22 +221,24 @@ struct bv_ctx {
   PinnedBuf pin_in, pin_out;
   DevBuf d_in;
   // work buffers
-  // Per-call work buffers in two slots: device-resident calls alternate
-  // slots, so a call waits only for the call before the previous one (the
-  // last user of its slot) and two batches can be in flight, e.g. the next
-  // batch's key tables building during this batch's k_verify_q when the
-  // caller alternates streams.
+  // Per-call work buffers in kSlots slots: device-resident calls rotate
+  // through them, so a call waits only for the last user of its slot and
+  // kSlots batches can be in flight, e.g. the next batch's key tables
+  // building during this batch's k_verify_q when the caller alternates
+  // streams.
   struct Slot {
     DevBuf digests, kstatus, kxy, bases_jac, key_sub, key_pscr, key_table, scratch, u12, rg, status, bits;
     DevBuf kc_tabs, kc_kst;  // key-cache table address / status per batch key
     PinnedBuf pin_small;     // their host staging
     // caller result ranges [lo, hi) of this slot's device calls that the
-    // other slot's calls have not yet been ordered after (deduplicated)
+    // other slots' calls have not yet been ordered after (deduplicated)
     std::vector<std::array<uintptr_t, 6>> uncovered;
     hipEvent_t ev[E_COUNT] = {};  // the slot's call's fork/join and timing events
     hipEvent_t done = nullptr;  // end of the last call that used this slot
     bool has_done = false;
-  } slot[2];
+  };
+  static constexpr int kSlots = BV_SLOTS;
+  Slot slot[kSlots];
   int cur = 0;
   Slot &S() { return slot[cur]; }
   std::vector<hipEvent_t> chunk_ev;

@@ -79,7 +79,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="headline only (profiler passes)")
     ap.add_argument("--inflight", type=int, default=2, choices=(1, 2),
-                    help="batches in flight: consecutive steps alternate two streams and two result buffers")
+                    help="batches in flight: consecutive steps rotate over this many streams and result buffers")
     return ap.parse_args()
 
 

@@ -144,13 +144,16 @@ def test_async_calls_on_two_streams_are_ordered():
         v.close()
 
 
+@pytest.mark.parametrize("n_streams", [2, 3])
 @pytest.mark.parametrize("flags", [0, native.F_KEY_CACHE], ids=["per_batch", "key_cache"])
-def test_async_calls_two_in_flight(flags):
-    """Two work-buffer slots: consecutive async device calls alternate them
-    and wait only for the slot's previous call, so calls on two streams
-    overlap.  Six calls over three batches of different sizes/keys (each
-    slot reused with other shapes), then a host-entry call (waits for all)
-    and one more async pair: every result exact."""
+def test_async_calls_two_in_flight(flags, n_streams):
+    """Work-buffer slots: consecutive async device calls rotate over them and
+    wait only for the slot's previous call (and for in-flight calls writing
+    the same results), so calls on several streams overlap.  Seven calls over
+    three batches of different sizes/keys on 2 or 3 streams (slots reused
+    with other shapes, the same result buffers on different streams), then a
+    host-entry call (waits for all) and one more async pair: every result
+    exact."""
     import torch
 
     from babble_amd.verifier import Verifier
@@ -160,10 +163,10 @@ def test_async_calls_two_in_flight(flags):
         bs = [synth.adversarial(n, seed=63 + i, n_creators=c, scale_per_million=MIX)
               for i, (n, c) in enumerate([(70_000, 8), (9_000, 3), (40_000, 12)])]
         ds = [v.to_device(b) for b in bs]
-        ss = [torch.cuda.Stream(0), torch.cuda.Stream(0)]
+        ss = [torch.cuda.Stream(0) for _ in range(n_streams)]
         torch.cuda.synchronize()
-        for k in range(6):
-            v.verify_device(ds[k % 3], stream=ss[k % 2].cuda_stream, sync=False)
+        for k in range(7):
+            v.verify_device(ds[k % 3], stream=ss[k % n_streams].cuda_stream, sync=False)
         torch.cuda.synchronize()
         for d, b in zip(ds, bs):
             oracle_check(d.result(), b)
