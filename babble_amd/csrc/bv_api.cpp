@@ -244,8 +244,16 @@ static int create_impl(bv_ctx *ctx) {
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
   HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
-  HIPCHK(hipStreamCreateWithPriority(&ctx->kstream, hipStreamNonBlocking, hi), BV_E_NODEVICE, "hipStreamCreate");
-  HIPCHK(hipStreamCreateWithFlags(&ctx->sstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
+#ifndef BV_KPRIO
+#define BV_KPRIO 1
+#endif
+#ifndef BV_SPRIO
+#define BV_SPRIO 0
+#endif
+  HIPCHK(hipStreamCreateWithPriority(&ctx->kstream, hipStreamNonBlocking, BV_KPRIO ? hi : lo), BV_E_NODEVICE,
+         "hipStreamCreate");
+  HIPCHK(hipStreamCreateWithPriority(&ctx->sstream, hipStreamNonBlocking, BV_SPRIO ? hi : lo), BV_E_NODEVICE,
+         "hipStreamCreate");
   HIPCHK(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
   for (auto &sl : ctx->slot)
     for (auto &e : sl.ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
