@@ -190,8 +190,12 @@ def timed_steps(step, steps: int, warmup: int, world: int, dist, local: int, ver
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    issue = 0.0
     for _ in range(steps):
+        t1 = time.perf_counter()
         step()
+        issue += time.perf_counter() - t1
+    timed_steps.issue_ms_per_step = issue / max(steps, 1) * 1e3
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -341,6 +345,9 @@ def main():
                 "k_verify_q": kq_ms,
                 "device_total": mean(iso, "ms_total"),
             },
+            # host time to issue one step (the library's launch work + Python):
+            # when it reaches ms_per_step the run is host-bound, not device-bound
+            "host_issue_ms_per_step": timed_steps.issue_ms_per_step,
             "in_flight_step_ms": {  # the last timed step's spans, overlapped with its neighbour
                 "device_total": mean(tms, "ms_total"),
                 "k_verify_g": mean(tms, "ms_verify_g"),
