@@ -37,6 +37,13 @@ from __future__ import annotations
 import argparse
 import json
 import os
+
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process
+# (default 4).  This process holds the verifier's streams (main, keys, s^-1,
+# copy), the key-cache verifier's and torch's two step streams: with 4 queues
+# some share one and their kernels serialise (373 vs 452 M verifies/s on the
+# same box).  Set before HIP initialises; an explicit value wins.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 import sys
 import time
 
