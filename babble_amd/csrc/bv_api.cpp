@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <thread>
 
 namespace {
@@ -126,6 +127,49 @@ int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e) {
     hipError_t _e = (expr);                                    \
     if (_e != hipSuccess) return bv_fail(ctx, code, what, _e); \
   } while (0)
+
+// ---------------------------------------------------------------------------
+// caller-visible pinned memory (bv_host_alloc): a host-entry call whose
+// arrays live in it is DMA'd straight from them, without the staging copy
+// ---------------------------------------------------------------------------
+namespace {
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pinned;  // base -> bytes
+}  // namespace
+
+extern "C" int bv_host_alloc(size_t bytes, void **out) {
+  if (!out) return BV_E_ARGS;
+  *out = nullptr;
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    return BV_E_OOM;
+  }
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pinned[(uintptr_t)p] = bytes ? bytes : 1;
+  *out = p;
+  return BV_OK;
+}
+
+extern "C" void bv_host_free(void *p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pinned.find((uintptr_t)p);
+    if (it == g_pinned.end()) return;  // not ours: ignored
+    g_pinned.erase(it);
+  }
+  (void)hipHostFree(p);
+}
+
+bool bv_is_pinned(const void *p, size_t n) {
+  if (!p || !n) return false;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pinned.upper_bound((uintptr_t)p);
+  if (it == g_pinned.begin()) return false;
+  --it;
+  return (uintptr_t)p + n <= it->first + it->second;
+}
 
 int bv_wait_all(bv_ctx *ctx) {
   for (auto &sl : ctx->slot)
@@ -237,24 +281,89 @@ static void gtable_release(int device) {
   }
 }
 
-static int create_impl(bv_ctx *ctx) {
-  HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
-  // the key-table stream runs a latency-bound chain (k_table_bases): give it
-  // the higher priority so its waves are scheduled ahead of the bulk kernels
-  int lo = 0, hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-  HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
+// Per-device, per-process stream set shared by every ctx (bv_internal.h).
+namespace {
+struct DevStreams {
+  hipStream_t lane[BV_SLOTS] = {};
+  hipStream_t kstream = nullptr, sstream = nullptr, cstream = nullptr;
+  int refs = 0;
+};
+std::mutex g_streams_mu;
+DevStreams g_streams[64];
+
+void streams_destroy(DevStreams &d) {
+  for (hipStream_t &s : d.lane)
+    if (s) (void)hipStreamDestroy(s), s = nullptr;
+  for (hipStream_t *s : {&d.kstream, &d.sstream, &d.cstream})
+    if (*s) (void)hipStreamDestroy(*s), *s = nullptr;
+}
+}  // namespace
+
 #ifndef BV_KPRIO
 #define BV_KPRIO 1
 #endif
 #ifndef BV_SPRIO
 #define BV_SPRIO 0
 #endif
-  HIPCHK(hipStreamCreateWithPriority(&ctx->kstream, hipStreamNonBlocking, BV_KPRIO ? hi : lo), BV_E_NODEVICE,
-         "hipStreamCreate");
-  HIPCHK(hipStreamCreateWithPriority(&ctx->sstream, hipStreamNonBlocking, BV_SPRIO ? hi : lo), BV_E_NODEVICE,
-         "hipStreamCreate");
-  HIPCHK(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking), BV_E_NODEVICE, "hipStreamCreate");
+
+static int streams_acquire(bv_ctx *ctx) {
+  if (ctx->device < 0 || ctx->device >= 64) return bv_fail(ctx, BV_E_NODEVICE, "device ordinal >= 64");
+  std::lock_guard<std::mutex> lk(g_streams_mu);
+  DevStreams &d = g_streams[ctx->device];
+  if (d.refs == 0) {
+    // the key-table stream runs a latency-bound chain (k_table_bases): give
+    // it the higher priority so its waves are scheduled ahead of bulk kernels
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    bool ok = true;
+    for (hipStream_t &s : d.lane) ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipStreamCreateWithPriority(&d.sstream, hipStreamNonBlocking, BV_SPRIO ? hi : lo) == hipSuccess;
+    ok = ok && hipStreamCreateWithPriority(&d.kstream, hipStreamNonBlocking, BV_KPRIO ? hi : lo) == hipSuccess;
+    if (!ok) {
+      (void)hipGetLastError();
+      streams_destroy(d);
+      return bv_fail(ctx, BV_E_NODEVICE, "hipStreamCreate");
+    }
+  }
+  d.refs++;
+  for (int k = 0; k < bv_ctx::kSlots; k++) ctx->lane[k] = d.lane[k];
+  ctx->stream = d.lane[0];
+  ctx->kstream = d.kstream;
+  ctx->sstream = d.sstream;
+  ctx->cstream = d.cstream;
+  return BV_OK;
+}
+
+static void streams_release(bv_ctx *ctx) {
+  if (!ctx->stream) return;
+  std::lock_guard<std::mutex> lk(g_streams_mu);
+  DevStreams &d = g_streams[ctx->device];
+  if (--d.refs == 0) streams_destroy(d);
+}
+
+hipStream_t bv_copy_stream(bv_ctx *ctx) {
+  if (ctx->cstream) return ctx->cstream;
+  std::lock_guard<std::mutex> lk(g_streams_mu);
+  DevStreams &d = g_streams[ctx->device];
+  if (!d.cstream && hipStreamCreateWithFlags(&d.cstream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    d.cstream = nullptr;
+  }
+  ctx->cstream = d.cstream;
+  return ctx->cstream;
+}
+
+int bv_drain(bv_ctx *ctx, hipStream_t st, int rc) {
+  for (hipStream_t s : {st, ctx->sstream, ctx->kstream, ctx->cstream})
+    if (s) (void)hipStreamSynchronize(s);
+  for (auto &sl : ctx->slot) sl.uncovered.clear();
+  (void)hipGetLastError();
+  return rc;
+}
+
+static int create_impl(bv_ctx *ctx) {
+  HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  if (streams_acquire(ctx) != BV_OK) return BV_E_NODEVICE;
   for (auto &sl : ctx->slot)
     for (auto &e : sl.ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
   HIPCHK(hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming), BV_E_NODEVICE, "hipEventCreate");
@@ -302,8 +411,12 @@ extern "C" int bv_create(bv_ctx **out, int device, uint32_t flags) {
 extern "C" void bv_destroy(bv_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  for (hipStream_t s : {ctx->stream, ctx->kstream, ctx->sstream, ctx->cstream})
-    if (s) (void)hipStreamSynchronize(s);
+  // every call of this ctx has finished before anything is released (an
+  // async call may still be reading slot buffers and key-cache tables)
+  if (ctx->stream) {
+    (void)bv_wait_all(ctx);
+    if (ctx->has_done) (void)hipEventSynchronize(ctx->ev_done);
+  }
   if (ctx->g_table) gtable_release(ctx->device);
   DevBuf *bufs[] = {&ctx->d_in, &ctx->kc_kxy,  &ctx->kc_btabs, &ctx->ev_lens,
                     &ctx->ev_ppos,   &ctx->ev_offs, &ctx->ev_bodies, &ctx->ev_tmp, &ctx->ev_iota, &ctx->ev_mid};
@@ -326,11 +439,12 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   for (auto &e : ctx->chunk_ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
-  for (hipStream_t s : {ctx->kstream, ctx->sstream, ctx->cstream, ctx->stream})
-    if (s) (void)hipStreamDestroy(s);
+  streams_release(ctx);
   delete ctx->pool;
   delete ctx;
 }
+
+extern "C" void *bv_last_stream(const bv_ctx *ctx) { return ctx ? (void *)ctx->last : nullptr; }
 
 extern "C" int bv_get_timing(const bv_ctx *ctx, bv_timing *out) {
   if (!ctx || !out) return BV_E_ARGS;
@@ -712,14 +826,31 @@ void bv_read_timing(bv_ctx *ctx) {
   t.ms_total = elapsed(ev[E_START], ev[E_END]);
 }
 
+static int verify_device_impl(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresult, hipStream_t st);
+
 extern "C" int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresult, void *stream,
                                       int async) {
   if (!ctx || !dbatch || !dresult) return BV_E_ARGS;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
   const auto t0 = std::chrono::steady_clock::now();
-  hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+  // NULL stream: the lane of the work slot this call takes (bv_slot_begin
+  // advances ctx->cur), so consecutive async calls land on two queues
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->lane[(ctx->cur + 1) % bv_ctx::kSlots];
+  ctx->last = st;
   ctx->timing = bv_timing{};
+  int rc = verify_device_impl(ctx, dbatch, dresult, st);
+  if (rc != BV_OK) return bv_drain(ctx, st, rc);
+  if (!async) {
+    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "verify sync");
+    bv_read_timing(ctx);
+    ctx->timing.ms_host =
+        std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return BV_OK;
+}
+
+static int verify_device_impl(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresult, hipStream_t st) {
   bool kc = false;
   if (bv_slot_begin(ctx, st, dbatch, dresult) != BV_OK) return BV_E_LAUNCH;
   if ((ctx->flags & BV_F_KEY_CACHE) && dbatch->n_keys && dbatch->n_keys <= kKcMaxBatchKeys) {
@@ -741,15 +872,7 @@ extern "C" int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_re
     int rc = bv_kc_prepare(ctx, nk, hkb.data(), hko.data(), dbatch->key_bytes, dbatch->key_off, st, &kc);
     if (rc != BV_OK) return rc;
   }
-  int rc = bv_run_device(ctx, dbatch, dresult->msg_hash, dresult->status, dresult->accept_bits, st, false, kc);
-  if (rc != BV_OK) return rc;
-  if (!async) {
-    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "verify sync");
-    bv_read_timing(ctx);
-    ctx->timing.ms_host =
-        std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  }
-  return BV_OK;
+  return bv_run_device(ctx, dbatch, dresult->msg_hash, dresult->status, dresult->accept_bits, st, false, kc);
 }
 
 extern "C" int bv_sync(bv_ctx *ctx) {
@@ -803,12 +926,14 @@ int bv_validate_host_batch(bv_ctx *ctx, const bv_batch *b) {
 // Stage a host batch into HBM (pinned chunks on the copy stream), hash the
 // messages chunk by chunk as they land and launch the verify pipeline.
 // Returns with the work enqueued; bv_host_finish waits and copies results.
-int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
+int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_result *res) {
   const auto t0 = std::chrono::steady_clock::now();
   call->t0 = t0;
   int rc = bv_validate_host_batch(ctx, b);
   if (rc != BV_OK) return rc;
-  hipStream_t st = ctx->stream, cs = ctx->cstream;
+  hipStream_t st = ctx->stream, cs = bv_copy_stream(ctx);
+  if (!cs) return bv_fail(ctx, BV_E_NODEVICE, "copy stream");
+  ctx->last = st;
   ctx->timing = bv_timing{};
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
@@ -844,6 +969,10 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
   HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
   uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
   HIPCHK(hipEventRecord(ctx->S().ev[E_CALL], cs), BV_E_LAUNCH, "event");
+  // arrays in bv_host_alloc memory are DMA'd from where they are
+  bool direct[9];
+  for (int i = 0; i < 9; i++) direct[i] = bv_is_pinned(segs[i].src, segs[i].n);
+  call->direct_in = direct[8];
 
   // keys and item arrays first (one contiguous region of the layout), in
   // kChunk pieces: the pool fills piece c+1 while the DMA engine moves piece c
@@ -859,13 +988,28 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
     for (size_t a = a0; a < a1; a += kChunk) {
       const size_t z = std::min(a1, a + kChunk);
       std::vector<CopyPool::Piece> pieces;
+      bool any_direct = false;
       for (int i = 0; i < 8; i++) {
         const Seg &s = segs[i];
         const size_t lo = std::max(a, s.off), hi = std::min(z, s.off + s.n);
-        if (lo < hi) pieces.push_back({pin + lo, (const uint8_t *)s.src + (lo - s.off), hi - lo});
+        if (lo >= hi) continue;
+        if (direct[i]) {
+          any_direct = true;
+          HIPCHK(hipMemcpyAsync(dev + lo, (const uint8_t *)s.src + (lo - s.off), hi - lo, hipMemcpyHostToDevice, cs),
+                 BV_E_LAUNCH, "h2d (pinned caller buffer)");
+        } else {
+          pieces.push_back({pin + lo, (const uint8_t *)s.src + (lo - s.off), hi - lo});
+        }
       }
       ctx->pool->copy_many(pieces);
-      HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
+      if (!any_direct) {
+        HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
+      } else {
+        for (const CopyPool::Piece &q : pieces) {
+          const size_t o = (uint8_t *)q.dst - pin;
+          HIPCHK(hipMemcpyAsync(dev + o, q.dst, q.n, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
+        }
+      }
     }
     return BV_OK;
   };
@@ -877,9 +1021,11 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
   HIPCHK(hipEventRecord(ctx->S().ev[E_SREADY], cs), BV_E_LAUNCH, "event");
   rc = stage(segs[0].off, segs[8].off);  // msg_off, item_msg, item_key, r
   if (rc != BV_OK) return rc;
-  // zero the message-bytes pad in the staging (the SHA kernel over-reads
-  // the last dword of a message into it)
-  if (msg_len) memset(pin + segs[8].off + msg_len, 0, 64);
+  // zero the message-bytes pad (the SHA kernel over-reads the last dword of
+  // a message into it): in the staging, or on the device for direct bytes
+  if (msg_len && !direct[8]) memset(pin + segs[8].off + msg_len, 0, 64);
+  if (msg_len && direct[8])
+    HIPCHK(hipMemsetAsync(dev + segs[8].off + msg_len, 0, 64, cs), BV_E_LAUNCH, "zero message pad");
   HIPCHK(hipEventRecord(ctx->S().ev[E_SMALL], cs), BV_E_LAUNCH, "event");
 
   bv_batch d = {};
@@ -931,10 +1077,15 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
     uint64_t m1 = std::upper_bound(b->msg_off + m0 + 1, b->msg_off + n_msgs + 1, base + kChunk) - b->msg_off - 1;
     if (m1 <= m0) m1 = m0 + 1;
     const uint64_t end = b->msg_off[m1];
-    const size_t len = end - base + (m1 == n_msgs ? 64 : 0);
-    ctx->pool->copy(pin + segs[8].off + base, b->msg_bytes + base, end - base);
-    HIPCHK(hipMemcpyAsync(dev + segs[8].off + base, pin + segs[8].off + base, len, hipMemcpyHostToDevice, cs),
-           BV_E_LAUNCH, "h2d msgs");
+    if (direct[8]) {
+      HIPCHK(hipMemcpyAsync(dev + segs[8].off + base, b->msg_bytes + base, end - base, hipMemcpyHostToDevice, cs),
+             BV_E_LAUNCH, "h2d msgs (pinned caller buffer)");
+    } else {
+      const size_t len = end - base + (m1 == n_msgs ? 64 : 0);
+      ctx->pool->copy(pin + segs[8].off + base, b->msg_bytes + base, end - base);
+      HIPCHK(hipMemcpyAsync(dev + segs[8].off + base, pin + segs[8].off + base, len, hipMemcpyHostToDevice, cs),
+             BV_E_LAUNCH, "h2d msgs");
+    }
     hipEvent_t e = chunk_event();
     HIPCHK(hipEventRecord(e, cs), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, e, 0), BV_E_LAUNCH, "join chunk");
@@ -966,12 +1117,19 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call) {
   call->pout = pout;
   call->o_st = o_st;
   call->o_bits = o_bits;
+  // results straight into the caller's bv_host_alloc buffers when they are
+  call->direct_hash = res && bv_is_pinned(res->msg_hash, n_msgs * 32);
+  call->direct_status = res && bv_is_pinned(res->status, n_items);
   if (n_msgs) {
     HIPCHK(hipStreamWaitEvent(cs, ctx->S().ev[E_HASHED], 0), BV_E_LAUNCH, "join");
-    HIPCHK(hipMemcpyAsync(pout, ctx->S().digests.p, n_msgs * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH, "d2h digests");
+    HIPCHK(hipMemcpyAsync(call->direct_hash ? res->msg_hash : pout, ctx->S().digests.p, n_msgs * 32,
+                          hipMemcpyDeviceToHost, cs),
+           BV_E_LAUNCH, "d2h digests");
   }
   if (n_items) {
-    HIPCHK(hipMemcpyAsync(pout + o_st, ctx->S().status.p, n_items, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
+    HIPCHK(hipMemcpyAsync(call->direct_status ? res->status : pout + o_st, ctx->S().status.p, n_items,
+                          hipMemcpyDeviceToHost, st),
+           BV_E_LAUNCH, "d2h status");
     HIPCHK(hipMemcpyAsync(pout + o_bits, ctx->S().bits.p, (n_items + 63) / 64 * 8, hipMemcpyDeviceToHost, st),
            BV_E_LAUNCH, "d2h bits");
   }
@@ -988,8 +1146,8 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
   HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "verify sync");
   const auto t_out = std::chrono::steady_clock::now();
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
-  if (res->msg_hash && n_msgs) ctx->pool->copy(res->msg_hash, call->pout, n_msgs * 32);
-  if (res->status && n_items) ctx->pool->copy(res->status, call->pout + call->o_st, n_items);
+  if (res->msg_hash && n_msgs && !call->direct_hash) ctx->pool->copy(res->msg_hash, call->pout, n_msgs * 32);
+  if (res->status && n_items && !call->direct_status) ctx->pool->copy(res->status, call->pout + call->o_st, n_items);
   if (bits_out && res->accept_bits && n_items)
     memcpy(res->accept_bits, call->pout + call->o_bits, (n_items + 63) / 64 * 8);
   bv_read_timing(ctx);
@@ -1007,8 +1165,8 @@ extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
   bv_host_call call;
-  int rc = bv_host_launch(ctx, b, &call);
-  if (rc != BV_OK) return rc;
+  int rc = bv_host_launch(ctx, b, &call, res);
+  if (rc != BV_OK) return bv_drain(ctx, ctx->stream, rc);
   return bv_host_finish(ctx, b, res, &call, true);
 }
 

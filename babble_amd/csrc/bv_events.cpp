@@ -82,10 +82,17 @@ int validate(bv_ctx *ctx, const bv_event_batch *b) {
 
 }  // namespace
 
+static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *res);
+
 extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result *res) {
   if (!ctx || !eb || !res) return BV_E_ARGS;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  const int rc = verify_events_impl(ctx, eb, res);
+  return rc == BV_OK ? rc : bv_drain(ctx, ctx->stream, rc);
+}
+
+static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *res) {
   bv_host_call call;
   call.t0 = std::chrono::steady_clock::now();
   int rc = validate(ctx, eb);
@@ -93,6 +100,7 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   ctx->timing = bv_timing{};
   const uint64_t n = eb->n_events;
   hipStream_t st = ctx->stream;
+  ctx->last = st;
   if (n == 0) return BV_OK;
 
   // DAG levels over in-batch parents (refs point backwards: one pass)
@@ -272,7 +280,8 @@ extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result
   uint32_t *dig = pipe.o.dig;
 
   // the first part: pinned copies by the pool, H2D on the copy stream
-  hipStream_t cs = ctx->cstream;
+  hipStream_t cs = bv_copy_stream(ctx);
+  if (!cs) return bv_fail(ctx, BV_E_NODEVICE, "copy stream");
   HIPCHK(hipEventRecord(ctx->S().ev[E_CALL], cs), BV_E_LAUNCH, "event");
   auto stage = [&](size_t a0, size_t a1) -> int {
     for (size_t a = a0; a < a1; a += kChunk) {

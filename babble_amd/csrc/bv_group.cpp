@@ -22,6 +22,7 @@
 #include <thread>
 
 #include "bv_internal.h"
+#include "hostplan.h"
 
 namespace {
 
@@ -91,23 +92,6 @@ static int gfail(bv_group *g, int code, const std::string &what) {
 
 extern "C" const char *bv_group_last_error(const bv_group *g) { return g ? g->err.c_str() : "null group"; }
 
-// Contiguous item ranges balanced by count, cut only where the next item
-// names a different message than the previous one (message-aligned), so the
-// items of one message are never split.  Empty shards are allowed.
-extern "C" int bv_plan_shards(const bv_batch *b, int n_shards, uint64_t *bounds) {
-  if (!b || n_shards <= 0 || !bounds) return BV_E_ARGS;
-  const uint64_t n = b->n_items;
-  if (n && !b->item_msg) return BV_E_ARGS;
-  bounds[0] = 0;
-  for (int g = 1; g < n_shards; g++) {
-    uint64_t c = std::max<uint64_t>(bounds[g - 1], (uint64_t)((__uint128_t)n * g / n_shards));
-    while (c > 0 && c < n && b->item_msg[c] == b->item_msg[c - 1]) c++;
-    bounds[g] = std::min(c, n);
-  }
-  bounds[n_shards] = n;
-  return BV_OK;
-}
-
 extern "C" void bv_group_destroy(bv_group *g) {
   if (!g) return;
   for (size_t i = 0; i < g->ctx.size(); i++) {
@@ -168,50 +152,58 @@ extern "C" int bv_group_get_timing(const bv_group *g, int i, bv_timing *out) {
   return bv_get_timing(g->ctx[i], out);
 }
 
+static int group_verify(bv_group *g, const bv_batch *b, bv_result *res, GroupPlan &p);
+
 extern "C" int bv_group_verify_batch(bv_group *g, const bv_batch *b, bv_result *res) {
   if (!g || !b || !res) return BV_E_ARGS;
   std::lock_guard<std::mutex> lk(g->mu);
+  GroupPlan p;
+  const int rc = group_verify(g, b, res, p);
+  if (rc != BV_OK)
+    for (bv_ctx *c : g->ctx) {  // nothing of the failed call stays in flight
+      std::lock_guard<std::mutex> clk(c->mu);
+      (void)hipSetDevice(c->device);
+      (void)bv_drain(c, c->stream, rc);
+    }
+  return rc;
+}
+
+static int group_verify(bv_group *g, const bv_batch *b, bv_result *res, GroupPlan &p) {
   const int D = (int)g->ctx.size();
   int rc = bv_validate_host_batch(g->ctx[0], b);
   if (rc != BV_OK) return gfail(g, rc, g->ctx[0]->err);
-  std::vector<uint64_t> bounds(D + 1);
-  bv_plan_shards(b, D, bounds.data());
+  bv_batch sorted;
+  plan_group(b, D, p, sorted);
+  const std::vector<uint64_t> &bounds = p.bounds;
 
-  // per-device sub-batches: the shard's items and the message range they
-  // name (re-based offsets and indices); keys are replicated (small)
+  // per-device sub-batches: the shard's items and its message range
+  // (re-based offsets and indices); keys are replicated (small)
   std::vector<bv_batch> sb(D);
-  std::vector<uint64_t> mlo(D, 0), mhi(D, 0);
   std::vector<std::vector<uint32_t>> item_msg(D);
   for (int d = 0; d < D; d++) {
-    const uint64_t a = bounds[d], z = bounds[d + 1];
-    uint64_t lo = b->n_msgs, hi = 0;
-    for (uint64_t i = a; i < z; i++) {
-      lo = std::min<uint64_t>(lo, b->item_msg[i]);
-      hi = std::max<uint64_t>(hi, b->item_msg[i] + 1ull);
-    }
-    if (a == z) lo = hi = 0;
-    mlo[d] = lo;
-    mhi[d] = hi;
+    const uint64_t a = bounds[d], z = bounds[d + 1], lo = p.mlo[d], hi = p.mhi[d];
     auto &off = g->sub_off[d];
     off.resize(hi - lo + 1);
     for (uint64_t m = lo; m <= hi; m++) off[m - lo] = b->msg_off[m] - b->msg_off[lo];
     item_msg[d].resize(z - a);
-    for (uint64_t i = a; i < z; i++) item_msg[d][i - a] = (uint32_t)(b->item_msg[i] - lo);
+    for (uint64_t i = a; i < z; i++) item_msg[d][i - a] = (uint32_t)(sorted.item_msg[i] - lo);
     bv_batch &s = sb[d];
-    s = *b;
+    s = sorted;
     s.n_msgs = hi - lo;
     s.msg_bytes = b->msg_bytes ? b->msg_bytes + (hi > lo ? b->msg_off[lo] : 0) : nullptr;
     s.msg_off = off.data();
     s.n_items = z - a;
     s.item_msg = item_msg[d].data();
-    s.item_key = b->item_key ? b->item_key + a : nullptr;
-    s.r_be = b->r_be ? b->r_be + 32 * a : nullptr;
-    s.s_be = b->s_be ? b->s_be + 32 * a : nullptr;
-    s.pre = b->pre ? b->pre + a : nullptr;
+    s.item_key = sorted.item_key ? sorted.item_key + a : nullptr;
+    s.r_be = sorted.r_be ? sorted.r_be + 32 * a : nullptr;
+    s.s_be = sorted.s_be ? sorted.s_be + 32 * a : nullptr;
+    s.pre = sorted.pre ? sorted.pre + a : nullptr;
   }
   uint64_t words = 1;
   for (int d = 0; d < D; d++) words = std::max<uint64_t>(words, (bounds[d + 1] - bounds[d] + 63) / 64);
 
+  if (p.permuted && res->status) p.s_status.resize(b->n_items);
+  uint8_t *st_out = p.permuted ? (res->status ? p.s_status.data() : nullptr) : res->status;
   // stage + launch every shard concurrently (one host thread per device)
   std::vector<bv_host_call> calls(D);
   std::vector<int> rcs(D, BV_OK);
@@ -224,7 +216,10 @@ extern "C" int bv_group_verify_batch(bv_group *g, const bv_batch *b, bv_result *
         rcs[d] = BV_E_NODEVICE;
         return;
       }
-      rcs[d] = bv_host_launch(c, &sb[d], &calls[d]);
+      bv_result sr = {};
+      sr.msg_hash = res->msg_hash ? res->msg_hash + 32 * p.mlo[d] : nullptr;
+      sr.status = st_out ? st_out + bounds[d] : nullptr;
+      rcs[d] = bv_host_launch(c, &sb[d], &calls[d], &sr);
       if (rcs[d] != BV_OK) return;
       // the shard's bits, zero-padded to `words`, as the all-gather send buffer
       if (g->send[d].ensure(words * 8) != hipSuccess || g->recv[d].ensure(words * 8 * D) != hipSuccess) {
@@ -254,33 +249,36 @@ extern "C" int bv_group_verify_batch(bv_group *g, const bv_batch *b, bv_result *
       hipSuccess)
     return gfail(g, BV_E_LAUNCH, "d2h gathered bits");
 
-  // per-device results (digests, statuses) straight into the caller's arrays
+  // per-device results (digests of its message range, statuses of its shard)
   for (int d = 0; d < D; d++) {
     bv_ctx *c = g->ctx[d];
     std::lock_guard<std::mutex> clk(c->mu);
     (void)hipSetDevice(c->device);
     if (bv_mark_done(c, c->stream) != BV_OK) return gfail(g, BV_E_LAUNCH, "event");
     bv_result sr = {};
-    sr.msg_hash = res->msg_hash ? res->msg_hash + 32 * mlo[d] : nullptr;
-    sr.status = res->status ? res->status + bounds[d] : nullptr;
+    sr.msg_hash = res->msg_hash ? res->msg_hash + 32 * p.mlo[d] : nullptr;
+    sr.status = st_out ? st_out + bounds[d] : nullptr;
     rc = bv_host_finish(c, &sb[d], &sr, &calls[d], false);
     if (rc != BV_OK) return gfail(g, rc, c->err);
   }
-  // merge the shard-local words into the global bitmask
-  if (res->accept_bits && b->n_items) {
-    const uint64_t W = (b->n_items + 63) / 64;
-    memset(res->accept_bits, 0, W * 8);
-    for (int d = 0; d < D; d++) {
-      const uint64_t a = bounds[d], n = bounds[d + 1] - a;
-      const uint64_t *src = gathered.data() + (uint64_t)d * words;
-      for (uint64_t w = 0; w < (n + 63) / 64; w++) {
-        uint64_t v = src[w];
-        const uint64_t valid = std::min<uint64_t>(64, n - 64 * w);
-        if (valid < 64) v &= (1ull << valid) - 1;
-        const uint64_t bit = a + 64 * w, q = bit / 64, s = bit % 64;
-        res->accept_bits[q] |= v << s;
-        if (s && q + 1 < W) res->accept_bits[q + 1] |= v >> (64 - s);
-      }
+  if (!res->accept_bits && !p.permuted) return BV_OK;
+  // merge the shard-local words into the bitmask (message order), then back
+  // to the caller's item order when the items were permuted
+  const uint64_t n = b->n_items, W = (n + 63) / 64;
+  uint64_t *merged = res->accept_bits;
+  if (p.permuted) {
+    p.s_bits.assign(std::max<uint64_t>(W, 1), 0);
+    merged = p.s_bits.data();
+  }
+  if (merged && bv_merge_shard_bits(gathered.data(), words, D, bounds.data(), merged) != BV_OK)
+    return gfail(g, BV_E_ARGS, "merge shard bits");
+  if (p.permuted) {
+    if (res->status)
+      for (uint64_t j = 0; j < n; j++) res->status[p.perm[j]] = p.s_status[j];
+    if (res->accept_bits) {
+      memset(res->accept_bits, 0, W * 8);
+      for (uint64_t j = 0; j < n; j++)
+        if (merged[j >> 6] >> (j & 63) & 1) res->accept_bits[p.perm[j] >> 6] |= 1ull << (p.perm[j] & 63);
     }
   }
   return BV_OK;

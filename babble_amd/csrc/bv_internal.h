@@ -206,13 +206,24 @@ struct KcSlot {
   bool free = false;
 };
 
+// The streams a context runs on are per device and per PROCESS, shared by
+// every ctx of that device (refcounted): HIP maps a process's streams onto
+// GPU_MAX_HW_QUEUES hardware queues (4 by default) and two streams on one
+// queue serialise.  A process holds one lane per work slot (the default
+// stream of that slot's calls), the s^-1 stream and the high-priority keys
+// stream — 3 normal-priority queues, so the caller's own stream (or torch's
+// default) still gets a queue of its own; the copy stream is created only
+// when a host-entry call first needs it.
 struct bv_ctx {
   int device = 0;
   uint32_t flags = 0;
-  hipStream_t stream = nullptr;   // main
+  static constexpr int kSlots = BV_SLOTS;
+  hipStream_t lane[kSlots] = {};  // slot k's default stream
+  hipStream_t stream = nullptr;   // lane[0]: host entry points, one-launch helpers
   hipStream_t kstream = nullptr;  // per-batch key tables (high priority)
-  hipStream_t sstream = nullptr;  // batched s^-1
-  hipStream_t cstream = nullptr;  // host-entry copies
+  hipStream_t sstream = nullptr;  // batched s^-1 (+ key decode)
+  hipStream_t cstream = nullptr;  // host-entry copies (bv_copy_stream: created on first use)
+  hipStream_t last = nullptr;     // the stream of the last device call (bv_last_stream)
   std::mutex mu;
   std::string err;
   const uint32_t *g_table = nullptr;  // process-wide, per device (gtable_acquire)
@@ -237,7 +248,6 @@ struct bv_ctx {
     hipEvent_t done = nullptr;  // end of the last call that used this slot
     bool has_done = false;
   };
-  static constexpr int kSlots = BV_SLOTS;
   Slot slot[kSlots];
   int cur = 0;
   Slot &S() { return slot[cur]; }
@@ -262,9 +272,17 @@ struct bv_host_call {
   float ms_prep = 0;
   uint8_t *pout = nullptr;
   size_t o_st = 0, o_bits = 0;
+  bool direct_in = false;                          // message bytes DMA'd from the caller's pinned buffer
+  bool direct_hash = false, direct_status = false;  // results DMA'd into the caller's pinned buffers
 };
+bool bv_is_pinned(const void *p, size_t n);  // [p, p+n) inside one bv_host_alloc block
 
 int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess);
+hipStream_t bv_copy_stream(bv_ctx *ctx);   // the device's copy stream (created on first use; nullptr on failure)
+// After a failed call: wait until nothing the call may have enqueued on the
+// ctx's streams (and on `st`) is still running, so no slot keeps orphaned
+// kernels that a later call would not wait for.  Returns `rc`.
+int bv_drain(bv_ctx *ctx, hipStream_t st, int rc);
 int bv_wait_all(bv_ctx *ctx);              // host: every call's device work has finished
 int bv_mark_done(bv_ctx *ctx, hipStream_t st);
 // Next slot for a device call writing `res`: st waits for the slot's last
@@ -301,6 +319,8 @@ int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
                   hipStream_t st, bool hashed, bool kc);
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
                   const uint64_t *dko, hipStream_t st, bool *use);
-int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call);
+// `res` (may be null): the caller's result buffers, written by DMA directly
+// when they are bv_host_alloc memory (else bv_host_finish copies them).
+int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_result *res = nullptr);
 int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call *call, bool bits_out);
 void bv_read_timing(bv_ctx *ctx);

@@ -198,7 +198,7 @@ def fast_forward_check(block: Block, frame: Frame, verifier=None) -> Optional[st
     for s in sigs:
         bb.add_item(m_block, bb.add_key(s.Validator or b""), s.Signature)
     res = v.verify(bb.pack())
-    outcomes = [_item_outcome(int(st)) for st in res.status]
+    outcomes = [_item_outcome(int(st), s.Signature) for st, s in zip(res.status, sigs)]
     if any(o.panic for o in outcomes):
         raise ReferencePanic("Block.Verify panics")
     valid = sum(1 for o in outcomes if o.ok)

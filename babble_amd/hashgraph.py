@@ -275,16 +275,24 @@ def _single(o: Outcome) -> Tuple[bool, Optional[str]]:
 # ----------------------------------------------------------------------------
 # batch verification (one bv_verify_batch per call)
 # ----------------------------------------------------------------------------
-_ERR_PARTS = "wrong number of values in signature"
+def parts_error(sig) -> str:
+    """keys.DecodeSignature's error (signature.go:31-35): strings.Split on
+    "|" gave len(values) != 2.  The device reports only the status
+    (REJECT_ERR); the part count is the host's, as in Go."""
+    if isinstance(sig, (bytes, bytearray)):
+        sig = bytes(sig).decode("utf-8", errors="surrogateescape")
+    return "wrong number of values in signature: got %d, want 2" % (sig.count("|") + 1)
 
 
-def _item_outcome(st: int) -> Outcome:
+def _item_outcome(st: int, sig="") -> Outcome:
+    """One item status as Go's (ok, err) / panic; `sig` is the item's
+    signature text (for the REJECT_ERR message)."""
     if st == ACCEPT:
         return Outcome(True)
     if st == REJECT:
         return Outcome(False)
     if st == REJECT_ERR:
-        return Outcome(False, _ERR_PARTS)
+        return Outcome(False, parts_error(sig))
     return Outcome(False, "reference panic (nil pointer dereference)", panic=True)
 
 
@@ -303,11 +311,11 @@ def verify_itxs(itxs: Sequence[InternalTransaction], verifier=None) -> List[Outc
     idx = [_add_itx(bb, t) for t in itxs]
     res = (verifier or default_verifier()).verify(bb.pack()) if bb._item_msg else None
     out = []
-    for k in idx:
+    for t, k in zip(itxs, idx):
         if k is None:
             out.append(Outcome(False, "slice bounds out of range", panic=True))
         else:
-            out.append(_item_outcome(int(res.status[k])))
+            out.append(_item_outcome(int(res.status[k]), t.Signature))
     return out
 
 
@@ -327,24 +335,25 @@ def verify_events(events: Sequence[Event], verifier=None) -> List[Outcome]:
     for ev, (itx_items, item, m) in zip(events, plan):
         ev._hash = res.msg_hash[m].tobytes()
         itx_st = [None if k is None else int(res.status[k]) for k in itx_items]
-        out.append(compose_event_outcome(itx_st, int(res.status[item])))
+        out.append(compose_event_outcome(itx_st, int(res.status[item]),
+                                         [t.Signature for t in (ev.Body.InternalTransactions or [])], ev.Signature))
     return out
 
 
-def compose_event_outcome(itx_statuses: Sequence[Optional[int]], event_status: int) -> Outcome:
+def compose_event_outcome(itx_statuses: Sequence[Optional[int]], event_status: int,
+                          itx_sigs: Sequence = (), event_sig="") -> Outcome:
     """Event.Verify's order (event.go:219-247): each ITX in order, the first
-    failure wins (None = PubKeyBytes panicked); then the event signature."""
-    for st in itx_statuses:  # event.go:222-230
+    failure wins (None = PubKeyBytes panicked); then the event signature.
+    An ITX's DecodeSignature error is returned unchanged (event.go:223-225)."""
+    for j, st in enumerate(itx_statuses):  # event.go:222-230
         if st is None:
             return Outcome(False, "slice bounds out of range", panic=True)
         if st == ACCEPT:
             continue
-        if st == REJECT_ERR:
-            return Outcome(False, _ERR_PARTS)
-        if st == REF_PANIC:
-            return _item_outcome(st)
+        if st in (REJECT_ERR, REF_PANIC):
+            return _item_outcome(st, itx_sigs[j] if j < len(itx_sigs) else "")
         return Outcome(False, "invalid signature on internal transaction")
-    return _item_outcome(event_status)
+    return _item_outcome(event_status, event_sig)
 
 
 def verify_block_signatures(block: Block, sigs: Sequence[BlockSignature], verifier=None) -> List[Outcome]:
@@ -356,7 +365,7 @@ def verify_block_signatures(block: Block, sigs: Sequence[BlockSignature], verifi
     m = bb.add_msg(block.Body.Marshal())
     items = [bb.add_item(m, bb.add_key(s.Validator or b""), s.Signature) for s in sigs]
     res = (verifier or default_verifier()).verify(bb.pack())
-    return [_item_outcome(int(res.status[k])) for k in items]
+    return [_item_outcome(int(res.status[k]), s.Signature) for s, k in zip(sigs, items)]
 
 
 def check_block(block: Block, peer_set: PeerSet, verifier=None) -> Optional[str]:
@@ -402,7 +411,7 @@ def process_sig_pool(pending: Sequence[BlockSignature], get_block: Callable[[int
     res = (verifier or default_verifier()).verify(bb.pack()) if items else None
     appended = []
     for (bs, blk), k in zip(cands, items):
-        o = _item_outcome(int(res.status[k]))
+        o = _item_outcome(int(res.status[k]), bs.Signature)
         if o.panic:
             raise ReferencePanic("Block.Verify panics")
         if o.err:

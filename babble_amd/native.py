@@ -23,7 +23,7 @@ REJECT, ACCEPT, REJECT_ERR, REF_PANIC = 0, 1, 2, 3
 SC_OK, SC_NIL, SC_NONPOS, SC_GE_N = 0, 1, 2, 3
 PRE_PARTS_BAD = 0x80
 F_DEFAULT = 0
-ABI_VERSION = 3
+ABI_VERSION = 4
 F_KEY_CACHE = 1
 F_K8 = 2
 
@@ -33,6 +33,7 @@ EXPORTS = (
     "bv_verify_batch_device", "bv_sha256_batch", "bv_get_timing", "bv_decode_signature",
     "bv_hex_decode", "bv_group_create", "bv_group_destroy", "bv_group_last_error", "bv_group_verify_batch",
     "bv_group_get_timing", "bv_plan_shards", "bv_sync", "bv_peer_set_hash", "bv_verify_events",
+    "bv_last_stream", "bv_host_alloc", "bv_host_free", "bv_merge_shard_bits", "bv_plan_group",
 )
 
 
@@ -143,6 +144,16 @@ def lib() -> ctypes.CDLL:
     L.bv_sync.restype = ctypes.c_int
     L.bv_plan_shards.argtypes = [ctypes.POINTER(BvBatch), ctypes.c_int, P]
     L.bv_plan_shards.restype = ctypes.c_int
+    L.bv_last_stream.argtypes = [P]
+    L.bv_last_stream.restype = P
+    L.bv_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(P)]
+    L.bv_host_alloc.restype = ctypes.c_int
+    L.bv_host_free.argtypes = [P]
+    L.bv_host_free.restype = None
+    L.bv_merge_shard_bits.argtypes = [P, ctypes.c_uint64, ctypes.c_int, P, P]
+    L.bv_merge_shard_bits.restype = ctypes.c_int
+    L.bv_plan_group.argtypes = [ctypes.POINTER(BvBatch), ctypes.c_int, P, P, P]
+    L.bv_plan_group.restype = ctypes.c_int
     if L.bv_abi_version() != ABI_VERSION:
         raise BvError(BV_E_ARGS, "ABI version mismatch")
     _lib = L

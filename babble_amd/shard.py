@@ -49,6 +49,26 @@ def plan_shards(item_msg: np.ndarray, world: int) -> List[int]:
     return bounds
 
 
+def plan_group(item_msg: np.ndarray, n_msgs: int, world: int):
+    """bv_plan_group (csrc/hostplan.cpp) restated: (permuted, perm,
+    item_bounds, msg_bounds).  Items are stably sorted by message when
+    item_msg is not non-decreasing; item shards follow plan_shards over that
+    order; device d hashes messages [msg_bounds[d], msg_bounds[d+1]) — a
+    partition of [0, n_msgs) cut at each shard's first message."""
+    im = np.asarray(item_msg, dtype=np.int64)
+    n = len(im)
+    permuted = bool(n > 1 and np.any(im[1:] < im[:-1]))
+    perm = np.argsort(im, kind="stable") if permuted else np.arange(n)
+    srt = im[perm]
+    bounds = plan_shards(srt, world)
+    mb, prev = [], 0
+    for d in range(world):
+        cut = 0 if d == 0 else (int(srt[bounds[d]]) if bounds[d] < n else n_msgs)
+        prev = max(prev, cut)
+        mb.append(prev)
+    return permuted, perm, bounds, mb + [n_msgs]
+
+
 def merge_bits(shard_words: Sequence[np.ndarray], bounds: Sequence[int]) -> np.ndarray:
     """Global accept bitmask from per-shard bitmasks whose bit 0 is the
     shard's first item (the host merge after bv_group's all-gather)."""

@@ -290,7 +290,7 @@ def sync_verify_device(wevents: Sequence[WireEvent], repertoire_by_id: Dict[int,
                                   Timestamp=we.Body.Timestamp), Signature=we.Signature)
         ev._hash = digests[i]
         events.append(ev)
-        o = _item_outcome(int(res.status[i]))
+        o = _item_outcome(int(res.status[i]), we.Signature)
         for io in itx_out.get(i, []):  # event.go:222-230: the first ITX failure wins
             if not io.ok or io.panic:
                 o = io if (io.panic or io.err) else Outcome(False, "invalid signature on internal transaction")

@@ -66,7 +66,7 @@ def events(n_events: int, n_creators: int = 64, seed: int = 2, n_tx: int = 1, tx
     if used == 0 and n_events > 0:
         raise RuntimeError("synth_events failed")
     key_off = np.arange(n_creators + 1, dtype=np.uint64) * 65
-    return PackedBatch(msg[:used].copy(), off, keys, key_off, np.arange(n_events, dtype=np.uint32), item_key, r, s,
+    return PackedBatch(msg[:used], off, keys, key_off, np.arange(n_events, dtype=np.uint32), item_key, r, s,
                        np.zeros(n_events, np.uint8))
 
 
@@ -116,6 +116,26 @@ def event_fields(n_events: int, n_creators: int = 64, seed: int = 2, n_tx: int =
         itx_json=np.zeros(0, np.uint8), bsig_off=None, bsig_json=np.zeros(0, np.uint8), r_be=r.copy(), s_be=s.copy(),
         pre=np.zeros(n_events, np.uint8))
     return packed, wire
+
+
+def c3_chunk(idx: int, n: int = 1_000_000, n_creators: int = 64):
+    """Chunk `idx` of the C3 workload (10^8 events, seed 3, 64
+    creators, streamed in chunks): seed 3 + idx; about one item in 10^4
+    (seeded) gets one r bit flipped, so the exact accept bitmask is known by
+    construction.  Returns (batch, sorted indices of the flipped items)."""
+    b = events(n, n_creators=n_creators, seed=3 + idx)
+    rng = np.random.default_rng(1000 + idx)
+    bad = np.sort(rng.choice(n, max(1, n // 10_000), replace=False))
+    b.r_be[bad, int(rng.integers(0, 32))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    return b, bad
+
+
+def expected_bits(n: int, rejected) -> np.ndarray:
+    """Accept bitmask words (LSB-first) with every item accepted except `rejected`."""
+    ok = np.ones(n, bool)
+    ok[np.asarray(rejected, dtype=np.int64)] = False
+    pk = np.packbits(ok, bitorder="little")
+    return np.concatenate([pk, np.zeros((-len(pk)) % 8, np.uint8)]).view(np.uint64)[: (n + 63) // 64]
 
 
 @dataclass

@@ -20,6 +20,7 @@
 #include <openssl/obj_mac.h>
 #include <openssl/sha.h>
 
+#include <array>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -87,14 +88,6 @@ void b64(std::string &o, const uint8_t *p, size_t n) {
   }
 }
 
-void hexup(std::string &o, const uint8_t *p, size_t n) {
-  static const char H[] = "0123456789ABCDEF";
-  for (size_t i = 0; i < n; i++) {
-    o += H[p[i] >> 4];
-    o += H[p[i] & 15];
-  }
-}
-
 struct Signer {
   BIGNUM *d = nullptr;
   std::vector<BIGNUM *> kinv;  // nonce pool: k^-1 mod N
@@ -127,26 +120,36 @@ struct Ctx {
       if (!BN_is_zero(x) && BN_cmp(x, n) < 0) return x;
     }
   }
+  // Nonce pool: k_j = k_0 + j delta (mod N) with k_0, delta from the DRBG,
+  // so R_j = R_(j-1) + delta G is one point addition instead of a full
+  // scalar multiplication per nonce (generation-side cost only; r = x(R_j)
+  // still varies like a random nonce's, the verifier cannot exploit it).
   void make_signer(Signer &s, Drbg &dr, uint32_t pool) {
     s.d = scalar(dr);
-    EC_POINT *P = EC_POINT_new(g);
+    EC_POINT *P = EC_POINT_new(g), *D = EC_POINT_new(g);
     EC_POINT_mul(g, P, s.d, nullptr, nullptr, bn);
     EC_POINT_point2oct(g, P, POINT_CONVERSION_UNCOMPRESSED, s.pub, 65, bn);
+    BIGNUM *k = scalar(dr), *delta = scalar(dr);
+    EC_POINT_mul(g, P, k, nullptr, nullptr, bn);
+    EC_POINT_mul(g, D, delta, nullptr, nullptr, bn);
     BIGNUM *x = BN_new(), *y = BN_new();
     for (uint32_t i = 0; i < pool; i++) {
-      BIGNUM *k = scalar(dr);
-      EC_POINT_mul(g, P, k, nullptr, nullptr, bn);
+      if (i) {
+        EC_POINT_add(g, P, P, D, bn);
+        BN_mod_add(k, k, delta, n, bn);
+      }
       EC_POINT_get_affine_coordinates(g, P, x, y, bn);
       BIGNUM *rr = BN_new();
       BN_nnmod(rr, x, n, bn);
-      BIGNUM *ki = BN_mod_inverse(nullptr, k, n, bn);
-      s.kinv.push_back(ki);
+      s.kinv.push_back(BN_mod_inverse(nullptr, k, n, bn));
       s.r.push_back(rr);
-      BN_free(k);
     }
+    BN_free(k);
+    BN_free(delta);
     BN_free(x);
     BN_free(y);
     EC_POINT_free(P);
+    EC_POINT_free(D);
   }
   // s = k^-1 (e + r d) mod N with pool entry j; writes 32-byte BE r, s
   void sign(const Signer &sg, uint32_t j, const uint8_t digest[32], uint8_t r_out[32], uint8_t s_out[32]) {
@@ -166,37 +169,6 @@ struct Ctx {
     for (auto *b : s.r) BN_free(b);
   }
 };
-
-std::string event_body(const std::vector<std::vector<uint8_t>> &txs, bool txs_nil, const std::string &p0,
-                       const std::string &p1, const uint8_t *creator, int64_t index, int64_t ts) {
-  std::string o;
-  o.reserve(512 + 96 * txs.size());
-  o += "{\"Transactions\":";
-  if (txs_nil) {
-    o += "null";
-  } else {
-    o += '[';
-    for (size_t i = 0; i < txs.size(); i++) {
-      if (i) o += ',';
-      o += '"';
-      b64(o, txs[i].data(), txs[i].size());
-      o += '"';
-    }
-    o += ']';
-  }
-  o += ",\"InternalTransactions\":null,\"Parents\":[\"";
-  o += p0;
-  o += "\",\"";
-  o += p1;
-  o += "\"],\"Creator\":\"";
-  b64(o, creator, 65);
-  o += "\",\"Index\":";
-  o += std::to_string(index);
-  o += ",\"BlockSignatures\":null,\"Timestamp\":";
-  o += std::to_string(ts);
-  o += "}\n";
-  return o;
-}
 
 }  // namespace
 
@@ -239,40 +211,75 @@ uint64_t synth_events_fields(uint64_t seed, uint32_t n_creators, uint64_t n_even
     memcpy(key_bytes + 65 * c, sg[c].pub, 65);
   }
   SplitMix rng(seed * 0x2545F4914F6CDD1Dull + 7);
-  std::vector<std::string> last_hex(n_creators);  // "0X..." of each creator's latest event
-  std::vector<int64_t> last_ev(n_creators, -1);   // ... and its batch index
+  // the body is written in place (no per-event allocation): constant JSON
+  // pieces, each creator's base64 key computed once, parents' "0X..." hex
+  // kept per creator (66 chars)
+  std::vector<std::string> creator_b64(n_creators);
+  for (uint32_t c = 0; c < n_creators; c++) b64(creator_b64[c], sg[c].pub, 65);
+  std::vector<std::array<char, 66>> last_hex(n_creators);  // "0X..." of each creator's latest event
+  std::vector<int64_t> last_ev(n_creators, -1);            // ... and its batch index
   std::vector<int64_t> next_index(n_creators, 0);
-  std::vector<std::vector<uint8_t>> txs(n_tx, std::vector<uint8_t>(tx_bytes));
+  std::vector<uint8_t> txs((size_t)n_tx * tx_bytes);
+  std::string tmp;
   uint64_t pos = 0;
   msg_off[0] = 0;
+  const uint64_t per_max = 400 + (uint64_t)n_tx * (4 * ((tx_bytes + 2) / 3) + 3) + 64;
   for (uint64_t i = 0; i < n_events; i++) {
     const uint32_t c = (uint32_t)(i % n_creators);
     const uint32_t other = (c + 1) % n_creators;
-    for (auto &t : txs) rng.fill(t.data(), t.size());
+    for (uint32_t t = 0; t < n_tx; t++) rng.fill(txs.data() + (size_t)t * tx_bytes, tx_bytes);
     const int64_t idx = next_index[c]++;
-    std::string p0, p1;
-    if (idx > 0) {
-      p0 = last_hex[c];
-      p1 = last_hex[other];  // may be "" if the other creator has no event yet
-    }
+    const bool has_p1 = idx > 0 && last_ev[other] >= 0;  // the other creator may have no event yet
     if (parent_out) {
       parent_out[2 * i] = idx > 0 ? last_ev[c] : -1;
-      parent_out[2 * i + 1] = idx > 0 && !p1.empty() ? last_ev[other] : -1;
+      parent_out[2 * i + 1] = has_p1 ? last_ev[other] : -1;
     }
     if (index_out) index_out[i] = idx;
     if (ts_out) ts_out[i] = ts0 + (int64_t)i;
-    if (tx_out)
-      for (uint32_t t = 0; t < n_tx; t++) memcpy(tx_out + ((uint64_t)i * n_tx + t) * tx_bytes, txs[t].data(), tx_bytes);
-    std::string body = event_body(txs, n_tx == 0, p0, p1, sg[c].pub, idx, ts0 + (int64_t)i);
-    if (pos + body.size() > msg_cap) return 0;
-    memcpy(msg_bytes + pos, body.data(), body.size());
-    pos += body.size();
+    if (tx_out) memcpy(tx_out + (uint64_t)i * n_tx * tx_bytes, txs.data(), (size_t)n_tx * tx_bytes);
+    if (pos + per_max > msg_cap) return 0;
+    char *o = (char *)msg_bytes + pos, *const o0 = o;
+    auto put = [&o](const char *p, size_t n) {
+      memcpy(o, p, n);
+      o += n;
+    };
+    auto lit = [&put](const char *p) { put(p, strlen(p)); };
+    lit("{\"Transactions\":");
+    if (n_tx == 0) {
+      lit("null");
+    } else {
+      *o++ = '[';
+      for (uint32_t t = 0; t < n_tx; t++) {
+        if (t) *o++ = ',';
+        *o++ = '"';
+        tmp.clear();
+        b64(tmp, txs.data() + (size_t)t * tx_bytes, tx_bytes);
+        put(tmp.data(), tmp.size());
+        *o++ = '"';
+      }
+      *o++ = ']';
+    }
+    lit(",\"InternalTransactions\":null,\"Parents\":[\"");
+    if (idx > 0) put(last_hex[c].data(), 66);
+    lit("\",\"");
+    if (has_p1) put(last_hex[other].data(), 66);
+    lit("\"],\"Creator\":\"");
+    put(creator_b64[c].data(), creator_b64[c].size());
+    lit("\",\"Index\":");
+    o += snprintf(o, 24, "%lld", (long long)idx);
+    lit(",\"BlockSignatures\":null,\"Timestamp\":");
+    o += snprintf(o, 24, "%lld", (long long)(ts0 + (int64_t)i));
+    lit("}\n");
+    const size_t len = (size_t)(o - o0);
+    pos += len;
     msg_off[i + 1] = pos;
     uint8_t dig[32];
-    SHA256((const uint8_t *)body.data(), body.size(), dig);
-    std::string hx = "0X";
-    hexup(hx, dig, 32);
-    last_hex[c] = hx;
+    SHA256((const uint8_t *)o0, len, dig);
+    static const char H[] = "0123456789ABCDEF";
+    char *hx = last_hex[c].data();
+    hx[0] = '0';
+    hx[1] = 'X';
+    for (int k = 0; k < 32; k++) hx[2 + 2 * k] = H[dig[k] >> 4], hx[3 + 2 * k] = H[dig[k] & 15];
     last_ev[c] = (int64_t)i;
     if (digest_out) memcpy(digest_out + 32 * i, dig, 32);
     item_key[i] = c;

@@ -151,6 +151,20 @@ class Verifier:
                                                    stream or 0, 0 if sync else 1))
         d._pending = None if sync else self
 
+    def last_stream(self) -> int:
+        """bv_last_stream: the hipStream_t the last call ran on (a NULL-stream
+        device call runs on the library's lane for its work slot)."""
+        return self._L.bv_last_stream(self._ctx) or 0
+
+    def verify_into(self, b: PackedBatch, res: VerifyResult) -> VerifyResult:
+        """bv_verify_batch into caller-owned result arrays (e.g. PinnedArena
+        arrays, which the results reach by DMA without a host copy)."""
+        keep: list = []
+        cb = _cbatch(b, keep)
+        r = native.BvResult(_p(res.msg_hash), _p(res.status), _p(res.accept_bits))
+        self._check(self._L.bv_verify_batch(self._ctx, ctypes.byref(cb), ctypes.byref(r)))
+        return res
+
     def sync(self) -> None:
         """bv_sync: wait for this ctx's last (async) call."""
         self._check(self._L.bv_sync(self._ctx))
@@ -275,3 +289,68 @@ class Group:
         if rc != native.BV_OK:
             raise native.BvError(rc, "bv_group_get_timing")
         return {k: getattr(t, k) for k, _ in native.BvTiming._fields_}
+
+
+def plan_group(b: PackedBatch, n_shards: int):
+    """bv_plan_group: (permuted, perm, item_bounds, msg_bounds) — the plan
+    bv_group_verify_batch follows (host only)."""
+    keep: list = []
+    cb = _cbatch(b, keep)
+    ib = np.zeros(n_shards + 1, np.uint64)
+    mb = np.zeros(n_shards + 1, np.uint64)
+    perm = np.zeros(max(b.n_items, 1), np.uint32)
+    rc = native.lib().bv_plan_group(ctypes.byref(cb), n_shards, ib.ctypes.data, mb.ctypes.data, perm.ctypes.data)
+    if rc < 0:
+        raise native.BvError(rc, "bv_plan_group")
+    return bool(rc), perm[: b.n_items], ib, mb
+
+
+def merge_shard_bits(gathered: np.ndarray, words_per_shard: int, bounds) -> np.ndarray:
+    """bv_merge_shard_bits: the global bitmask from all-gathered shard words
+    (host only; what bv_group_verify_batch does after its all-gather)."""
+    g = np.ascontiguousarray(gathered, dtype=np.uint64)
+    bd = np.ascontiguousarray(bounds, dtype=np.uint64)
+    out = np.zeros(max((int(bd[-1]) + 63) // 64, 1), np.uint64)
+    rc = native.lib().bv_merge_shard_bits(_p(g), words_per_shard, len(bd) - 1, bd.ctypes.data, out.ctypes.data)
+    if rc != native.BV_OK:
+        raise native.BvError(rc, "bv_merge_shard_bits")
+    return out[: (int(bd[-1]) + 63) // 64]
+
+
+class PinnedArena:
+    """Arrays in bv_host_alloc memory (page-locked): a batch built here is
+    DMA'd by bv_verify_batch without the staging copy (what the cgo shim does
+    instead of C.CBytes).  Freed with close()."""
+
+    def __init__(self):
+        self._L = native.lib()
+        self._blocks = []
+
+    def array(self, shape, dtype) -> np.ndarray:
+        dtype = np.dtype(dtype)
+        n = int(np.prod(shape)) * dtype.itemsize
+        p = ctypes.c_void_p()
+        rc = self._L.bv_host_alloc(max(n, 1), ctypes.byref(p))
+        if rc != native.BV_OK:
+            raise native.BvError(rc, "bv_host_alloc")
+        self._blocks.append(p.value)
+        buf = (ctypes.c_uint8 * max(n, 1)).from_address(p.value)
+        return np.frombuffer(buf, dtype=np.uint8, count=n).view(dtype).reshape(shape)
+
+    def copy(self, a: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(a)
+        out = self.array(a.shape, a.dtype)
+        out[...] = a
+        return out
+
+    def batch(self, b: PackedBatch) -> PackedBatch:
+        """The same batch with every array in pinned memory."""
+        return PackedBatch(self.copy(b.msg_bytes), self.copy(b.msg_off.astype(np.uint64)), self.copy(b.key_bytes),
+                           self.copy(b.key_off.astype(np.uint64)), self.copy(b.item_msg.astype(np.uint32)),
+                           self.copy(b.item_key.astype(np.uint32)), self.copy(b.r_be), self.copy(b.s_be),
+                           None if b.pre is None else self.copy(b.pre))
+
+    def close(self):
+        for p in self._blocks:
+            self._L.bv_host_free(p)
+        self._blocks = []

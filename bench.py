@@ -38,12 +38,11 @@ import argparse
 import json
 import os
 
-# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process
-# (default 4).  This process holds the verifier's streams (main, keys, s^-1,
-# copy), the key-cache verifier's and torch's two step streams: with 4 queues
-# some share one and their kernels serialise (373 vs 452 M verifies/s on the
-# same box).  Set before HIP initialises; an explicit value wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
+# default) and streams sharing a queue run serially.  The library owns every
+# stream a step uses — one lane per work slot, s^-1, the high-priority key
+# tables; one set per device shared by all its contexts — so the headline
+# holds at the default 4 queues (the bench creates no streams of its own).
 import sys
 import time
 
@@ -164,19 +163,21 @@ def pmc_profile(n_items: int):
     return tj if tj.get("items_per_launch") == n_items else None
 
 
-def corrupted(rank: int, n: int):
-    """The seeded items of rank `rank`'s shard whose r has a bit flipped."""
+def corrupted(rank: int, n: int, buf: int = 0):
+    """The seeded items of rank `rank`'s shard (in-flight buffer `buf`) whose
+    r has a bit flipped: each buffer has its own set, so a race between two
+    overlapping steps cannot write the other buffer's (identical) answer."""
     import numpy as np
 
-    rng = np.random.default_rng(7919 + rank)
+    rng = np.random.default_rng(7919 + rank + 100_003 * buf)
     return np.sort(rng.choice(n, max(1, n // 10_000), replace=False))
 
 
-def expected_words(rank: int, n: int):
+def expected_words(rank: int, n: int, buf: int = 0):
     import numpy as np
 
     ok = np.ones(n, bool)
-    ok[corrupted(rank, n)] = False
+    ok[corrupted(rank, n, buf)] = False
     packed = np.packbits(ok, bitorder="little")
     words = (n + 63) // 64
     return np.concatenate([packed, np.zeros(words * 8 - len(packed), np.uint8)]).view(np.uint64)
@@ -236,51 +237,60 @@ def main():
 
     dist = None
     torch.cuda.set_device(local)
+    torch.zeros(1, device=f"cuda:{local}")  # torch's default stream takes its queue first (idle while timed)
     if world > 1:
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     # Per-rank shard: same 64 creators (seeded keys), disjoint events.  One
-    # item in 10^4 (seeded by rank) has an r bit flipped, so the all-gathered
-    # accept bitmask has known zeros and is checked bit for bit below.
+    # item in 10^4 (seeded by rank and in-flight buffer) has an r bit flipped,
+    # so every accept bitmask has known zeros and is checked bit for bit below.
     batch = synth.events(args.events, n_creators=args.creators, seed=2,
                          ts0=synth.TS0 + rank * args.events * 8)
-    batch.r_be[corrupted(rank, args.events), 31] ^= 1
+    clean_r = batch.r_be.copy()
     v = Verifier(device=local)
-    # Consecutive steps alternate two streams and two result buffers (the
-    # library alternates its two work-buffer slots), so one batch's key
-    # tables and hashing overlap the previous batch's k_verify_q tail — a
+    # Consecutive steps alternate two result buffers and the library's two
+    # work slots, each slot on its own library lane (stream), so one batch's
+    # key tables and hashing overlap the previous batch's k_verify_q tail — a
     # node verifying back-to-back SyncResponses.  Every step still verifies
     # its whole batch; the result of each buffer's last step is checked.
-    devs = [v.to_device(batch) for _ in range(args.inflight)]
-    streams = [torch.cuda.Stream(device=local) for _ in range(args.inflight)]
+    devs = []
+    for j in range(args.inflight):
+        batch.r_be = clean_r.copy()
+        batch.r_be[corrupted(rank, args.events, j), 31] ^= 1
+        devs.append(v.to_device(batch))
+    batch.r_be = clean_r
+    batch.r_be[corrupted(rank, args.events, 0), 31] ^= 1  # the CPU baseline's sample = buffer 0's batch
     torch.cuda.synchronize()
     words = devs[0].accept_bits.numel()
     gathered = ([torch.empty(words * world, dtype=torch.int64, device=f"cuda:{local}") for _ in devs]
                 if world > 1 else None)
+    ext = {}
     k = [0]
 
     def step_with(ver):
         def step():
             j = k[0] % len(devs)
             k[0] += 1
-            with torch.cuda.stream(streams[j]):
-                ver.verify_device(devs[j], sync=False)  # on streams[j]
-                if world > 1:  # ordered after the verify on the same stream
+            ver.verify_device(devs[j], stream=0, sync=False)  # on the library lane of the call's slot
+            if world > 1:  # ordered after the verify: the gather is issued on the same lane
+                h = ver.last_stream()
+                if h not in ext:
+                    ext[h] = torch.cuda.ExternalStream(h, device=f"cuda:{local}")
+                with torch.cuda.stream(ext[h]):
                     dist.all_gather_into_tensor(gathered[j], devs[j].accept_bits)
         return step
 
     elapsed, tms = timed_steps(step_with(v), args.steps, args.warmup, world, dist, local, v)
-    want = expected_words(rank, args.events)
     for j, dev in enumerate(devs):
         res = dev.result()
-        if not np.array_equal(res.accept_bits, want):
+        if not np.array_equal(res.accept_bits, expected_words(rank, args.events, j)):
             raise SystemExit(f"rank {rank}: accept bitmask (buffer {j}) differs from the expected one")
         if world > 1:  # the all-gathered mask of the buffer's last step: every rank's shard, bit for bit
             got = gathered[j].cpu().numpy().view(np.uint64).reshape(world, -1)
             for q in range(world):
-                if not np.array_equal(got[q], expected_words(q, args.events)):
+                if not np.array_equal(got[q], expected_words(q, args.events, j)):
                     raise SystemExit(f"rank {rank}: gathered bitmask of rank {q} differs from the expected one")
 
     # Kernel durations for the roofline: with two batches in flight the
@@ -362,7 +372,9 @@ def main():
             },
             "roofline": roof,
             "bitmask_check": f"exact: {world} x {args.events} events, accept bits all-gathered and equal to the "
-                             f"expected mask ({len(corrupted(0, args.events))} seeded r-bit flips per rank rejected)",
+                             f"expected mask ({len(corrupted(0, args.events))} seeded r-bit flips per rank and "
+                             f"in-flight buffer, a different set per buffer, rejected)",
+            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
         }
     if rank == 0 and world == 1 and not args.no_extras:
         line["warm"] = warm_leg(args, devs, world, dist, local, step_with)
@@ -394,8 +406,8 @@ def warm_leg(args, devs, world, dist, local, step_with):
     cold_ms = (time.perf_counter() - t0) * 1e3
     builds = vc.timing()["kc_builds"]
     elapsed, tms = timed_steps(step_with(vc), args.steps, 1, 1, None, local, vc)
-    for dev in devs:
-        assert np.array_equal(dev.result().accept_bits, expected_words(0, args.events))
+    for j, dev in enumerate(devs):
+        assert np.array_equal(dev.result().accept_bits, expected_words(0, args.events, j))
     out = {"value": args.events * args.steps / elapsed, "unit": "verifies/s",
            "ms_per_step": elapsed / args.steps * 1e3, "first_call_ms": cold_ms, "tables_built_first_call": builds,
            "key_path": int(tms[-1]["key_path"]),

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define BV_ABI_VERSION 3
+#define BV_ABI_VERSION 4
 
 /* Return codes (per-item outcomes are never errors; they go to status[]). */
 #define BV_OK 0
@@ -131,8 +131,18 @@ int bv_create(bv_ctx **out, int device, uint32_t flags);
 void bv_destroy(bv_ctx *ctx);
 const char *bv_last_error(const bv_ctx *ctx);
 
-/* Synchronous batch verify from host buffers (the cgo entry point). */
+/* Synchronous batch verify from host buffers (the cgo entry point).  Any
+ * input array or result buffer that lies in memory from bv_host_alloc is
+ * moved by DMA from / to where it is; other (pageable) buffers go through
+ * the ctx's pinned staging, one extra host copy each. */
 int bv_verify_batch(bv_ctx *ctx, const bv_batch *batch, bv_result *result);
+
+/* Page-locked host memory (hipHostMalloc, portable to every device) for
+ * callers that build their batches in place (the cgo shim allocates its
+ * bv_batch arrays here instead of C.CBytes copies).  bv_host_free ignores
+ * pointers it did not allocate.  No device context is needed. */
+int bv_host_alloc(size_t bytes, void **out);
+void bv_host_free(void *p);
 
 /* Same, with every bv_batch / bv_result pointer in device memory of the ctx's
  * device (inputs already resident in HBM).  `stream` is a hipStream_t (NULL =
@@ -142,6 +152,16 @@ int bv_verify_batch(bv_ctx *ctx, const bv_batch *batch, bv_result *result);
  * aligned vector loads; the host entry points pad their staging copies). */
 int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dresult,
                            void *stream, int async);
+/* Streams: a process holds ONE set per device, shared by all its contexts
+ * (HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES hardware
+ * queues, 4 by default; streams sharing a queue run serially): one lane per
+ * work slot, the s^-1 stream and a high-priority key-table stream, plus a
+ * copy stream created by the first host-entry call.  A NULL `stream` above
+ * runs the call on its slot's lane, so consecutive async calls overlap
+ * without the caller creating streams.  bv_last_stream returns the stream
+ * the ctx's last call ran on (a hipStream_t), to order the caller's own
+ * work after an async NULL-stream call. */
+void *bv_last_stream(const bv_ctx *ctx);
 /* The ctx holds two sets of work buffers.  Consecutive bv_verify_batch_device
  * calls alternate them, and each waits (on the device) only for the last call
  * that used the same set — and for the call before it when their result
@@ -226,6 +246,26 @@ int bv_group_get_timing(const bv_group *g, int i, bv_timing *out);
 /* Host helper (no device): the shard plan bv_group_verify_batch uses.
  * Writes n_shards + 1 item bounds (bounds[0] = 0, bounds[n] = n_items). */
 int bv_plan_shards(const bv_batch *batch, int n_shards, uint64_t *bounds);
+/* Host helper (no device): the bitmask merge bv_group_verify_batch does
+ * after its all-gather.  Shard d's words start at gathered[d *
+ * words_per_shard]; its bit 0 is item bounds[d].  Writes
+ * ceil(bounds[n_shards] / 64) words to `out`; BV_E_ARGS on non-monotone
+ * bounds or a shard wider than words_per_shard words.
+ * bv_group_verify_batch accepts items in any message order: the items are
+ * sorted by message (stably) for sharding, the messages are partitioned into
+ * contiguous device ranges (each hashed once, also messages no item names),
+ * and statuses / bits come back in the caller's item order. */
+int bv_merge_shard_bits(const uint64_t *gathered, uint64_t words_per_shard, int n_shards,
+                        const uint64_t *bounds, uint64_t *out);
+/* Host helper (no device): the whole plan of bv_group_verify_batch.  perm
+ * (n_items entries, may be NULL): the item order used, perm[j] = the caller's
+ * index of the j-th item (identity when item_msg is non-decreasing);
+ * item_bounds (n_shards + 1): the shards over that order (bv_plan_shards);
+ * msg_bounds (n_shards + 1): device d hashes messages [msg_bounds[d],
+ * msg_bounds[d+1]) — a partition of [0, n_msgs).  Returns 1 when the items
+ * were permuted, 0 when not, BV_E_ARGS on bad arguments. */
+int bv_plan_group(const bv_batch *batch, int n_shards, uint64_t *item_bounds, uint64_t *msg_bounds,
+                  uint32_t *perm);
 
 /* SHA-256 of n messages (host buffers) -> 32*n bytes. */
 int bv_sha256_batch(bv_ctx *ctx, uint64_t n_msgs, const uint8_t *msg_bytes,

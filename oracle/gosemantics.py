@@ -244,6 +244,13 @@ def DecodeSignature(sig: GoStr) -> Tuple[Optional[int], Optional[int], bool]:
     return go_big_setstring36(parts[0]), go_big_setstring36(parts[1]), True
 
 
+def DecodeSignatureError(sig: GoStr) -> Optional[str]:
+    """The error value of keys.DecodeSignature (signature.go:33-35), None when
+    strings.Split gives exactly 2 parts."""
+    n = len(_b(sig).split(b"|"))
+    return None if n == 2 else "wrong number of values in signature: got %d, want 2" % n
+
+
 def scalar_class(v: Optional[int]) -> int:
     if v is None:
         return SC_NIL
@@ -676,6 +683,17 @@ def event_status(body: EventBody, signature: GoStr) -> int:
     pub = body.Creator if body.Creator is not None else b""
     st = item_status_from_sigstr(pub, body.Hash(), signature)
     return {ACCEPT: EV_ACCEPT, REJECT: EV_REJECT, REJECT_ERR: EV_ERR, REF_PANIC: EV_PANIC}[st]
+
+
+def event_verify_error(body: EventBody, signature: GoStr) -> Optional[str]:
+    """The error Event.Verify returns for EV_ERR (event.go:222-247): the
+    first failing ITX's DecodeSignature error, else the event's own."""
+    for itx in body.InternalTransactions or []:
+        st = itx_status(itx)
+        if st == ACCEPT:
+            continue
+        return DecodeSignatureError(itx.Signature) if st == REJECT_ERR else None
+    return DecodeSignatureError(signature)
 
 
 def peer_set_hash(peers: Sequence[Peer]) -> bytes:

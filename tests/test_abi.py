@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_code_object():
     L = native.lib()
-    assert L.bv_abi_version() == native.ABI_VERSION == 3
+    assert L.bv_abi_version() == native.ABI_VERSION == 4
     # the library carries gfx950 device code (offload bundle entry name)
     blob = open(native.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
@@ -106,3 +106,68 @@ def test_plan_shards_balanced_and_message_aligned():
     # ragged: more shards than messages, empty batch
     assert plan_shards(batch(np.repeat([0, 1], 5)), 4).tolist() == [0, 5, 5, 10, 10]
     assert plan_shards(batch(np.zeros(0, np.int64)), 3).tolist() == [0, 0, 0, 0]
+
+
+def test_merge_shard_bits_equals_python_merge():
+    """bv_merge_shard_bits (the host merge after bv_group's all-gather) equals
+    shard.merge_bits on unaligned, empty and single-item shards; bits past a
+    shard's end (padding garbage) never leak into the next shard."""
+    import numpy as np
+
+    from babble_amd import shard
+    from babble_amd.verifier import merge_shard_bits
+
+    rng = np.random.default_rng(11)
+    for _ in range(300):
+        n = int(rng.integers(0, 900))
+        D = int(rng.integers(1, 9))
+        cuts = sorted(rng.integers(0, n + 1, size=D - 1).tolist()) if n else [0] * (D - 1)
+        bounds = [0] + cuts + [n]
+        ok = rng.random(n) < 0.6
+        words = max(1, max((bounds[d + 1] - bounds[d] + 63) // 64 for d in range(D)))
+        g = rng.integers(0, 2**63, size=(D, words), dtype=np.int64).view(np.uint64)  # garbage everywhere
+        parts = []
+        for d in range(D):
+            a, z = bounds[d], bounds[d + 1]
+            pk = np.packbits(ok[a:z], bitorder="little")
+            pk = np.concatenate([pk, np.zeros((-len(pk)) % 8, np.uint8)]).view(np.uint64)
+            g[d, :len(pk)] = pk
+            if z > a and (z - a) % 64:  # garbage above the last valid bit of the shard
+                g[d, (z - a) // 64] |= ~np.uint64(0) << np.uint64((z - a) % 64)
+            parts.append(g[d].copy())
+        got = merge_shard_bits(g.reshape(-1), words, bounds)
+        want = shard.merge_bits(parts, bounds)
+        assert np.array_equal(got, want), (n, bounds)
+        pk = np.packbits(ok, bitorder="little")
+        full = np.concatenate([pk, np.zeros((-len(pk)) % 8, np.uint8)]).view(np.uint64)
+        assert np.array_equal(got, full[: (n + 63) // 64])
+
+
+def test_merge_shard_bits_rejects_bad_bounds():
+    import numpy as np
+
+    L = native.lib()
+    g = np.zeros(4, np.uint64)
+    out = np.zeros(4, np.uint64)
+    for bounds in ([0, 70, 60], [1, 5, 9], [0, 200, 210]):  # non-monotone, not from 0, shard wider than 2 words
+        b = np.asarray(bounds, np.uint64)
+        assert L.bv_merge_shard_bits(g.ctypes.data, 2, 2, b.ctypes.data, out.ctypes.data) == native.BV_E_ARGS
+
+
+def test_host_alloc_fails_loudly_or_frees():
+    """bv_host_alloc needs the HIP runtime: without a device it reports an
+    error (never a silent pageable fallback); bv_host_free ignores foreign
+    pointers."""
+    import torch
+
+    L = native.lib()
+    p = ctypes.c_void_p()
+    rc = L.bv_host_alloc(4096, ctypes.byref(p))
+    if torch.cuda.is_available():
+        assert rc == native.BV_OK and p.value
+    else:
+        assert rc != native.BV_OK and not p.value
+    L.bv_host_free(p)
+    buf = ctypes.create_string_buffer(16)
+    L.bv_host_free(ctypes.cast(buf, ctypes.c_void_p))  # not ours: ignored
+    assert native.lib().bv_last_stream(None) is None

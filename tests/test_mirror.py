@@ -112,8 +112,8 @@ def test_verify_events_matches_oracle():
         want = gs.event_status(b, s)
         seen.add(want)
         assert (o.ok, o.panic) == codes[want], (want, o)
-        if want == gs.EV_ERR:
-            assert o.err and "wrong number" in o.err
+        if want == gs.EV_ERR:  # signature.go:34: Go's text with the part count, passed up unchanged
+            assert o.err == gs.event_verify_error(b, s) and o.err.endswith(", want 2"), o.err
         if want == gs.EV_ITX_INVALID:
             assert o.err == "invalid signature on internal transaction"
         assert ev.Hash() == hashlib.sha256(b.Marshal()).digest()  # digest filled by the batch
@@ -183,7 +183,7 @@ def test_process_sig_pool_order_and_abort():
     pending.insert(1, H.BlockSignature(sg.key()[1], 1, "a|b"))    # not a member: skipped
     pending.insert(0, H.BlockSignature(vals[0][1], 99, "a|b"))    # unknown block: skipped
     appended, err = H.process_sig_pool(pending, lambda i: blk if i == 1 else None, lambda r: ps)
-    assert err == "wrong number of values in signature"
+    assert err == "wrong number of values in signature: got 1, want 2"  # signature.go:34 ("broken")
     # the first signature (index 0 of sigs) is the corrupted one; two valid ones precede the abort
     assert [a.Signature for a in appended] == [s for s in list(sigs.values())[1:3]]
     assert set(blk.Signatures) == {a.ValidatorHex() for a in appended}
