@@ -481,7 +481,7 @@ def events_entry_leg(args):
                    "bytes_staged": wb, "bytes_per_event": wb / args.events,
                    "pcie_gb_s": wb / (tm["ms_h2d"] * 1e-3) / 1e9 if tm["ms_h2d"] > 0 else None}
     v.close()
-    _, dag = synth.event_fields(1000, n_creators=4, seed=31, parents="event")
+    dag_packed, dag = synth.event_fields(1000, n_creators=4, seed=31, parents="event")
     vc = Verifier(device=local, flags=native.F_KEY_CACHE)
     vc.verify_events(dag)
     ts = []
@@ -490,14 +490,49 @@ def events_entry_leg(args):
         res = vc.verify_events(dag)
         ts.append((time.perf_counter() - t0) * 1e3)
     assert np.all(res.status == 1)
-    out["sync_dag_1000"] = {"ms_median": float(np.median(ts)), "creators": 4,
-                            "dag_levels": int(1000 // 4)}
     vc.close()
+    out["sync_dag_1000"] = {"ms_median": float(np.median(ts)), "creators": 4, "dag_levels": int(1000 // 4),
+                            "cpu": None if args.no_cpu else cpu_sync_dag(dag_packed)}
     return out
 
 
+def cpu_sync_dag(packed) -> dict:
+    """The same 1000-event SyncResponse on the host's cores, the way a CPU
+    node ingests it (core.go:214-245): SHA-256 of every body in topological
+    order (each body embeds its parents' hashes, so hashing is serial; the
+    serialized bodies are GIVEN to the CPU — the device builds them from wire
+    fields), then every signature verified on all cores by the C port
+    (oracle/oracle.c port_verify_batch: Go's ecdsa.Verify over btcec).
+    Median of 7 runs.  Returns ms."""
+    import hashlib
+
+    import numpy as np
+
+    from oracle import coracle  # CPU baseline leg only
+
+    cores = cpu_threads()
+    d = packed.as_dict()
+    bodies = [packed.message(m) for m in range(packed.n_msgs)]
+    coracle.port_verify_batch(_sample(packed, 16), n_threads=1)
+    t_hash, t_ver = [], []
+    for _ in range(7):
+        t0 = time.perf_counter()
+        digests = [hashlib.sha256(b).digest() for b in bodies]  # topological order
+        t1 = time.perf_counter()
+        st = coracle.port_verify_batch(d, n_threads=cores)
+        t2 = time.perf_counter()
+        t_hash.append((t1 - t0) * 1e3)
+        t_ver.append((t2 - t1) * 1e3)
+    assert len(digests) == packed.n_msgs and np.all(st == 1)
+    tot = [a + b for a, b in zip(t_hash, t_ver)]
+    return {"ms_median": float(np.median(tot)), "hash_ms": float(np.median(t_hash)),
+            "verify_ms": float(np.median(t_ver)), "cores": cores,
+            "what": "hashlib SHA-256 of the serialized bodies in order + oracle.c port_verify_batch on all cores"}
+
+
 def latency_leg(args):
-    """bv_verify_batch latency (host buffers in, results out) by batch size."""
+    """bv_verify_batch latency (host buffers in, results out) by batch size,
+    beside the C port of the reference path on this host's cores."""
     import numpy as np
 
     from babble_amd import native, synth
@@ -506,9 +541,21 @@ def latency_leg(args):
     out = {}
     vc = Verifier(device=int(os.environ.get("LOCAL_RANK", "0")), flags=native.F_KEY_CACHE)
     v0 = Verifier(device=int(os.environ.get("LOCAL_RANK", "0")))
+    cores = cpu_threads()
     for n in (1, 100, 1000, 10_000, 100_000):
         b = synth.events(n, n_creators=min(4, n), seed=900 + n)
         row = {}
+        if not args.no_cpu:  # the same batch on the host: the C port, all cores (SHA-256 + decode + verify)
+            from oracle import coracle  # CPU baseline leg only
+
+            d = b.as_dict()
+            coracle.port_verify_batch(d, n_threads=cores)
+            tc = []
+            for _ in range(3 if n >= 10_000 else 7):
+                t0 = time.perf_counter()
+                coracle.port_verify_batch(d, n_threads=cores)
+                tc.append((time.perf_counter() - t0) * 1e3)
+            row["cpu_port_all_cores"] = float(np.median(tc))
         for name, ver in (("cold", v0), ("warm_key_cache", vc)):
             ver.verify(b)  # warm-up (and, for the cache, the table build)
             ts = []
