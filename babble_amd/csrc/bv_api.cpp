@@ -46,7 +46,7 @@ constexpr uint32_t kMaxK12Keys = 1024;         // K12: 2.8 GiB
 constexpr uint32_t kKcMaxBatchKeys = 4096;     // key cache: batches with more keys use per-batch tables
 constexpr uint32_t kKcBuildGroup = 8;          // keys per KC build launch (pscr: 403 MB per key)
 constexpr uint32_t kPrepM = 16;                // items per s^-1 batch
-constexpr uint32_t kRgWords = 25;              // R_G words per item
+constexpr uint32_t kRgWords = 33;              // R_G words per item (XYZZ + inf: verify_core.h RG_WORDS)
 #ifndef BV_FUSED_KC
 #define BV_FUSED_KC 1
 #endif

@@ -669,8 +669,10 @@ __global__ void __launch_bounds__(256) k_verify_g(uint64_t n_items, uint64_t lo,
     verify_item_g<LAT>(i, n_items, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, u12, g_table, rg);
 }
 
+// Throughput variants: 4 waves per SIMD (128 VGPRs: the XYZZ accumulator
+// fits; at 3 waves the bulk launch loses a quarter of its latency hiding).
 template <int W, int NWIN, bool LAT>
-__global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, uint64_t lo, uint64_t hi,
+__global__ void __launch_bounds__(256, LAT ? 1 : 4) k_verify_q(uint64_t n_items, uint64_t lo, uint64_t hi,
                                                   const uint32_t *__restrict__ item_key,
                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
@@ -688,7 +690,7 @@ __global__ void __launch_bounds__(256) k_verify_q(uint64_t n_items, uint64_t lo,
 
 // Key-cache path, G and Q parts fused (verify_core.h: verify_item_gq_kc).
 template <bool LAT>
-__global__ void __launch_bounds__(256) k_verify_gq(uint64_t n_items, uint64_t lo, uint64_t hi,
+__global__ void __launch_bounds__(256, LAT ? 1 : 4) k_verify_gq(uint64_t n_items, uint64_t lo, uint64_t hi,
                                                    const uint32_t *__restrict__ item_key,
                                                    const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                    const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,

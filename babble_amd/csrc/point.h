@@ -223,3 +223,135 @@ DEV void gej_add(gej &r, bool &rinf, const gej &b, bool binf) {
   fe_dbl(J, J);
   fe_sub(r.Y, t, J);
 }
+
+// ---------------------------------------------------------------------------
+// Extended Jacobian "XYZZ" coordinates for the verify kernels' accumulators
+// (x = X / ZZ, y = Y / ZZZ, ZZ^3 = ZZZ^2): a mixed addition is madd-2008-s,
+// 8M + 2S, against 8M + 3S for Jacobian madd (the accumulator's ZZ and ZZZ
+// replace Z1^2 and Z1^3: one squaring fewer per table lookup), and the final
+// check x(R) == r needs X == r ZZ (1M instead of 1S + 1M).  The verify
+// kernels only add affine table points to an accumulator (no doublings), so
+// the dearer XYZZ doubling (dbl-2008-s-1) is only the exceptional P + P case.
+// Same group law and identity handling as gej (btcec's exceptional cases).
+// ---------------------------------------------------------------------------
+struct gexz {
+  fe X, Y, ZZ, ZZZ;
+};
+
+// r = 2 a (dbl-2008-s-1, a = 0): 6M + 3S.  a is not the identity; Y == 0
+// cannot occur on secp256k1.
+DEV void gexz_double(gexz &r, const gexz &a) {
+  fe U, V, W, S, M, t;
+  fe_dbl(U, a.Y);
+  fe_sqr(V, U);
+  fe_mul(W, U, V);
+  fe_mul(S, a.X, V);
+  fe_sqr(M, a.X);
+  fe_dbl(t, M);
+  fe_add(M, M, t);            // 3 X1^2
+  fe_sqr(t, M);
+  fe_dbl(r.X, S);
+  fe_sub(r.X, t, r.X);        // M^2 - 2S
+  fe_sub(t, S, r.X);
+  fe_mul(t, M, t);
+  fe_mul(U, W, a.Y);
+  fe_sub(r.Y, t, U);          // M (S - X3) - W Y1
+  fe_mul(r.ZZ, V, a.ZZ);
+  fe_mul(r.ZZZ, W, a.ZZZ);
+}
+
+DEV void gexz_set_ge(gexz &r, const fe &x, const fe &y) {
+  r.X = x;
+  r.Y = y;
+  fe_set(r.ZZ, 1);
+  fe_set(r.ZZZ, 1);
+}
+
+// r += (x2, y2) (affine), madd-2008-s: 8M + 2S + 6 add/sub.
+DEV void gexz_add_ge(gexz &r, bool &inf, const fe &x2, const fe &y2) {
+  if (inf) {
+    gexz_set_ge(r, x2, y2);
+    inf = false;
+    return;
+  }
+  fe P, R, PP, PPP, Q, t;
+  fe_mul(P, x2, r.ZZ);       // U2
+  fe_sub(P, P, r.X);         // P = U2 - X1
+  fe_mul(R, y2, r.ZZZ);      // S2
+  fe_sub(R, R, r.Y);         // R = S2 - Y1
+  if (fe_is_zero(P)) {
+    if (fe_is_zero(R)) {
+      gexz d;
+      gexz_double(d, r);
+      r = d;
+    } else {
+      inf = true;
+    }
+    return;
+  }
+  fe_sqr(PP, P);
+  fe_mul(PPP, P, PP);
+  fe_mul(Q, r.X, PP);
+  fe_mul(r.ZZ, r.ZZ, PP);
+  // X3 = R^2 - PPP - 2Q
+  fe_sqr(t, R);
+  fe_sub(t, t, PPP);
+  fe_sub(t, t, Q);
+  fe_sub(r.X, t, Q);
+  // Y3 = R (Q - X3) - Y1 PPP, ZZZ3 = ZZZ1 PPP
+  fe_sub(t, Q, r.X);
+  fe_mul(t, R, t);
+  fe_mul(r.ZZZ, r.ZZZ, PPP);
+  fe_mul(PPP, r.Y, PPP);
+  fe_sub(r.Y, t, PPP);
+}
+
+// The same for latency-bound launches: four dependent levels of
+// multiplies, each one interleaved asm program (field_asm.h gen_zip):
+// {x2 ZZ1, y2 ZZZ1} -> {P^2, R^2} -> {P PP, X1 PP, ZZ1 PP} ->
+// {R (Q - X3), Y1 PPP, ZZZ1 PPP}.  Same values and exceptional cases.
+DEV void gexz_add_ge_lat(gexz &r, bool &inf, const fe &x2, const fe &y2) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (inf) {
+    gexz_set_ge(r, x2, y2);
+    inf = false;
+    return;
+  }
+  fe P, R, PP, RR, PPP, Q, ZZ3, t, u;
+  fe_mul_mul_zip_asm(P, x2, r.ZZ, R, y2, r.ZZZ);
+  fe_sub(P, P, r.X);
+  fe_sub(R, R, r.Y);
+  if (fe_is_zero(P)) {
+    if (fe_is_zero(R)) {
+      gexz d;
+      gexz_double(d, r);
+      r = d;
+    } else {
+      inf = true;
+    }
+    return;
+  }
+  fe_sqr_sqr_zip_asm(PP, P, RR, R);
+  fe_mul_mul_mul_zip_asm(PPP, P, PP, Q, r.X, PP, ZZ3, r.ZZ, PP);
+  r.ZZ = ZZ3;
+  fe_sub(t, RR, PPP);
+  fe_sub(t, t, Q);
+  fe_sub(r.X, t, Q);
+  fe_sub(t, Q, r.X);
+  fe_mul_mul_mul_zip_asm(t, R, t, u, r.Y, PPP, ZZ3, r.ZZZ, PPP);
+  r.ZZZ = ZZ3;
+  fe_sub(r.Y, t, u);
+#else
+  gexz_add_ge(r, inf, x2, y2);
+#endif
+}
+
+template <bool LAT>
+DEV void pt_add_ge(gexz &r, bool &inf, const fe &x2, const fe &y2) {
+  if (LAT) gexz_add_ge_lat(r, inf, x2, y2);
+  else gexz_add_ge(r, inf, x2, y2);
+}
+template <bool LAT>
+DEV void pt_add_ge(gej &r, bool &inf, const fe &x2, const fe &y2) {
+  gej_add_ge_sel<LAT>(r, inf, x2, y2);
+}

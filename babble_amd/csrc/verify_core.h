@@ -440,13 +440,31 @@ DEV bool final_check(const gej &R, bool inf, const fe &r) {
   return false;
 }
 
+// The same check on an XYZZ accumulator: x = X / ZZ, so X == r ZZ (or
+// (r + N) ZZ): one multiply, no squaring.
+DEV bool final_check(const gexz &R, bool inf, const fe &r) {
+  if (inf) return false;
+  fe t;
+  fe_mul(t, r, R.ZZ);
+  if (fe_eq(t, R.X)) return true;
+  if (u256_lt(r.v, P_MINUS_N)) {
+    fe rn;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) rn.v[i] = addc32(r.v[i], SC_N[i], c);
+    fe_mul(t, rn, R.ZZ);
+    if (fe_eq(t, R.X)) return true;
+  }
+  return false;
+}
+
 // R += sum_j T[j][digit_j(u)] over the 256-bit u1 (8 limbs, consumed:
 // shifted right W bits per window, so digits never straddle limbs) with
 // SIGNED digits in (-2^(W-1), 2^(W-1)] by carry recoding: T[j][|d|], y
 // negated for d < 0 (geometry.h).  u < N < 2^256 and W NWIN >= 257, so no
 // carry is left after the top window.
-template <int W, int NWIN, bool LAT = false>
-DEV void g_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t u[8]) {
+template <int W, int NWIN, bool LAT = false, class PT = gej>
+DEV void g_table_add(PT &R, bool &inf, const uint32_t *tab, uint32_t u[8]) {
   constexpr uint32_t ENT = 1u << (W - 1);
   static_assert(W * NWIN >= 257 && W < 32, "signed G windows must absorb the last carry");
   uint32_t carry = 0;
@@ -464,7 +482,7 @@ DEV void g_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t u[8]) {
       fe_load4(x, e);
       fe_load4(y, e + 8);
       if (dneg) fe_neg(y, y);
-      gej_add_ge_sel<LAT>(R, inf, x, y);
+      pt_add_ge<LAT>(R, inf, x, y);
     }
   }
 }
@@ -478,26 +496,29 @@ DEV void load_k(uint32_t k1[4], uint32_t k2[4], uint32_t &signs, const uint32_t 
   signs = c.x;
 }
 
-// Partial point R_G = u1 G, kept in HBM between k_verify_g and k_verify_q as
-// 25 SoA words per item (X, Y, Z limbs, inf flag) for coalesced access.
-#define RG_WORDS 25
-DEV void rg_store(uint32_t *rg, uint64_t n, uint64_t i, const gej &R, bool inf) {
+// Partial point R_G = u1 G (XYZZ), kept in HBM between k_verify_g and
+// k_verify_q as 33 SoA words per item (X, Y, ZZ, ZZZ limbs, inf flag) for
+// coalesced access.
+#define RG_WORDS 33
+DEV void rg_store(uint32_t *rg, uint64_t n, uint64_t i, const gexz &R, bool inf) {
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     rg[(uint64_t)k * n + i] = R.X.v[k];
     rg[(uint64_t)(8 + k) * n + i] = R.Y.v[k];
-    rg[(uint64_t)(16 + k) * n + i] = R.Z.v[k];
+    rg[(uint64_t)(16 + k) * n + i] = R.ZZ.v[k];
+    rg[(uint64_t)(24 + k) * n + i] = R.ZZZ.v[k];
   }
-  rg[(uint64_t)24 * n + i] = inf ? 1u : 0u;
+  rg[(uint64_t)32 * n + i] = inf ? 1u : 0u;
 }
-DEV void rg_load(const uint32_t *rg, uint64_t n, uint64_t i, gej &R, bool &inf) {
+DEV void rg_load(const uint32_t *rg, uint64_t n, uint64_t i, gexz &R, bool &inf) {
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     R.X.v[k] = rg[(uint64_t)k * n + i];
     R.Y.v[k] = rg[(uint64_t)(8 + k) * n + i];
-    R.Z.v[k] = rg[(uint64_t)(16 + k) * n + i];
+    R.ZZ.v[k] = rg[(uint64_t)(16 + k) * n + i];
+    R.ZZZ.v[k] = rg[(uint64_t)(24 + k) * n + i];
   }
-  inf = rg[(uint64_t)24 * n + i] != 0;
+  inf = rg[(uint64_t)32 * n + i] != 0;
 }
 
 // Phase 1 (overlaps the key-table build): R_G = u1 G for items that reach
@@ -515,11 +536,12 @@ DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const u
   q[0] = make_uint4(k1[0], k1[1], k1[2], k1[3]);
   q[1] = make_uint4(k2[0], k2[1], k2[2], k2[3]);
   q[2] = make_uint4(signs, 0u, 0u, 0u);
-  gej R;
+  gexz R;
   bool inf = true;
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
-  fe_set(R.Z, 0);
+  fe_set(R.ZZ, 0);
+  fe_set(R.ZZZ, 0);
   g_table_add<BV_GW, BV_GNWIN, LAT>(R, inf, g_table, u);
   rg_store(rg, n, i, R, inf);
 }
@@ -531,8 +553,8 @@ DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const u
 // and W NWIN >= 129 bits, so no carry is left after the top window.
 // `phi`: the table holds T (the k1 half) and this half needs phi(T) =
 // (beta x, y): one multiply per lookup instead of a stored phi half (KC).
-template <int W, int NWIN, bool SIGNED, bool LAT = false>
-DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bool neg, bool phi = false) {
+template <int W, int NWIN, bool SIGNED, bool LAT = false, class PT = gexz>
+DEV void key_table_add(PT &R, bool &inf, const uint32_t *tab, uint32_t k[4], bool neg, bool phi = false) {
   constexpr uint32_t ENT = SIGNED ? (1u << (W - 1)) : (1u << W);
   static_assert(!SIGNED || W * NWIN >= 129, "signed windows must absorb the last carry");
   if (neg) fe_neg(R.Y, R.Y);
@@ -562,7 +584,7 @@ DEV void key_table_add(gej &R, bool &inf, const uint32_t *tab, uint32_t k[4], bo
         fe_mul(x, x, beta);
       }
       if (dneg) fe_neg(y, y);
-      gej_add_ge_sel<LAT>(R, inf, x, y);
+      pt_add_ge<LAT>(R, inf, x, y);
     }
   }
   if (neg) fe_neg(R.Y, R.Y);
@@ -587,7 +609,7 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
   if (st != 0xFF) return st;
   uint32_t k1[4], k2[4], signs;
   load_k(k1, k2, signs, u12, i);
-  gej R;
+  gexz R;
   bool inf;
   rg_load(rg, n, i, R, inf);
   const uint32_t *tab = key_tabs ? (const uint32_t *)key_tabs[item_key[i]]
@@ -619,11 +641,12 @@ DEV uint8_t verify_item_gq_kc(uint64_t i, const uint32_t *item_key, const uint32
   if (st != 0xFF) return st;
   uint32_t u[8], k1[4], k2[4], signs;
   item_scalars(i, r_be, item_msg, digest_words, w_in, u, k1, k2, signs);
-  gej R;
+  gexz R;
   bool inf = true;
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
-  fe_set(R.Z, 0);
+  fe_set(R.ZZ, 0);
+  fe_set(R.ZZZ, 0);
   g_table_add<BV_GW, BV_GNWIN, LAT>(R, inf, g_table, u);
   const uint32_t *tab = (const uint32_t *)key_tabs[item_key[i]];
 #pragma unroll 1

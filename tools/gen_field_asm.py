@@ -689,7 +689,8 @@ PROGRAMS = {"fe_mul": gen_mul, "fe_sqr": gen_sqr, "fe_add": gen_add, "fe_sub": g
 # one or two waves per SIMD) uses them.
 ZIP_KINDS = {"mul": gen_mul, "sqr": gen_sqr}
 ZIP_COMBOS = [("sqr", "sqr", "mul"), ("sqr", "sqr", "sqr"),      # gej_double_lat
-              ("mul", "mul"), ("mul", "sqr"), ("mul", "mul", "mul", "sqr")]  # gej_add_ge_lat
+              ("mul", "mul"), ("mul", "sqr"), ("mul", "mul", "mul", "sqr"),  # gej_add_ge_lat
+              ("sqr", "sqr"), ("mul", "mul", "mul")]  # gexz_add_ge_lat (with ("mul", "mul"))
 
 
 def _rename(g: Prog, f) -> Prog:

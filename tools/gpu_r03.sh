@@ -10,6 +10,14 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for step in "$@"; do
   case "$step" in
+    quick)  # the GPU suite with C3 shortened to 2 chunks
+      BV_C3_EVENTS=2000000 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > gpurun_out/pytest_quick.log 2>&1 || { echo QUICK FAILED; tail -40 gpurun_out/pytest_quick.log; exit 1; }
+      tail -3 gpurun_out/pytest_quick.log ;;
+    abvar)  # same-box A/B of the library builds in gpurun_var/
+      timeout -k 10 400 python3 -u tools/ab_steps.py gpurun_var/*.so > gpurun_out/ab_steps.log 2>&1 \
+        || { echo ABVAR FAILED; tail -20 gpurun_out/ab_steps.log; exit 1; }
+      tail -1 gpurun_out/ab_steps.log ;;
     tests)
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
         > gpurun_out/pytest_gpu.log 2>&1 || { echo TESTS FAILED; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
