@@ -43,6 +43,35 @@ DEV void rounds_wk_hkw(uint32_t h[8], const uint32_t *wk) {
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
 
+// ... and d + (h + K + W) formed one round early too (d of round i+1 is c of
+// round i), so e' = add3(dhkw, S1(e), Ch(e, f, g)): one dependent add fewer
+// on the e -> e' chain per round (one more instruction per round)
+DEV void rounds_wk_dhkw(uint32_t h[8], const uint32_t *wk) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  uint32_t hkw = hh + wk[0];
+  uint32_t dhkw = d + hkw;
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    const uint32_t s1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t ne = dhkw + s1 + ch;
+    const uint32_t t1 = hkw + s1 + ch;
+    const uint32_t nhkw = i < 63 ? g + wk[i + 1] : 0;
+    const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, b, c);
+    hh = g;
+    g = f;
+    f = e;
+    e = ne;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+    hkw = nhkw;
+    dhkw = d + hkw;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
 template <int MODE>
 __global__ void k(uint64_t *out, int nblk) {
   __shared__ uint32_t sW[64 * 64];
@@ -66,6 +95,8 @@ __global__ void k(uint64_t *out, int nblk) {
         sha256_rounds_wk(h, sW + (b & 63) * 64);  // sha256.h: 8-trip loop of 8 rounds
       } else if (MODE == 4) {
         rounds_wk_hkw(h, sW + (b & 63) * 64);
+      } else if (MODE == 5) {
+        rounds_wk_dhkw(h, sW + (b & 63) * 64);
       } else {
         // the k_ev_hash_chain tail: a 446-byte T=1 body from block 2 (6
         // blocks, the last two partial) out of an LDS slot, byte shift 2
@@ -107,5 +138,6 @@ int main() {
   run<2>("sha256_blocks tail (6 blocks/iter)");
   run<3>("rounds only, 8x8 loop (sha256.h)");
   run<4>("rounds only, hkw early, unrolled");
+  run<5>("rounds only, d+hkw early, unrolled");
   return 0;
 }
