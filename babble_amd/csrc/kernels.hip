@@ -259,6 +259,21 @@ __device__ __noinline__ void evc_hash_padded(uint32_t h[8], const uint32_t *slot
     sha256_compress(h, w16);
   }
 }
+// Diagnostic build only (-DBV_CHAIN_STAMPS, tools/chain_stamps.py): wave 0
+// lane 0 stamps s_memrealtime (100 MHz) at each phase boundary of the first
+// EVC_NSTAMP levels of a launch, kept in LDS and written out at the end.
+#ifdef BV_CHAIN_STAMPS
+#define EVC_NSTAMP 96
+__device__ uint64_t g_chain_stamps[5 * EVC_NSTAMP + 1];
+#define EVC_STAMP(L, k)                                                                   \
+  do {                                                                                    \
+    if (t == 0 && (L) < EVC_NSTAMP) sStamp[5 * (L) + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define EVC_STAMP(L, k) \
+  do {                  \
+  } while (0)
+#endif
 __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t l1,
                                                         const uint32_t *__restrict__ level_off,
                                                         const uint32_t *__restrict__ order,
@@ -276,6 +291,9 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
   // (lanes in lockstep read distinct banks)
   __shared__ uint32_t sWK[EVC_WEV * EVC_WBLK * 64];
   __shared__ uint32_t sLof[EVC_CAP + 1];               // level offsets, relative to the launch
+#ifdef BV_CHAIN_STAMPS
+  __shared__ uint64_t sStamp[5 * EVC_NSTAMP];
+#endif
   const uint32_t t = threadIdx.x;
   const uint32_t E0 = level_off[l0], E1 = level_off[l1], nl = l1 - l0;
   const uint32_t *bw = (const uint32_t *)bodies;
@@ -313,8 +331,10 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
   for (uint32_t L = 0; L < nl; L++) {
     const uint32_t lo = sLof[L], w = sLof[L + 1] - lo;
     uint32_t *sBody = sBodyB + (L & 1) * EVC_SLOTS * EVC_SLOT_DW, *sMid = sMidB + (L & 1) * EVC_SLOTS * 8;
-    // ---- B: parents' hex into the tails, one lane per (event, parent)
-    for (uint32_t x = t; x < 2 * w; x += EVC_NT) {
+    EVC_STAMP(L, 0);
+    // ---- B: parents' hex into the tails, one lane per (event, parent), on
+    // waves 1-3 first (wave 0 stays free for the rounds)
+    for (uint32_t x = (t + EVC_NT - 64) % EVC_NT; x < 2 * w; x += EVC_NT) {
       const uint32_t i = x >> 1, p = x & 1;
       const uint32_t *d = sDesc + EVC_DESC * (lo + i);
       const uint32_t rel = d[6 + p];
@@ -343,11 +363,28 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
       }
     }
     __syncthreads();
-    // ---- C: message schedules, one lane per (event, block)
-    {
-      const uint32_t wv = w < EVC_WEV ? w : EVC_WEV;
-      for (uint32_t x = t; x < wv * EVC_WBLK; x += EVC_NT) {
-        const uint32_t i = x / EVC_WBLK, j = x % EVC_WBLK;
+    EVC_STAMP(L, 1);
+    // ---- D0 (wave 0) beside C (waves 1-3): the first tail block of each LDS
+    // event is compressed at once with its schedule inline (one lane per
+    // event), while waves 1-3 expand the W+K schedules of the later blocks
+    // into LDS (one lane per (event, block)); D1 then runs those blocks'
+    // rounds from LDS.  The first block's inline schedule costs less than
+    // waiting for it (tools/chain_stamps.py).
+    const uint32_t wv = w < EVC_WEV ? w : EVC_WEV;
+    uint32_t h0[8];
+    if (t < wv) {
+      const uint32_t *d = sDesc + EVC_DESC * (lo + t);
+      if (evc_lds_event(t, d[4], d[5])) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) h0[k] = sMid[8 * t + k];
+        uint32_t w16[16];
+        sha256_block_words_padded(w16, sBody + t * EVC_SLOT_DW, d[3] >> 24);
+        sha256_compress(h0, w16);
+      }
+    }
+    if (t >= 64) {
+      for (uint32_t x = t - 64; x < wv * (EVC_WBLK - 1); x += EVC_NT - 64) {
+        const uint32_t i = x / (EVC_WBLK - 1), j = 1 + x % (EVC_WBLK - 1);
         const uint32_t *d = sDesc + EVC_DESC * (lo + i);
         const uint32_t nb = d[4], len = d[5];
         if (!evc_lds_event(i, nb, len) || j >= (uint32_t)sha256_nblocks(len) - nb) continue;
@@ -357,7 +394,8 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
       }
     }
     __syncthreads();
-    // ---- A (waves 1-3, beside D): level L+1's tails and midstates into the
+    EVC_STAMP(L, 2);
+    // ---- A (waves 1-3, beside D1): level L+1's tails and midstates into the
     // other buffer (its loads were issued during level L-1), then the loads
     // for level L+2.  Only when level L has <= 64 events: then D runs on
     // wave 0 alone and waves 1-3 are free.
@@ -367,7 +405,7 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
                 sMidB + ((L + 1) & 1) * EVC_SLOTS * 8);
       evc_load(L + 2, nl, t - 64, sLof, sDesc, bw, mid, pf);
     }
-    // ---- D: the rounds (the serial part)
+    // ---- D1: the rounds (the serial part)
     for (uint32_t i = t; i < w; i += EVC_NT) {
       const uint32_t *d = sDesc + EVC_DESC * (lo + i);
       const uint32_t sh = d[3] >> 24, nb = d[4], len = d[5];
@@ -376,11 +414,8 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
       if (i < EVC_WEV && evc_lds_event(i, nb, len)) {
         // the common path stays in registers (the out-of-line paths below
         // take their state by pointer, which would put it in scratch)
-        uint32_t h[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) h[k] = sMid[8 * i + k];
-        for (uint32_t j = 0; j < nblk - nb; j++) sha256_rounds_wk(h, sWK + (j * 16 * EVC_WEV + i) * 4, 4 * EVC_WEV);
-        ev_digest_words(wd, h);
+        for (uint32_t j = 1; j < nblk - nb; j++) sha256_rounds_wk(h0, sWK + (j * 16 * EVC_WEV + i) * 4, 4 * EVC_WEV);
+        ev_digest_words(wd, h0);
       } else {
         uint32_t hm[8];
         if (i < EVC_SLOTS) {
@@ -399,6 +434,7 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
 #pragma unroll
       for (int k = 0; k < 8; k++) sDig[8 * (lo + i) + k] = wd[k];
     }
+    EVC_STAMP(L, 3);
     if (!beside && L + 1 < nl) {  // a wide level: stage the next one after its rounds
       __syncthreads();
       if (t >= 64) {
@@ -408,9 +444,14 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
       }
     }
     __syncthreads();
+    EVC_STAMP(L, 4);
   }
   // ---- epilogue: the digests to HBM
   for (uint32_t x = t; x < (E1 - E0) * 8; x += EVC_NT) dig[8 * (uint64_t)sDesc[EVC_DESC * (x / 8)] + x % 8] = sDig[x];
+#ifdef BV_CHAIN_STAMPS
+  for (uint32_t x = t; x < 5 * (nl < EVC_NSTAMP ? nl : EVC_NSTAMP); x += EVC_NT) g_chain_stamps[x] = sStamp[x];
+  if (t == 0) g_chain_stamps[5 * EVC_NSTAMP] = nl;
+#endif
 }
 
 __global__ void __launch_bounds__(256) k_iota(uint64_t n, uint32_t *__restrict__ out) {
@@ -872,6 +913,15 @@ hipError_t ev_hash_chain(hipStream_t st, uint32_t l0, uint32_t l1, const uint32_
                      offs, mid, dig);
   return hipGetLastError();
 }
+
+#ifdef BV_CHAIN_STAMPS
+}  // namespace bvk
+// the last chain launch's stamps (diagnostic build): out[5 L + k], then nl
+extern "C" int bv_debug_chain_stamps(uint64_t *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_stamps), sizeof(g_chain_stamps)) == hipSuccess ? 0 : -4;
+}
+namespace bvk {
+#endif
 
 hipError_t iota(hipStream_t st, uint64_t n, uint32_t *out) {
   if (n == 0) return hipSuccess;

@@ -52,19 +52,20 @@ sys.path.insert(0, ROOT)
 # ROOFLINE.  The verify kernels are VALU-integer bound (no MFMA, not HBM:
 # ~2.1 KB of table gathers per item).  Work per item of the EXECUTED
 # schedule, in 256-bit modular multiplications (squarings included), each
-# 64 schoolbook 32x32 products + 16 reduction products = 80 IMUL32:
+# 64 schoolbook 32x32 products + 16 reduction products = 80 IMUL32.  The
+# accumulators are XYZZ (point.h gexz): a mixed addition is madd-2008-s,
+# 8M + 2S = 10 modmuls:
 #   u1 G:  10 signed windows of the 26-bit G table, the first lands on the
-#          identity (a copy), 9 mixed additions x (8M + 3S) =  99
-#   u2 Q:  22 windows of the K12 GLV key tables, 22 x 11    = 242
+#          identity (a copy), 9 mixed additions x 10             =  90
+#   u2 Q:  22 windows of the K12 GLV key tables, 22 x 10         = 220
 #   u1, u2 = e w, r w (2 Montgomery products), GLV split (2 wide products
-#          + 2 products) and the projective check X == r Z^2 (1S + 1M)
-#                                                           ~   8
-#   = 349 modmuls = 27,920 IMUL32 per item.
-# `achieved` = items x 27,920 / (k_verify_g + k_verify_q time); `peak` = the
+#          + 2 products) and the check X == r ZZ (1M)            ~   7
+#   = 317 modmuls = 25,360 IMUL32 per item.
+# `achieved` = items x 25,360 / (k_verify_g + k_verify_q time); `peak` = the
 # v_mad_u64_u32 rate measured on MI355X (tools/ubench_int.hip,
 # profiles/r01_ubench_int.txt).  SURVEY §8d's canonical Strauss schedule
 # (4,050 modmuls per verify) is reported only as `speedup_vs_canonical`.
-MODMUL_PER_ITEM_EXEC = 349
+MODMUL_PER_ITEM_EXEC = 317
 IMUL32_PER_MODMUL = 80
 CANONICAL_MODMUL_PER_VERIFY = 4050
 PEAK_IMUL32_PER_S = 31.76e12
@@ -313,7 +314,7 @@ def main():
             "kernel": "k_verify_g<false> + k_verify_q<12, 11, false>",
             "achieved": achieved / 1e12,
             "peak": PEAK_IMUL32_PER_S / 1e12,
-            "unit": "T IMUL32/s (executed schedule: 349 modmuls x 80 IMUL32 per item; bench.py ROOFLINE)",
+            "unit": "T IMUL32/s (executed schedule: 317 modmuls x 80 IMUL32 per item; bench.py ROOFLINE)",
             "frac": achieved / PEAK_IMUL32_PER_S,
             "traffic": None,
             "speedup_vs_canonical": CANONICAL_MODMUL_PER_VERIFY / MODMUL_PER_ITEM_EXEC,
@@ -379,6 +380,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         line["warm"] = warm_leg(args, devs, world, dist, local, step_with)
         line["host_entry"] = host_entry_leg(args, v, batch)
+        line["host_entry_pinned"] = host_entry_pinned_leg(args, v, batch)
         line["latency_ms"] = latency_leg(args)
         line["events_entry"] = events_entry_leg(args)
     if rank == 0:
@@ -446,6 +448,41 @@ def host_entry_leg(args, v, batch):
             "pcie_gb_s": staged / (h2d * 1e-3) / 1e9 if h2d > 0 else None,
             "note": "inputs in pageable host memory; staged through pinned chunks, hashing overlaps the transfer; "
                     "PCIe-bound (~520 B per event crosses the link)"}
+
+
+def host_entry_pinned_leg(args, v, batch):
+    """bv_verify_batch over a batch the caller built in bv_host_alloc memory
+    (page-locked; the cgo shim allocates its arrays there instead of
+    C.CBytes): the library DMAs the inputs from where they
+    are and the digests / statuses straight into the caller's pinned result
+    arrays — no staging copy, the call is the PCIe transfer overlapped with
+    the kernels."""
+    import numpy as np
+
+    from babble_amd.verifier import PinnedArena, VerifyResult
+
+    arena = PinnedArena()
+    try:
+        pb = arena.batch(batch)
+        res = VerifyResult(arena.array((batch.n_msgs, 32), np.uint8), arena.array(batch.n_items, np.uint8),
+                           arena.array((batch.n_items + 63) // 64, np.uint64))
+        v.verify_into(pb, res)
+        ts = []
+        reps = max(2, min(5, args.steps))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            v.verify_into(pb, res)
+            ts.append(v.timing())
+        elapsed = time.perf_counter() - t0
+        assert np.array_equal(res.accept_bits, expected_words(0, args.events, 0))
+        h2d = mean(ts, "ms_h2d")
+        staged = sum(a.nbytes for a in (pb.msg_bytes, pb.msg_off, pb.r_be, pb.s_be, pb.item_msg, pb.item_key))
+        return {"value": args.events * reps / elapsed, "unit": "verifies/s", "ms_per_call": elapsed / reps * 1e3,
+                "ms_h2d": h2d, "host_breakdown_ms": host_breakdown(ts), "bytes_staged": staged,
+                "pcie_gb_s": staged / (h2d * 1e-3) / 1e9 if h2d > 0 else None,
+                "note": "inputs and results in bv_host_alloc (pinned) memory: DMA'd in place, no staging copy"}
+    finally:
+        arena.close()
 
 
 def events_entry_leg(args):
