@@ -696,8 +696,14 @@ __device__ __forceinline__ void write_status(uint64_t i, uint64_t hi, uint8_t st
   if ((threadIdx.x & 63) == 0 && i < hi) bits[i >> 6] = mask;
 }
 
+#ifndef BV_GWAVES
+#define BV_GWAVES 1
+#endif
+#ifndef BV_LWAVES  // latency variants (zipped point ops, small batches)
+#define BV_LWAVES 1
+#endif
 template <bool LAT>
-__global__ void __launch_bounds__(256) k_verify_g(uint64_t n_items, uint64_t lo, uint64_t hi,
+__global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_GWAVES) k_verify_g(uint64_t n_items, uint64_t lo, uint64_t hi,
                                                   const uint32_t *__restrict__ item_key,
                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
@@ -710,10 +716,14 @@ __global__ void __launch_bounds__(256) k_verify_g(uint64_t n_items, uint64_t lo,
     verify_item_g<LAT>(i, n_items, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, u12, g_table, rg);
 }
 
-// Throughput variants: 4 waves per SIMD (128 VGPRs: the XYZZ accumulator
-// fits; at 3 waves the bulk launch loses a quarter of its latency hiding).
+// Throughput variants: BV_QWAVES waves per SIMD (4: 128 VGPRs, the XYZZ
+// accumulator fits; at 3 waves the bulk launch loses a quarter of its
+// latency hiding).
+#ifndef BV_QWAVES
+#define BV_QWAVES 4
+#endif
 template <int W, int NWIN, bool LAT>
-__global__ void __launch_bounds__(256, LAT ? 1 : 4) k_verify_q(uint64_t n_items, uint64_t lo, uint64_t hi,
+__global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_QWAVES) k_verify_q(uint64_t n_items, uint64_t lo, uint64_t hi,
                                                   const uint32_t *__restrict__ item_key,
                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
@@ -731,7 +741,7 @@ __global__ void __launch_bounds__(256, LAT ? 1 : 4) k_verify_q(uint64_t n_items,
 
 // Key-cache path, G and Q parts fused (verify_core.h: verify_item_gq_kc).
 template <bool LAT>
-__global__ void __launch_bounds__(256, LAT ? 1 : 4) k_verify_gq(uint64_t n_items, uint64_t lo, uint64_t hi,
+__global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_QWAVES) k_verify_gq(uint64_t n_items, uint64_t lo, uint64_t hi,
                                                    const uint32_t *__restrict__ item_key,
                                                    const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                    const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,

@@ -351,6 +351,23 @@ DEV void pt_add_ge(gexz &r, bool &inf, const fe &x2, const fe &y2) {
   if (LAT) gexz_add_ge_lat(r, inf, x2, y2);
   else gexz_add_ge(r, inf, x2, y2);
 }
+
+// One table lookup step of the verify kernels: r += (x2, y2) in lanes with
+// `take` (a nonzero digit).  Measured alternatives (profiles/r03_ab_step.log,
+// same-box PMC A/B): a straight-line common path under wave-uniform
+// branches for the identity / P == 0 lanes cuts the compiler's phi moves
+// (VALU -2 %) but needs more live registers than the 128 of 4 waves per SIMD
+// (scratch spills in the loop: k_verify_q +3 %), and the zipped latency
+// variants at 2-3 waves per SIMD run 10-15 % slower; this per-lane form
+// stays.
+template <bool LAT>
+DEV void pt_add_ge_step(gexz &r, bool &inf, const fe &x2, const fe &y2, bool take) {
+  if (take) pt_add_ge<LAT>(r, inf, x2, y2);
+}
+template <bool LAT>
+DEV void pt_add_ge_step(gej &r, bool &inf, const fe &x2, const fe &y2, bool take) {
+  if (take) gej_add_ge_sel<LAT>(r, inf, x2, y2);
+}
 template <bool LAT>
 DEV void pt_add_ge(gej &r, bool &inf, const fe &x2, const fe &y2) {
   gej_add_ge_sel<LAT>(r, inf, x2, y2);

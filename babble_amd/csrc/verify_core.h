@@ -47,7 +47,14 @@ DEV void fe_load(fe &a, const uint32_t *p) {
   for (int i = 0; i < 8; i++) a.v[i] = p[i];
 }
 DEV void fe_load4(fe &a, const uint32_t *p) {  // 16-byte aligned: 2 x dwordx4
+#if defined(__HIP_DEVICE_COMPILE__)
+  // table entries live in global memory: global_load, not flat_load (a flat
+  // access also counts against lgkmcnt and takes the aperture check)
+  typedef const __attribute__((address_space(1))) uint4 *gptr;
+  const gptr q = (gptr)p;
+#else
   const uint4 *q = (const uint4 *)p;
+#endif
   uint4 l = q[0], h = q[1];
   a.v[0] = l.x; a.v[1] = l.y; a.v[2] = l.z; a.v[3] = l.w;
   a.v[4] = h.x; a.v[5] = h.y; a.v[6] = h.z; a.v[7] = h.w;
@@ -476,14 +483,14 @@ DEV void g_table_add(PT &R, bool &inf, const uint32_t *tab, uint32_t u[8]) {
     carry = d > ENT ? 1u : 0u;
     const bool dneg = carry != 0;
     if (dneg) d = (1u << W) - d;  // |d - 2^W|, 0 when d == 2^W
-    if (d) {
-      const uint32_t *e = tab + ((uint64_t)j * ENT + d) * BV_ENTRY_U32;
-      fe x, y;
-      fe_load4(x, e);
-      fe_load4(y, e + 8);
-      if (dneg) fe_neg(y, y);
-      pt_add_ge<LAT>(R, inf, x, y);
-    }
+    // loaded unconditionally (d == 0 reads the window's slot 0, a valid
+    // entry that is then not added): no per-lane branch around the lookup
+    const uint32_t *e = tab + ((uint64_t)j * ENT + d) * BV_ENTRY_U32;
+    fe x, y;
+    fe_load4(x, e);
+    fe_load4(y, e + 8);
+    fe_cneg_canon(y, dneg);
+    pt_add_ge_step<LAT>(R, inf, x, y, d != 0);
   }
 }
 
@@ -573,19 +580,17 @@ DEV void key_table_add(PT &R, bool &inf, const uint32_t *tab, uint32_t k[4], boo
         dneg = true;
       }
     }
-    if (d) {
-      const uint32_t *e = tab + ((uint64_t)j * ENT + d) * BV_ENTRY_U32;
-      fe x, y;
-      fe_load4(x, e);
-      fe_load4(y, e + 8);
-      if (phi) {
-        fe beta;
-        fe_load(beta, FE_BETA);
-        fe_mul(x, x, beta);
-      }
-      if (dneg) fe_neg(y, y);
-      pt_add_ge<LAT>(R, inf, x, y);
+    const uint32_t *e = tab + ((uint64_t)j * ENT + d) * BV_ENTRY_U32;  // d == 0: a valid, unused slot
+    fe x, y;
+    fe_load4(x, e);
+    fe_load4(y, e + 8);
+    if (phi) {
+      fe beta;
+      fe_load(beta, FE_BETA);
+      fe_mul(x, x, beta);
     }
+    fe_cneg_canon(y, dneg);
+    pt_add_ge_step<LAT>(R, inf, x, y, d != 0);
   }
   if (neg) fe_neg(R.Y, R.Y);
 }

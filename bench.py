@@ -154,11 +154,15 @@ def cpu_baseline(batch, target_s: float) -> dict:
 
 
 def pmc_profile(n_items: int):
-    """PMC counters of the headline verify kernels (profiles/r02_kverify_pmc.json,
-    tools/gpu_pmc.sh + tools/pmc_summary.py on the same workload)."""
-    path = os.path.join(ROOT, "profiles", "r02_kverify_pmc.json")
-    if not os.path.exists(path):
+    """PMC counters of the headline verify kernels (the newest
+    profiles/rNN_kverify_pmc.json: tools/gpu_pmc.sh + tools/pmc_summary.py on
+    the same workload)."""
+    import glob
+
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_kverify_pmc.json")))
+    if not found:
         return None
+    path = found[-1]
     with open(path) as f:
         tj = json.load(f)
     return tj if tj.get("items_per_launch") == n_items else None

@@ -12,7 +12,10 @@
 // OP_ZSSM + k: component k of the zipped (x^2, y^2, x y) program;
 // OP_ZSSS + k: component k of the zipped (x^2, y^2, (x ^ y)^2) program
 // (field_asm.h gen_zip, used by the key-table doubling chain).
-enum { OP_MUL = 0, OP_SQR = 1, OP_ADD = 2, OP_SUB = 3, OP_MONT = 4, OP_INV = 5, OP_ZSSM = 6, OP_ZSSS = 9, OP_LAST = 11 };
+// OP_CNEG: fe_cneg_canon(x, y.v[0] & 1) (branch-free conditional negate of
+// a canonical element, the verify kernels' signed-digit lookup).
+enum { OP_MUL = 0, OP_SQR = 1, OP_ADD = 2, OP_SUB = 3, OP_MONT = 4, OP_INV = 5, OP_ZSSM = 6, OP_ZSSS = 9,
+       OP_CNEG = 12, OP_LAST = 12 };
 
 __global__ void __launch_bounds__(256) k_field(int op, uint32_t n, const uint32_t *__restrict__ a,
                                                const uint32_t *__restrict__ b, uint32_t *__restrict__ r) {
@@ -39,6 +42,7 @@ __global__ void __launch_bounds__(256) k_field(int op, uint32_t n, const uint32_
       break;
     }
     case OP_INV: fe_inv_var(z, x); break;
+    case OP_CNEG: z = x; fe_cneg_canon(z, (y.v[0] & 1u) != 0); break;
     default: {
       fe w, o[3];
 #pragma unroll

@@ -18,7 +18,7 @@ P = 2**256 - 2**32 - 977
 N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 M32 = 2**32 - 1
 OPS = {"mul": 0, "sqr": 1, "add": 2, "sub": 3, "mont": 4, "inv": 5,
-       "zssm0": 6, "zssm1": 7, "zssm2": 8, "zsss0": 9, "zsss1": 10, "zsss2": 11}
+       "zssm0": 6, "zssm1": 7, "zssm2": 8, "zsss0": 9, "zsss1": 10, "zsss2": 11, "cneg": 12}
 
 pytestmark = pytest.mark.gpu
 
@@ -101,6 +101,51 @@ def test_fold_carry_blocks_are_hit_and_exact():
         r = _run(op, a, bb)
         for x, y, z in zip(a, bb, r):
             assert z < 2**256 and (z - x * y) % P == 0, (op, hex(x), hex(y), hex(z))
+
+
+def test_add_sub_carry_propagation_blocks_are_exact():
+    """fe_add / fe_sub apply K = 2^32 + 977 to limbs 0..1 after a wrap and
+    propagate the carry through limbs 2..7 in a rare block: operand pairs
+    whose wrapped sum / difference has limbs 0..1 within K of 2^64 (and
+    limbs 2..7 all ones, which wrap a second time) enter it."""
+    rng = random.Random(9)
+    K = 2**32 + 977
+    a_add, b_add, a_sub, b_sub = [], [], [], []
+    for _ in range(4096):
+        lo = 2**64 - 1 - rng.randrange(K + 8)             # low 64 bits of the wrapped value
+        hi = rng.choice([rng.getrandbits(192), 2**192 - 1, 2**192 - 2, 0])
+        w = (hi << 64) | lo                                # the wrapped value, < 2^256
+        a = rng.getrandbits(256)
+        if w + 2**256 - a < 2**256:                        # a + b = 2^256 + w
+            a_add.append(a)
+            b_add.append(w + 2**256 - a)
+        lo2 = rng.randrange(K + 8)                         # a - b + 2^256 = w2, limbs 0..1 < K
+        w2 = (rng.choice([rng.getrandbits(192), 0, 2**192 - 1]) << 64) | lo2
+        b = rng.getrandbits(256)
+        if b >= 2**256 - w2 and b + w2 - 2**256 < b:       # a = b + w2 - 2^256 >= 0, a < b
+            a_sub.append(b + w2 - 2**256)
+            b_sub.append(b)
+    assert len(a_add) > 1000 and len(a_sub) > 1000
+    for op, xs, ys, f in (("add", a_add, b_add, lambda x, y: x + y), ("sub", a_sub, b_sub, lambda x, y: x - y)):
+        r = _run(op, xs, ys)
+        bad = [(hex(x), hex(y), hex(z)) for x, y, z in zip(xs, ys, r) if z >= 2**256 or (z - f(x, y)) % P]
+        assert not bad, (op, bad[:5])
+
+
+def test_cneg_canon_matches_python_ints():
+    """fe_cneg_canon (the signed-digit table lookups' y negation) on
+    canonical operands, including limb patterns that borrow past limb 1."""
+    rng = random.Random(13)
+    xs = [0, 1, P - 1, P - 2, 2**64 - 1, 2**64, 2**64 - 977, 2**32 + 976, 2**32 + 977, 2**32 + 978]
+    xs += [(rng.getrandbits(192) << 64) | rng.choice([0xFFFFFFFFFFFFFFFF, 0xFFFFFFFF00000000 | rng.getrandbits(32),
+                                                        0xFFFFFFFEFFFFFC2F, rng.getrandbits(64)])
+           for _ in range(3000)]
+    xs = [x % P for x in xs]
+    flags = [rng.getrandbits(1) for _ in xs]
+    r = _run("cneg", xs, flags)
+    bad = [(hex(x), f, hex(z)) for x, f, z in zip(xs, flags, r)
+           if z >= 2**256 or (z - (-x if f else x)) % P or (not f and z != x)]
+    assert not bad, bad[:5]
 
 
 def test_sc_mont_matches_python_ints():

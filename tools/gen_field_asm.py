@@ -15,8 +15,9 @@ Programs emitted:
           the high word of the next column's pair, so a product costs one mad
           + one addc and a column one v_mov; then the fold 2^256 = 2^32 + 977
           as two interleaved carry chains and a short tail.
-  fe_add  s = a + b, then s + c0 (2^32 + 977) on the carry-out c0 (18 VALU);
-          the once-in-2^222 second wrap goes to a uniform slow block.
+  fe_add  s = a + b, then s + c0 (2^32 + 977) on the carry-out c0 into limbs
+          0..1 (13 VALU); the carry past limb 1 (~2^-31) and the
+          once-in-2^222 second wrap go to nested uniform slow blocks.
   fe_sub  same with borrows and s - c0 (2^32 + 977).
 
 Each program is written in logical order over named registers, then list-
@@ -554,10 +555,12 @@ def gen_sqr(base: int = MUL_BASE) -> Prog:
 def _addsub(name: str, sub: bool) -> Prog:
     """r = a +/- b mod p, weakly reduced.  Chain s = a +/- b (carry c0);
     then s -/+ (c0 ? 0 : K)... i.e. on a wrap past 2^256 apply
-    K = 2^256 - p = 2^32 + 977 once (chain 2, carry c1): 18 VALU.  Only a
-    result within K of the wrap carries again (probability ~2^-222 for
-    random operands); that lane needs K applied once more, done in a
-    uniform slow block entered iff some lane's c1 is set."""
+    K = 2^256 - p = 2^32 + 977 once to limbs 0..1 (carry c1): 13 VALU.  The
+    carry past limb 1 (~2^-31 per lane) is propagated through limbs 2..7
+    in a uniform rare block entered iff some lane's c1 is set; only a
+    result within K of the wrap carries out of limb 7 (probability ~2^-222
+    for random operands) and needs K applied once more (a nested rare
+    block).  Before the propagation block: 19 VALU."""
     g = Prog(name)
     A = [f"%[a{i}]" for i in range(8)]
     B = [f"%[b{i}]" for i in range(8)]
@@ -574,8 +577,14 @@ def _addsub(name: str, sub: bool) -> Prog:
     g.cnd(k1, 0, 1, c0)                      # c0 (limb 1 of K c0)
     first(R[0], c1, R[0], k0)
     nxt(R[1], c1, R[1], k1, c1)
+    # The carry of K's two limbs past limb 1 needs limbs 0..1 of the wrapped
+    # value within K of 2^64 (~2^-31 per lane): propagating it into limbs
+    # 2..7 is a rare block (a no-op for lanes without c1), not six
+    # unconditional links of every add / sub.
+    p = Prog(name + "_prop")
+    pn = p.subb if sub else p.addc
     for i in range(2, 8):
-        nxt(R[i], c1, R[i], 0, c1)
+        pn(R[i], c1, R[i], 0, c1)
     s = Prog(name + "_tail")
     sf = s.sub_co if sub else s.add_co
     sn = s.subb if sub else s.addc
@@ -586,7 +595,8 @@ def _addsub(name: str, sub: bool) -> Prog:
     sn(R[1], c2, R[1], k1, c2)
     for i in range(2, 8):
         sn(R[i], c2, R[i], 0, c2)
-    g.slow = (c1, s)
+    p.slow = (c1, s)
+    g.slow = (c1, p)
     return g
 
 
@@ -848,13 +858,41 @@ def stats(g: Prog) -> dict:
     return out
 
 
+def _all_reads(g: Prog) -> list[tuple]:
+    out = []
+    for x in g.ins:
+        if x[0] == "slow":
+            out += _all_reads(x[2])
+        else:
+            out.append(x)
+    if g.slow is not None:
+        out += _all_reads(g.slow[1])
+    return out
+
+
+def outputs_after_inputs(g: Prog) -> bool:
+    """True when every read of an input operand (%[a*] / %[b*], zipped
+    %[zKa*] / %[zKb*]) precedes every write of an output (%[r*] / %[zKr*])
+    in program order (rare blocks included, at their position).  The
+    outputs may then share registers with inputs that die at the asm
+    statement (no early-clobber "&"): the register allocator gets up to 8
+    VGPRs per multiply back at the verify kernels' 128-VGPR budget."""
+    seq = _all_reads(g)
+    is_in = re.compile(r"%\[(z\d+)?[ab]\d+\]")
+    is_out = re.compile(r"%\[(z\d+)?r\d+\]")
+    last_in = max((i for i, x in enumerate(seq) if any(is_in.fullmatch(r) for r in reads(x))), default=-1)
+    first_out = min((i for i, x in enumerate(seq) if any(is_out.fullmatch(w) for w in writes(x))), default=len(seq))
+    return last_in < first_out
+
+
 def zip_wrapper(kinds) -> str:
     """C++ wrapper of a zipped program: fe_<kinds>_zip_asm(r0, a0[, b0], r1, ...)."""
     g = build(zip_name(kinds))
+    ec = "=v" if outputs_after_inputs(g) else "=&v"
     params, outs, ins, cys = [], [], [], []
     for k, kind in enumerate(kinds):
         params.append(f"fe &r{k}, const fe &a{k}" + (f", const fe &b{k}" if kind == "mul" else ""))
-        outs += [f'[z{k}r{i}] "=&v"(r{k}.v[{i}])' for i in range(8)]
+        outs += [f'[z{k}r{i}] "{ec}"(r{k}.v[{i}])' for i in range(8)]
         outs += [f'[z{k}c{i}] "=&s"(c{k}_{i})' for i in range(NCARRY)]
         cys += [f"c{k}_{i}" for i in range(NCARRY)]
         ins += [f'[z{k}a{i}] "v"(a{k}.v[{i}])' for i in range(8)]
@@ -887,6 +925,8 @@ def header() -> str:
     a_in = ", ".join(f'[a{i}] "v"(a.v[{i}])' for i in range(8))
     b_in = ", ".join(f'[b{i}] "v"(b.v[{i}])' for i in range(8))
     r_out = ", ".join(f'[r{i}] "=&v"(r.v[{i}])' for i in range(8))
+    assert outputs_after_inputs(mul) and outputs_after_inputs(sqr) and outputs_after_inputs(mont)
+    r_late = ", ".join(f'[r{i}] "=v"(r.v[{i}])' for i in range(8))  # outputs_after_inputs
     t_out = ", ".join(f'[t{i}] "=&v"(t[{i}])' for i in range(8))
     c_out = ", ".join(f'[c{i}] "=&s"(c{i})' for i in range(NCARRY))
     c3_out = ", ".join(f'[c{i}] "=&s"(c{i})' for i in range(3))
@@ -912,7 +952,7 @@ __device__ __forceinline__ void fe_mul_asm(fe &r, const fe &a, const fe &b) {{
   uint64_t {", ".join(f"c{i}" for i in range(NCARRY))};
   asm volatile(
 {asm_body(mul)}
-      : {r_out}, {c_out}
+      : {r_late}, {c_out}
       : {a_in}, {b_in}
       : {clob}, "scc");
 }}
@@ -922,7 +962,7 @@ __device__ __forceinline__ void fe_sqr_asm(fe &r, const fe &a) {{
   uint64_t {", ".join(f"c{i}" for i in range(NCARRY))};
   asm volatile(
 {asm_body(sqr)}
-      : {r_out}, {c_out}
+      : {r_late}, {c_out}
       : {a_in}
       : {clob}, "scc");
 }}
@@ -955,7 +995,7 @@ __device__ __forceinline__ void sc_mont_asm(sc &r, const sc &a, const sc &b) {{
   uint64_t c0, c1, c2;
   asm volatile(
 {asm_body(mont)}
-      : {r_out}, {c3_out}
+      : {r_late}, {c3_out}
       : {a_in}, {b_in}, {n_in}, {nc_in}, [ninv] "v"({hex(NINV)}u)
       : {clob_m});
 }}

@@ -33,10 +33,14 @@ for step in "$@"; do
       done
       grep -ho '"value": [0-9.]*' gpurun_out/ab_q4.json gpurun_out/ab_q8.json ;;
     prof)
-      GPU_MAX_HW_QUEUES=4 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
+      GPU_MAX_HW_QUEUES=4 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
         python3 -u bench.py --no-extras --no-cpu --inflight 1 > gpurun_out/prof_bench.json 2> gpurun_out/prof.err \
         || { echo PROF FAILED; tail -20 gpurun_out/prof.err; exit 1; }
       find gpurun_out/prof -name "*kernel_stats.csv" | head -3 ;;
+    pmc)
+      bash tools/gpu_pmc.sh > gpurun_out/pmc.log 2>&1 || { echo PMC FAILED; tail -20 gpurun_out/pmc.log; exit 1; }
+      cp gpurun_out/r03_kverify_pmc.json profiles/r03_kverify_pmc.json  # read by the bench steps after this one
+      tail -5 gpurun_out/pmc.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
