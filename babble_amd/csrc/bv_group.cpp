@@ -14,6 +14,14 @@
 // RCCL is loaded with dlopen at bv_group_create (the PyTorch process may
 // already hold it), so libbabbleverify.so has no link-time RCCL dependency
 // and single-device users never load it.
+//
+// Logical shards: a device list that names ONE device several times makes
+// that many shards (one ctx each) on it; the shard bitmasks are then copied
+// into the gather buffer on the device instead of an RCCL all-gather (RCCL
+// needs distinct devices per rank).  Everything else — the shard plan, the
+// concurrent per-shard staging threads, the shifted merge — is the
+// multi-device code path, so it runs on hardware with one GPU
+// (tests/test_gpu_cache_group.py::test_group_logical_shards).
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -79,6 +87,7 @@ struct bv_group {
   std::vector<int> devices;
   std::vector<bv_ctx *> ctx;
   std::vector<nccl_comm> comms;
+  bool logical = false;  // every entry of `devices` is the same device: no RCCL
   std::vector<DevBuf> send, recv;  // per device: shard bits, gathered bits
   std::vector<std::vector<uint64_t>> sub_off, sub_msg;
   std::string err;
@@ -110,11 +119,14 @@ extern "C" void bv_group_destroy(bv_group *g) {
 extern "C" int bv_group_create(bv_group **out, const int *devices, int n_devices, uint32_t flags) {
   if (!out || !devices || n_devices <= 0 || n_devices > 64) return BV_E_ARGS;
   *out = nullptr;
-  for (int i = 0; i < n_devices; i++)
+  bool same = true;
+  for (int i = 1; i < n_devices; i++) same = same && devices[i] == devices[0];
+  for (int i = 0; i < n_devices && !same; i++)
     for (int j = 0; j < i; j++)
-      if (devices[i] == devices[j]) return BV_E_ARGS;
+      if (devices[i] == devices[j]) return BV_E_ARGS;  // repeats only as logical shards of one device
   bv_group *g = new bv_group();
   g->devices.assign(devices, devices + n_devices);
+  g->logical = same && n_devices > 1;
   for (int i = 0; i < n_devices; i++) {
     bv_ctx *c = nullptr;
     int rc = bv_create(&c, devices[i], flags);
@@ -122,7 +134,16 @@ extern "C" int bv_group_create(bv_group **out, const int *devices, int n_devices
       bv_group_destroy(g);
       return rc;
     }
+    if (g->logical) c->kc_budget /= (uint64_t)n_devices;  // the shards share the device's HBM
     g->ctx.push_back(c);
+  }
+  g->send.resize(n_devices);
+  g->recv.resize(n_devices);
+  g->sub_off.resize(n_devices);
+  g->sub_msg.resize(n_devices);
+  if (g->logical) {
+    *out = g;
+    return BV_OK;
   }
   {
     std::lock_guard<std::mutex> lk(g_rccl_mu);
@@ -139,10 +160,6 @@ extern "C" int bv_group_create(bv_group **out, const int *devices, int n_devices
     bv_group_destroy(g);
     return BV_E_COMM;
   }
-  g->send.resize(n_devices);
-  g->recv.resize(n_devices);
-  g->sub_off.resize(n_devices);
-  g->sub_msg.resize(n_devices);
   *out = g;
   return BV_OK;
 }
@@ -235,14 +252,25 @@ static int group_verify(bv_group *g, const bv_batch *b, bv_result *res, GroupPla
   for (int d = 0; d < D; d++)
     if (rcs[d] != BV_OK) return gfail(g, rcs[d], "device " + std::to_string(g->devices[d]) + ": " + g->ctx[d]->err);
 
-  // ONE all-gather of the accept bitmasks over RCCL (xGMI)
-  int r = g_rccl.group_start();
-  for (int d = 0; d < D && r == 0; d++) {
-    (void)hipSetDevice(g->devices[d]);
-    r = g_rccl.all_gather(g->send[d].p, g->recv[d].p, words, kNcclUint64, g->comms[d], g->ctx[d]->stream);
+  if (g->logical) {
+    // logical shards of one device: the gather is D copies into shard 0's
+    // buffer, on the device's lane 0 (every shard's ctx->stream), so each
+    // copy is ordered after that shard's bits
+    (void)hipSetDevice(g->devices[0]);
+    for (int d = 0; d < D; d++)
+      if (hipMemcpyAsync((uint8_t *)g->recv[0].p + (size_t)d * words * 8, g->send[d].p, words * 8,
+                         hipMemcpyDeviceToDevice, g->ctx[0]->stream) != hipSuccess)
+        return gfail(g, BV_E_LAUNCH, "gather shard bits");
+  } else {
+    // ONE all-gather of the accept bitmasks over RCCL (xGMI)
+    int r = g_rccl.group_start();
+    for (int d = 0; d < D && r == 0; d++) {
+      (void)hipSetDevice(g->devices[d]);
+      r = g_rccl.all_gather(g->send[d].p, g->recv[d].p, words, kNcclUint64, g->comms[d], g->ctx[d]->stream);
+    }
+    const int r2 = g_rccl.group_end();
+    if (r != 0 || r2 != 0) return gfail(g, BV_E_COMM, std::string("ncclAllGather: ") + g_rccl.errstr(r ? r : r2));
   }
-  const int r2 = g_rccl.group_end();
-  if (r != 0 || r2 != 0) return gfail(g, BV_E_COMM, std::string("ncclAllGather: ") + g_rccl.errstr(r ? r : r2));
   std::vector<uint64_t> gathered(words * D);
   (void)hipSetDevice(g->devices[0]);
   if (hipMemcpyAsync(gathered.data(), g->recv[0].p, words * 8 * D, hipMemcpyDeviceToHost, g->ctx[0]->stream) !=

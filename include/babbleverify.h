@@ -235,7 +235,11 @@ int bv_verify_events(bv_ctx *ctx, const bv_event_batch *events, bv_result *resul
  * through ONE RCCL all-gather (ncclAllGather over xGMI, librccl loaded at
  * bv_group_create) into device 0, from which the merged bitmask is copied
  * once.  Digests and statuses come back per device.  Errors: BV_E_COMM if
- * RCCL is unavailable or a collective fails. */
+ * RCCL is unavailable or a collective fails; BV_E_ARGS if a device appears
+ * twice in a list of several devices.  A list naming ONE device n times
+ * makes n logical shards on it (one ctx each, no RCCL: the shard bitmasks
+ * are gathered by device copies; the key-cache budget is split between the
+ * shards). */
 typedef struct bv_group bv_group;
 int bv_group_create(bv_group **out, const int *devices, int n_devices, uint32_t flags);
 void bv_group_destroy(bv_group *g);

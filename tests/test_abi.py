@@ -65,8 +65,8 @@ def test_unknown_flags_rejected_before_any_device_call():
     ctx = ctypes.c_void_p()
     assert native.lib().bv_create(ctypes.byref(ctx), 0, 0x80) == native.BV_E_ARGS and not ctx.value
     g = ctypes.c_void_p()
-    devs = (ctypes.c_int * 2)(0, 0)  # duplicate device
-    assert native.lib().bv_group_create(ctypes.byref(g), devs, 2, 0) == native.BV_E_ARGS
+    devs = (ctypes.c_int * 3)(0, 1, 0)  # a repeated device in a list of several devices
+    assert native.lib().bv_group_create(ctypes.byref(g), devs, 3, 0) == native.BV_E_ARGS and not g.value
 
 
 def test_group_null_args():

@@ -144,20 +144,39 @@ def test_verify_events_chunk_boundaries(monkeypatch):
     """Bulk batches (no in-batch parents) stage their per-event fields in
     event chunks (bv_events.cpp); a tiny chunk size puts chunk boundaries
     through nil / empty transaction lists, nil transactions and ITX /
-    BlockSignature fragments: digests equal the oracle's, statuses and bits
-    equal the single-chunk run's."""
+    BlockSignature fragments.  Digests, statuses and bits equal the C
+    oracle's over the oracle-serialized bodies (no
+    longer compared with a one-chunk run of the same kernels); a signed
+    C2-shaped batch with corrupted signatures crosses chunks the same way."""
+    from babble_amd.batch import PackedBatch
     from babble_amd.verifier import Verifier
+    from oracle import coracle
 
     v = Verifier(0)
     try:
+        monkeypatch.setenv("BV_EV_CHUNK_MB", "0.001")  # 256-event chunks
         for seed in (6, 7):
-            wire, want, wd = random_wire(seed, n=1100, in_batch=False)
-            monkeypatch.setenv("BV_EV_CHUNK_MB", "0")
-            one = v.verify_events(wire)
-            monkeypatch.setenv("BV_EV_CHUNK_MB", "0.001")  # 256-event chunks
+            wire, bodies, wd = random_wire(seed, n=1100, in_batch=False)
             many = v.verify_events(wire)
             assert [d.tobytes() for d in many.msg_hash] == wd
-            assert np.array_equal(many.status, one.status) and np.array_equal(many.accept_bits, one.accept_bits)
+            n = wire.n_events
+            off = np.zeros(n + 1, np.uint64)
+            off[1:] = np.cumsum([len(x) for x in bodies])
+            packed = PackedBatch(np.frombuffer(b"".join(bodies), np.uint8).copy(), off, wire.key_bytes,
+                                 wire.key_off, np.arange(n, dtype=np.uint32), wire.creator.astype(np.uint32),
+                                 wire.r_be, wire.s_be,
+                                 wire.pre if wire.pre is not None else np.zeros(n, np.uint8))
+            h, st, bits = coracle.verify_batch(packed.as_dict())
+            assert np.array_equal(many.status, st) and np.array_equal(many.accept_bits, bits)
+        packed, wire = synth.event_fields(3000, n_creators=8, seed=19, parents="hash")
+        bad = np.random.default_rng(19).choice(3000, 40, replace=False)
+        wire.s_be[bad, 3] ^= 0x08
+        packed.s_be[bad, 3] ^= 0x08
+        res = v.verify_events(wire)
+        h, st, bits = coracle.verify_batch(packed.as_dict())
+        assert np.array_equal(res.msg_hash, h)
+        assert np.array_equal(res.status, st) and np.array_equal(res.accept_bits, bits)
+        assert int((st != 1).sum()) == len(bad)
     finally:
         v.close()
 
