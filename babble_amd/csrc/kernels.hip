@@ -26,7 +26,10 @@
 
 #include <hipcub/hipcub.hpp>
 
-__global__ void __launch_bounds__(256) k_sha256(uint64_t n_msgs, const uint8_t *__restrict__ bytes,
+#ifndef BV_SHA_WAVES
+#define BV_SHA_WAVES 1
+#endif
+__global__ void __launch_bounds__(256, BV_SHA_WAVES) k_sha256(uint64_t n_msgs, const uint8_t *__restrict__ bytes,
                                                 const uint64_t *__restrict__ off,
                                                 uint32_t *__restrict__ digest_words) {
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

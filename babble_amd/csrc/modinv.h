@@ -21,6 +21,13 @@
 //   bounded by 2^30); (d, e) <- t (d, e) / 2^30 mod m; (f, g) <- t (f, g) /
 //   2^30 (exact); until g = 0.  Then f = +-1 and x^-1 = +-d mod m.
 // Invariants (as in the published analysis): d, e in (-2m, m).
+//
+// Attribution: the structure of this implementation (signed30 limbs, the
+// divsteps matrix, update_de / update_fg, the modinfo constants) follows
+// libsecp256k1's src/modinv32_impl.h (Copyright (c) 2020 Peter Dettman,
+// Pieter Wuille; MIT license, https://github.com/bitcoin-core/secp256k1),
+// restated here for one GPU lane; the safegcd paper is Bernstein & Yang,
+// "Fast constant-time gcd computation and modular inversion", TCHES 2019.
 #pragma once
 #include <stdint.h>
 
