@@ -43,6 +43,16 @@ constexpr uint32_t kBasesPerKey = 22;       // max(K8 16, K12 22, KC 14) bases p
 constexpr uint64_t kK12MinItemsPerKey = 2048;  // K12 pays for its 11x larger build above this
 constexpr uint32_t kMaxTableKeys = 8192;       // K8: 4 GiB of key tables
 constexpr uint32_t kMaxK12Keys = 1024;         // K12: 2.8 GiB
+// Latency rule: a small batch from a few keys is bound by its longest serial
+// chain, not by total work.  The per-lane generic path runs 128 doublings
+// AND ~128 additions in one lane per item; the K8 tables cost one lane's 120
+// doublings per key plus wide fills, so they finish first even at one item
+// per key (a single event: 1.66 -> see profiles/r03_bench.json latency_ms).
+#ifndef BV_LAT_TABLE_KEYS
+#define BV_LAT_TABLE_KEYS 16
+#endif
+constexpr uint32_t kLatTableKeys = BV_LAT_TABLE_KEYS;
+constexpr uint64_t kLatTableItems = 4096;
 constexpr uint32_t kKcMaxBatchKeys = 4096;     // key cache: batches with more keys use per-batch tables
 constexpr uint32_t kKcBuildGroup = 8;          // keys per KC build launch (pscr: 403 MB per key)
 constexpr uint32_t kPrepM = 16;                // items per s^-1 batch
@@ -627,7 +637,8 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   // Key path: the key cache when prepared; otherwise per-batch fixed-base
   // tables once a key signs enough items (K12 for large batches, K8 for
   // mid-size), else the generic per-lane path.
-  const bool table_mode = kc || (n_keys <= kMaxTableKeys && n_items >= 16ull * n_keys);
+  const bool table_mode = kc || (n_keys <= kMaxTableKeys && n_items >= 16ull * n_keys) ||
+                          (n_keys <= kLatTableKeys && n_items <= kLatTableItems && n_items > 0);
   const int key_w = kc ? BV_KCW
                     : !table_mode ? 0
                     : (n_keys <= kMaxK12Keys && n_items >= kK12MinItemsPerKey * n_keys && !(ctx->flags & BV_F_K8))
