@@ -58,42 +58,8 @@ DEV uint32_t be_word_at(uint32_t hi, uint32_t lo, uint32_t sh) {
 #endif
 }
 
-#ifndef BV_SHA_ROLL
-#define BV_SHA_ROLL 0
-#endif
 DEV void sha256_compress(uint32_t h[8], uint32_t w[16]) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#if BV_SHA_ROLL
-  // 4 trips of 16 unrolled rounds (static ring indices, K from the scalar
-  // cache): the fully unrolled 64 rounds let the compiler hoist far ahead
-  // and hold ~115 VGPRs (4 waves per SIMD)
-#pragma unroll 1
-  for (int r = 0; r < 64; r += 16) {
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      uint32_t wi;
-      if (r == 0) {
-        wi = w[u];
-      } else {
-        uint32_t w15 = w[(u + 1) & 15], w2 = w[(u + 14) & 15];
-        uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
-        uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
-        wi = w[u] + s0 + w[(u + 9) & 15] + s1;
-        w[u] = wi;
-      }
-      uint32_t t1 = hh + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g)) + SHA_K[r + u] + wi;
-      uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, b, c);
-      hh = g;
-      g = f;
-      f = e;
-      e = d + t1;
-      d = c;
-      c = b;
-      b = a;
-      a = t1 + t2;
-    }
-  }
-#else
 #pragma unroll
   for (int i = 0; i < 64; i++) {
     uint32_t wi;
@@ -117,7 +83,6 @@ DEV void sha256_compress(uint32_t h[8], uint32_t w[16]) {
     b = a;
     a = t1 + t2;
   }
-#endif
   h[0] += a;
   h[1] += b;
   h[2] += c;

@@ -176,6 +176,20 @@ def test_generic_path_few_items_per_key(verifier):
     assert verifier.timing()["key_path"] == 0
 
 
+def test_small_batch_latency_rule_takes_k8_tables(verifier):
+    """Batches of <= 16 keys and <= 4096 items take the K8 tables even below
+    16 items per key (the per-lane generic path's 128 doublings + ~128
+    additions in one lane are the longer chain): a single event, and 40
+    events from 8 keys with adversarial items, both equal to the oracle."""
+    b1 = synth.events(1, n_creators=1, seed=901)
+    check_against_oracle(verifier, b1)
+    assert verifier.timing()["key_path"] == 8
+    b40 = synth.adversarial(40, seed=902, n_creators=8, scale_per_million=MIX)
+    assert b40.n_keys <= 16 and b40.n_items < 16 * b40.n_keys
+    check_against_oracle(verifier, b40)
+    assert verifier.timing()["key_path"] == 8
+
+
 def test_c5_blocks_check_block(verifier):
     wb = synth.blocks(200, n_validators=100, seed=5)
     b = wb.batch
