@@ -37,6 +37,9 @@ for step in "$@"; do
         python3 -u bench.py --no-extras --no-cpu --inflight 1 > gpurun_out/prof_bench.json 2> gpurun_out/prof.err \
         || { echo PROF FAILED; tail -20 gpurun_out/prof.err; exit 1; }
       find gpurun_out/prof -name "*kernel_stats.csv" | head -3 ;;
+    c4)
+      timeout -k 10 300 python3 -u tools/c4_ossl_xcheck.py > gpurun_out/c4_ossl.log 2>&1 || { echo C4 FAILED; tail -20 gpurun_out/c4_ossl.log; exit 1; }
+      tail -3 gpurun_out/c4_ossl.log ;;
     pmc)
       bash tools/gpu_pmc.sh > gpurun_out/pmc.log 2>&1 || { echo PMC FAILED; tail -20 gpurun_out/pmc.log; exit 1; }
       cp gpurun_out/r03_kverify_pmc.json profiles/r03_kverify_pmc.json  # read by the bench steps after this one
