@@ -216,20 +216,39 @@ DEV void sha256_schedule_wk(uint32_t *wk, const uint32_t w[16], uint32_t stride 
 // e -> e' chain: e' = d + (hkw + S1(e) + Ch(e, f, g)).  One wave, 4 lanes:
 // 1.66 us per block against 2.51 us for an 8-trip loop of 8 rounds
 // (tools/ubench_sha.hip, profiles/r02_ubench_sha_lat.txt).
-#ifndef BV_SHA_DHKW
-#define BV_SHA_DHKW 1  // k_ev_hash_chain D: 13.56 -> 12.48 us per level (tools/chain_stamps.py)
+// Round forms (BV_SHA_RW, A/B in tools/chain_stamps.py): 0 plain (t1 = h +
+// S1 + Ch + WK, the compiler schedules), 1 h + K + W formed one round early,
+// 2 also d + (h + K + W) one round early (e' = add3(dhkw, S1(e), Ch)).
+#ifndef BV_SHA_RW
+#define BV_SHA_RW 0
 #endif
 DEV void sha256_rounds_wk(uint32_t h[8], const uint32_t *wk, uint32_t stride = 4) {
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#if BV_SHA_RW == 0
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    const uint32_t t1 = hh + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g)) +
+                        wk[(i >> 2) * stride + (i & 3)];
+    const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, b, c);
+    hh = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+#else
   uint32_t hkw = hh + wk[0];
-#if BV_SHA_DHKW
+#if BV_SHA_RW == 2
   // d + (h + K + W) one round early too (round i+1's d is round i's c):
   // e' = add3(dhkw, S1(e), Ch) — one dependent add fewer on the e chain
   uint32_t dhkw = d + hkw;
 #endif
 #pragma unroll
   for (int i = 0; i < 64; i++) {
-#if BV_SHA_DHKW
+#if BV_SHA_RW == 2
     const uint32_t s1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)), ch = (e & f) ^ (~e & g);
     const uint32_t ne = dhkw + s1 + ch;
     const uint32_t t1 = hkw + s1 + ch;
@@ -241,7 +260,7 @@ DEV void sha256_rounds_wk(uint32_t h[8], const uint32_t *wk, uint32_t stride = 4
     hh = g;
     g = f;
     f = e;
-#if BV_SHA_DHKW
+#if BV_SHA_RW == 2
     e = ne;
     if (i < 63) dhkw = c + hkw;
 #else
@@ -252,6 +271,7 @@ DEV void sha256_rounds_wk(uint32_t h[8], const uint32_t *wk, uint32_t stride = 4
     b = a;
     a = t1 + t2;
   }
+#endif
   h[0] += a;
   h[1] += b;
   h[2] += c;
