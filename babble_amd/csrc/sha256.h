@@ -100,6 +100,29 @@ DEV void sha256_init(uint32_t h[8]) {
 
 DEV uint64_t sha256_nblocks(uint64_t len) { return (len + 9 + 63) / 64; }
 
+// 17 aligned dwords of a full data block (the realignment reads one past):
+// 4 dwordx4 loads at dword alignment (gfx950 global loads need not be
+// 16-byte aligned): a quarter of the load instructions, and each lane
+// touches a cache line once per load instead of four times
+DEV void sha256_load17(uint32_t d[17], const uint32_t *src) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+  const u32x4a4 *v = (const u32x4a4 *)src;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const u32x4a4 x = v[i];
+    d[4 * i] = x.x;
+    d[4 * i + 1] = x.y;
+    d[4 * i + 2] = x.z;
+    d[4 * i + 3] = x.w;
+  }
+  d[16] = src[16];
+#else
+#pragma unroll
+  for (int i = 0; i < 17; i++) d[i] = src[i];
+#endif
+}
+
 // The 16 big-endian message words of block `blk` of a len-byte message
 // (FIPS padding and length included).  `src0` is the 4-byte aligned dword
 // holding message byte 64 blk0, `sh` that byte's offset within it; the
@@ -110,27 +133,8 @@ DEV void sha256_block_words(uint32_t w[16], const uint32_t *src0, uint32_t sh, u
   const uint64_t p0 = blk * 64;  // byte position of this block in the message
   if (p0 + 64 <= len) {
     // full data block: 17 aligned dwords, realigned
-    const uint32_t *src = src0 + (blk - blk0) * 16;
     uint32_t d[17];
-#if defined(__HIP_DEVICE_COMPILE__)
-    // 4 dwordx4 loads at dword alignment (gfx950 global loads need not be
-    // 16-byte aligned): a quarter of the load instructions, and each lane
-    // touches a cache line once per load instead of four times
-    typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-    const u32x4a4 *v = (const u32x4a4 *)src;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const u32x4a4 x = v[i];
-      d[4 * i] = x.x;
-      d[4 * i + 1] = x.y;
-      d[4 * i + 2] = x.z;
-      d[4 * i + 3] = x.w;
-    }
-    d[16] = src[16];
-#else
-#pragma unroll
-    for (int i = 0; i < 17; i++) d[i] = src[i];
-#endif
+    sha256_load17(d, src0 + (blk - blk0) * 16);
 #pragma unroll
     for (int i = 0; i < 16; i++) w[i] = be_word_at(d[i + 1], d[i], sh);
     return;
