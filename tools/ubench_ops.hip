@@ -29,6 +29,10 @@ __global__ void __launch_bounds__(256) kop(uint32_t *out, uint32_t seed, int ite
     w[c] = ((uint64_t)a[c] << 7) ^ c;
   }
   const uint32_t b = seed * 2654435761u;
+  uint64_t cy[16];
+#pragma unroll
+  for (int c = 0; c < 16; c++) cy[c] = (uint64_t)(seed >> c) & 0x5555555555555555ull;
+  const uint64_t m = 0xF0F0F0F0F0F0F0F0ull ^ seed;
   for (int i = 0; i < iters; i++) {
 #define BODY(c)                                                                                      \
   if constexpr (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[c]) : "v"(b));                 \
@@ -43,13 +47,19 @@ __global__ void __launch_bounds__(256) kop(uint32_t *out, uint32_t seed, int ite
   if constexpr (OP == 9) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[c]) : "v"(b), "v"(a[(c + 1) & 15])); \
   if constexpr (OP == 10) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[c]) : "v"(b), "v"(a[(c + 1) & 15])); \
   if constexpr (OP == 11) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[c]) : "v"(b));                 \
-  if constexpr (OP == 12) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a[c]));
+  if constexpr (OP == 12) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a[c]));                       \
+  if constexpr (OP == 13) asm volatile("v_addc_co_u32_e64 %0, %1, %0, %2, %1" : "+v"(a[c]), "+s"(cy[c]) : "v"(b)); \
+  if constexpr (OP == 14) asm volatile("v_mov_b32 %0, %1" : "=v"(a[c]) : "v"(a[(c + 1) & 15]));       \
+  if constexpr (OP == 15) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[c]) : "v"(b), "s"(m)); \
+  if constexpr (OP == 16) asm volatile("v_sub_co_u32_e64 %0, %1, %0, %2" : "+v"(a[c]), "=s"(cy[c]) : "v"(b)); \
+  if constexpr (OP == 17) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1" : "+v"(a[c]) : "v"(b) : "vcc"); \
+  if constexpr (OP == 18) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[c]) : "v"(b), "v"(a[(c + 1) & 15]));
     REP16(BODY)
 #undef BODY
   }
   uint32_t s = 0;
 #pragma unroll
-  for (int c = 0; c < 16; c++) s ^= a[c] ^ (uint32_t)w[c] ^ (uint32_t)(w[c] >> 32);
+  for (int c = 0; c < 16; c++) s ^= a[c] ^ (uint32_t)w[c] ^ (uint32_t)(w[c] >> 32) ^ (uint32_t)cy[c];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
@@ -94,5 +104,11 @@ int main() {
   run<10>("v_add3_u32", out, blocks);
   run<11>("v_xor_b32", out, blocks);
   run<12>("v_lshrrev_b32", out, blocks);
+  run<13>("v_addc_co_u32_e64", out, blocks);
+  run<14>("v_mov_b32", out, blocks);
+  run<15>("v_cndmask_b32_e64", out, blocks);
+  run<16>("v_sub_co_u32_e64", out, blocks);
+  run<17>("v_add_co_u32_e32", out, blocks);
+  run<18>("v_perm_b32", out, blocks);
   return 0;
 }
