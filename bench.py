@@ -387,6 +387,7 @@ def main():
         line["host_entry_pinned"] = host_entry_pinned_leg(args, v, batch)
         line["latency_ms"] = latency_leg(args)
         line["events_entry"] = events_entry_leg(args)
+        line["tx_sweep"] = tx_sweep_leg(args, v, local)
     if rank == 0:
         if world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(batch, args.cpu_seconds)
@@ -421,6 +422,40 @@ def warm_leg(args, devs, world, dist, local, step_with):
                             "k_verify_g": mean(tms, "ms_verify_g"), "k_verify_q": mean(tms, "ms_verify"),
                             "device_total": mean(tms, "ms_total")}}
     vc.close()
+    return out
+
+
+def tx_sweep_leg(args, v, local, n=250_000, steps=10):
+    """SURVEY §8d C2's sweep over transactions per event, T in {0, 4, 16}
+    (T = 1 is the headline): 250k events per batch, 64 creators, the same
+    cold path (per-key tables rebuilt every step, two batches in flight);
+    the body grows from 6 to 29 SHA-256 blocks while the ECDSA work per
+    item stays fixed.  Every result is checked (all signatures valid)."""
+    import numpy as np
+
+    from babble_amd import synth
+
+    out = {}
+    for t in (0, 4, 16):
+        b = synth.events(n, n_creators=args.creators, seed=20 + t, n_tx=t)
+        devs = [v.to_device(b) for _ in range(2)]
+        k = [0]
+
+        def step():
+            v.verify_device(devs[k[0] % 2], stream=0, sync=False)
+            k[0] += 1
+
+        elapsed, _ = timed_steps(step, steps, 2, 1, None, local, v)
+        for d in devs:
+            if not np.all(d.result().status == 1):
+                raise SystemExit(f"tx_sweep T={t}: a valid signature was rejected")
+        v.verify_device(devs[0], sync=True)
+        t_iso = v.timing()
+        body = float(np.diff(b.msg_off).mean())
+        out[str(t)] = {"value": n * steps / elapsed, "unit": "verifies/s", "ms_per_step": elapsed / steps * 1e3,
+                       "events": n, "body_bytes_mean": body, "sha_blocks": int((body + 9 + 63) // 64),
+                       "k_sha256_ms": t_iso["ms_sha256"], "k_verify_ms": t_iso["ms_verify_g"] + t_iso["ms_verify"]}
+        del devs
     return out
 
 
