@@ -15,6 +15,13 @@ Programs emitted:
           the high word of the next column's pair, so a product costs one mad
           + one addc and a column one v_mov; then the fold 2^256 = 2^32 + 977
           as two interleaved carry chains and a short tail.
+          FAST_FIRST: the first product of each counted column does not
+          count its carry-out (it would be one addc); the carries are OR-ed
+          into one SALU lane mask instead, and a uniform rare block re-runs
+          the whole product phase with full counting when any lane carried
+          (P ~ 2^-32 per first product on uniform operands; all-ones
+          operands take it, tests/test_field_asm.py).  fe_mul 71 -> 58
+          addc, fe_sqr 64 -> 52.
   fe_add  s = a + b, then s + c0 (2^32 + 977) on the carry-out c0 into limbs
           0..1 (13 VALU); the carry past limb 1 (~2^-31) and the
           once-in-2^222 second wrap go to nested uniform slow blocks.
@@ -386,19 +393,27 @@ class Machine:
 CY = ["%[c0]", "%[c1]", "%[c2]", "%[c3]"]
 
 
-def gen_mul(base: int = MUL_BASE) -> Prog:
-    """r = a * b mod p, weakly reduced (< 2^256).
-    Operands %[a0..7], %[b0..7] -> %[r0..7]; physical temporaries
-    v[base, base+34); carries %[c0..3]."""
-    g = Prog("fe_mul")
+# The carry of a column's FIRST product: its 64-bit addend is the previous
+# column's high word plus 2^32 times that column's carry count c, so
+# a b + addend < 2^64 unless c >= 2 (or c = 1 with a full high word) AND
+# a b is within ~c 2^32 of 2^64 — both limbs within a few units of 2^32.
+# Random operands never do that; crafted ones can.  So the fast product
+# phase does not count first-product carries (13 of fe_mul's 71 carry
+# instructions, 12 of fe_sqr's 64; a carry-writing VALU op costs 4.7-4.9
+# cycles, profiles/r03_ubench_ops.txt) but ORs them into RARE (SALU), and a
+# uniform rare block re-runs the product phase with every carry counted
+# (from the inputs, which are still live: outputs are written in the fold).
+FAST_FIRST = True
+RARE = "%[c8]"  # free during the product phases (the fold's CANY, written after)
+
+
+def _mul_product(g: Prog, base: int, fast: bool):
     A = [f"%[a{i}]" for i in range(8)]
     B = [f"%[b{i}]" for i in range(8)]
-    R = [f"%[r{i}]" for i in range(8)]
     Pl = [v(base + 2 * k) for k in range(15)]
     Ph = [v(base + 2 * k + 1) for k in range(15)]
     PP = [pair(x) for x in Pl]
-
-    # ---- 512-bit product ----
+    first = True
     for k in range(15):
         terms = [(i, k - i) for i in range(8) if 0 <= k - i < 8]
         src = 0 if k == 0 else PP[k]
@@ -408,8 +423,13 @@ def gen_mul(base: int = MUL_BASE) -> Prog:
             cy = CY[j % 3]
             g.mad(PP[k], cy, A[i], B[jj], src)
             src = PP[k]
-            if counted:
-                g.addc(c2, cy, 0 if j == 0 else c2, 0, cy)
+            if not counted:
+                continue
+            if fast and j == 0:  # first product: only the rare mask
+                g.sor(RARE, cy, cy if first else RARE)
+                first = False
+            else:
+                g.addc(c2, cy, 0 if j == (1 if fast else 0) else c2, 0, cy)
         if k < 14:
             g.mov(Pl[k + 1], Ph[k])
             if not counted:
@@ -417,6 +437,20 @@ def gen_mul(base: int = MUL_BASE) -> Prog:
         if k >= 8:
             g.mov(Ph[k - 8], Pl[k])  # P_(k-8) = {w_(k-8), w_k} for the fold
     g.mov(Ph[7], Ph[14])             # P_7 = {w_7, w_15}
+    return Pl, Ph, PP
+
+
+def gen_mul(base: int = MUL_BASE) -> Prog:
+    """r = a * b mod p, weakly reduced (< 2^256).
+    Operands %[a0..7], %[b0..7] -> %[r0..7]; physical temporaries
+    v[base, base+34); carries %[c0..3]; RARE %[c8] during the product."""
+    g = Prog("fe_mul")
+    R = [f"%[r{i}]" for i in range(8)]
+    Pl, Ph, PP = _mul_product(g, base, FAST_FIRST)
+    if FAST_FIRST:
+        blk = Prog("fe_mul_recount")
+        _mul_product(blk, base, False)
+        g.slow_block(RARE, blk)
     return _fold(g, base, R, Pl, Ph, PP)
 
 
@@ -499,6 +533,35 @@ def _fold(g: Prog, base: int, R, Pl, Ph, PP) -> Prog:
     return g
 
 
+def _sqr_offdiag(g: Prog, base: int, fast: bool):
+    A = [f"%[a{i}]" for i in range(8)]
+    Pl = [v(base + 2 * k) for k in range(15)]
+    Ph = [v(base + 2 * k + 1) for k in range(15)]
+    PP = [pair(x) for x in Pl]
+    first = True
+    for k in range(1, 14):
+        terms = [(i, k - i) for i in range(8) if i < k - i <= 7]
+        src = 0 if k == 1 else PP[k]
+        counted = k > 1  # column 1: one product, zero addend: no carry
+        c2 = Ph[k + 1]
+        for j, (i, jj) in enumerate(terms):
+            cy = CY[j % 3]
+            g.mad(PP[k], cy, A[i], A[jj], src)
+            src = PP[k]
+            if not counted:
+                continue
+            if fast and j == 0:
+                g.sor(RARE, cy, cy if first else RARE)
+                first = False
+                if len(terms) == 1:
+                    g.mov(c2, 0)
+            else:
+                g.addc(c2, cy, 0 if j == (1 if fast else 0) else c2, 0, cy)
+        if not counted:
+            g.mov(c2, 0)
+        g.mov(Pl[k + 1], Ph[k])
+
+
 def gen_sqr(base: int = MUL_BASE) -> Prog:
     """r = a^2 mod p, weakly reduced.  Comba squaring: the 28 off-diagonal
     products a_i a_j (i < j) once, in the column scheme of gen_mul; then
@@ -512,21 +575,13 @@ def gen_sqr(base: int = MUL_BASE) -> Prog:
     PP = [pair(x) for x in Pl]
     T01, T23 = pair(v(base + 30)), pair(v(base + 32))
 
-    # ---- off-diagonal D = sum_{i<j} a_i a_j 2^(32(i+j)): columns 1..13 ----
-    for k in range(1, 14):
-        terms = [(i, k - i) for i in range(8) if i < k - i <= 7]
-        src = 0 if k == 1 else PP[k]
-        counted = k > 1  # column 1: one product, zero addend: no carry
-        c2 = Ph[k + 1]
-        for j, (i, jj) in enumerate(terms):
-            cy = CY[j % 3]
-            g.mad(PP[k], cy, A[i], A[jj], src)
-            src = PP[k]
-            if counted:
-                g.addc(c2, cy, 0 if j == 0 else c2, 0, cy)
-        if not counted:
-            g.mov(c2, 0)
-        g.mov(Pl[k + 1], Ph[k])
+    # ---- off-diagonal D = sum_{i<j} a_i a_j 2^(32(i+j)): columns 1..13
+    # (first-product carries as in gen_mul: a rare re-count) ----
+    _sqr_offdiag(g, base, FAST_FIRST)
+    if FAST_FIRST:
+        blk = Prog("fe_sqr_recount")
+        _sqr_offdiag(blk, base, False)
+        g.slow_block(RARE, blk)
     # D: d_0 = 0, d_m = P_m.lo (1 <= m <= 14), d_15 = P_14.hi
     Dw = [None] + [Pl[m] for m in range(1, 15)] + [Ph[14]]
 
