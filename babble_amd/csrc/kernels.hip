@@ -172,7 +172,9 @@ __global__ void __launch_bounds__(256) k_ev_mid(uint64_t count, const uint32_t *
 //    B  lane i splices the i-th event's parents' hex into its LDS tail from
 //       the LDS digest cache (parents hashed by an earlier launch: HBM);
 //    C  one lane per (event, block) expands the block's W+K schedule into LDS
-//       (interleaved across events, so the round lanes read distinct banks);
+//       (interleaved across events, so the round lanes read distinct banks),
+//       16 words at a time while lane i runs the first block's rounds 16 at
+//       a time (D0);
 //    D  lane i runs the 64 rounds per block from its midstate (registers
 //       only: sha256_rounds_wk, 1.66 us per block on one wave); the digest
 //       goes to the LDS cache;
@@ -367,35 +369,45 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
     }
     __syncthreads();
     EVC_STAMP(L, 1);
-    // ---- D0 (wave 0) beside C (waves 1-3): the first tail block of each LDS
-    // event is compressed at once with its schedule inline (one lane per
-    // event), while waves 1-3 expand the W+K schedules of the later blocks
-    // into LDS (one lane per (event, block)); D1 then runs those blocks'
-    // rounds from LDS.  The first block's inline schedule costs less than
-    // waiting for it (tools/chain_stamps.py).
+    // ---- D0 (wave 0) beside C (waves 1-3): the first tail block of each
+    // LDS event runs its rounds 16 at a time on wave 0 (one lane per event)
+    // while waves 1-3 expand the W+K schedules of all the event's blocks
+    // into LDS in chunks of 16 words (one lane per (event, block)), a
+    // barrier between chunks: rounds 0-15 need only the message words,
+    // rounds 16c.. the chunk expanded during the previous 16 rounds.  D1
+    // then runs rounds 48-63 and the later blocks from LDS.  (Round 2 ran
+    // the first block with its schedule inline on wave 0: 4.1 us per level;
+    // one lane's whole expansion before the rounds: ~1.5-2 us.)
+    static_assert(EVC_WEV * EVC_WBLK <= EVC_NT - 64, "one schedule lane per (event, block)");
     const uint32_t wv = w < EVC_WEV ? w : EVC_WEV;
-    uint32_t h0[8];
-    if (t < wv) {
-      const uint32_t *d = sDesc + EVC_DESC * (lo + t);
-      if (evc_lds_event(t, d[4], d[5])) {
+    uint32_t h0[8], s0[8];
+    const bool r0 = t < wv && evc_lds_event(t, sDesc[EVC_DESC * (lo + t) + 4], sDesc[EVC_DESC * (lo + t) + 5]);
+    if (r0) {
 #pragma unroll
-        for (int k = 0; k < 8; k++) h0[k] = sMid[8 * t + k];
-        uint32_t w16[16];
-        sha256_block_words_padded(w16, sBody + t * EVC_SLOT_DW, d[3] >> 24);
-        sha256_compress(h0, w16);
+      for (int k = 0; k < 8; k++) s0[k] = h0[k] = sMid[8 * t + k];
+      uint32_t w16[16];
+      sha256_block_words_padded(w16, sBody + t * EVC_SLOT_DW, sDesc[EVC_DESC * (lo + t) + 3] >> 24);
+      sha256_rounds_first16(s0, w16);
+    }
+    uint32_t xs[16];
+    uint32_t *wkp = nullptr;
+    if (t >= 64 && t - 64 < wv * EVC_WBLK) {
+      const uint32_t i = (t - 64) / EVC_WBLK, j = (t - 64) % EVC_WBLK;
+      const uint32_t *d = sDesc + EVC_DESC * (lo + i);
+      const uint32_t nb = d[4], len = d[5];
+      if (evc_lds_event(i, nb, len) && j < (uint32_t)sha256_nblocks(len) - nb) {
+        sha256_block_words_padded(xs, sBody + i * EVC_SLOT_DW + 16 * j, d[3] >> 24);
+        wkp = sWK + (j * 16 * EVC_WEV + i) * 4;
+        sha256_schedule_chunk(xs, wkp, 4 * EVC_WEV, 0);
+        sha256_schedule_chunk(xs, wkp, 4 * EVC_WEV, 1);
       }
     }
-    if (t >= 64) {
-      for (uint32_t x = t - 64; x < wv * (EVC_WBLK - 1); x += EVC_NT - 64) {
-        const uint32_t i = x / (EVC_WBLK - 1), j = 1 + x % (EVC_WBLK - 1);
-        const uint32_t *d = sDesc + EVC_DESC * (lo + i);
-        const uint32_t nb = d[4], len = d[5];
-        if (!evc_lds_event(i, nb, len) || j >= (uint32_t)sha256_nblocks(len) - nb) continue;
-        uint32_t w16[16];
-        sha256_block_words_padded(w16, sBody + i * EVC_SLOT_DW + 16 * j, d[3] >> 24);
-        sha256_schedule_wk(sWK + (j * 16 * EVC_WEV + i) * 4, w16, 4 * EVC_WEV);
-      }
-    }
+    __syncthreads();
+    if (r0) sha256_rounds16_wk(s0, sWK + t * 4, 4 * EVC_WEV, 16);
+    if (wkp) sha256_schedule_chunk(xs, wkp, 4 * EVC_WEV, 2);
+    __syncthreads();
+    if (r0) sha256_rounds16_wk(s0, sWK + t * 4, 4 * EVC_WEV, 32);
+    if (wkp) sha256_schedule_chunk(xs, wkp, 4 * EVC_WEV, 3);
     __syncthreads();
     EVC_STAMP(L, 2);
     // ---- A (waves 1-3, beside D1): level L+1's tails and midstates into the
@@ -417,6 +429,9 @@ __global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t 
       if (i < EVC_WEV && evc_lds_event(i, nb, len)) {
         // the common path stays in registers (the out-of-line paths below
         // take their state by pointer, which would put it in scratch)
+        sha256_rounds16_wk(s0, sWK + i * 4, 4 * EVC_WEV, 48);
+#pragma unroll
+        for (int k = 0; k < 8; k++) h0[k] += s0[k];
         for (uint32_t j = 1; j < nblk - nb; j++) sha256_rounds_wk(h0, sWK + (j * 16 * EVC_WEV + i) * 4, 4 * EVC_WEV);
         ev_digest_words(wd, h0);
       } else {

@@ -286,6 +286,53 @@ DEV void sha256_rounds_wk(uint32_t h[8], const uint32_t *wk, uint32_t stride = 4
   h[7] += hh;
 }
 
+// A block's rounds in two pieces on the working state s = (a, ..., h):
+// rounds 0-15 straight from the 16 message words (no schedule needed yet),
+// then rounds 16-63, 16 at a time, from a W + K schedule other lanes expand
+// meanwhile (wk laid out as in sha256_schedule_wk); the caller adds s into the
+// chaining state afterwards (k_ev_hash_chain's first tail block).
+DEV void sha256_round(uint32_t s[8], uint32_t kw) {
+  const uint32_t a = s[0], e = s[4];
+  const uint32_t t1 = s[7] + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & s[5]) ^ (~e & s[6])) + kw;
+  const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, s[1], s[2]);
+  s[7] = s[6];
+  s[6] = s[5];
+  s[5] = e;
+  s[4] = s[3] + t1;
+  s[3] = s[2];
+  s[2] = s[1];
+  s[1] = a;
+  s[0] = t1 + t2;
+}
+DEV void sha256_rounds_first16(uint32_t s[8], const uint32_t w[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) sha256_round(s, w[i] + SHA_K[i]);
+}
+// rounds r0 .. r0 + 15 from the W + K schedule
+DEV void sha256_rounds16_wk(uint32_t s[8], const uint32_t *wk, uint32_t stride, int r0) {
+#pragma unroll
+  for (int u = 0; u < 16; u++) sha256_round(s, wk[((r0 + u) >> 2) * stride + (u & 3)]);
+}
+// The schedule in chunks of 16 (x: the 16-word ring, initially the block's
+// message words): chunk 0 stores W_0..15 + K, chunk c (1..3) expands and
+// stores W_16c..16c+15 + K, so a consumer can run 16 rounds per chunk
+// while the next chunk is expanded (k_ev_hash_chain's first tail block).
+DEV void sha256_schedule_chunk(uint32_t x[16], uint32_t *wk, uint32_t stride, int c) {
+  if (c == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) wk[(i >> 2) * stride + (i & 3)] = x[i] + SHA_K[i];
+    return;
+  }
+#pragma unroll
+  for (int u = 0; u < 16; u++) {
+    const uint32_t w15 = x[(u + 1) & 15], w2 = x[(u + 14) & 15];
+    const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+    const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+    x[u] = x[u] + s0 + x[(u + 9) & 15] + s1;
+    wk[((16 * c + u) >> 2) * stride + (u & 3)] = x[u] + SHA_K[16 * c + u];
+  }
+}
+
 // SHA-256 of bytes [off, off+len) of `base` (a 4-byte aligned buffer padded
 // by >= 8 bytes past its end).  Output: the 8 state words h[0..7] (digest =
 // big-endian serialisation of h).

@@ -44,6 +44,9 @@ for lib in sys.argv[1:]:
         "us_per_level_median": {"B_splice": float(np.median(ph[:, 0])), "C_sched": float(np.median(ph[:, 1])),
                                 "D_rounds": float(np.median(ph[:, 2])), "E_barrier": float(np.median(ph[:, 3])),
                                 "between_levels": float(np.median(nxt)) if len(nxt) else None,
-                                "total": float(np.median(s[:, 4] - s[:, 0]) * 10.0 / 1000.0)}}
+                                "total": float(np.median(s[:, 4] - s[:, 0]) * 10.0 / 1000.0)},
+        "us_per_level_mean": {k: round(float(np.mean(ph[:, c])), 2) for c, k in enumerate(("B", "C", "D", "E"))},
+        "total_p10_p90_max": [round(float(np.percentile(s[:, 4] - s[:, 0], q)) * 0.01, 2) for q in (10, 90, 100)],
+        "launch_us": round(float(s[-1, 4] - s[0, 0]) * 0.01, 1)}
     v.close()
     print(os.path.basename(lib), json.dumps(out[os.path.basename(lib)]), flush=True)
