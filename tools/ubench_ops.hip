@@ -53,7 +53,13 @@ __global__ void __launch_bounds__(256) kop(uint32_t *out, uint32_t seed, int ite
   if constexpr (OP == 15) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[c]) : "v"(b), "s"(m)); \
   if constexpr (OP == 16) asm volatile("v_sub_co_u32_e64 %0, %1, %0, %2" : "+v"(a[c]), "=s"(cy[c]) : "v"(b)); \
   if constexpr (OP == 17) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1" : "+v"(a[c]) : "v"(b) : "vcc"); \
-  if constexpr (OP == 18) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[c]) : "v"(b), "v"(a[(c + 1) & 15]));
+  if constexpr (OP == 18) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[c]) : "v"(b), "v"(a[(c + 1) & 15])); \
+  if constexpr (OP >= 19 && OP <= 22) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(w[c]) : "v"(a[c]), "v"(b) : "vcc"); \
+  if constexpr (OP >= 20 && OP <= 22) asm volatile("s_xor_b64 %0, %0, %1" : "+s"(cy[c]) : "s"(m) : "scc");     \
+  if constexpr (OP >= 21 && OP <= 22) asm volatile("s_and_b64 %0, %0, %1" : "+s"(cy[(c + 5) & 15]) : "s"(m) : "scc"); \
+  if constexpr (OP == 22) asm volatile("s_or_b64 %0, %0, %1\n s_xor_b64 %0, %0, %1" : "+s"(cy[(c + 9) & 15]) : "s"(m) : "scc"); \
+  if constexpr (OP == 23) asm volatile("v_addc_co_u32_e64 %0, %1, %0, %2, %1" : "+v"(a[c]), "+s"(cy[c]) : "v"(b)); \
+  if constexpr (OP == 23) asm volatile("s_xor_b64 %0, %0, %1\n s_and_b64 %0, %0, %1" : "+s"(cy[(c + 5) & 15]) : "s"(m) : "scc");
     REP16(BODY)
 #undef BODY
   }
@@ -86,6 +92,7 @@ static int run(const char *name, uint32_t *out, int blocks) {
 }
 
 int main() {
+  setvbuf(stdout, nullptr, _IONBF, 0);
   hipDeviceProp_t p;
   CHECK(hipGetDeviceProperties(&p, 0));
   uint32_t *out;
@@ -110,5 +117,12 @@ int main() {
   run<16>("v_sub_co_u32_e64", out, blocks);
   run<17>("v_add_co_u32_e32", out, blocks);
   run<18>("v_perm_b32", out, blocks);
+  // SALU beside VALU (per 16 mads: 0 / 16 / 32 / 64 independent 64-bit SALU
+  // ops; per 16 addc: 32): whether the scalar ops cost VALU issue slots
+  run<19>("mad + 0 salu", out, blocks);
+  run<20>("mad + 1 salu", out, blocks);
+  run<21>("mad + 2 salu", out, blocks);
+  run<22>("mad + 4 salu", out, blocks);
+  run<23>("addc + 2 salu", out, blocks);
   return 0;
 }
