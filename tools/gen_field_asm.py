@@ -421,13 +421,17 @@ def _mul_product(g: Prog, base: int, fast: bool):
         c2 = Ph[k + 1] if k < 14 else None
         for j, (i, jj) in enumerate(terms):
             cy = CY[j % 3]
-            g.mad(PP[k], cy, A[i], B[jj], src)
+            # first product with a check: the first one writes the mask itself
+            direct = fast and counted and j == 0 and k > 1 and first
+            g.mad(PP[k], RARE if direct else cy, A[i], B[jj], src)
             src = PP[k]
             if not counted:
                 continue
             if fast and j == 0:  # first product: only the rare mask
-                g.sor(RARE, cy, cy if first else RARE)
-                first = False
+                # column 1's addend is {w_0 hi, 0} < 2^32: a b + addend < 2^64
+                if k > 1 and not direct:
+                    g.sor(RARE, cy, RARE)
+                first = first and not direct
             else:
                 g.addc(c2, cy, 0 if j == (1 if fast else 0) else c2, 0, cy)
         if k < 14:
@@ -546,13 +550,16 @@ def _sqr_offdiag(g: Prog, base: int, fast: bool):
         c2 = Ph[k + 1]
         for j, (i, jj) in enumerate(terms):
             cy = CY[j % 3]
-            g.mad(PP[k], cy, A[i], A[jj], src)
+            direct = fast and counted and j == 0 and k > 2 and first
+            g.mad(PP[k], RARE if direct else cy, A[i], A[jj], src)
             src = PP[k]
             if not counted:
                 continue
             if fast and j == 0:
-                g.sor(RARE, cy, cy if first else RARE)
-                first = False
+                # column 2's addend is {column 1 hi, 0} < 2^32: no carry
+                if k > 2 and not direct:
+                    g.sor(RARE, cy, RARE)
+                first = first and not direct
                 if len(terms) == 1:
                     g.mov(c2, 0)
             else:
