@@ -62,6 +62,9 @@ constexpr uint32_t kRgWords = 33;              // R_G words per item (XYZZ + inf
 #endif
 constexpr bool kFusedKc = BV_FUSED_KC;         // key cache: one fused verify kernel (k_verify_gq)
 constexpr size_t kChunk = 16ull << 20;         // host-entry staging / PCIe chunk
+// host batches whose whole staging layout is at most this cross PCIe as ONE
+// copy: each extra small H2D costs ~20 us of DMA latency on a lone call
+constexpr size_t kSmallStage = 1ull << 20;
 
 }  // namespace
 
@@ -1024,20 +1027,32 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
     }
     return BV_OK;
   };
-  rc = stage(0, segs[6].off);  // the keys
-  if (rc != BV_OK) return rc;
-  HIPCHK(hipEventRecord(ctx->S().ev[E_KREADY], cs), BV_E_LAUNCH, "event");
-  rc = stage(segs[6].off, segs[0].off);  // s, pre
-  if (rc != BV_OK) return rc;
-  HIPCHK(hipEventRecord(ctx->S().ev[E_SREADY], cs), BV_E_LAUNCH, "event");
-  rc = stage(segs[0].off, segs[8].off);  // msg_off, item_msg, item_key, r
-  if (rc != BV_OK) return rc;
-  // zero the message-bytes pad (the SHA kernel over-reads the last dword of
-  // a message into it): in the staging, or on the device for direct bytes
-  if (msg_len && !direct[8]) memset(pin + segs[8].off + msg_len, 0, 64);
-  if (msg_len && direct[8])
-    HIPCHK(hipMemsetAsync(dev + segs[8].off + msg_len, 0, 64, cs), BV_E_LAUNCH, "zero message pad");
-  HIPCHK(hipEventRecord(ctx->S().ev[E_SMALL], cs), BV_E_LAUNCH, "event");
+  // a small batch (every array in pageable memory) crosses in ONE copy: the
+  // whole layout, message bytes and their zero pad included
+  bool one_copy = total <= kSmallStage;
+  for (int i = 0; i < 9; i++) one_copy = one_copy && !direct[i];
+  if (one_copy) {
+    for (int i = 0; i < 9; i++)
+      if (segs[i].n) memcpy(pin + segs[i].off, segs[i].src, segs[i].n);
+    if (msg_len) memset(pin + segs[8].off + msg_len, 0, 64);
+    HIPCHK(hipMemcpyAsync(dev, pin, total, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d (one copy)");
+    for (int e : {E_KREADY, E_SREADY, E_SMALL}) HIPCHK(hipEventRecord(ctx->S().ev[e], cs), BV_E_LAUNCH, "event");
+  } else {
+    rc = stage(0, segs[6].off);  // the keys
+    if (rc != BV_OK) return rc;
+    HIPCHK(hipEventRecord(ctx->S().ev[E_KREADY], cs), BV_E_LAUNCH, "event");
+    rc = stage(segs[6].off, segs[0].off);  // s, pre
+    if (rc != BV_OK) return rc;
+    HIPCHK(hipEventRecord(ctx->S().ev[E_SREADY], cs), BV_E_LAUNCH, "event");
+    rc = stage(segs[0].off, segs[8].off);  // msg_off, item_msg, item_key, r
+    if (rc != BV_OK) return rc;
+    // zero the message-bytes pad (the SHA kernel over-reads the last dword of
+    // a message into it): in the staging, or on the device for direct bytes
+    if (msg_len && !direct[8]) memset(pin + segs[8].off + msg_len, 0, 64);
+    if (msg_len && direct[8])
+      HIPCHK(hipMemsetAsync(dev + segs[8].off + msg_len, 0, 64, cs), BV_E_LAUNCH, "zero message pad");
+    HIPCHK(hipEventRecord(ctx->S().ev[E_SMALL], cs), BV_E_LAUNCH, "event");
+  }
 
   bv_batch d = {};
   d.n_msgs = n_msgs;
@@ -1088,7 +1103,9 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
     uint64_t m1 = std::upper_bound(b->msg_off + m0 + 1, b->msg_off + n_msgs + 1, base + kChunk) - b->msg_off - 1;
     if (m1 <= m0) m1 = m0 + 1;
     const uint64_t end = b->msg_off[m1];
-    if (direct[8]) {
+    if (one_copy) {
+      // already on the device
+    } else if (direct[8]) {
       HIPCHK(hipMemcpyAsync(dev + segs[8].off + base, b->msg_bytes + base, end - base, hipMemcpyHostToDevice, cs),
              BV_E_LAUNCH, "h2d msgs (pinned caller buffer)");
     } else {

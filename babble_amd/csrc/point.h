@@ -74,8 +74,8 @@ DEV void gej_double_lat(gej &r, const gej &a) {
 
 // r += (x2, y2) (affine): 8M + 3S + 7 add/sub (madd with Z3 = Z1 H; fewer
 // additions and live temporaries than madd-2007-bl's 7M + 4S + 11: trading
-// one squaring for a multiply costs 34 VALU on gfx950 — fe_sqr 141 against
-// fe_mul 175, field_asm.h — while the four extra add/sub would cost 52).
+// one squaring for a multiply costs 30 VALU on gfx950 — fe_sqr 132 against
+// fe_mul 162, field_asm.h — while the four extra add/sub would cost 52).
 // `inf` is r's identity flag.
 DEV void gej_add_ge(gej &r, bool &inf, const fe &x2, const fe &y2) {
   if (inf) {

@@ -14,6 +14,9 @@ import torch  # noqa: E402,F401
 from babble_amd import native, synth  # noqa: E402
 from babble_amd import verifier as V  # noqa: E402
 
+if len(sys.argv) > 1:  # a library build other than the in-tree one
+    native.LIB_PATH = os.path.abspath(sys.argv[1])
+    native._lib = None
 b = synth.events(1, n_creators=1, seed=901)
 for mode, flags in (("cold", native.F_DEFAULT), ("warm", native.F_KEY_CACHE)):
     v = V.Verifier(0, flags=flags)
