@@ -55,7 +55,10 @@ constexpr uint32_t kLatTableKeys = BV_LAT_TABLE_KEYS;
 constexpr uint64_t kLatTableItems = 4096;
 constexpr uint32_t kKcMaxBatchKeys = 4096;     // key cache: batches with more keys use per-batch tables
 constexpr uint32_t kKcBuildGroup = 8;          // keys per KC build launch (pscr: 403 MB per key)
-constexpr uint32_t kPrepM = 16;                // items per s^-1 batch
+#ifndef BV_PREP_M
+#define BV_PREP_M 16
+#endif
+constexpr uint32_t kPrepM = BV_PREP_M;         // items per s^-1 batch
 constexpr uint32_t kRgWords = 33;              // R_G words per item (XYZZ + inf: verify_core.h RG_WORDS)
 #ifndef BV_FUSED_KC
 #define BV_FUSED_KC 1
