@@ -146,6 +146,25 @@ def test_host_entry_item_order(verifier):
     check_against_oracle(verifier, dataclasses.replace(b, item_msg=late))
 
 
+def test_host_entry_single_copy_staging(verifier):
+    """Host batches whose staging layout is <= 1 MB cross PCIe as one copy
+    (bv_api.cpp kSmallStage): a ~0.8 MB adversarial batch in message order
+    and shuffled (items verified after the whole transfer), and one just
+    above the threshold (staged in pieces), all equal to the oracle."""
+    import dataclasses
+
+    b = synth.adversarial(1500, seed=71, n_creators=8, scale_per_million=MIX)
+    assert b.msg_bytes.nbytes + 80 * b.n_items < (1 << 20)
+    check_against_oracle(verifier, b)
+    perm = np.random.default_rng(71).permutation(b.n_items)
+    pre = None if b.pre is None else b.pre[perm]
+    check_against_oracle(verifier, dataclasses.replace(b, item_msg=b.item_msg[perm], item_key=b.item_key[perm],
+                                                       r_be=b.r_be[perm], s_be=b.s_be[perm], pre=pre))
+    big = synth.adversarial(2600, seed=72, n_creators=8, scale_per_million=MIX)
+    assert big.msg_bytes.nbytes > (1 << 20)
+    check_against_oracle(verifier, big)
+
+
 def test_throughput_variants_above_latency_threshold(verifier):
     """Batches of <= 128k items take the verify kernels' latency variants
     (zipped point ops), larger ones the throughput variants: just above the
