@@ -283,17 +283,36 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   hipStream_t cs = bv_copy_stream(ctx);
   if (!cs) return bv_fail(ctx, BV_E_NODEVICE, "copy stream");
   HIPCHK(hipEventRecord(ctx->S().ev[E_CALL], cs), BV_E_LAUNCH, "event");
+  // arrays in bv_host_alloc memory are DMA'd from where they are (no
+  // staging copy: what a cgo caller gets by building the wire batch there)
+  std::vector<char> direct(segs.size());
+  for (size_t i = 0; i < segs.size(); i++) direct[i] = segs[i].src && bv_is_pinned(segs[i].src, segs[i].n);
   auto stage = [&](size_t a0, size_t a1) -> int {
     for (size_t a = a0; a < a1; a += kChunk) {
       const size_t z = std::min(a1, a + kChunk);
       std::vector<CopyPool::Piece> pieces;
-      for (const Seg &g : segs) {
+      bool any_direct = false;
+      for (size_t i = 0; i < segs.size(); i++) {
+        const Seg &g = segs[i];
         const size_t lo = std::max(a, g.off), hi = std::min(z, g.off + g.n);
-        if (g.kind == ALL && g.src && lo < hi)
+        if (g.kind != ALL || !g.src || lo >= hi) continue;
+        if (direct[i]) {
+          any_direct = true;
+          HIPCHK(hipMemcpyAsync(dev + lo, (const uint8_t *)g.src + (lo - g.off), hi - lo, hipMemcpyHostToDevice, cs),
+                 BV_E_LAUNCH, "h2d (pinned caller buffer)");
+        } else {
           pieces.push_back({pin + lo, (const uint8_t *)g.src + (lo - g.off), hi - lo});
+        }
       }
       ctx->pool->copy_many(pieces);
-      HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
+      if (!any_direct) {
+        HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
+      } else {  // the staged pieces only: the range also holds direct segments
+        for (const CopyPool::Piece &q : pieces) {
+          const size_t o = (uint8_t *)q.dst - pin;
+          HIPCHK(hipMemcpyAsync(dev + o, q.dst, q.n, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
+        }
+      }
     }
     return BV_OK;
   };
@@ -323,13 +342,19 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   for (size_t c = 0; c + 1 < cb.size(); c++) {
     const uint64_t e0 = cb[c], e1 = cb[c + 1];
     std::vector<CopyPool::Piece> pieces;
-    for (const Seg &g : segs) {
+    for (size_t i = 0; i < segs.size(); i++) {
+      const Seg &g = segs[i];
       if (g.kind == ALL || !g.src) continue;
       size_t lo, hi;
       seg_range(g, e0, e1, &lo, &hi);
-      if (lo < hi) pieces.push_back({pin + g.off + lo, (const uint8_t *)g.src + lo, hi - lo});
+      if (lo >= hi) continue;
+      if (direct[i])
+        HIPCHK(hipMemcpyAsync(dev + g.off + lo, (const uint8_t *)g.src + lo, hi - lo, hipMemcpyHostToDevice, cs),
+               BV_E_LAUNCH, "h2d (pinned caller buffer)");
+      else
+        pieces.push_back({pin + g.off + lo, (const uint8_t *)g.src + lo, hi - lo});
     }
-    ctx->pool->copy_many(pieces);  // the whole chunk into pinned memory, then its DMA
+    ctx->pool->copy_many(pieces);  // the rest of the chunk into pinned memory, then its DMA
     for (const CopyPool::Piece &q : pieces) {
       const size_t o = (uint8_t *)q.dst - pin;
       HIPCHK(hipMemcpyAsync(dev + o, pin + o, q.n, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
@@ -386,12 +411,16 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   call.o_st = o_st;
   call.o_bits = o_bits;
   HIPCHK(hipStreamWaitEvent(cs, ctx->S().ev[E_HASHED], 0), BV_E_LAUNCH, "join");
-  HIPCHK(hipMemcpyAsync(pout, dig, n * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH, "d2h digests");
+  call.direct_hash = res && bv_is_pinned(res->msg_hash, n * 32);  // results straight into pinned caller buffers
+  call.direct_status = res && bv_is_pinned(res->status, n);
+  HIPCHK(hipMemcpyAsync(call.direct_hash ? res->msg_hash : pout, dig, n * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH,
+         "d2h digests");
   HIPCHK(hipEventRecord(ctx->S().ev[E_CSDONE], cs), BV_E_LAUNCH, "event");
 
   rc = pipe.finish();  // bulk: the last chunk's items; DAG: all of them
   if (rc != BV_OK) return rc;
-  HIPCHK(hipMemcpyAsync(pout + o_st, pipe.o.status, n, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h status");
+  HIPCHK(hipMemcpyAsync(call.direct_status ? res->status : pout + o_st, pipe.o.status, n, hipMemcpyDeviceToHost, st),
+         BV_E_LAUNCH, "d2h status");
   HIPCHK(hipMemcpyAsync(pout + o_bits, pipe.o.bits, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
          "d2h bits");
   HIPCHK(hipEventRecord(ctx->S().ev[E_OUT], st), BV_E_LAUNCH, "event");

@@ -193,6 +193,16 @@ class Verifier:
         self._check(self._L.bv_verify_events(self._ctx, ctypes.byref(cb), ctypes.byref(res)))
         return VerifyResult(h[:n], st[:n], bits[: (n + 63) // 64])
 
+    def verify_events_into(self, eb, res: VerifyResult) -> VerifyResult:
+        """bv_verify_events into caller-owned result arrays (PinnedArena
+        arrays are reached by DMA; so are the wire fields of a batch built by
+        PinnedArena.wire)."""
+        keep: list = []
+        cb = eb.c_struct(keep)
+        r = native.BvResult(_p(res.msg_hash), _p(res.status), _p(res.accept_bits))
+        self._check(self._L.bv_verify_events(self._ctx, ctypes.byref(cb), ctypes.byref(r)))
+        return res
+
     def peer_set_hash(self, pubkeys: Sequence[bytes]) -> bytes:
         """bv_peer_set_hash: PeerSet.Hash over the peers' key bytes (b"" for
         an empty set, as Go's []byte{})."""
@@ -349,6 +359,20 @@ class PinnedArena:
                            self.copy(b.key_off.astype(np.uint64)), self.copy(b.item_msg.astype(np.uint32)),
                            self.copy(b.item_key.astype(np.uint32)), self.copy(b.r_be), self.copy(b.s_be),
                            None if b.pre is None else self.copy(b.pre))
+
+    def wire(self, eb):
+        """The same events.EventWireBatch with every array in pinned memory
+        (in the dtypes the C struct takes, so none is converted again)."""
+        import dataclasses
+
+        dt = {"key_off": np.uint64, "creator": np.uint32, "index": np.int64, "timestamp": np.int64,
+              "parent_kind": np.uint8, "parent_ref": np.uint64, "tx_start": np.uint64, "tx_off": np.uint64,
+              "itx_off": np.uint64, "bsig_off": np.uint64}
+        out = {}
+        for f in dataclasses.fields(eb):
+            a = getattr(eb, f.name)
+            out[f.name] = None if a is None else self.copy(np.asarray(a).astype(dt.get(f.name, a.dtype), copy=False))
+        return type(eb)(**out)
 
     def close(self):
         for p in self._blocks:

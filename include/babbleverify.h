@@ -223,7 +223,8 @@ typedef struct {
 
 /* Host buffers in, results out (msg_hash: 32 * n_events; status, accept_bits
  * per event).  BV_E_ARGS for a bad reference (an EVENT parent not earlier in
- * the batch, an out-of-range key / hash / offset). */
+ * the batch, an out-of-range key / hash / offset).  As for bv_verify_batch,
+ * arrays and result buffers in bv_host_alloc memory are DMA'd in place. */
 int bv_verify_events(bv_ctx *ctx, const bv_event_batch *events, bv_result *result);
 
 /* Multi-GPU: one verifier over several devices of this process (one bv_ctx

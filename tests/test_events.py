@@ -212,3 +212,43 @@ def test_verify_events_rejects_forward_reference():
             v.verify_events(wire)
     finally:
         v.close()
+
+
+@pytest.mark.gpu
+def test_verify_events_from_pinned_buffers(monkeypatch):
+    """Wire fields and results in bv_host_alloc memory (PinnedArena.wire):
+    the library DMAs them in place, chunk by chunk (small chunks here), and
+    the digests / statuses land in the pinned result arrays — equal to the
+    oracle on a signed bulk batch with corruptions and to the pageable call
+    on the edge-case wire batches (nil / empty lists, fragments, in-batch
+    parents)."""
+    from babble_amd.verifier import PinnedArena, Verifier, VerifyResult
+    from oracle import coracle
+
+    monkeypatch.setenv("BV_EV_CHUNK_MB", "0.05")
+    v = Verifier(0)
+    arena = PinnedArena()
+    try:
+        packed, wire = synth.event_fields(5000, n_creators=8, seed=23, parents="hash")
+        bad = np.random.default_rng(23).choice(5000, 50, replace=False)
+        wire.s_be[bad, 9] ^= 0x04
+        packed.s_be[bad, 9] ^= 0x04
+        pw = arena.wire(wire)
+        res = VerifyResult(arena.array((5000, 32), np.uint8), arena.array(5000, np.uint8),
+                           arena.array((5000 + 63) // 64, np.uint64))
+        v.verify_events_into(pw, res)
+        h, st, bits = coracle.verify_batch(packed.as_dict())
+        assert np.array_equal(res.msg_hash, h)
+        assert np.array_equal(res.status, st) and np.array_equal(res.accept_bits, bits)
+        for seed in (8, 9):
+            w2, _, wd = random_wire(seed, n=700)
+            n = w2.n_events
+            r2 = VerifyResult(arena.array((n, 32), np.uint8), arena.array(n, np.uint8),
+                              arena.array((n + 63) // 64, np.uint64))
+            v.verify_events_into(arena.wire(w2), r2)
+            assert [d.tobytes() for d in r2.msg_hash] == wd
+            ref = v.verify_events(w2)
+            assert np.array_equal(r2.status, ref.status) and np.array_equal(r2.accept_bits, ref.accept_bits)
+    finally:
+        v.close()
+        arena.close()
