@@ -65,6 +65,11 @@ constexpr uint32_t kRgWords = 33;              // R_G words per item (XYZZ + inf
 #endif
 constexpr bool kFusedKc = BV_FUSED_KC;         // key cache: one fused verify kernel (k_verify_gq)
 constexpr size_t kChunk = 16ull << 20;         // host-entry staging / PCIe chunk
+// message bytes hashed (and their items verified) per chunk: 64 MB keeps
+// each chunk's verify launches at full occupancy (1M C2 events from pinned
+// arrays, same box: 16 / 64 / 128 MB = 15.0-15.7 / 11.0 / 10.9-11.0 ms per
+// call; pageable 15.2 / 12.0 ms, tools/host_prof.py)
+constexpr size_t kMsgChunk = 64ull << 20;
 // host batches whose whole staging layout is at most this cross PCIe as ONE
 // copy: each extra small H2D costs ~20 us of DMA latency on a lone call
 constexpr size_t kSmallStage = 1ull << 20;
@@ -1099,11 +1104,13 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order");
   HIPCHK(hipEventRecord(ctx->S().ev[E_HASH0], st), BV_E_LAUNCH, "event");
   HIPCHK(hipEventRecord(ctx->S().ev[E_FORK], st), BV_E_LAUNCH, "event");
+  const char *env_chunk = getenv("BV_HOST_CHUNK_MB");  // A/B knob
+  const uint64_t msg_chunk = env_chunk ? std::max<uint64_t>(1, (uint64_t)(atof(env_chunk) * (1 << 20))) : kMsgChunk;
   uint64_t m0 = 0;
   while (m0 < n_msgs) {
-    // messages [m0, m1) holding about kChunk bytes (at least one message)
+    // messages [m0, m1) holding about msg_chunk bytes (at least one message)
     const uint64_t base = b->msg_off[m0];
-    uint64_t m1 = std::upper_bound(b->msg_off + m0 + 1, b->msg_off + n_msgs + 1, base + kChunk) - b->msg_off - 1;
+    uint64_t m1 = std::upper_bound(b->msg_off + m0 + 1, b->msg_off + n_msgs + 1, base + msg_chunk) - b->msg_off - 1;
     if (m1 <= m0) m1 = m0 + 1;
     const uint64_t end = b->msg_off[m1];
     if (one_copy) {

@@ -27,7 +27,12 @@ namespace {
 
 constexpr uint32_t kNarrowLevel = 768;   // events per level run by k_ev_hash_chain (<= kChainCap)
 constexpr uint32_t kChainCap = 768;      // events per k_ev_hash_chain launch (EVC_CAP)
-constexpr size_t kChunk = 16ull << 20;  // staged bytes per PCIe piece / event chunk
+// staged bytes per PCIe piece / event chunk: 64 MB (~250k C2 events) keeps
+// each chunk's verify launches at full occupancy while the next chunk
+// crosses PCIe (1M bulk events, same box: 16 / 32 / 64 / 128 MB / one
+// chunk = 8.6-9.0 / 7.8-8.3 / 7.25-7.5 / 7.7 / 7.7-8.2 ms per call from
+// pinned arrays, tools/events_prof.py)
+constexpr size_t kChunk = 64ull << 20;
 
 int validate(bv_ctx *ctx, const bv_event_batch *b) {
   const uint64_t n = b->n_events;

@@ -124,14 +124,15 @@ def test_k12_tables_adversarial(verifier):
     assert verifier.timing()["key_path"] == 12
 
 
-def test_host_entry_item_order(verifier):
+def test_host_entry_item_order(verifier, monkeypatch):
     """bv_verify_batch verifies items chunk by chunk as their messages land
     when item_msg is non-decreasing, and after the whole transfer otherwise:
-    the same batch (several 16 MB staging chunks, K12 tables, the C4 mix) in
-    message order, shuffled, and with a run of 63 items re-hitting an early
-    message: every status equal to the oracle's."""
+    the same batch (several 8 MB message chunks via BV_HOST_CHUNK_MB, K12
+    tables, the C4 mix) in message order, shuffled, and with a run of 63
+    items re-hitting an early message: every status equal to the oracle's."""
     import dataclasses
 
+    monkeypatch.setenv("BV_HOST_CHUNK_MB", "8")
     b = synth.adversarial(120_000, seed=13, n_creators=16, scale_per_million=MIX)
     assert np.all(np.diff(b.item_msg.astype(np.int64)) >= 0)
     check_against_oracle(verifier, b)
