@@ -279,7 +279,15 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   vb.s_be = d.s_be;
   vb.pre = d.pre;
   bool kc = false;
-  bv_item_pipe pipe{ctx, &vb, {}, st, false};
+  // bulk batches: each chunk's verify kernels go on the keys stream (idle
+  // once the tables are built), so they run beside the next chunk's body
+  // build and hashing on the main stream instead of after them
+  // (1M bulk events from pinned arrays, same box: 7.37-7.41 -> 6.90-7.01 ms
+  // per call; BV_EV_VERIFY_STREAM=0 keeps them on the main stream)
+  const char *env_vs = getenv("BV_EV_VERIFY_STREAM");
+  const bool split_verify = !dag && (env_vs == nullptr || atoi(env_vs) != 0);
+  hipStream_t vst = split_verify ? ctx->kstream : st;
+  bv_item_pipe pipe{ctx, &vb, {}, vst, false};
   rc = bv_out_bufs(ctx, &vb, nullptr, nullptr, nullptr, true, &pipe.o);
   if (rc != BV_OK) return rc;
   uint32_t *dig = pipe.o.dig;
@@ -372,6 +380,11 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
     if (!dag) {
       HIPCHK(bvk::ev_hash(st, e1 - e0, nullptr, e0, d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
       HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is used
+      if (split_verify) {
+        hipEvent_t hashed = ctx->chunk_ev[(c + 32) % ctx->chunk_ev.size()];  // waited on at once: reuse is safe
+        HIPCHK(hipEventRecord(hashed, st), BV_E_LAUNCH, "event");
+        HIPCHK(hipStreamWaitEvent(vst, hashed, 0), BV_E_LAUNCH, "join chunk digests");
+      }
       rc = pipe.upto(e1);
       if (rc != BV_OK) return rc;
     }
@@ -424,6 +437,7 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
 
   rc = pipe.finish();  // bulk: the last chunk's items; DAG: all of them
   if (rc != BV_OK) return rc;
+  if (split_verify) HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_END], 0), BV_E_LAUNCH, "join verify");
   HIPCHK(hipMemcpyAsync(call.direct_status ? res->status : pout + o_st, pipe.o.status, n, hipMemcpyDeviceToHost, st),
          BV_E_LAUNCH, "d2h status");
   HIPCHK(hipMemcpyAsync(pout + o_bits, pipe.o.bits, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
