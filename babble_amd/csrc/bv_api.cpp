@@ -37,8 +37,6 @@ constexpr uint64_t kKTableBytes = BV_KTABLE_U32 * 4;
 constexpr uint64_t kK12TableBytes = BV_K12TABLE_U32 * 4;
 constexpr uint64_t kK12SubBytes = BV_K12SUB_U32 * 4;
 constexpr uint64_t kK12PrefixBytes = (uint64_t)BV_K12NWIN * BV_K12ENT * 32;  // one fe per entry
-constexpr uint64_t kKcTableBytes = BV_KCTABLE_U32 * 4;                      // 805 MB per cached key
-constexpr uint64_t kKcSubBytes = BV_KCSUB_U32 * 4;
 constexpr uint32_t kBasesPerKey = 22;       // max(K8 16, K12 22, KC 14) bases per key
 constexpr uint64_t kK12MinItemsPerKey = 2048;  // K12 pays for its 11x larger build above this
 constexpr uint32_t kMaxTableKeys = 8192;       // K8: 4 GiB of key tables
@@ -53,8 +51,6 @@ constexpr uint32_t kMaxK12Keys = 1024;         // K12: 2.8 GiB
 #endif
 constexpr uint32_t kLatTableKeys = BV_LAT_TABLE_KEYS;
 constexpr uint64_t kLatTableItems = 4096;
-constexpr uint32_t kKcMaxBatchKeys = 4096;     // key cache: batches with more keys use per-batch tables
-constexpr uint32_t kKcBuildGroup = 8;          // keys per KC build launch (pscr: 403 MB per key)
 #ifndef BV_PREP_M
 #define BV_PREP_M 16
 #endif
@@ -396,11 +392,7 @@ static int create_impl(bv_ctx *ctx) {
   if (!ctx->g_table) return bv_fail(ctx, BV_E_OOM, "generator table (geometry.h, ~21.5 GB of HBM) build failed");
   const unsigned hw = std::thread::hardware_concurrency();
   ctx->pool = new CopyPool((int)std::min<unsigned>(hw ? hw - 1 : 0, 7));
-  if (ctx->flags & BV_F_KEY_CACHE) {
-    double gb = 96.0;  // 119 KC tables: C5's 100 validators fit
-    if (const char *s = getenv("BV_KEY_CACHE_GB")) gb = atof(s);
-    ctx->kc_budget = (uint64_t)(std::max(gb, 0.0) * 1e9);
-  }
+  if (ctx->flags & BV_F_KEY_CACHE) bv_kc_init(ctx);
   return BV_OK;
 }
 
@@ -445,13 +437,12 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   for (auto &sl : ctx->slot) {
     DevBuf *sb[] = {&sl.digests,   &sl.kstatus, &sl.kxy, &sl.bases_jac, &sl.key_sub, &sl.key_pscr,
                     &sl.key_table, &sl.scratch, &sl.u12, &sl.rg,        &sl.status,  &sl.bits,
-                    &sl.kc_tabs,   &sl.kc_kst};
+                    &sl.kc_tabs};
     for (auto *b : sb) b->release();
     sl.pin_small.release();
     if (sl.done) (void)hipEventDestroy(sl.done);
   }
-  for (auto &s : ctx->kc_slots)
-    if (s.table) (void)hipFree(s.table);
+  bv_kc_release(ctx);
   ctx->pin_in.release();
   ctx->pin_out.release();
   for (auto &sl : ctx->slot)
@@ -470,149 +461,6 @@ extern "C" void *bv_last_stream(const bv_ctx *ctx) { return ctx ? (void *)ctx->l
 extern "C" int bv_get_timing(const bv_ctx *ctx, bv_timing *out) {
   if (!ctx || !out) return BV_E_ARGS;
   *out = ctx->timing;
-  return BV_OK;
-}
-
-// ---------------------------------------------------------------------------
-// key cache (BV_F_KEY_CACHE)
-// ---------------------------------------------------------------------------
-// Resolves the batch's keys against the cache: hits need nothing; valid
-// misses get a KC table built now (cold); malformed keys are remembered with
-// their status and no table.  On success fills ctx->S().kc_tabs / kc_kst (device,
-// per batch key) and returns BV_OK with *use = true; *use = false when the
-// batch cannot use the cache (too many keys, budget) and must take the
-// per-batch path.  hkb/hko: host copies of the key bytes; dkb/dko: device.
-int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
-                      const uint64_t *dko, hipStream_t st, bool *use) {
-  *use = false;
-  if (n_keys == 0 || n_keys > kKcMaxBatchKeys) return BV_OK;
-  if (ctx->S().has_done)  // the slot's pin_small may still feed its previous (async) call
-    HIPCHK(hipEventSynchronize(ctx->S().done), BV_E_LAUNCH, "sync slot");
-  ctx->kc_clock++;
-  std::vector<int> slot_of(n_keys, -1);
-  std::vector<uint32_t> miss;
-  uint32_t hits = 0;
-  for (uint32_t k = 0; k < n_keys; k++) {
-    std::string key((const char *)hkb + hko[k], (size_t)(hko[k + 1] - hko[k]));
-    auto it = ctx->kc_index.find(key);
-    if (it != ctx->kc_index.end()) {
-      slot_of[k] = it->second;
-      ctx->kc_slots[it->second].last_use = ctx->kc_clock;
-      hits++;
-    } else {
-      miss.push_back(k);
-    }
-  }
-  uint32_t builds = 0;
-  if (!miss.empty()) {
-    // statuses of the missing keys: k_key_decode on the device (the product
-    // path for elliptic.Unmarshal), then one small synchronous copy back
-    HIPCHK(ctx->S().kstatus.ensure(n_keys), BV_E_OOM, "alloc kstatus");
-    HIPCHK(ctx->S().kxy.ensure((uint64_t)n_keys * 64), BV_E_OOM, "alloc kxy");
-    HIPCHK(bvk::key_decode(st, n_keys, dkb, dko, ctx->S().kstatus.as<uint8_t>(), ctx->S().kxy.as<uint32_t>()), BV_E_LAUNCH,
-           "k_key_decode");
-    std::vector<uint8_t> kst(n_keys);
-    HIPCHK(hipMemcpyAsync(kst.data(), ctx->S().kstatus.p, n_keys, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h kst");
-    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
-    std::vector<uint32_t> build;  // valid misses
-    for (uint32_t k : miss)
-      if (kst[k] == KS_OK) build.push_back(k);
-    // budget: evict least-recently-used tables not used by this batch
-    uint64_t need = (uint64_t)build.size() * kKcTableBytes;
-    if (need > ctx->kc_budget) return BV_OK;  // this batch's keys alone exceed the budget
-    while (ctx->kc_bytes + need > ctx->kc_budget) {
-      int victim = -1;
-      for (size_t i = 0; i < ctx->kc_slots.size(); i++) {
-        const auto &s = ctx->kc_slots[i];
-        if (s.table && s.last_use != ctx->kc_clock && (victim < 0 || s.last_use < ctx->kc_slots[victim].last_use))
-          victim = (int)i;
-      }
-      if (victim < 0) return BV_OK;
-      if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // sync before eviction
-      auto &s = ctx->kc_slots[victim];
-      HIPCHK(hipFree(s.table), BV_E_LAUNCH, "free cached table");
-      s.table = nullptr;
-      ctx->kc_bytes -= kKcTableBytes;
-      ctx->kc_index.erase(s.bytes);
-      s.bytes.clear();
-      s.free = true;
-    }
-    // allocate slots for every miss (malformed keys: status only, no table)
-    for (uint32_t k : miss) {
-      int si = -1;
-      for (size_t i = 0; i < ctx->kc_slots.size(); i++)
-        if (ctx->kc_slots[i].free) {
-          si = (int)i;
-          break;
-        }
-      if (si < 0) {
-        ctx->kc_slots.emplace_back();
-        si = (int)ctx->kc_slots.size() - 1;
-      }
-      auto &s = ctx->kc_slots[si];
-      s.free = false;
-      s.bytes.assign((const char *)hkb + hko[k], (size_t)(hko[k + 1] - hko[k]));
-      s.status = kst[k];
-      s.last_use = ctx->kc_clock;
-      s.table = nullptr;
-      if (kst[k] == KS_OK) {
-        hipError_t e = hipMalloc(&s.table, kKcTableBytes);
-        if (e != hipSuccess) {
-          (void)hipGetLastError();
-          s.table = nullptr;
-          s.free = true;
-          s.bytes.clear();
-          return BV_OK;  // HBM exhausted: per-batch path for this call
-        }
-        ctx->kc_bytes += kKcTableBytes;
-      }
-      ctx->kc_index[s.bytes] = si;
-      slot_of[k] = si;
-    }
-    // build the new tables, kKcBuildGroup keys per launch
-    const uint32_t G = std::min<uint32_t>(kKcBuildGroup, (uint32_t)std::max<size_t>(build.size(), 1));
-    HIPCHK(ctx->kc_kxy.ensure((uint64_t)G * 64), BV_E_OOM, "alloc kc kxy");
-    HIPCHK(ctx->kc_btabs.ensure((uint64_t)G * 8), BV_E_OOM, "alloc kc tabs");
-    HIPCHK(ctx->S().bases_jac.ensure((uint64_t)G * kBasesPerKey * 96), BV_E_OOM, "alloc bases");
-    HIPCHK(ctx->S().key_sub.ensure((uint64_t)G * kKcSubBytes), BV_E_OOM, "alloc kc sub-tables");
-    HIPCHK(ctx->S().key_pscr.ensure((uint64_t)G * bvk::kc_pscr_bytes()), BV_E_OOM, "alloc kc prefix scratch");
-    HIPCHK(ctx->S().pin_small.ensure(4096), BV_E_OOM, "alloc pinned");
-    for (size_t g0 = 0; g0 < build.size(); g0 += G) {
-      const uint32_t n = (uint32_t)std::min<size_t>(G, build.size() - g0);
-      uint64_t *tabs = (uint64_t *)ctx->S().pin_small.p;
-      HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");  // pin_small reuse
-      for (uint32_t i = 0; i < n; i++) {
-        const uint32_t k = build[g0 + i];
-        HIPCHK(hipMemcpyAsync(ctx->kc_kxy.as<uint8_t>() + 64ull * i, ctx->S().kxy.as<uint8_t>() + 64ull * k, 64,
-                              hipMemcpyDeviceToDevice, st),
-               BV_E_LAUNCH, "gather kxy");
-        tabs[i] = (uint64_t)(uintptr_t)ctx->kc_slots[slot_of[k]].table;
-      }
-      HIPCHK(hipMemcpyAsync(ctx->kc_btabs.p, tabs, n * 8ull, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d tabs");
-      HIPCHK(bvk::build_kc(st, n, ctx->kc_kxy.as<uint32_t>(), nullptr, ctx->S().bases_jac.as<uint32_t>(),
-                           ctx->S().key_sub.as<uint32_t>(), ctx->S().key_pscr.as<uint32_t>(), ctx->kc_btabs.as<uint64_t>()),
-             BV_E_LAUNCH, "KC key tables");
-      builds += n;
-    }
-    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
-  }
-  // per-batch arrays: table address and status of every batch key
-  HIPCHK(ctx->S().pin_small.ensure((uint64_t)n_keys * 9 + 64), BV_E_OOM, "alloc pinned");
-  uint64_t *tabs = (uint64_t *)ctx->S().pin_small.p;
-  uint8_t *kst = (uint8_t *)(tabs + n_keys);
-  for (uint32_t k = 0; k < n_keys; k++) {
-    const auto &s = ctx->kc_slots[slot_of[k]];
-    tabs[k] = (uint64_t)(uintptr_t)s.table;
-    kst[k] = s.status;
-  }
-  HIPCHK(ctx->S().kc_tabs.ensure((uint64_t)n_keys * 8), BV_E_OOM, "alloc kc tabs");
-  HIPCHK(ctx->S().kc_kst.ensure(n_keys), BV_E_OOM, "alloc kc kst");
-  HIPCHK(hipMemcpyAsync(ctx->S().kc_tabs.p, tabs, n_keys * 8ull, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d tabs");
-  HIPCHK(hipMemcpyAsync(ctx->S().kc_kst.p, kst, n_keys, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d kst");
-  ctx->timing.kc_hits = hits;
-  ctx->timing.kc_builds = builds;
-  ctx->timing.kc_keys = (uint32_t)ctx->kc_index.size();
-  *use = true;
   return BV_OK;
 }
 
@@ -676,12 +524,13 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   // (kstream) may queue behind another in-flight call's build.
   HIPCHK(hipStreamWaitEvent(ctx->sstream, keys_ready, 0), BV_E_LAUNCH, "fork");
   HIPCHK(hipEventRecord(ev[E_START], ctx->sstream), BV_E_LAUNCH, "event");
-  if (!kc) {
+  // (key cache: every batch decodes its keys too — statuses never come from
+  // the cache — unless bv_kc_prepare already did on the call's stream)
+  if (!(kc && ctx->S().kc_decoded))
     HIPCHK(bvk::key_decode(ctx->sstream, n_keys, b->key_bytes, b->key_off, ctx->S().kstatus.as<uint8_t>(),
                            ctx->S().kxy.as<uint32_t>()),
            BV_E_LAUNCH, "k_key_decode");
-    HIPCHK(hipEventRecord(ev[E_KDEC], ctx->sstream), BV_E_LAUNCH, "event");
-  }
+  HIPCHK(hipEventRecord(ev[E_KDEC], ctx->sstream), BV_E_LAUNCH, "event");
   // s^-1 needs only s: concurrent with everything up to k_verify_g
   HIPCHK(hipStreamWaitEvent(ctx->sstream, s_ready, 0), BV_E_LAUNCH, "fork");
   // items per lane: kPrepM amortises the inversion in large batches; a small
@@ -691,7 +540,7 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   HIPCHK(bvk::sinv(ctx->sstream, n_items, M, (const uint32_t *)b->s_be, b->pre, ctx->S().scratch.as<uint32_t>()),
          BV_E_LAUNCH, "k_sinv");
   HIPCHK(hipEventRecord(ev[E_SINV], ctx->sstream), BV_E_LAUNCH, "event");
-  HIPCHK(hipStreamWaitEvent(ctx->kstream, kc ? keys_ready : ev[E_KDEC], 0), BV_E_LAUNCH, "fork");
+  HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_KDEC], 0), BV_E_LAUNCH, "fork");
   if (!kc) {
     if (table_mode)
       HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->S().kxy.as<uint32_t>(), ctx->S().kstatus.as<uint8_t>(),
@@ -734,7 +583,7 @@ int bv_out_bufs(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_
 int bv_launch_items(bv_ctx *ctx, const bv_batch *b, const bv_out &o, hipStream_t st, bool kc, uint64_t lo,
                     uint64_t hi, int part) {
   const uint64_t n = b->n_items;
-  const uint8_t *kst = kc ? ctx->S().kc_kst.as<uint8_t>() : ctx->S().kstatus.as<uint8_t>();
+  const uint8_t *kst = ctx->S().kstatus.as<uint8_t>();
   const uint32_t *r32 = (const uint32_t *)b->r_be, *s32 = (const uint32_t *)b->s_be;
   uint32_t *w = ctx->S().scratch.as<uint32_t>(), *u12 = ctx->S().u12.as<uint32_t>();
   const bool fused = kc && kFusedKc;  // key cache: G and Q parts in one kernel (R_G stays in registers)

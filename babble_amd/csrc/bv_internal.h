@@ -13,6 +13,7 @@
 #include <thread>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <array>
 
 #ifndef BV_SLOTS
@@ -198,9 +199,10 @@ enum {
   E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_KDEC, E_COUNT
 };
 
+constexpr uint32_t kKcMaxBatchKeys = 4096;  // key cache: batches with more keys use per-batch tables
+
 struct KcSlot {
   std::string bytes;      // raw pubkey bytes (the cache key)
-  uint8_t status = 0;     // k_key_decode status
   void *table = nullptr;  // KC table (valid keys only)
   uint64_t last_use = 0;
   bool free = false;
@@ -239,8 +241,9 @@ struct bv_ctx {
   // streams.
   struct Slot {
     DevBuf digests, kstatus, kxy, bases_jac, key_sub, key_pscr, key_table, scratch, u12, rg, status, bits;
-    DevBuf kc_tabs, kc_kst;  // key-cache table address / status per batch key
-    PinnedBuf pin_small;     // their host staging
+    DevBuf kc_tabs;          // key-cache table address per batch key
+    PinnedBuf pin_small;     // its host staging
+    bool kc_decoded = false; // bv_kc_prepare already ran k_key_decode into kstatus / kxy on the call stream
     // caller result ranges [lo, hi) of this slot's device calls that the
     // other slots' calls have not yet been ordered after (deduplicated)
     std::vector<std::array<uintptr_t, 6>> uncovered;
@@ -257,9 +260,15 @@ struct bv_ctx {
   bool table_mode = false;
   int key_w = 0;  // 8, 12 or 20 (KC) in table mode
   bv_timing timing = {};
-  // key cache (BV_F_KEY_CACHE)
-  std::unordered_map<std::string, int> kc_index;
+  // key cache (BV_F_KEY_CACHE, bv_keycache.cpp)
+  std::unordered_map<std::string, int> kc_index;  // keys whose table build has been enqueued
   std::vector<KcSlot> kc_slots;
+  std::unordered_set<std::string> kc_registered;  // bv_kc_register: the validator set
+  std::unordered_map<std::string, uint32_t> kc_seen;  // valid keys without a table: batches seen (bounded)
+  std::unordered_set<std::string> kc_bad;  // 65-byte 0x04 keys off the curve (bounded)
+  uint32_t kc_admit = 2;                   // batches before an unregistered valid key gets a table
+  int kc_fail_alloc = 0, kc_fail_build = 0;  // fault injection (BV_KC_FAIL), tests only
+  uint64_t kc_allocs = 0, kc_build_calls = 0;
   uint64_t kc_clock = 0, kc_bytes = 0, kc_budget = 0;
   DevBuf kc_kxy, kc_btabs;
   // bv_verify_events: body lengths, parent-hex positions, offsets, bodies
@@ -318,7 +327,9 @@ struct bv_item_pipe {
 int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc);
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
-                  const uint64_t *dko, hipStream_t st, bool *use);
+                  const uint64_t *dko, hipStream_t st, bool *use, bool force_build = false);
+void bv_kc_init(bv_ctx *ctx);     // budget, admission and fault-injection settings (bv_create)
+void bv_kc_release(bv_ctx *ctx);  // free every cached table (bv_destroy, after all calls finished)
 // `res` (may be null): the caller's result buffers, written by DMA directly
 // when they are bv_host_alloc memory (else bv_host_finish copies them).
 int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_result *res = nullptr);

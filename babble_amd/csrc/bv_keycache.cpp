@@ -1,0 +1,336 @@
+// bv_keycache.cpp — the key cache of a bv_ctx (BV_F_KEY_CACHE): per-validator
+// KC tables (22-bit signed GLV windows, 805 MB each) kept in HBM across calls,
+// keyed by the raw pubkey bytes.  Babble's validator set is stable
+// (src/peers/peer_set.go), so the tables of the PeerSet's keys are built once
+// and every later batch of their events skips the per-batch table build.
+//
+// Invariants:
+//  * kc_index maps a key ONLY to a slot whose table build has been enqueued
+//    successfully on the call's stream (and every later call on the ctx is
+//    ordered after that stream's work).  A call that fails part-way — a
+//    table hipMalloc, a scratch allocation or a build launch — frees and
+//    unindexes every slot it allocated, so no later call can hit an unbuilt
+//    table.
+//  * Admission: a valid key gets a table when it is registered
+//    (bv_kc_register: the PeerSet) or once it has been seen in kc_admit
+//    batches (default 2).  Registered tables are never evicted to make room
+//    for unregistered keys.  Keys that are malformed by their form (length !=
+//    65 or prefix != 0x04) are never remembered; 65-byte keys found off the
+//    curve and valid keys waiting for admission are remembered in two sets of
+//    at most kKcMemoMax entries each (cleared when full), so attacker-chosen
+//    keys (processJoinRequest, src/node/node_rpc.go:250-260) bound host memory
+//    and cannot evict a validator's table.
+//  * Key statuses never come from the cache: every batch runs k_key_decode
+//    (the product's elliptic.Unmarshal), so a cached table is only ever read
+//    for a key whose batch decode says KS_OK.
+//  * Fault injection for tests (BV_KC_FAIL="alloc:N" or "build:N", read once
+//    at bv_create): the N-th KC table allocation / build launch of the ctx
+//    fails once.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "bv_internal.h"
+
+#define HIPCHK(expr, code, what)                               \
+  do {                                                         \
+    hipError_t _e = (expr);                                    \
+    if (_e != hipSuccess) return bv_fail(ctx, code, what, _e); \
+  } while (0)
+
+namespace {
+constexpr uint64_t kKcTableBytes = BV_KCTABLE_U32 * 4;  // 805 MB per cached key
+constexpr uint64_t kKcSubBytes = BV_KCSUB_U32 * 4;
+constexpr uint32_t kKcBases = 22;       // bases_jac stride (bv_api.cpp kBasesPerKey)
+constexpr uint32_t kKcBuildGroup = 8;   // keys per KC build launch (pscr: 403 MB per key)
+constexpr size_t kKcMemoMax = 4096;     // entries of kc_seen / kc_bad
+
+bool key_form_ok(const uint8_t *p, uint64_t len) { return len == 65 && p[0] == 4; }
+
+template <class Set>
+void memo_insert(Set &s, const std::string &k) {
+  if (s.size() >= kKcMemoMax) s.clear();  // bounded: forget everything rather than grow
+  s.insert(k);
+}
+}  // namespace
+
+void bv_kc_init(bv_ctx *ctx) {
+  double gb = 96.0;  // 119 KC tables: C5's 100 validators fit
+  if (const char *s = getenv("BV_KEY_CACHE_GB")) gb = atof(s);
+  ctx->kc_budget = (uint64_t)(std::max(gb, 0.0) * 1e9);
+  if (const char *s = getenv("BV_KC_ADMIT")) ctx->kc_admit = (uint32_t)std::max(1, atoi(s));
+  if (const char *s = getenv("BV_KC_FAIL")) {
+    int n = 0;
+    if (sscanf(s, "alloc:%d", &n) == 1) ctx->kc_fail_alloc = n;
+    else if (sscanf(s, "build:%d", &n) == 1) ctx->kc_fail_build = n;
+  }
+}
+
+void bv_kc_release(bv_ctx *ctx) {
+  for (auto &s : ctx->kc_slots)
+    if (s.table) (void)hipFree(s.table);
+  ctx->kc_slots.clear();
+  ctx->kc_index.clear();
+  ctx->kc_bytes = 0;
+}
+
+static hipError_t kc_table_alloc(bv_ctx *ctx, void **p) {
+  if (++ctx->kc_allocs == (uint64_t)ctx->kc_fail_alloc) return hipErrorOutOfMemory;  // injected
+  hipError_t e = hipMalloc(p, kKcTableBytes);
+  if (e != hipSuccess) (void)hipGetLastError();
+  return e;
+}
+
+// Resolves the batch's keys against the cache.  On BV_OK with *use = true the
+// slot's kc_tabs holds one table address per batch key (null for keys whose
+// decode is not KS_OK, never read) and every valid key has a built table;
+// *use = false sends the batch down the per-batch table path (too many keys,
+// a valid key not admitted yet, budget or HBM exhausted).  `force_build`
+// (bv_kc_register) builds the admitted keys even when the batch itself could
+// not use the cache.  hkb/hko: host copies of the key bytes; dkb/dko: device.
+int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
+                  const uint64_t *dko, hipStream_t st, bool *use, bool force_build) {
+  *use = false;
+  ctx->S().kc_decoded = false;
+  if (n_keys == 0 || n_keys > kKcMaxBatchKeys) return BV_OK;
+  if (ctx->S().has_done)  // the slot's pin_small may still feed its previous (async) call
+    HIPCHK(hipEventSynchronize(ctx->S().done), BV_E_LAUNCH, "sync slot");
+  const uint64_t clock = ++ctx->kc_clock;
+  std::vector<int> slot_of(n_keys, -1);
+  std::vector<uint32_t> alias(n_keys);  // a repeated key -> its first index in the batch
+  std::unordered_map<std::string, uint32_t> first;
+  std::vector<uint32_t> unknown, admit;
+  bool blocked = false;
+  uint32_t hits = 0;
+  auto key_of = [&](uint32_t k) { return std::string((const char *)hkb + hko[k], (size_t)(hko[k + 1] - hko[k])); };
+  auto admitted = [&](const std::string &key, uint32_t seen) {
+    return ctx->kc_registered.count(key) != 0 || seen >= ctx->kc_admit;
+  };
+  for (uint32_t k = 0; k < n_keys; k++) {
+    alias[k] = k;
+    if (!key_form_ok(hkb + hko[k], hko[k + 1] - hko[k])) continue;  // malformed by form: no table, no memo
+    const std::string key = key_of(k);
+    auto f = first.emplace(key, k);
+    if (!f.second) {
+      alias[k] = f.first->second;
+      continue;
+    }
+    auto it = ctx->kc_index.find(key);
+    if (it != ctx->kc_index.end()) {
+      slot_of[k] = it->second;
+      ctx->kc_slots[it->second].last_use = clock;
+      hits++;
+      continue;
+    }
+    if (ctx->kc_bad.count(key)) continue;
+    auto s = ctx->kc_seen.find(key);
+    if (s != ctx->kc_seen.end()) {
+      if (admitted(key, ++s->second)) admit.push_back(k);
+      else blocked = true;
+      continue;
+    }
+    unknown.push_back(k);
+  }
+  if (!unknown.empty()) {
+    // classify the new 65-byte keys: k_key_decode on the device (the product
+    // path of elliptic.Unmarshal), one small synchronous copy back
+    HIPCHK(ctx->S().kstatus.ensure(n_keys), BV_E_OOM, "alloc kstatus");
+    HIPCHK(ctx->S().kxy.ensure((uint64_t)n_keys * 64), BV_E_OOM, "alloc kxy");
+    HIPCHK(bvk::key_decode(st, n_keys, dkb, dko, ctx->S().kstatus.as<uint8_t>(), ctx->S().kxy.as<uint32_t>()),
+           BV_E_LAUNCH, "k_key_decode");
+    std::vector<uint8_t> kst(n_keys);
+    HIPCHK(hipMemcpyAsync(kst.data(), ctx->S().kstatus.p, n_keys, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h kst");
+    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+    ctx->S().kc_decoded = true;  // this batch's statuses and points are in the slot (bv_run_keys reuses them)
+    for (uint32_t k : unknown) {
+      const std::string key = key_of(k);
+      if (kst[k] != KS_OK) {
+        memo_insert(ctx->kc_bad, key);
+        continue;
+      }
+      if (ctx->kc_seen.size() >= kKcMemoMax) ctx->kc_seen.clear();
+      ctx->kc_seen[key] = 1;
+      if (admitted(key, 1)) admit.push_back(k);
+      else blocked = true;
+    }
+  }
+  if (blocked && !force_build) return BV_OK;  // a valid key without a table: per-batch path
+
+  uint32_t builds = 0;
+  if (!admit.empty()) {
+    if (!ctx->S().kc_decoded) {  // the admitted keys' points: decode the batch now
+      HIPCHK(ctx->S().kstatus.ensure(n_keys), BV_E_OOM, "alloc kstatus");
+      HIPCHK(ctx->S().kxy.ensure((uint64_t)n_keys * 64), BV_E_OOM, "alloc kxy");
+      HIPCHK(bvk::key_decode(st, n_keys, dkb, dko, ctx->S().kstatus.as<uint8_t>(), ctx->S().kxy.as<uint32_t>()),
+             BV_E_LAUNCH, "k_key_decode");
+      ctx->S().kc_decoded = true;  // ordered before the builds and the verify on `st`; sstream waits (bv_run_keys)
+    }
+    const uint64_t need = (uint64_t)admit.size() * kKcTableBytes;
+    if (need > ctx->kc_budget) return BV_OK;  // this batch's keys alone exceed the budget
+    bool all_registered = true;
+    for (uint32_t k : admit) all_registered = all_registered && ctx->kc_registered.count(key_of(k));
+    // evict least-recently-used tables this batch does not use: unregistered
+    // keys first; a registered key's table only to make room for registered keys
+    while (ctx->kc_bytes + need > ctx->kc_budget) {
+      int victim = -1;
+      bool victim_reg = true;
+      for (size_t i = 0; i < ctx->kc_slots.size(); i++) {
+        const auto &s = ctx->kc_slots[i];
+        if (s.free || !s.table || s.last_use == clock) continue;
+        const bool reg = ctx->kc_registered.count(s.bytes) != 0;
+        if (reg && !all_registered) continue;
+        if (victim < 0 || (victim_reg && !reg) ||
+            (victim_reg == reg && s.last_use < ctx->kc_slots[victim].last_use)) {
+          victim = (int)i;
+          victim_reg = reg;
+        }
+      }
+      if (victim < 0) return BV_OK;
+      if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // no call in flight may still read it
+      auto &s = ctx->kc_slots[victim];
+      HIPCHK(hipFree(s.table), BV_E_LAUNCH, "free cached table");
+      ctx->kc_index.erase(s.bytes);
+      s = KcSlot{};
+      s.free = true;
+      ctx->kc_bytes -= kKcTableBytes;
+    }
+    // Allocate this call's slots.  They are indexed only after their build
+    // is enqueued; `rollback` frees them on any failure.
+    std::vector<int> fresh;
+    bool launched = false;
+    auto rollback = [&]() {
+      if (launched) (void)hipStreamSynchronize(st);  // enqueued builds may still write the tables
+      for (int si : fresh) {
+        auto &s = ctx->kc_slots[si];
+        if (s.table) {
+          (void)hipFree(s.table);
+          ctx->kc_bytes -= kKcTableBytes;
+        }
+        s = KcSlot{};
+        s.free = true;
+      }
+      (void)hipGetLastError();
+    };
+    for (uint32_t k : admit) {
+      int si = -1;
+      for (size_t i = 0; i < ctx->kc_slots.size(); i++)
+        if (ctx->kc_slots[i].free) {
+          si = (int)i;
+          break;
+        }
+      if (si < 0) {
+        ctx->kc_slots.emplace_back();
+        si = (int)ctx->kc_slots.size() - 1;
+      }
+      auto &s = ctx->kc_slots[si];
+      s = KcSlot{};
+      s.bytes = key_of(k);
+      s.last_use = clock;
+      fresh.push_back(si);
+      if (kc_table_alloc(ctx, &s.table) != hipSuccess) {
+        s.table = nullptr;
+        rollback();
+        return BV_OK;  // HBM exhausted: per-batch path for this call, nothing indexed
+      }
+      ctx->kc_bytes += kKcTableBytes;
+      slot_of[k] = si;
+    }
+    // build the new tables, kKcBuildGroup keys per launch
+    auto fail = [&](int code, const char *what, hipError_t e) {
+      rollback();
+      return bv_fail(ctx, code, what, e);
+    };
+    const uint32_t G = std::min<uint32_t>(kKcBuildGroup, (uint32_t)admit.size());
+    hipError_t e;
+    if ((e = ctx->kc_kxy.ensure((uint64_t)G * 64)) != hipSuccess ||
+        (e = ctx->kc_btabs.ensure((uint64_t)G * 8)) != hipSuccess ||
+        (e = ctx->S().bases_jac.ensure((uint64_t)G * kKcBases * 96)) != hipSuccess ||
+        (e = ctx->S().key_sub.ensure((uint64_t)G * kKcSubBytes)) != hipSuccess ||
+        (e = ctx->S().key_pscr.ensure((uint64_t)G * bvk::kc_pscr_bytes())) != hipSuccess ||
+        (e = ctx->S().pin_small.ensure(4096)) != hipSuccess)
+      return fail(BV_E_OOM, "alloc KC build scratch", e);
+    for (size_t g0 = 0; g0 < admit.size(); g0 += G) {
+      const uint32_t n = (uint32_t)std::min<size_t>(G, admit.size() - g0);
+      uint64_t *tabs = (uint64_t *)ctx->S().pin_small.p;
+      if (launched && (e = hipStreamSynchronize(st)) != hipSuccess) return fail(BV_E_LAUNCH, "sync", e);  // pin_small reuse
+      for (uint32_t i = 0; i < n; i++) {
+        const uint32_t k = admit[g0 + i];
+        if ((e = hipMemcpyAsync(ctx->kc_kxy.as<uint8_t>() + 64ull * i, ctx->S().kxy.as<uint8_t>() + 64ull * k, 64,
+                                hipMemcpyDeviceToDevice, st)) != hipSuccess)
+          return fail(BV_E_LAUNCH, "gather kxy", e);
+        tabs[i] = (uint64_t)(uintptr_t)ctx->kc_slots[slot_of[k]].table;
+      }
+      if ((e = hipMemcpyAsync(ctx->kc_btabs.p, tabs, n * 8ull, hipMemcpyHostToDevice, st)) != hipSuccess)
+        return fail(BV_E_LAUNCH, "h2d tabs", e);
+      launched = true;
+      e = ++ctx->kc_build_calls == (uint64_t)ctx->kc_fail_build
+              ? hipErrorLaunchFailure  // injected
+              : bvk::build_kc(st, n, ctx->kc_kxy.as<uint32_t>(), nullptr, ctx->S().bases_jac.as<uint32_t>(),
+                              ctx->S().key_sub.as<uint32_t>(), ctx->S().key_pscr.as<uint32_t>(),
+                              ctx->kc_btabs.as<uint64_t>());
+      if (e != hipSuccess) return fail(BV_E_LAUNCH, "KC key tables", e);
+      builds += n;
+    }
+    // every build is enqueued on `st`, ahead of this call's verify and of
+    // every later call (they order after this one): index the slots now
+    for (int si : fresh) {
+      ctx->kc_index[ctx->kc_slots[si].bytes] = si;
+      ctx->kc_seen.erase(ctx->kc_slots[si].bytes);
+    }
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return bv_fail(ctx, BV_E_LAUNCH, "sync", e);  // pin_small
+  }
+  for (uint32_t k = 0; k < n_keys; k++)
+    if (alias[k] != k) slot_of[k] = slot_of[alias[k]];
+  ctx->timing.kc_hits = hits;
+  ctx->timing.kc_builds = builds;
+  ctx->timing.kc_keys = (uint32_t)ctx->kc_index.size();
+  if (blocked) return BV_OK;  // force_build: the tables are built, this batch still takes the per-batch path
+  // per-batch array: the table address of every batch key (null: no table;
+  // only keys whose batch decode is not KS_OK have none, and theirs is never read)
+  HIPCHK(ctx->S().pin_small.ensure((uint64_t)n_keys * 8 + 64), BV_E_OOM, "alloc pinned");
+  uint64_t *tabs = (uint64_t *)ctx->S().pin_small.p;
+  for (uint32_t k = 0; k < n_keys; k++)
+    tabs[k] = slot_of[k] >= 0 ? (uint64_t)(uintptr_t)ctx->kc_slots[slot_of[k]].table : 0;
+  HIPCHK(ctx->S().kc_tabs.ensure((uint64_t)n_keys * 8), BV_E_OOM, "alloc kc tabs");
+  HIPCHK(hipMemcpyAsync(ctx->S().kc_tabs.p, tabs, n_keys * 8ull, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d tabs");
+  *use = true;
+  return BV_OK;
+}
+
+extern "C" int bv_kc_register(bv_ctx *ctx, uint32_t n_keys, const uint8_t *key_bytes, const uint64_t *key_off) {
+  if (!ctx || (n_keys && !key_off)) return BV_E_ARGS;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!(ctx->flags & BV_F_KEY_CACHE)) return bv_fail(ctx, BV_E_ARGS, "bv_kc_register needs BV_F_KEY_CACHE");
+  if (n_keys > kKcMaxBatchKeys) return bv_fail(ctx, BV_E_ARGS, "more than 4096 registered keys");
+  if (n_keys && key_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "key_off[0] != 0");
+  for (uint32_t k = 0; k < n_keys; k++)
+    if (key_off[k] > key_off[k + 1]) return bv_fail(ctx, BV_E_ARGS, "key_off not monotone");
+  const uint64_t len = n_keys ? key_off[n_keys] : 0;
+  if (len && !key_bytes) return bv_fail(ctx, BV_E_ARGS, "null key bytes");
+  HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  ctx->kc_registered.clear();
+  for (uint32_t k = 0; k < n_keys; k++)
+    if (key_form_ok(key_bytes + key_off[k], key_off[k + 1] - key_off[k]))
+      ctx->kc_registered.emplace((const char *)key_bytes + key_off[k], (size_t)(key_off[k + 1] - key_off[k]));
+  ctx->timing = bv_timing{};
+  if (ctx->kc_registered.empty()) return BV_OK;
+  // the keys on the device (k_key_decode reads 64 bytes past the last one)
+  if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;
+  hipStream_t st = ctx->stream;
+  const size_t o_off = align256(len + 64), total = o_off + align256((n_keys + 1) * 8ull);
+  HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
+  HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
+  uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
+  if (len) memcpy(pin, key_bytes, len);
+  memset(pin + len, 0, 64);
+  memcpy(pin + o_off, key_off, (n_keys + 1) * 8ull);
+  HIPCHK(hipMemcpyAsync(dev, pin, total, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d keys");
+  ctx->cur = (ctx->cur + 1) % bv_ctx::kSlots;
+  bool use = false;
+  int rc = bv_kc_prepare(ctx, n_keys, key_bytes, key_off, dev, (const uint64_t *)(dev + o_off), st, &use, true);
+  if (rc != BV_OK) return bv_drain(ctx, st, rc);
+  rc = bv_mark_done(ctx, st);
+  if (rc != BV_OK) return bv_drain(ctx, st, rc);
+  HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+  return BV_OK;
+}

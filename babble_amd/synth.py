@@ -120,10 +120,12 @@ def event_fields(n_events: int, n_creators: int = 64, seed: int = 2, n_tx: int =
 
 def c3_chunk(idx: int, n: int = 1_000_000, n_creators: int = 64):
     """Chunk `idx` of the C3 workload (10^8 events, seed 3, 64
-    creators, streamed in chunks): seed 3 + idx; about one item in 10^4
-    (seeded) gets one r bit flipped, so the exact accept bitmask is known by
-    construction.  Returns (batch, sorted indices of the flipped items)."""
-    b = events(n, n_creators=n_creators, seed=3 + idx)
+    creators, streamed in chunks): the same 64 creators (seed 3) in every
+    chunk, chunk idx's events timestamped after chunk idx-1's (one stream of
+    10^8 distinct bodies); about one item in 10^4 (seeded by idx) gets one r
+    bit flipped, so the exact accept bitmask is known by construction.
+    Returns (batch, sorted indices of the flipped items)."""
+    b = events(n, n_creators=n_creators, seed=3, ts0=TS0 + idx * n)
     rng = np.random.default_rng(1000 + idx)
     bad = np.sort(rng.choice(n, max(1, n // 10_000), replace=False))
     b.r_be[bad, int(rng.integers(0, 32))] ^= np.uint8(1 << int(rng.integers(0, 8)))

@@ -217,6 +217,15 @@ class Verifier:
                                              out.ctypes.data))
         return out.tobytes()
 
+    def register_keys(self, pubkeys: Sequence[bytes]) -> None:
+        """bv_kc_register: the key cache's registered keys (the PeerSet's
+        PubKeyBytes) replace the previous set; their tables are built now."""
+        pubkeys = [bytes(k) for k in pubkeys]
+        buf = np.frombuffer(b"".join(pubkeys) or b"\0", np.uint8).copy()
+        off = np.zeros(len(pubkeys) + 1, np.uint64)
+        off[1:] = np.cumsum([len(k) for k in pubkeys], dtype=np.uint64)
+        self._check(self._L.bv_kc_register(self._ctx, len(pubkeys), buf.ctypes.data, off.ctypes.data))
+
     def timing(self) -> dict:
         t = native.BvTiming()
         self._check(self._L.bv_get_timing(self._ctx, ctypes.byref(t)))

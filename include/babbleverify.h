@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define BV_ABI_VERSION 4
+#define BV_ABI_VERSION 5
 
 /* Return codes (per-item outcomes are never errors; they go to status[]). */
 #define BV_OK 0
@@ -65,11 +65,16 @@ extern "C" {
 #define BV_F_KEY_CACHE 1u /* keep per-key tables in HBM across calls, keyed by
                              the raw pubkey bytes (validator sets are stable,
                              peers/peer_set.go): 22-bit signed-window GLV
-                             tables, 805 MB per valid key, built on first use,
-                             LRU-evicted past the cache budget (env
-                             BV_KEY_CACHE_GB, default 96).  Malformed keys are
-                             never given a table.  Off by default: tables are
-                             then rebuilt for every batch.                     */
+                             tables, 805 MB per valid key.  A key gets a table
+                             when it is registered (bv_kc_register: the
+                             PeerSet) or once it has been seen in 2 batches
+                             (env BV_KC_ADMIT); tables are LRU-evicted past
+                             the cache budget (env BV_KEY_CACHE_GB, default
+                             96), registered keys only for other registered
+                             keys.  Malformed keys are never given a table;
+                             a batch with a valid key that has no table takes
+                             the per-batch table path.  Off by default: tables
+                             are then rebuilt for every batch.                 */
 #define BV_F_K8 2u        /* per-batch tables: never use the 12-bit tables
                              (2.75 MiB per key); 8-bit only (512 KiB per key) */
 #define BV_F_KNOWN (BV_F_KEY_CACHE | BV_F_K8)
@@ -118,7 +123,7 @@ typedef struct {
                          last input copy enqueued                               */
   float ms_host_out;  /* host: results copied out after the device finished    */
   uint32_t key_path; /* 0: per-lane generic path; 8 / 12: per-batch K8 / K12
-                        key tables; 20: key-cache (KC) tables                   */
+                        key tables; 22: key-cache (KC) tables                   */
   uint32_t kc_hits;   /* batch keys found in the key cache                      */
   uint32_t kc_builds; /* key tables built into the cache by this call           */
   uint32_t kc_keys;   /* keys held by the cache after the call                  */
@@ -130,6 +135,15 @@ int bv_abi_version(void);
 int bv_create(bv_ctx **out, int device, uint32_t flags);
 void bv_destroy(bv_ctx *ctx);
 const char *bv_last_error(const bv_ctx *ctx);
+
+/* Key cache (BV_F_KEY_CACHE contexts only): set the registered keys — the
+ * PeerSet's PubKeyBytes (src/peers/peer_set.go; Babble calls this where the
+ * peer set changes) — replacing the previous set, and build the tables of the
+ * registered valid keys that have none, before returning.  Registered tables
+ * are never evicted for unregistered keys.  BV_E_ARGS on a ctx without the
+ * cache or more than 4096 keys.  bv_get_timing's kc_builds / kc_keys report
+ * what was built. */
+int bv_kc_register(bv_ctx *ctx, uint32_t n_keys, const uint8_t *key_bytes, const uint64_t *key_off);
 
 /* Synchronous batch verify from host buffers (the cgo entry point).  Any
  * input array or result buffer that lies in memory from bv_host_alloc is

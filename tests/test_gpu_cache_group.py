@@ -43,36 +43,49 @@ def verifier_default():
     v.close()
 
 
-def test_key_cache_cold_then_warm(cached):
-    """First call builds a KC table per valid key (malformed keys get none);
-    the second call hits every key and builds nothing; both bit-exact."""
+def valid_keys(b):
+    return [b.key(k) for k in range(b.n_keys) if gs.Unmarshal(b.key(k)) is not None]
+
+
+def test_key_cache_admission_cold_then_warm(cached):
+    """Admission: an unregistered valid key gets a KC table
+    once it has been seen in 2 batches.  First call: per-batch tables, nothing
+    built; second: a table per distinct valid key (malformed keys get none);
+    third: every valid key hits and nothing is built.  All bit-exact."""
     b = synth.adversarial(30_000, seed=41, n_creators=6, scale_per_million=MIX)
     st = oracle_check(cached.verify(b), b)
     t = cached.timing()
-    assert t["key_path"] == 22
-    n_valid = sum(1 for k in range(b.n_keys) if gs.Unmarshal(b.key(k)) is not None)
-    assert 0 < n_valid < b.n_keys  # the mix carries malformed keys
-    assert t["kc_builds"] == n_valid and t["kc_hits"] == 0
+    assert t["key_path"] in (8, 12) and t["kc_builds"] == 0
+    n_valid = len(set(valid_keys(b)))
+    assert 0 < n_valid < b.n_keys  # the mix carries malformed keys (and one repeated valid key)
     assert set(np.unique(st)) == {0, 1, 2, 3}
     oracle_check(cached.verify(b), b)
     t = cached.timing()
-    assert t["kc_builds"] == 0 and t["kc_hits"] == b.n_keys and t["key_path"] == 22
+    assert t["key_path"] == 22 and t["kc_builds"] == n_valid and t["kc_hits"] == 0
+    oracle_check(cached.verify(b), b)
+    t = cached.timing()
+    assert t["kc_builds"] == 0 and t["kc_hits"] == n_valid and t["key_path"] == 22
 
 
 def test_key_cache_small_batches(cached):
-    """Latency-sized batches (1, 100, 1000 = SyncLimit, config.go:44) on the
-    cached tables: same results as the oracle."""
+    """Latency-sized batches (1, 100, 1000 = SyncLimit, config.go:44) of
+    registered creators take the cached tables on the first call; same
+    results as the oracle."""
     for n in (1, 100, 1000):
         b = synth.events(n, n_creators=4, seed=100 + n)
+        cached.register_keys([b.key(k) for k in range(b.n_keys)])
+        assert cached.timing()["kc_builds"] == b.n_keys
         oracle_check(cached.verify(b), b)
-        assert cached.timing()["key_path"] == 22
+        t = cached.timing()
+        assert t["key_path"] == 22 and t["kc_builds"] == 0 and t["kc_hits"] == b.n_keys
 
 
 def test_key_cache_device_entry(cached):
     b = synth.adversarial(20_000, seed=42, n_creators=6, scale_per_million=MIX)
     d = cached.to_device(b)
-    cached.verify_device(d)
-    oracle_check(d.result(), b)
+    for call in range(2):
+        cached.verify_device(d)
+        oracle_check(d.result(), b)
     assert cached.timing()["key_path"] == 22
 
 
@@ -82,6 +95,7 @@ def test_key_cache_eviction(monkeypatch):
     from babble_amd.verifier import Verifier
 
     monkeypatch.setenv("BV_KEY_CACHE_GB", "2.5")
+    monkeypatch.setenv("BV_KC_ADMIT", "1")
     v = Verifier(device=0, flags=native.F_KEY_CACHE)
     try:
         a = synth.events(3000, n_creators=2, seed=51)
@@ -92,6 +106,91 @@ def test_key_cache_eviction(monkeypatch):
         t = v.timing()
         assert t["kc_builds"] == 2 and t["kc_keys"] <= 3
         oracle_check(v.verify(a), a)
+    finally:
+        v.close()
+
+
+@pytest.mark.parametrize("fail", ["alloc:3", "build:2"])
+def test_key_cache_failure_leaves_no_unbuilt_slot(monkeypatch, fail):
+    """a KC table allocation (the 3rd of a 64-key miss batch)
+    or a build launch (the 2nd group of 8 keys) fails part-way.  The call
+    either takes the per-batch path (allocation: results exact) or returns
+    an error (launch); either way nothing is indexed, so the NEXT call on the
+    same keys builds every table afresh and equals the oracle bit for bit,
+    and the call after that hits all 64."""
+    from babble_amd.verifier import Verifier
+
+    monkeypatch.setenv("BV_KC_ADMIT", "1")
+    monkeypatch.setenv("BV_KC_FAIL", fail)
+    b = synth.adversarial(40_000, seed=44, n_creators=64, scale_per_million=MIX)
+    n_valid = len(set(valid_keys(b)))
+    v = Verifier(device=0, flags=native.F_KEY_CACHE)
+    try:
+        if fail.startswith("alloc"):
+            oracle_check(v.verify(b), b)
+            t = v.timing()
+            assert t["key_path"] == 12 and t["kc_keys"] == 0 and t["kc_builds"] == 0
+        else:
+            with pytest.raises(native.BvError):
+                v.verify(b)
+        oracle_check(v.verify(b), b)
+        t = v.timing()
+        assert t["key_path"] == 22 and t["kc_builds"] == n_valid and t["kc_keys"] == n_valid
+        d = v.to_device(b)
+        v.verify_device(d)
+        oracle_check(d.result(), b)
+        t = v.timing()
+        assert t["kc_hits"] == n_valid and t["kc_builds"] == 0
+    finally:
+        v.close()
+
+
+def _rss_mb() -> float:
+    with open("/proc/self/status") as f:
+        for line in f:
+            if line.startswith("VmRSS:"):
+                return int(line.split()[1]) / 1024
+    return 0.0
+
+
+def test_key_cache_admission_control():
+    """with the 64 validators registered (bv_kc_register, the
+    PeerSet), 10k distinct malformed 65-byte keys and 1k fresh valid keys
+    (each seen once, as a flood of join requests would be) go through the
+    same ctx: every result equals the oracle, no table is built for them,
+    the 64 registered tables stay resident (the next validator batch hits all
+    64 and builds nothing) and host memory stays bounded."""
+    from babble_amd.batch import PackedBatch
+    from babble_amd.verifier import Verifier
+
+    vb = synth.events(20_000, n_creators=64, seed=2)
+    v = Verifier(device=0, flags=native.F_KEY_CACHE)
+    try:
+        v.register_keys([vb.key(k) for k in range(vb.n_keys)])
+        assert v.timing()["kc_builds"] == 64 and v.timing()["kc_keys"] == 64
+        rng = np.random.default_rng(123)
+        rss0 = None
+        for j in range(5):  # 5 x 2000 distinct off-curve keys
+            fb = synth.events(2000, n_creators=4, seed=300 + j)
+            bad = np.concatenate([np.full((2000, 1), 4, np.uint8), rng.integers(0, 256, (2000, 64), dtype=np.uint8)],
+                                 axis=1)
+            mb = PackedBatch(fb.msg_bytes, fb.msg_off, bad.reshape(-1).copy(),
+                             np.arange(2001, dtype=np.uint64) * 65, fb.item_msg, np.arange(2000, dtype=np.uint32),
+                             fb.r_be, fb.s_be, fb.pre)
+            st = oracle_check(v.verify(mb), mb)
+            assert np.all(st == native.REF_PANIC)
+            assert v.timing()["key_path"] == 22 and v.timing()["kc_builds"] == 0
+            if rss0 is None:
+                rss0 = _rss_mb()
+        for j in range(4):  # 4 x 250 fresh valid creators, one batch each (16 events per creator)
+            fb = synth.events(4000, n_creators=250, seed=400 + j)
+            oracle_check(v.verify(fb), fb)
+            t = v.timing()
+            assert t["kc_builds"] == 0 and t["key_path"] == 8
+        assert _rss_mb() - rss0 < 64, "host memory grew with attacker-chosen keys"
+        oracle_check(v.verify(vb), vb)
+        t = v.timing()
+        assert t["kc_hits"] == 64 and t["kc_builds"] == 0 and t["kc_keys"] == 64 and t["key_path"] == 22
     finally:
         v.close()
 
@@ -256,6 +355,8 @@ def test_c5_full_size_check_block(cached, verifier_default, key_cache):
     bad = rng.choice(b.n_items, size=b.n_items // 20, replace=False)
     b.s_be[bad, 7] ^= 0x40
     v = cached if key_cache else verifier_default
+    if key_cache:  # the validator set is registered, as CheckBlock's PeerSet is known
+        v.register_keys([b.key(k) for k in range(b.n_keys)])
     res = v.verify(b)
     assert v.timing()["key_path"] == (22 if key_cache else 12)
     st = oracle_check(res, b)
