@@ -87,7 +87,75 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="headline only (profiler passes)")
     ap.add_argument("--inflight", type=int, default=2, choices=(1, 2),
                     help="batches in flight: consecutive steps rotate over this many streams and result buffers")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rank plumbing only, on CPU over gloo: no GPU, no verification (tests)")
     return ap.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) outside torch.distributed.run: start the N ranks as
+    ONE child process (python -m torch.distributed.run, one rank per GPU,
+    rendezvous on 127.0.0.1) before this process imports torch or touches a
+    GPU, and return its exit code.  Ranks that find fewer than N GPUs exit
+    non-zero without printing a line, so the launcher fails too."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def check_rank_env(args) -> int:
+    """Inside a rank: the world must be exactly --gpus ranks and every rank
+    needs its own GPU.  Returns the world size or exits non-zero."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to print a line", file=sys.stderr)
+        raise SystemExit(3)
+    if not args.dry_run:
+        import torch
+
+        if torch.cuda.device_count() < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+            raise SystemExit(4)
+    return world
+
+
+def dry_run(args, world: int, rank: int) -> None:
+    """The N-rank plumbing on CPU (gloo): each rank's expected accept bitmask
+    of its shard, all-gathered and checked as the GPU run checks its own;
+    rank 0 prints a line with value null."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    words = expected_words(rank, args.events)
+    t0 = time.perf_counter()
+    mine = torch.from_numpy(words.view(np.int64).copy())
+    if world > 1:
+        got = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(got, mine)
+    else:
+        got = [mine]
+    for q in range(world):
+        if not np.array_equal(got[q].numpy().view(np.uint64), expected_words(q, args.events)):
+            raise SystemExit(f"rank {rank}: gathered bitmask of rank {q} differs")
+    el = time.perf_counter() - t0
+    if rank == 0:
+        print(json.dumps({"metric": "ECDSA event verifies/sec", "value": None, "unit": "verifies/s", "n_gpus": world,
+                          "steps": 0, "warmup": 0, "ms_per_step": el * 1e3, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "dry run (no GPU)",
+                          "dry_run": True, "config": {"workload": "launcher plumbing only",
+                                                      "parallelism": f"shard{world}" if world > 1 else "single"}}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def cpu_threads() -> int:
@@ -231,9 +299,13 @@ def mean(xs, k):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args))  # before torch is imported or a GPU touched
+    world = check_rank_env(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     import numpy as np
     import torch
 
@@ -352,7 +424,9 @@ def main():
             "data": "synthetic (seeded DRBG keys, OpenSSL-signed canonical EventBody JSON; resident in HBM)",
             "config": {
                 "workload": "C2: VerifyBatch of 1M signed Events per GPU (64 creators, 1x64-B tx, ~446-B bodies); "
-                            "per-key tables rebuilt every step",
+                            "per-key tables rebuilt every step"
+                            + ("; N GPUs = C2 weak scaling (1M events per GPU per step, bitmasks all-gathered "
+                               "over RCCL), not C3's 10^8 (tests/test_gpu_c3.py)" if world > 1 else ""),
                 "events_per_gpu": args.events,
                 "creators": args.creators,
                 "parallelism": f"shard{world}" if world > 1 else "single",

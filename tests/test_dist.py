@@ -1,6 +1,7 @@
 """Multi-rank path on CPU (gloo, world size 2 and 3): each rank verifies its
 64-aligned shard (host build of the device code, tests/emu) and the accept
 bitmasks are all-gathered; the global bitmask equals the oracle's."""
+import json
 import os
 import socket
 
@@ -161,3 +162,38 @@ def test_merge_bits_shifts():
         pk = np.packbits(ok, bitorder="little")
         want = np.concatenate([pk, np.zeros((-len(pk)) % 8, np.uint8)]).view(np.uint64)
         assert np.array_equal(shard.merge_bits(parts, bounds), want)
+
+
+def _bench(args, env=None, timeout=240):
+    import subprocess
+    import sys
+
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=e, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_bench_launcher_starts_n_ranks_dry_run():
+    """`bench.py --gpus 2` outside torch.distributed.run starts
+    two ranks itself (one child torch.distributed.run, rendezvous on
+    127.0.0.1); in gloo dry-run mode rank 0 prints ONE line with n_gpus 2
+    after the all-gathered bitmasks check out."""
+    p = _bench(["--gpus", "2", "--dry-run", "--events", "5000"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["dry_run"] and line["config"]["parallelism"] == "shard2"
+
+
+def test_bench_rank_refuses_world_mismatch():
+    """A rank whose WORLD_SIZE differs from --gpus exits non-zero and prints
+    no line (never a one-GPU line labelled as N)."""
+    p = _bench(["--gpus", "2", "--dry-run", "--events", "5000"], env={"WORLD_SIZE": "1", "RANK": "0",
+                                                                       "LOCAL_RANK": "0"})
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

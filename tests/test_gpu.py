@@ -319,3 +319,21 @@ def test_shared_context_threads(verifier):
 def test_native_library_is_the_one_loaded():
     maps = open("/proc/self/maps").read()
     assert native.LIB_PATH in maps
+
+
+def test_bench_gpus_beyond_the_box_fails():
+    """`bench.py --gpus N` with fewer than N GPUs exits
+    non-zero without printing a line (it used to print a one-GPU line)."""
+    import subprocess
+    import sys
+
+    import torch
+
+    n = torch.cuda.device_count() + 1
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--steps", "1",
+                        "--warmup", "0", "--events", "4096", "--no-cpu", "--no-extras"], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
