@@ -61,11 +61,10 @@ constexpr uint32_t kRgWords = 33;              // R_G words per item (XYZZ + inf
 #endif
 constexpr bool kFusedKc = BV_FUSED_KC;         // key cache: one fused verify kernel (k_verify_gq)
 constexpr size_t kChunk = 16ull << 20;         // host-entry staging / PCIe chunk
-// message bytes hashed (and their items verified) per chunk: 64 MB keeps
-// each chunk's verify launches at full occupancy (1M C2 events from pinned
-// arrays, same box: 16 / 64 / 128 MB = 15.0-15.7 / 11.0 / 10.9-11.0 ms per
-// call; pageable 15.2 / 12.0 ms, tools/host_prof.py)
-constexpr size_t kMsgChunk = 64ull << 20;
+// message bytes hashed (and their items verified) per chunk: ctx->host_msg_chunk,
+// 64 MB by default — it keeps each chunk's verify launches at full occupancy
+// (1M C2 events from pinned arrays, same box: 16 / 64 / 128 MB = 15.0-15.7 /
+// 11.0 / 10.9-11.0 ms per call; pageable 15.2 / 12.0 ms, tools/host_prof.py)
 // host batches whose whole staging layout is at most this cross PCIe as ONE
 // copy: each extra small H2D costs ~20 us of DMA latency on a lone call
 constexpr size_t kSmallStage = 1ull << 20;
@@ -393,6 +392,14 @@ static int create_impl(bv_ctx *ctx) {
   const unsigned hw = std::thread::hardware_concurrency();
   ctx->pool = new CopyPool((int)std::min<unsigned>(hw ? hw - 1 : 0, 7));
   if (ctx->flags & BV_F_KEY_CACHE) bv_kc_init(ctx);
+  // A/B knobs (bv_internal.h), read once here
+  if (const char *s = getenv("BV_HOST_CHUNK_MB")) ctx->host_msg_chunk = (uint64_t)(std::max(1.0, atof(s)) * (1 << 20));
+  if (const char *s = getenv("BV_EV_CHUNK_MB")) {
+    const double mb = atof(s);
+    ctx->ev_chunk = mb <= 0 ? 0 : std::max<uint64_t>(1, (uint64_t)(mb * (1 << 20)));  // >= 256 events a chunk anyway
+  }
+  if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
+  if (const char *s = getenv("BV_EV_DAG_DEVICE")) ctx->dag_on_device = atoi(s) != 0;
   return BV_OK;
 }
 
@@ -953,8 +960,7 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order");
   HIPCHK(hipEventRecord(ctx->S().ev[E_HASH0], st), BV_E_LAUNCH, "event");
   HIPCHK(hipEventRecord(ctx->S().ev[E_FORK], st), BV_E_LAUNCH, "event");
-  const char *env_chunk = getenv("BV_HOST_CHUNK_MB");  // A/B knob
-  const uint64_t msg_chunk = env_chunk ? std::max<uint64_t>(1, (uint64_t)(atof(env_chunk) * (1 << 20))) : kMsgChunk;
+  const uint64_t msg_chunk = ctx->host_msg_chunk;
   uint64_t m0 = 0;
   while (m0 < n_msgs) {
     // messages [m0, m1) holding about msg_chunk bytes (at least one message)

@@ -89,6 +89,123 @@ int validate(bv_ctx *ctx, const bv_event_batch *b) {
 
 static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *res);
 
+// A batch with in-batch parents (a SyncResponse, core.go:214-245): the host
+// builds and hashes the bodies in topological order (hostdag.cpp) while the
+// device runs key decode, the key tables and s^-1 on the keys / s / pre that
+// crossed PCIe first; then only the 32-byte digests cross and the verify
+// kernels run.  The bodies never reach the device.
+static int verify_events_dag_host(bv_ctx *ctx, const bv_event_batch *eb, bv_result *res,
+                                  const std::vector<uint32_t> &order, const std::vector<uint32_t> &level_off,
+                                  bv_host_call &call) {
+  const uint64_t n = eb->n_events;
+  hipStream_t st = ctx->stream;
+  const uint64_t key_len = eb->key_off[eb->n_keys];
+  // staging layout: keys | s, pre | r, creators | digests
+  size_t total = 0;
+  auto at = [&](size_t bytes, size_t pad = 0) {
+    const size_t o = total;
+    total += align256(bytes + pad);
+    return o;
+  };
+  const size_t o_koff = at((eb->n_keys + 1) * 8ull), o_kb = at(key_len, 64), keys_end = total;
+  const size_t o_s = at(n * 32), o_pre = at(eb->pre ? n : 0), s_end = total;
+  const size_t o_r = at(n * 32), o_cr = at(n * 4), small_end = total;
+  const size_t o_dig = at(n * 32);
+  if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // previous calls' work buffers / staging
+  HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
+  HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
+  HIPCHK(ctx->ev_iota.ensure(n * 4), BV_E_OOM, "alloc item index");
+  uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
+  hipStream_t cs = bv_copy_stream(ctx);
+  if (!cs) return bv_fail(ctx, BV_E_NODEVICE, "copy stream");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_CALL], cs), BV_E_LAUNCH, "event");
+  auto put = [&](size_t o, const void *src, size_t bytes) {
+    if (bytes) memcpy(pin + o, src, bytes);
+  };
+  auto h2d = [&](size_t a, size_t z) -> int {
+    HIPCHK(hipMemcpyAsync(dev + a, pin + a, z - a, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d");
+    return BV_OK;
+  };
+  put(o_koff, eb->key_off, (eb->n_keys + 1) * 8ull);
+  put(o_kb, eb->key_bytes, key_len);
+  memset(pin + o_kb + key_len, 0, 64);
+  int rc = h2d(0, keys_end);
+  if (rc != BV_OK) return rc;
+  HIPCHK(hipEventRecord(ctx->S().ev[E_KREADY], cs), BV_E_LAUNCH, "event");
+  bv_batch vb = {};
+  vb.n_msgs = n;
+  vb.n_keys = eb->n_keys;
+  vb.key_bytes = dev + o_kb;
+  vb.key_off = (const uint64_t *)(dev + o_koff);
+  vb.n_items = n;
+  vb.item_msg = ctx->ev_iota.as<uint32_t>();
+  vb.item_key = (const uint32_t *)(dev + o_cr);
+  vb.r_be = dev + o_r;
+  vb.s_be = dev + o_s;
+  vb.pre = eb->pre ? dev + o_pre : nullptr;
+  bool kc = false;
+  if (ctx->flags & BV_F_KEY_CACHE) {
+    HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_KREADY], 0), BV_E_LAUNCH, "join");
+    rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, vb.key_bytes, vb.key_off, st, &kc);
+    if (rc != BV_OK) return rc;
+  }
+  put(o_s, eb->s_be, n * 32);
+  if (eb->pre) put(o_pre, eb->pre, n);
+  if ((rc = h2d(keys_end, s_end)) != BV_OK) return rc;
+  HIPCHK(hipEventRecord(ctx->S().ev[E_SREADY], cs), BV_E_LAUNCH, "event");
+  rc = bv_run_keys(ctx, &vb, ctx->S().ev[E_KREADY], ctx->S().ev[E_SREADY], kc);
+  if (rc != BV_OK) return rc;
+  put(o_r, eb->r_be, n * 32);
+  put(o_cr, eb->creator, n * 4);
+  if ((rc = h2d(s_end, small_end)) != BV_OK) return rc;
+  HIPCHK(hipEventRecord(ctx->S().ev[E_SMALL], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SMALL], 0), BV_E_LAUNCH, "join");
+  HIPCHK(bvk::iota(st, n, ctx->ev_iota.as<uint32_t>()), BV_E_LAUNCH, "k_iota");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_FORK], st), BV_E_LAUNCH, "event");
+
+  // the host's part, overlapping the device's key / s^-1 work
+  const HostParFor pf = [ctx](uint64_t cnt, uint64_t grain, const std::function<void(uint64_t, uint64_t)> &fn) {
+    ctx->pool->parallel_for(cnt, grain, [&fn](uint64_t lo, uint64_t hi) {
+      fn(lo, hi);
+      return true;
+    });
+  };
+  bv_host_dag_hash(*eb, order.data(), level_off.data(), (uint32_t)level_off.size() - 1, pf, ctx->dag_scratch,
+                   pin + o_dig);
+  if ((rc = h2d(o_dig, o_dig + n * 32)) != BV_OK) return rc;
+  HIPCHK(hipEventRecord(ctx->S().ev[E_STAGED], cs), BV_E_LAUNCH, "event");
+  call.ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call.t0).count();
+  HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_STAGED], 0), BV_E_LAUNCH, "join digests");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_SHA], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");
+  bv_item_pipe pipe{ctx, &vb, {}, st, kc};
+  rc = bv_out_bufs(ctx, &vb, nullptr, nullptr, nullptr, true, &pipe.o);
+  if (rc != BV_OK) return rc;
+  pipe.o.dig = (uint32_t *)(dev + o_dig);
+  rc = pipe.finish();
+  if (rc != BV_OK) return rc;
+  const size_t o_bits = align256(n);
+  HIPCHK(ctx->pin_out.ensure(o_bits + align256((n + 63) / 64 * 8) + 256), BV_E_OOM, "alloc pinned results");
+  uint8_t *pout = (uint8_t *)ctx->pin_out.p;
+  call.pout = pout;
+  call.o_st = 0;
+  call.o_bits = o_bits;
+  call.direct_hash = true;  // the digests are already on the host: copied below
+  call.direct_status = res && bv_is_pinned(res->status, n);
+  HIPCHK(hipMemcpyAsync(call.direct_status ? res->status : pout, pipe.o.status, n, hipMemcpyDeviceToHost, st),
+         BV_E_LAUNCH, "d2h status");
+  HIPCHK(hipMemcpyAsync(pout + o_bits, pipe.o.bits, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
+         "d2h bits");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_OUT], st), BV_E_LAUNCH, "event");
+  rc = bv_mark_done(ctx, st);
+  if (rc != BV_OK) return rc;
+  if (res->msg_hash) memcpy(res->msg_hash, pin + o_dig, n * 32);
+  bv_batch sizes = {};
+  sizes.n_msgs = n;
+  sizes.n_items = n;
+  return bv_host_finish(ctx, &sizes, res, &call, true);
+}
+
 extern "C" int bv_verify_events(bv_ctx *ctx, const bv_event_batch *eb, bv_result *res) {
   if (!ctx || !eb || !res) return BV_E_ARGS;
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -130,6 +247,8 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
     posin.resize(n);
     for (uint64_t i = 0; i < n; i++) posin[order[i]] = (uint32_t)i;
   }
+
+  if (dag && !ctx->dag_on_device) return verify_events_dag_host(ctx, eb, res, order, level_off, call);
 
   // staging layout (pinned host and HBM): the compact wire arrays
   const uint64_t n_tx = eb->tx_start[n];
@@ -206,8 +325,7 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   // chunk's items fill whole words of the accept bitmask); a DAG batch is
   // hashed level by level across all its events: one chunk
   std::vector<uint64_t> cb{0};
-  const char *env_chunk = getenv("BV_EV_CHUNK_MB");  // A/B knob: 0 = one chunk
-  const uint64_t chunk_bytes = env_chunk ? (uint64_t)(atof(env_chunk) * (1 << 20)) : kChunk;
+  const uint64_t chunk_bytes = ctx->ev_chunk;  // 0 = one chunk (A/B knob, bv_create)
   if (!dag && chunk_bytes > 0) {
     const uint64_t per_ev = std::max<uint64_t>(1, (total - small_end) / n);
     const uint64_t per = std::max<uint64_t>(256, chunk_bytes / per_ev / 256 * 256);
@@ -279,14 +397,15 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   vb.s_be = d.s_be;
   vb.pre = d.pre;
   bool kc = false;
-  // bulk batches: each chunk's verify kernels go on the keys stream (idle
-  // once the tables are built), so they run beside the next chunk's body
-  // build and hashing on the main stream instead of after them
-  // (1M bulk events from pinned arrays, same box: 7.37-7.41 -> 6.90-7.01 ms
-  // per call; BV_EV_VERIFY_STREAM=0 keeps them on the main stream)
-  const char *env_vs = getenv("BV_EV_VERIFY_STREAM");
-  const bool split_verify = !dag && (env_vs == nullptr || atoi(env_vs) != 0);
-  hipStream_t vst = split_verify ? ctx->kstream : st;
+  // bulk batches: each chunk's verify kernels go on the s^-1 stream (idle
+  // once this batch's s^-1 is done; normal priority — the high-priority keys
+  // stream stays for the latency-bound table chains), so they run
+  // beside the next chunk's body build and hashing on the main stream
+  // instead of after them (1M bulk events from pinned arrays, same box:
+  // 7.37-7.41 -> 6.90-7.01 ms per call; BV_EV_VERIFY_STREAM=0 keeps them on
+  // the main stream)
+  const bool split_verify = !dag && ctx->ev_split_verify;
+  hipStream_t vst = split_verify ? ctx->sstream : st;
   bv_item_pipe pipe{ctx, &vb, {}, vst, false};
   rc = bv_out_bufs(ctx, &vb, nullptr, nullptr, nullptr, true, &pipe.o);
   if (rc != BV_OK) return rc;

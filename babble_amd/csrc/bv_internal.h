@@ -23,6 +23,7 @@
 
 #include "../../include/babbleverify.h"
 #include "geometry.h"
+#include "hostdag.h"
 
 #define KS_OK 0  // k_key_decode statuses (verify_core.h)
 
@@ -273,6 +274,14 @@ struct bv_ctx {
   DevBuf kc_kxy, kc_btabs;
   // bv_verify_events: body lengths, parent-hex positions, offsets, bodies
   DevBuf ev_lens, ev_ppos, ev_offs, ev_bodies, ev_tmp, ev_iota, ev_mid;
+  HostDagScratch dag_scratch;  // in-batch DAG batches: bodies built and hashed on the host (hostdag.cpp)
+  // A/B knobs, read once at bv_create (never per call): host-entry message
+  // chunk (BV_HOST_CHUNK_MB, >= 1 MB), event staging chunk (BV_EV_CHUNK_MB,
+  // 0 = one chunk; chunks hold >= 256 events), bulk events' verify beside the next chunk
+  // (BV_EV_VERIFY_STREAM=0: on the main stream), DAG batches hashed on the
+  // device instead of the host (BV_EV_DAG_DEVICE=1)
+  uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
+  bool ev_split_verify = true, dag_on_device = false;
 };
 
 // one in-flight host-entry call (bv_host_launch -> bv_host_finish)

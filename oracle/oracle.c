@@ -521,19 +521,91 @@ static void *worker(void *arg) {
   return NULL;
 }
 
+/* A persistent pool (the CPU comparators must not pay a
+ * thread spawn and join per call): workers are created on first need and
+ * sleep between calls; a phase uses min(n_threads, items) participants —
+ * the caller plus workers — pulling chunks from an atomic counter, and a
+ * one-participant phase runs inline on the caller. */
+#define POOL_MAX 256
+static pthread_mutex_t g_pmu = PTHREAD_MUTEX_INITIALIZER;   /* one phase at a time */
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t g_go = PTHREAD_COND_INITIALIZER, g_fin = PTHREAD_COND_INITIALIZER;
+static int g_workers, g_want, g_left;
+static uint64_t g_gen;
+static struct {
+  const bv_batch *b;
+  uint8_t *hash, *status;
+  uint64_t n, chunk;
+  int phase;
+  uint64_t next; /* atomic */
+} g_task;
+
+static void run_chunks(void) {
+  for (;;) {
+    const uint64_t lo = __atomic_fetch_add(&g_task.next, g_task.chunk, __ATOMIC_RELAXED);
+    if (lo >= g_task.n) return;
+    job_t j = {g_task.b, g_task.hash, g_task.status, lo, lo + g_task.chunk < g_task.n ? lo + g_task.chunk : g_task.n,
+               g_task.phase};
+    worker(&j);
+  }
+}
+
+static void *pool_main(void *arg) {
+  const int id = (int)(intptr_t)arg;
+  uint64_t seen = 0;
+  pthread_mutex_lock(&g_mu);
+  for (;;) {
+    while (g_gen == seen || id >= g_want) {
+      if (g_gen != seen) seen = g_gen; /* not a participant of this phase */
+      pthread_cond_wait(&g_go, &g_mu);
+    }
+    seen = g_gen;
+    pthread_mutex_unlock(&g_mu);
+    run_chunks();
+    pthread_mutex_lock(&g_mu);
+    if (--g_left == 0) pthread_cond_signal(&g_fin);
+  }
+  return NULL;
+}
+
 static void run_phase(const bv_batch *b, uint8_t *hash, uint8_t *status, uint64_t n, int phase, int nt) {
   if (nt < 1) nt = 1;
-  if (nt > 256) nt = 256;
-  pthread_t th[256];
-  job_t jobs[256];
-  uint64_t chunk = (n + nt - 1) / nt;
-  for (int t = 0; t < nt; t++) {
-    jobs[t].b = b; jobs[t].hash = hash; jobs[t].status = status; jobs[t].phase = phase;
-    jobs[t].lo = chunk * t < n ? chunk * t : n;
-    jobs[t].hi = chunk * (t + 1) < n ? chunk * (t + 1) : n;
-    pthread_create(&th[t], NULL, worker, &jobs[t]);
+  if (nt > POOL_MAX) nt = POOL_MAX;
+  /* hashing is ~1 us a message: don't wake a thread for fewer than 256 */
+  const uint64_t grain = phase == 0 ? 256 : 1;
+  const uint64_t max_part = (n + grain - 1) / grain;
+  const int k = (uint64_t)nt < max_part ? nt : (int)max_part;
+  if (k <= 1) {
+    job_t j = {b, hash, status, 0, n, phase};
+    worker(&j);
+    return;
   }
-  for (int t = 0; t < nt; t++) pthread_join(th[t], NULL);
+  pthread_mutex_lock(&g_pmu);
+  pthread_mutex_lock(&g_mu);
+  while (g_workers < k - 1) {
+    pthread_t t;
+    pthread_create(&t, NULL, pool_main, (void *)(intptr_t)g_workers);
+    pthread_detach(t);
+    g_workers++;
+  }
+  g_task.b = b;
+  g_task.hash = hash;
+  g_task.status = status;
+  g_task.n = n;
+  g_task.phase = phase;
+  g_task.chunk = n / ((uint64_t)k * 4) ? n / ((uint64_t)k * 4) : 1;
+  g_task.chunk = g_task.chunk > grain ? g_task.chunk : grain;
+  __atomic_store_n(&g_task.next, 0, __ATOMIC_RELAXED);
+  g_want = k - 1;
+  g_left = k - 1;
+  g_gen++;
+  pthread_cond_broadcast(&g_go);
+  pthread_mutex_unlock(&g_mu);
+  run_chunks();
+  pthread_mutex_lock(&g_mu);
+  while (g_left > 0) pthread_cond_wait(&g_fin, &g_mu);
+  pthread_mutex_unlock(&g_mu);
+  pthread_mutex_unlock(&g_pmu);
 }
 
 /* Verify a whole batch on the CPU: the oracle for parity tests and the

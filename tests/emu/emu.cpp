@@ -5,13 +5,18 @@
 // serially, so tests can check index logic and arithmetic on the CPU (and
 // under AddressSanitizer, tests/emu/Makefile `asan`) before a GPU run.
 // Not linked into libbabbleverify.so; the product never runs this.
+#include <algorithm>
+#include <atomic>
 #include <cstdlib>
+#include <functional>
 #include <cstring>
 #include <mutex>
 #include <thread>
 #include <vector>
 
 #include "../../babble_amd/csrc/evjson.h"
+#include "../../babble_amd/csrc/hostdag.h"
+#include "../../babble_amd/csrc/hostsha.h"
 #include "../../babble_amd/csrc/verify_core.h"
 
 namespace {
@@ -258,6 +263,49 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
 // device kernels' per-event code, evjson.h + sha256.h), in event order
 // (parents precede children).  bodies: sum of lengths + 64 bytes; offs:
 // n + 1; digests: 32 * n.  Returns the total body bytes.
+// The product's host DAG hasher (hostdag.cpp) over a batch: levels and order
+// as bv_events.cpp computes them; `threads` > 1 runs the parallel steps on
+// that many threads; `portable` selects the portable SHA-256 compressor.
+void emu_host_dag_hash(const bv_event_batch *b, uint8_t *digests, int threads, int portable) {
+  const uint64_t n = b->n_events;
+  std::vector<uint32_t> level(n, 0), order(n), level_off;
+  uint32_t nl = 1;
+  for (uint64_t e = 0; e < n; e++) {
+    uint32_t l = 0;
+    for (int p = 0; p < 2; p++)
+      if (b->parent_kind[2 * e + p] == BV_PARENT_EVENT) l = std::max(l, level[b->parent_ref[2 * e + p]] + 1);
+    level[e] = l;
+    nl = std::max(nl, l + 1);
+  }
+  level_off.assign(nl + 1, 0);
+  for (uint64_t e = 0; e < n; e++) level_off[level[e] + 1]++;
+  for (uint32_t l = 0; l < nl; l++) level_off[l + 1] += level_off[l];
+  std::vector<uint32_t> fill(level_off.begin(), level_off.end() - 1);
+  for (uint64_t e = 0; e < n; e++) order[fill[level[e]]++] = (uint32_t)e;
+  const HostParFor pf = [threads](uint64_t cnt, uint64_t grain, const std::function<void(uint64_t, uint64_t)> &fn) {
+    if (threads <= 1 || cnt <= grain) return fn(0, cnt);
+    std::vector<std::thread> th;
+    std::atomic<uint64_t> next{0};
+    for (int t = 0; t < threads; t++)
+      th.emplace_back([&]() {
+        for (uint64_t lo; (lo = next.fetch_add(grain)) < cnt;) fn(lo, std::min(cnt, lo + grain));
+      });
+    for (auto &x : th) x.join();
+  };
+  hsha::force_portable(portable != 0);
+  HostDagScratch w;
+  bv_host_dag_hash(*b, order.data(), level_off.data(), nl, pf, w, digests);
+  hsha::force_portable(false);
+}
+
+void emu_host_sha256(const uint8_t *msg, uint64_t len, uint8_t *out, int portable) {
+  hsha::force_portable(portable != 0);
+  hsha::digest(msg, len, out);
+  hsha::force_portable(false);
+}
+
+int emu_host_sha_accelerated() { return hsha::accelerated(); }
+
 uint64_t emu_ev_bodies(const bv_event_batch *b, uint8_t *bodies, uint64_t cap, uint64_t *offs, uint8_t *digests) {
   const uint64_t n = b->n_events;
   std::vector<uint32_t> ppos(2 * n);

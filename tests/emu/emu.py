@@ -132,3 +132,30 @@ def ev_bodies(eb):
     total = L.emu_ev_bodies(ctypes.byref(cb), bodies.ctypes.data, cap, offs.ctypes.data, dig.ctypes.data)
     assert total == offs[n]
     return [bodies[offs[i]:offs[i + 1]].tobytes() for i in range(n)], dig[:n]
+
+
+def host_dag_hash(eb, threads: int = 1, portable: bool = False) -> np.ndarray:
+    """The product's host DAG hasher (babble_amd/csrc/hostdag.cpp, linked
+    into the emulator library): digests[n, 32] of an events.EventWireBatch."""
+    L = lib()
+    L.emu_host_dag_hash.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    L.emu_host_dag_hash.restype = None
+    keep: list = []
+    cb = eb.c_struct(keep)
+    dig = np.zeros((max(eb.n_events, 1), 32), np.uint8)
+    L.emu_host_dag_hash(ctypes.byref(cb), dig.ctypes.data, threads, 1 if portable else 0)
+    return dig[: eb.n_events]
+
+
+def host_sha256(msg: bytes, portable: bool = False) -> bytes:
+    """The product's host SHA-256 (babble_amd/csrc/hostsha.cpp)."""
+    L = lib()
+    L.emu_host_sha256.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
+    L.emu_host_sha256.restype = None
+    out = ctypes.create_string_buffer(32)
+    L.emu_host_sha256(msg, len(msg), out, 1 if portable else 0)
+    return out.raw
+
+
+def host_sha_accelerated() -> bool:
+    return bool(lib().emu_host_sha_accelerated())

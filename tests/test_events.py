@@ -152,9 +152,9 @@ def test_verify_events_chunk_boundaries(monkeypatch):
     from babble_amd.verifier import Verifier
     from oracle import coracle
 
+    monkeypatch.setenv("BV_EV_CHUNK_MB", "0.001")  # 256-event chunks (read at bv_create)
     v = Verifier(0)
     try:
-        monkeypatch.setenv("BV_EV_CHUNK_MB", "0.001")  # 256-event chunks
         for seed in (6, 7):
             wire, bodies, wd = random_wire(seed, n=1100, in_batch=False)
             many = v.verify_events(wire)
@@ -252,3 +252,44 @@ def test_verify_events_from_pinned_buffers(monkeypatch):
     finally:
         v.close()
         arena.close()
+
+
+# ---------------------------------------------------------------------------
+# The host DAG hasher (babble_amd/csrc/hostdag.cpp + hostsha.cpp): the path
+# bv_verify_events takes for batches with in-batch parents, run here on the
+# CPU through the emulator library, which links the same source.
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("portable", [False, True], ids=["sha_ext", "portable"])
+def test_host_sha256_every_padding_boundary(portable):
+    if not portable and not emu.host_sha_accelerated():
+        pytest.skip("no SHA extensions on this CPU")
+    rng = np.random.default_rng(5)
+    for n in list(range(0, 200)) + [447, 448, 1000, 4095, 4096, 65537]:
+        m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert emu.host_sha256(m, portable) == hashlib.sha256(m).digest(), n
+    assert emu.host_sha256(b"abc", portable).hex() == \
+        "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"  # FIPS 180-4 B.1
+
+
+@pytest.mark.parametrize("threads,portable", [(1, False), (4, False), (1, True)])
+def test_host_dag_hash_equals_synth_and_oracle(threads, portable):
+    """SyncResponse-shaped DAGs (in-batch parents by index, 333 levels of 3
+    events) and the random edge-case batches (nil / empty lists, nil
+    transactions, fragments, negative Index / Timestamp, odd key lengths,
+    HASH / EVENT / no parents): every digest equals hashlib over the
+    generator's bodies / the Go-semantics restatement's."""
+    packed, wire = synth.event_fields(1000, n_creators=4, seed=31, parents="event")
+    dig = emu.host_dag_hash(wire, threads, portable)
+    for i in range(packed.n_items):
+        assert dig[i].tobytes() == hashlib.sha256(packed.message(i)).digest(), i
+    for seed in (1, 2, 3):
+        w, _, wd = random_wire(seed, n=400)
+        assert [d.tobytes() for d in emu.host_dag_hash(w, threads, portable)] == wd
+
+
+def test_host_dag_hash_wide_levels():
+    """Levels wider than the parallel threshold (128 events): 300 creators
+    give 11 levels of 300 events, hashed on 6 threads."""
+    packed, wire = synth.event_fields(3000, n_creators=300, seed=33, parents="event")
+    dig = emu.host_dag_hash(wire, threads=6)
+    assert all(dig[i].tobytes() == hashlib.sha256(packed.message(i)).digest() for i in range(3000))

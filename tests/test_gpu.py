@@ -124,7 +124,7 @@ def test_k12_tables_adversarial(verifier):
     assert verifier.timing()["key_path"] == 12
 
 
-def test_host_entry_item_order(verifier, monkeypatch):
+def test_host_entry_item_order(monkeypatch):
     """bv_verify_batch verifies items chunk by chunk as their messages land
     when item_msg is non-decreasing, and after the whole transfer otherwise:
     the same batch (several 8 MB message chunks via BV_HOST_CHUNK_MB, K12
@@ -132,7 +132,10 @@ def test_host_entry_item_order(verifier, monkeypatch):
     items re-hitting an early message: every status equal to the oracle's."""
     import dataclasses
 
-    monkeypatch.setenv("BV_HOST_CHUNK_MB", "8")
+    from babble_amd.verifier import Verifier
+
+    monkeypatch.setenv("BV_HOST_CHUNK_MB", "8")  # read at bv_create
+    verifier = Verifier(device=0)
     b = synth.adversarial(120_000, seed=13, n_creators=16, scale_per_million=MIX)
     assert np.all(np.diff(b.item_msg.astype(np.int64)) >= 0)
     check_against_oracle(verifier, b)
@@ -145,6 +148,7 @@ def test_host_entry_item_order(verifier, monkeypatch):
     late = b.item_msg.copy()
     late[-63:] = 0  # the last word's items point back at message 0: out of order
     check_against_oracle(verifier, dataclasses.replace(b, item_msg=late))
+    verifier.close()
 
 
 def test_host_entry_single_copy_staging(verifier):
