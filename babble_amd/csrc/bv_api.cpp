@@ -399,7 +399,6 @@ static int create_impl(bv_ctx *ctx) {
     ctx->ev_chunk = mb <= 0 ? 0 : std::max<uint64_t>(1, (uint64_t)(mb * (1 << 20)));  // >= 256 events a chunk anyway
   }
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
-  if (const char *s = getenv("BV_EV_DAG_DEVICE")) ctx->dag_on_device = atoi(s) != 0;
   return BV_OK;
 }
 
@@ -439,7 +438,7 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   }
   if (ctx->g_table) gtable_release(ctx->device);
   DevBuf *bufs[] = {&ctx->d_in, &ctx->kc_kxy,  &ctx->kc_btabs, &ctx->ev_lens,
-                    &ctx->ev_ppos,   &ctx->ev_offs, &ctx->ev_bodies, &ctx->ev_tmp, &ctx->ev_iota, &ctx->ev_mid};
+                    &ctx->ev_ppos,   &ctx->ev_offs, &ctx->ev_bodies, &ctx->ev_tmp, &ctx->ev_iota};
   for (auto *b : bufs) b->release();
   for (auto &sl : ctx->slot) {
     DevBuf *sb[] = {&sl.digests,   &sl.kstatus, &sl.kxy, &sl.bases_jac, &sl.key_sub, &sl.key_pscr,

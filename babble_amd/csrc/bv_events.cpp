@@ -1,21 +1,22 @@
-// bv_events.cpp — bv_verify_events: canonical EventBody JSON built on the
-// device from wire fields, in-batch DAG-level hashing, then the verify
-// pipeline (include/babbleverify.h).
+// bv_verify_events: canonical EventBody JSON built from wire fields, hashed,
+// then the verify pipeline (include/babbleverify.h).
 //
-// Host work is validation, the DAG levels (only when an event names an
-// in-batch parent) and one pinned staging copy of the compact arrays; the
-// bodies never cross PCIe.  Device: k_ev_len -> inclusive scan (hipcub) ->
-// k_ev_write -> level 0 in one grid launch -> the remaining levels, wide ones
-// as grid launches and runs of narrow ones (<= 1024 events) as ONE
-// single-workgroup launch each (k_ev_hash_chain) -> bv_run_verify on the
-// hashed bodies.  s^-1 and the key tables (bv_run_keys) start as soon as the
-// keys, r, s and pre (staged first) have landed.
+// Bulk batches (no in-batch parent: a store / bootstrap replay, parents by
+// known hash): host work is validation and the staging of the compact wire
+// arrays; the bodies are built and hashed on the device chunk by chunk
+// (k_ev_len -> inclusive scan (hipcub) -> k_ev_write -> k_ev_hash) while the
+// next chunk crosses PCIe, and each chunk's items are verified beside the
+// next chunk's build.  Batches with in-batch parents (a SyncResponse's DAG:
+// each body embeds its parents' hashes) are built and hashed on the host in
+// topological order instead (hostdag.cpp; the serial chain is ~50x faster on
+// one CPU core than on one GPU wave: 0.8 vs 5.5 ms per 1000-event
+// SyncResponse, profiles/r04_ab_dag.log) while the device runs key decode,
+// key tables and s^-1; only the digests cross PCIe.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
 #include "bv_internal.h"
-#include "evjson.h"  // EV_MID_U32
 
 #define HIPCHK(expr, code, what)                               \
   do {                                                         \
@@ -25,8 +26,6 @@
 
 namespace {
 
-constexpr uint32_t kNarrowLevel = 768;   // events per level run by k_ev_hash_chain (<= kChainCap)
-constexpr uint32_t kChainCap = 768;      // events per k_ev_hash_chain launch (EVC_CAP)
 // staged bytes per PCIe piece / event chunk: 64 MB (~250k C2 events) keeps
 // each chunk's verify launches at full occupancy while the next chunk
 // crosses PCIe (1M bulk events, same box: 16 / 32 / 64 / 128 MB / one
@@ -226,7 +225,7 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   if (n == 0) return BV_OK;
 
   // DAG levels over in-batch parents (refs point backwards: one pass)
-  std::vector<uint32_t> level, order, level_off, posin;
+  std::vector<uint32_t> level, order, level_off;
   const bool dag = memchr(eb->parent_kind, BV_PARENT_EVENT, 2 * n) != nullptr;
   if (dag) {
     level.assign(n, 0);
@@ -244,11 +243,8 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
     order.resize(n);
     std::vector<uint32_t> fill(level_off.begin(), level_off.end() - 1);
     for (uint64_t e = 0; e < n; e++) order[fill[level[e]]++] = (uint32_t)e;
-    posin.resize(n);
-    for (uint64_t i = 0; i < n; i++) posin[order[i]] = (uint32_t)i;
+    return verify_events_dag_host(ctx, eb, res, order, level_off, call);
   }
-
-  if (dag && !ctx->dag_on_device) return verify_events_dag_host(ctx, eb, res, order, level_off, call);
 
   // staging layout (pinned host and HBM): the compact wire arrays
   const uint64_t n_tx = eb->tx_start[n];
@@ -288,9 +284,6 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   const size_t o_r = add(eb->r_be, n * 32, ALL);
   const size_t o_cr = add(eb->creator, n * 4, ALL);
   const size_t o_ph = add(eb->parent_hashes, eb->parent_hashes ? eb->n_parent_hashes * 32 : 0, ALL);
-  const size_t o_ord = add(dag ? order.data() : nullptr, dag ? n * 4 : 0, ALL);
-  const size_t o_lof = add(dag ? level_off.data() : nullptr, dag ? level_off.size() * 4 : 0, ALL);
-  const size_t o_pin = add(dag ? posin.data() : nullptr, dag ? n * 4 : 0, ALL);
   const size_t small_end = total;
   const size_t o_ix = add(eb->index, n * 8, EV, 8);
   const size_t o_ts = add(eb->timestamp, n * 8, EV, 8);
@@ -322,11 +315,10 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   };
 
   // event chunks of ~kChunk staged bytes (whole 256-event groups, so each
-  // chunk's items fill whole words of the accept bitmask); a DAG batch is
-  // hashed level by level across all its events: one chunk
+  // chunk's items fill whole words of the accept bitmask)
   std::vector<uint64_t> cb{0};
   const uint64_t chunk_bytes = ctx->ev_chunk;  // 0 = one chunk (A/B knob, bv_create)
-  if (!dag && chunk_bytes > 0) {
+  if (chunk_bytes > 0) {
     const uint64_t per_ev = std::max<uint64_t>(1, (total - small_end) / n);
     const uint64_t per = std::max<uint64_t>(256, chunk_bytes / per_ev / 256 * 256);
     for (uint64_t e = per; e < n; e += per) cb.push_back(e);
@@ -377,7 +369,6 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   HIPCHK(ctx->ev_offs.ensure((n + 1) * 8), BV_E_OOM, "alloc offs");
   HIPCHK(ctx->ev_bodies.ensure(bound), BV_E_OOM, "alloc bodies");
   HIPCHK(ctx->ev_tmp.ensure(std::max<size_t>(tmp_bytes, 256)), BV_E_OOM, "alloc scan scratch");
-  if (dag) HIPCHK(ctx->ev_mid.ensure((size_t)n * EV_MID_U32 * 4), BV_E_OOM, "alloc midstates");
   uint64_t *offs = ctx->ev_offs.as<uint64_t>();
   uint32_t *ppos = ctx->ev_ppos.as<uint32_t>();
   uint8_t *bodies = ctx->ev_bodies.as<uint8_t>();
@@ -404,7 +395,7 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   // instead of after them (1M bulk events from pinned arrays, same box:
   // 7.37-7.41 -> 6.90-7.01 ms per call; BV_EV_VERIFY_STREAM=0 keeps them on
   // the main stream)
-  const bool split_verify = !dag && ctx->ev_split_verify;
+  const bool split_verify = ctx->ev_split_verify;
   hipStream_t vst = split_verify ? ctx->sstream : st;
   bv_item_pipe pipe{ctx, &vb, {}, vst, false};
   rc = bv_out_bufs(ctx, &vb, nullptr, nullptr, nullptr, true, &pipe.o);
@@ -496,48 +487,19 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
     HIPCHK(hipStreamWaitEvent(st, landed, 0), BV_E_LAUNCH, "join chunk");
     HIPCHK(bvk::ev_build(st, d, e0, e1, ctx->ev_lens.as<uint64_t>(), ppos, offs, bodies, ctx->ev_tmp.p, &tmp_bytes),
            BV_E_LAUNCH, "event bodies");
-    if (!dag) {
-      HIPCHK(bvk::ev_hash(st, e1 - e0, nullptr, e0, d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
-      HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is used
-      if (split_verify) {
-        hipEvent_t hashed = ctx->chunk_ev[(c + 32) % ctx->chunk_ev.size()];  // waited on at once: reuse is safe
-        HIPCHK(hipEventRecord(hashed, st), BV_E_LAUNCH, "event");
-        HIPCHK(hipStreamWaitEvent(vst, hashed, 0), BV_E_LAUNCH, "join chunk digests");
-      }
-      rc = pipe.upto(e1);
-      if (rc != BV_OK) return rc;
+    HIPCHK(bvk::ev_hash(st, e1 - e0, e0, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
+    HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is used
+    if (split_verify) {
+      hipEvent_t hashed = ctx->chunk_ev[(c + 32) % ctx->chunk_ev.size()];  // waited on at once: reuse is safe
+      HIPCHK(hipEventRecord(hashed, st), BV_E_LAUNCH, "event");
+      HIPCHK(hipStreamWaitEvent(vst, hashed, 0), BV_E_LAUNCH, "join chunk digests");
     }
+    rc = pipe.upto(e1);
+    if (rc != BV_OK) return rc;
   }
   HIPCHK(hipEventRecord(ctx->S().ev[E_STAGED], cs), BV_E_LAUNCH, "event");
   call.ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call.t0).count();
 
-  if (dag) {  // level by level over the in-batch DAG
-    const uint32_t *dord = (const uint32_t *)(dev + o_ord), *dlof = (const uint32_t *)(dev + o_lof);
-    const uint32_t *dpin = (const uint32_t *)(dev + o_pin);
-    const uint32_t nl = (uint32_t)level_off.size() - 1;
-    // midstates of every event above level 0, in one wide launch
-    uint32_t *mid = ctx->ev_mid.as<uint32_t>();
-    HIPCHK(bvk::ev_mid(st, n - level_off[1], dord + level_off[1], bodies, offs, ppos, mid), BV_E_LAUNCH, "k_ev_mid");
-    uint32_t L = 0;
-    while (L < nl) {
-      const uint32_t w = level_off[L + 1] - level_off[L];
-      if (w > kNarrowLevel || L == 0) {
-        HIPCHK(bvk::ev_hash(st, w, dord + level_off[L], 0, d, ppos, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
-        L++;
-        continue;
-      }
-      // a run of narrow levels, at most kChainCap events per launch (the
-      // chain kernel keeps the launch's descriptors and digests in LDS)
-      uint32_t L1 = L;
-      while (L1 < nl && level_off[L1 + 1] - level_off[L1] <= kNarrowLevel &&
-             level_off[L1 + 1] - level_off[L] <= kChainCap)
-        L1++;
-      HIPCHK(bvk::ev_hash_chain(st, L, L1, dlof, dord, dpin, d, ppos, bodies, offs, mid, dig), BV_E_LAUNCH,
-             "k_ev_hash_chain");
-      L = L1;
-    }
-    HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");
-  }
   HIPCHK(hipEventRecord(ctx->S().ev[E_SHA], st), BV_E_LAUNCH, "event");
 
   // the digests go back on the copy stream while the last verify kernels run
@@ -554,7 +516,7 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
          "d2h digests");
   HIPCHK(hipEventRecord(ctx->S().ev[E_CSDONE], cs), BV_E_LAUNCH, "event");
 
-  rc = pipe.finish();  // bulk: the last chunk's items; DAG: all of them
+  rc = pipe.finish();  // the last chunk's items
   if (rc != BV_OK) return rc;
   if (split_verify) HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_END], 0), BV_E_LAUNCH, "join verify");
   HIPCHK(hipMemcpyAsync(call.direct_status ? res->status : pout + o_st, pipe.o.status, n, hipMemcpyDeviceToHost, st),

@@ -33,13 +33,7 @@ hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, 
 hipError_t sha256_chain(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
 hipError_t ev_build(hipStream_t, const bv_event_batch &, uint64_t, uint64_t, uint64_t *, uint32_t *, uint64_t *,
                     uint8_t *, void *, size_t *);
-hipError_t ev_hash(hipStream_t, uint64_t, const uint32_t *, uint64_t, const bv_event_batch &, const uint32_t *,
-                   uint8_t *, const uint64_t *, uint32_t *);
-hipError_t ev_mid(hipStream_t, uint64_t, const uint32_t *, const uint8_t *, const uint64_t *, const uint32_t *,
-                  uint32_t *);
-hipError_t ev_hash_chain(hipStream_t, uint32_t, uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
-                         const bv_event_batch &, const uint32_t *, uint8_t *, const uint64_t *, const uint32_t *,
-                         uint32_t *);
+hipError_t ev_hash(hipStream_t, uint64_t, uint64_t, uint8_t *, const uint64_t *, uint32_t *);
 hipError_t iota(hipStream_t, uint64_t, uint32_t *);
 hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
                         uint32_t *, uint32_t *, uint64_t n_items);
@@ -273,15 +267,14 @@ struct bv_ctx {
   uint64_t kc_clock = 0, kc_bytes = 0, kc_budget = 0;
   DevBuf kc_kxy, kc_btabs;
   // bv_verify_events: body lengths, parent-hex positions, offsets, bodies
-  DevBuf ev_lens, ev_ppos, ev_offs, ev_bodies, ev_tmp, ev_iota, ev_mid;
+  DevBuf ev_lens, ev_ppos, ev_offs, ev_bodies, ev_tmp, ev_iota;
   HostDagScratch dag_scratch;  // in-batch DAG batches: bodies built and hashed on the host (hostdag.cpp)
   // A/B knobs, read once at bv_create (never per call): host-entry message
   // chunk (BV_HOST_CHUNK_MB, >= 1 MB), event staging chunk (BV_EV_CHUNK_MB,
   // 0 = one chunk; chunks hold >= 256 events), bulk events' verify beside the next chunk
-  // (BV_EV_VERIFY_STREAM=0: on the main stream), DAG batches hashed on the
-  // device instead of the host (BV_EV_DAG_DEVICE=1)
+  // (BV_EV_VERIFY_STREAM=0: on the main stream)
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
-  bool ev_split_verify = true, dag_on_device = false;
+  bool ev_split_verify = true;
 };
 
 // one in-flight host-entry call (bv_host_launch -> bv_host_finish)

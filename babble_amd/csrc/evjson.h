@@ -212,100 +212,15 @@ DEV void evj_write(const bv_event_batch &b, uint64_t e, uint8_t *o) {
 }
 
 // ---------------------------------------------------------------------------
-// Hashing along the in-batch DAG (k_ev_mid / k_ev_hash_chain).  A body's
-// blocks that lie wholly before its first in-batch parent's hex do not
-// depend on any other event: they are compressed once, all events in
-// parallel, into a midstate; only the remaining blocks sit on the serial
-// chain (T=1 bodies: 6 of 8 blocks).
+// Hashing along the in-batch DAG (hostdag.cpp).  A body's blocks that lie
+// wholly before its first in-batch parent's hex do not depend on any other
+// event: they are compressed once, all events in parallel, into a midstate;
+// only the remaining blocks sit on the serial chain (T=1 bodies: 6 of 8
+// blocks).
 // ---------------------------------------------------------------------------
-#define EV_MID_U32 16  // per event: SHA-256 state h[8], first chained block, pad
-
 DEV uint32_t ev_mid_blocks(const uint32_t pp[2]) {
   uint32_t m = EVJ_NOPOS;
   for (int p = 0; p < 2; p++)
     if (pp[p] != EVJ_NOPOS && pp[p] < m) m = pp[p];
   return m == EVJ_NOPOS ? 0u : m / 64u;
-}
-
-DEV void ev_midstate(uint64_t e, const uint8_t *bodies, const uint64_t *offs, const uint32_t *ppos, uint32_t *mid) {
-  const uint64_t o = offs[e], len = offs[e + 1] - o;
-  const uint32_t nb = ev_mid_blocks(ppos + 2 * e);
-  uint32_t h[8];
-  sha256_init(h);
-  sha256_blocks(h, (const uint32_t *)(bodies + (o & ~(uint64_t)3)), (uint32_t)(o & 3), len, 0, nb);
-  uint32_t *m = mid + (uint64_t)EV_MID_U32 * e;
-  for (int k = 0; k < 8; k++) m[k] = h[k];
-  m[8] = nb;
-}
-
-// digest words as stored by sha256_one: the 32 big-endian digest bytes
-DEV void ev_digest_words(uint32_t out[8], const uint32_t h[8]) {
-#pragma unroll
-  for (int k = 0; k < 8; k++) out[k] = bswap32(h[k]);
-}
-
-// bytes of {hi, lo} selected by `sel` (v_perm_b32: selector 0-3 = lo's bytes, 4-7 = hi's)
-DEV uint32_t evj_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_perm(hi, lo, sel);
-#else
-  const uint64_t v = (uint64_t)hi << 32 | lo;
-  uint32_t r = 0;
-  for (int k = 0; k < 4; k++) r |= (uint32_t)((v >> (8 * ((sel >> (8 * k)) & 7))) & 0xFF) << (8 * k);
-  return r;
-#endif
-}
-
-// four nibbles (one per byte, 0..15) -> uppercase ASCII hex, SWAR
-DEV uint32_t evj_hexnib4(uint32_t n) {
-  const uint32_t ge10 = ((n + 0x06060606u) >> 4) & 0x01010101u;
-  return n + 0x30303030u + 7u * ge10;
-}
-
-// evj_hex32 over digest words (byte c of wd[k] = digest byte 4k+c): the 64
-// hex characters as 16 little-endian words (memory order)
-DEV void evj_hex32_words(uint32_t out[16], const uint32_t wd[8]) {
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t hi = evj_hexnib4((wd[k] >> 4) & 0x0F0F0F0Fu), lo = evj_hexnib4(wd[k] & 0x0F0F0F0Fu);
-    out[2 * k] = evj_perm(lo, hi, 0x05010400u);      // hi0 lo0 hi1 lo1
-    out[2 * k + 1] = evj_perm(lo, hi, 0x07030602u);  // hi2 lo2 hi3 lo3
-  }
-}
-
-// store 64 bytes (16 LE words) at byte offset `rel` of a dword buffer with
-// aligned dword stores (read-modify-write of the two edge dwords)
-DEV void evj_put64(uint32_t *buf, uint32_t rel, const uint32_t v[16]) {
-  const uint32_t q = rel >> 2, sh = (rel & 3) * 8;
-  if (sh == 0) {
-#pragma unroll
-    for (int k = 0; k < 16; k++) buf[q + k] = v[k];
-    return;
-  }
-  const uint32_t keep = (1u << sh) - 1u;
-  buf[q] = (buf[q] & keep) | (v[0] << sh);
-#pragma unroll
-  for (int k = 1; k < 16; k++) buf[q + k] = (v[k - 1] >> (32 - sh)) | (v[k] << sh);
-  buf[q + 16] = (buf[q + 16] & ~keep) | (v[15] >> (32 - sh));
-}
-
-// Dword q of a buffer holding a message tail whose bytes end at E, padded
-// per FIPS 180-4 up to F (the end of the final block): bytes < E keep `v`,
-// byte E is 0x80, the last 8 bytes before F hold the big-endian bit length,
-// the rest are zero.
-DEV uint32_t evj_pad_word(uint32_t v, uint32_t q, uint32_t E, uint32_t F, uint64_t bitlen) {
-  if (4 * q + 4 <= E) return v;
-  uint32_t out = 0;
-  for (uint32_t c = 0; c < 4; c++) {
-    const uint32_t b = 4 * q + c;
-    uint32_t byte = 0;
-    if (b < E)
-      byte = (v >> (8 * c)) & 0xFFu;
-    else if (b == E)
-      byte = 0x80u;
-    else if (b + 8 >= F && b < F)
-      byte = (uint32_t)(bitlen >> (8 * (F - 1 - b))) & 0xFFu;
-    out |= byte << (8 * c);
-  }
-  return out;
 }

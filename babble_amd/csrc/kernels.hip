@@ -108,37 +108,13 @@ __global__ void __launch_bounds__(EV_WRITE_NT) k_ev_write(bv_event_batch b, uint
   }
 }
 
-// Splice the in-batch parents' hex (their digests final) into event e's
-// body, then hash it.  `coherent`: parents were hashed by other threads of
-// this launch (k_ev_hash_chain), so their digest words are read at agent
-// scope, past the non-coherent vector L1.
-__device__ __forceinline__ void ev_splice_hash(uint64_t e, const bv_event_batch &b, const uint32_t *ppos,
-                                               uint8_t *bodies, const uint64_t *offs, uint32_t *dig,
-                                               bool coherent) {
-  for (int p = 0; p < 2; p++) {
-    const uint32_t pos = ppos[2 * e + p];
-    if (pos == EVJ_NOPOS) continue;
-    const uint64_t q = b.parent_ref[2 * e + p];
-    uint32_t w[8];
-    for (int k = 0; k < 8; k++)
-      w[k] = coherent ? __hip_atomic_load(dig + 8 * q + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : dig[8 * q + k];
-    uint8_t d[32];
-    for (int k = 0; k < 8; k++)
-      for (int c = 0; c < 4; c++) d[4 * k + c] = (uint8_t)(w[k] >> (8 * c));  // words hold BE digest bytes
-    evj_hex32(bodies + offs[e] + pos, d);
-  }
-  sha256_one(e, bodies, offs, dig);
-}
-
-// One DAG level (or events e0 .. e0 + count - 1 when list == null): a grid
-// over its events.
-__global__ void __launch_bounds__(256) k_ev_hash(uint64_t count, const uint32_t *__restrict__ list, uint64_t e0,
-                                                 bv_event_batch b, const uint32_t *__restrict__ ppos,
-                                                 uint8_t *__restrict__ bodies, const uint64_t *__restrict__ offs,
-                                                 uint32_t *__restrict__ dig) {
+// Events e0 .. e0 + count - 1 of a batch without in-batch parents (their
+// bodies are complete): SHA-256 of each, one lane per event.  Batches WITH
+// in-batch parents are hashed on the host (hostdag.cpp).
+__global__ void __launch_bounds__(256) k_ev_hash(uint64_t count, uint64_t e0, uint8_t *__restrict__ bodies,
+                                                 const uint64_t *__restrict__ offs, uint32_t *__restrict__ dig) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) ev_splice_hash(list ? list[i] : e0 + i, b, ppos, bodies, offs, dig, false);
+  if (i < count) sha256_one(e0 + i, bodies, offs, dig);
 }
 
 // offs[0, count) += *base (the end of the previous chunk's bodies)
@@ -146,330 +122,6 @@ __global__ void __launch_bounds__(256) k_add_base(uint64_t count, uint64_t *__re
                                                   const uint64_t *__restrict__ base) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < count) offs[i] += *base;
-}
-
-// Midstates (evjson.h: ev_midstate) of `count` events (list[i]): the
-// blocks before each body's first in-batch parent, all events in parallel.
-__global__ void __launch_bounds__(256) k_ev_mid(uint64_t count, const uint32_t *__restrict__ list,
-                                                const uint8_t *__restrict__ bodies, const uint64_t *__restrict__ offs,
-                                                const uint32_t *__restrict__ ppos, uint32_t *__restrict__ mid) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) ev_midstate(list[i], bodies, offs, ppos, mid);
-}
-
-// Consecutive NARROW levels [l0, l1) in one launch of one workgroup
-// (core.sync's SyncResponse: ~SyncLimit events, a few per level, hundreds
-// of levels).  The DAG makes this a serial chain of SHA-256 compressions: a
-// lane can only start an event once its parents' digests exist.  A single
-// wave issues about one VALU per 6 cycles (tools/ubench_sha.hip), so the
-// design keeps everything but the rounds off the hashing lanes, and keeps
-// wave 0 (the hashing lanes) free of global memory operations, so no
-// s_waitcnt on HBM traffic ever lands on the chain:
-//  * prologue: the launch's events (<= EVC_CAP, host-guaranteed) get an LDS
-//    descriptor (tail location, hex positions, parents as LDS digest slots),
-//    built by the whole workgroup in parallel;
-//  * per level L (tails and midstates double-buffered: level L in buffer L & 1):
-//    B  lane i splices the i-th event's parents' hex into its LDS tail from
-//       the LDS digest cache (parents hashed by an earlier launch: HBM);
-//    C  one lane per (event, block) expands the block's W+K schedule into LDS
-//       (interleaved across events, so the round lanes read distinct banks),
-//       16 words at a time while lane i runs the first block's rounds 16 at
-//       a time (D0);
-//    D  lane i runs the 64 rounds per block from its midstate (registers
-//       only: sha256_rounds_wk, 1.66 us per block on one wave); the digest
-//       goes to the LDS cache;
-//    A  beside D, waves 1-3 move level L+1's body tails (padded to whole
-//       SHA-256 blocks) and midstates (k_ev_mid), loaded into their
-//       registers during level L, into the other buffer, then issue the
-//       loads for level L+2;
-//  * epilogue: the launch's digests go to HBM (coalesced).
-// Events past EVC_SLOTS / EVC_WEV in a level, or with tails longer than
-// EVC_SLOT_DW or more than EVC_WBLK blocks, take the same steps with the
-// schedule inline (and from HBM when not in LDS).
-#define EVC_SLOTS 64
-#define EVC_SLOT_DW 128
-#define EVC_CAP 768
-#define EVC_WEV 8    // events per level with LDS schedules
-#define EVC_WBLK 7   // tail blocks of an LDS event: 7 x 16 + 1 dwords fit a slot
-#define EVC_NT 256   // one wave per SIMD: the hashing lanes get the full register file (no spills)
-#define EVC_LT (EVC_NT - 64)                                     // loader lanes: waves 1-3
-#define EVC_PF ((EVC_SLOTS * EVC_SLOT_DW + EVC_LT - 1) / EVC_LT)  // tail dwords per loader lane
-#define EVC_PM ((EVC_SLOTS * 8 + EVC_LT - 1) / EVC_LT)            // midstate words per loader lane
-// descriptor words: e | a0 lo | a0 hi | tail dwords in HBM (<= 2^24 - 1) + sh << 24 | nb | len |
-// hex pos 0, 1 (within the tail) | parent 0, 1 LDS slot | parent 0, 1 event
-#define EVC_DESC 12
-// An event is hashed from LDS when its tail, padded to whole blocks, fits a
-// slot: nblk - nb <= EVC_WBLK.
-DEV bool evc_lds_event(uint32_t i, uint32_t nb, uint32_t len) {
-  return i < EVC_SLOTS && (uint32_t)sha256_nblocks(len) - nb <= EVC_WBLK;
-}
-// loader lane u of waves 1-3: level L's tails and midstates into registers
-// (only the dwords the LDS events need)
-__device__ __forceinline__ void evc_load(uint32_t L, uint32_t nl, uint32_t u, const uint32_t *sLof,
-                                         const uint32_t *sDesc, const uint32_t *bw, const uint32_t *mid,
-                                         uint32_t pf[EVC_PF + EVC_PM]) {
-  if (L >= nl) return;
-  const uint32_t lo = sLof[L], w = sLof[L + 1] - lo, ws = w < EVC_SLOTS ? w : EVC_SLOTS;
-#pragma unroll
-  for (int r = 0; r < EVC_PF; r++) {
-    const uint32_t x = u + EVC_LT * r, i = x / EVC_SLOT_DW, k = x % EVC_SLOT_DW;
-    if (i >= ws) break;
-    const uint32_t *d = sDesc + EVC_DESC * (lo + i);
-    if (k < (d[3] & 0xFFFFFFu) && evc_lds_event(i, d[4], d[5])) pf[r] = bw[((uint64_t)d[1] | ((uint64_t)d[2] << 32)) + k];
-  }
-#pragma unroll
-  for (int r = 0; r < EVC_PM; r++) {
-    const uint32_t x = u + EVC_LT * r, i = x / 8, k = x % 8;
-    if (i >= ws) break;
-    pf[EVC_PF + r] = mid[(uint64_t)EV_MID_U32 * sDesc[EVC_DESC * (lo + i)] + k];
-  }
-}
-__device__ __noinline__ uint32_t evc_pad(uint32_t v, uint32_t q, uint32_t E, uint32_t F, uint64_t bitlen) {
-  return evj_pad_word(v, q, E, F, bitlen);
-}
-// ... and into LDS, each tail padded to whole blocks (FIPS 180-4: 0x80,
-// zeros, the 64-bit bit length) so C reads whole blocks only
-__device__ __forceinline__ void evc_stage(uint32_t L, uint32_t u, const uint32_t *sLof, const uint32_t *sDesc,
-                                          const uint32_t pf[EVC_PF + EVC_PM], uint32_t *sBody, uint32_t *sMid) {
-  const uint32_t lo = sLof[L], w = sLof[L + 1] - lo, ws = w < EVC_SLOTS ? w : EVC_SLOTS;
-#pragma unroll
-  for (int r = 0; r < EVC_PF; r++) {
-    const uint32_t x = u + EVC_LT * r, i = x / EVC_SLOT_DW, k = x % EVC_SLOT_DW;
-    if (i >= ws) break;
-    const uint32_t *d = sDesc + EVC_DESC * (lo + i);
-    const uint32_t nb = d[4], len = d[5], sh = d[3] >> 24;
-    if (!evc_lds_event(i, nb, len)) continue;
-    const uint32_t nt = (uint32_t)sha256_nblocks(len) - nb, E = len - 64 * nb + sh;
-    if (k > 16 * nt) continue;  // 16 nt + 1 dwords: the realignment reads one past the last block
-    uint32_t v = k < (d[3] & 0xFFFFFFu) ? pf[r] : 0u;
-    if (4 * k + 4 > E) v = evc_pad(v, k, E, 64 * nt + sh, 8ull * len);
-    sBody[x] = v;
-  }
-#pragma unroll
-  for (int r = 0; r < EVC_PM; r++) {
-    const uint32_t x = u + EVC_LT * r;
-    if (x / 8 >= ws) break;
-    sMid[x] = pf[EVC_PF + r];
-  }
-}
-// the slower paths of phase D, out of line (keeps the chain's code small)
-__device__ __noinline__ void evc_hash_inline(uint32_t h[8], const uint32_t *src, uint32_t sh, uint32_t len,
-                                             uint32_t nb, uint32_t nblk) {
-  sha256_blocks(h, src, sh, len, nb, nblk);
-}
-__device__ __noinline__ void evc_hash_padded(uint32_t h[8], const uint32_t *slot, uint32_t sh, uint32_t nt) {
-  for (uint32_t j = 0; j < nt; j++) {
-    uint32_t w16[16];
-    sha256_block_words_padded(w16, slot + 16 * j, sh);
-    sha256_compress(h, w16);
-  }
-}
-// Diagnostic build only (-DBV_CHAIN_STAMPS, tools/chain_stamps.py): wave 0
-// lane 0 stamps s_memrealtime (100 MHz) at each phase boundary of the first
-// EVC_NSTAMP levels of a launch, kept in LDS and written out at the end.
-#ifdef BV_CHAIN_STAMPS
-#define EVC_NSTAMP 96
-__device__ uint64_t g_chain_stamps[5 * EVC_NSTAMP + 1];
-#define EVC_STAMP(L, k)                                                                   \
-  do {                                                                                    \
-    if (t == 0 && (L) < EVC_NSTAMP) sStamp[5 * (L) + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define EVC_STAMP(L, k) \
-  do {                  \
-  } while (0)
-#endif
-__global__ void __launch_bounds__(EVC_NT) k_ev_hash_chain(uint32_t l0, uint32_t l1,
-                                                        const uint32_t *__restrict__ level_off,
-                                                        const uint32_t *__restrict__ order,
-                                                        const uint32_t *__restrict__ posin, bv_event_batch b,
-                                                        const uint32_t *__restrict__ ppos, uint8_t *__restrict__ bodies,
-                                                        const uint64_t *__restrict__ offs,
-                                                        const uint32_t *__restrict__ mid, uint32_t *__restrict__ dig) {
-  // double-buffered (level L in buffer L & 1): waves 1-3 stage level L+1
-  // while wave 0 runs level L's rounds
-  __shared__ uint32_t sBodyB[2 * EVC_SLOTS * EVC_SLOT_DW];  // 64 KB: body tails
-  __shared__ uint32_t sMidB[2 * EVC_SLOTS * 8];             //  4 KB: midstates
-  __shared__ uint32_t sDig[EVC_CAP * 8];                    // 24 KB: digests hashed in this launch
-  __shared__ uint32_t sDesc[EVC_CAP * EVC_DESC];            // 36 KB: per-event descriptors
-  // 14 KB: W+K schedules of the level, [block][16-byte chunk][event][4]
-  // (lanes in lockstep read distinct banks)
-  __shared__ uint32_t sWK[EVC_WEV * EVC_WBLK * 64];
-  __shared__ uint32_t sLof[EVC_CAP + 1];               // level offsets, relative to the launch
-#ifdef BV_CHAIN_STAMPS
-  __shared__ uint64_t sStamp[5 * EVC_NSTAMP];
-#endif
-  const uint32_t t = threadIdx.x;
-  const uint32_t E0 = level_off[l0], E1 = level_off[l1], nl = l1 - l0;
-  const uint32_t *bw = (const uint32_t *)bodies;
-  // ---- prologue: level offsets and descriptors, all lanes in parallel
-  for (uint32_t x = t; x <= nl; x += EVC_NT) sLof[x] = level_off[l0 + x] - E0;
-  for (uint32_t s = t; s < E1 - E0; s += EVC_NT) {
-    const uint32_t e = order[E0 + s];
-    const uint64_t o = offs[e], len = offs[e + 1] - o;
-    const uint32_t nb = mid[(uint64_t)EV_MID_U32 * e + 8];
-    const uint64_t a0 = (o + 64ull * nb) >> 2, nd = ((o + len + 8 + 3) >> 2) - a0;  // + the 8-byte over-read pad
-    uint32_t *d = sDesc + EVC_DESC * s;
-    d[0] = e;
-    d[1] = (uint32_t)a0;
-    d[2] = (uint32_t)(a0 >> 32);
-    d[3] = (uint32_t)(nd < 0xFFFFFFu ? nd : 0xFFFFFFu) | (uint32_t)(o & 3) << 24;
-    d[4] = nb;
-    d[5] = (uint32_t)len;
-    for (int p = 0; p < 2; p++) {
-      const uint32_t pos = ppos[2 * e + p];
-      const uint32_t q = pos == EVJ_NOPOS ? 0u : (uint32_t)b.parent_ref[2 * e + p];
-      const uint32_t sq = pos == EVJ_NOPOS ? 0u : posin[q];
-      d[6 + p] = pos == EVJ_NOPOS ? EVJ_NOPOS : (uint32_t)(o + pos - 4 * a0);
-      d[8 + p] = (pos != EVJ_NOPOS && sq >= E0 && sq < E1) ? sq - E0 : EVJ_NOPOS;
-      d[10 + p] = q;
-    }
-  }
-  __syncthreads();
-  uint32_t pf[EVC_PF + EVC_PM];
-  if (t >= 64) {  // level 0 staged up front, level 1's loads issued
-    evc_load(0, nl, t - 64, sLof, sDesc, bw, mid, pf);
-    evc_stage(0, t - 64, sLof, sDesc, pf, sBodyB, sMidB);
-    evc_load(1, nl, t - 64, sLof, sDesc, bw, mid, pf);
-  }
-  __syncthreads();
-  for (uint32_t L = 0; L < nl; L++) {
-    const uint32_t lo = sLof[L], w = sLof[L + 1] - lo;
-    uint32_t *sBody = sBodyB + (L & 1) * EVC_SLOTS * EVC_SLOT_DW, *sMid = sMidB + (L & 1) * EVC_SLOTS * 8;
-    EVC_STAMP(L, 0);
-    // ---- B: parents' hex into the tails, one lane per (event, parent), on
-    // waves 1-3 first (wave 0 stays free for the rounds)
-    for (uint32_t x = (t + EVC_NT - 64) % EVC_NT; x < 2 * w; x += EVC_NT) {
-      const uint32_t i = x >> 1, p = x & 1;
-      const uint32_t *d = sDesc + EVC_DESC * (lo + i);
-      const uint32_t rel = d[6 + p];
-      if (rel == EVJ_NOPOS) continue;
-      const uint32_t ps = d[8 + p], q = d[10 + p];
-      uint32_t wd[8];  // unrolled: a dynamically indexed array would live in scratch
-      if (ps != EVJ_NOPOS) {  // separate loads: a selected pointer would be a FLAT access
-#pragma unroll
-        for (int k = 0; k < 8; k++) wd[k] = sDig[8 * ps + k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; k++) wd[k] = dig[8 * (uint64_t)q + k];
-      }
-      if (evc_lds_event(i, d[4], d[5])) {
-        uint32_t hx[16];
-        evj_hex32_words(hx, wd);
-        evj_put64(sBody + i * EVC_SLOT_DW, rel, hx);
-      } else {
-        const uint64_t a0 = (uint64_t)d[1] | ((uint64_t)d[2] << 32);
-        uint8_t dd[32];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-#pragma unroll
-          for (int c = 0; c < 4; c++) dd[4 * k + c] = (uint8_t)(wd[k] >> (8 * c));  // words hold BE digest bytes
-        evj_hex32(bodies + 4 * a0 + rel, dd);  // hashed from HBM in D
-      }
-    }
-    __syncthreads();
-    EVC_STAMP(L, 1);
-    // ---- D0 (wave 0) beside C (waves 1-3): the first tail block of each
-    // LDS event runs its rounds 16 at a time on wave 0 (one lane per event)
-    // while waves 1-3 expand the W+K schedules of all the event's blocks
-    // into LDS in chunks of 16 words (one lane per (event, block)), a
-    // barrier between chunks: rounds 0-15 need only the message words,
-    // rounds 16c.. the chunk expanded during the previous 16 rounds.  D1
-    // then runs rounds 48-63 and the later blocks from LDS.  (Round 2 ran
-    // the first block with its schedule inline on wave 0: 4.1 us per level;
-    // one lane's whole expansion before the rounds: ~1.5-2 us.)
-    static_assert(EVC_WEV * EVC_WBLK <= EVC_NT - 64, "one schedule lane per (event, block)");
-    const uint32_t wv = w < EVC_WEV ? w : EVC_WEV;
-    uint32_t h0[8], s0[8];
-    const bool r0 = t < wv && evc_lds_event(t, sDesc[EVC_DESC * (lo + t) + 4], sDesc[EVC_DESC * (lo + t) + 5]);
-    if (r0) {
-#pragma unroll
-      for (int k = 0; k < 8; k++) s0[k] = h0[k] = sMid[8 * t + k];
-      uint32_t w16[16];
-      sha256_block_words_padded(w16, sBody + t * EVC_SLOT_DW, sDesc[EVC_DESC * (lo + t) + 3] >> 24);
-      sha256_rounds_first16(s0, w16);
-    }
-    uint32_t xs[16];
-    uint32_t *wkp = nullptr;
-    if (t >= 64 && t - 64 < wv * EVC_WBLK) {
-      const uint32_t i = (t - 64) / EVC_WBLK, j = (t - 64) % EVC_WBLK;
-      const uint32_t *d = sDesc + EVC_DESC * (lo + i);
-      const uint32_t nb = d[4], len = d[5];
-      if (evc_lds_event(i, nb, len) && j < (uint32_t)sha256_nblocks(len) - nb) {
-        sha256_block_words_padded(xs, sBody + i * EVC_SLOT_DW + 16 * j, d[3] >> 24);
-        wkp = sWK + (j * 16 * EVC_WEV + i) * 4;
-        sha256_schedule_chunk(xs, wkp, 4 * EVC_WEV, 0);
-        sha256_schedule_chunk(xs, wkp, 4 * EVC_WEV, 1);
-      }
-    }
-    __syncthreads();
-    if (r0) sha256_rounds16_wk(s0, sWK + t * 4, 4 * EVC_WEV, 16);
-    if (wkp) sha256_schedule_chunk(xs, wkp, 4 * EVC_WEV, 2);
-    __syncthreads();
-    if (r0) sha256_rounds16_wk(s0, sWK + t * 4, 4 * EVC_WEV, 32);
-    if (wkp) sha256_schedule_chunk(xs, wkp, 4 * EVC_WEV, 3);
-    __syncthreads();
-    EVC_STAMP(L, 2);
-    // ---- A (waves 1-3, beside D1): level L+1's tails and midstates into the
-    // other buffer (its loads were issued during level L-1), then the loads
-    // for level L+2.  Only when level L has <= 64 events: then D runs on
-    // wave 0 alone and waves 1-3 are free.
-    const bool beside = w <= 64;
-    if (beside && t >= 64 && L + 1 < nl) {
-      evc_stage(L + 1, t - 64, sLof, sDesc, pf, sBodyB + ((L + 1) & 1) * EVC_SLOTS * EVC_SLOT_DW,
-                sMidB + ((L + 1) & 1) * EVC_SLOTS * 8);
-      evc_load(L + 2, nl, t - 64, sLof, sDesc, bw, mid, pf);
-    }
-    // ---- D1: the rounds (the serial part)
-    for (uint32_t i = t; i < w; i += EVC_NT) {
-      const uint32_t *d = sDesc + EVC_DESC * (lo + i);
-      const uint32_t sh = d[3] >> 24, nb = d[4], len = d[5];
-      const uint32_t nblk = (uint32_t)sha256_nblocks(len);
-      uint32_t wd[8];
-      if (i < EVC_WEV && evc_lds_event(i, nb, len)) {
-        // the common path stays in registers (the out-of-line paths below
-        // take their state by pointer, which would put it in scratch)
-        sha256_rounds16_wk(s0, sWK + i * 4, 4 * EVC_WEV, 48);
-#pragma unroll
-        for (int k = 0; k < 8; k++) h0[k] += s0[k];
-        for (uint32_t j = 1; j < nblk - nb; j++) sha256_rounds_wk(h0, sWK + (j * 16 * EVC_WEV + i) * 4, 4 * EVC_WEV);
-        ev_digest_words(wd, h0);
-      } else {
-        uint32_t hm[8];
-        if (i < EVC_SLOTS) {
-#pragma unroll
-          for (int k = 0; k < 8; k++) hm[k] = sMid[8 * i + k];
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; k++) hm[k] = mid[(uint64_t)EV_MID_U32 * d[0] + k];
-        }
-        if (evc_lds_event(i, nb, len))  // in LDS, schedule inline (padded: whole blocks)
-          evc_hash_padded(hm, sBody + i * EVC_SLOT_DW, sh, nblk - nb);
-        else
-          evc_hash_inline(hm, bw + ((uint64_t)d[1] | ((uint64_t)d[2] << 32)), sh, len, nb, nblk);
-        ev_digest_words(wd, hm);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) sDig[8 * (lo + i) + k] = wd[k];
-    }
-    EVC_STAMP(L, 3);
-    if (!beside && L + 1 < nl) {  // a wide level: stage the next one after its rounds
-      __syncthreads();
-      if (t >= 64) {
-        evc_stage(L + 1, t - 64, sLof, sDesc, pf, sBodyB + ((L + 1) & 1) * EVC_SLOTS * EVC_SLOT_DW,
-                  sMidB + ((L + 1) & 1) * EVC_SLOTS * 8);
-        evc_load(L + 2, nl, t - 64, sLof, sDesc, bw, mid, pf);
-      }
-    }
-    __syncthreads();
-    EVC_STAMP(L, 4);
-  }
-  // ---- epilogue: the digests to HBM
-  for (uint32_t x = t; x < (E1 - E0) * 8; x += EVC_NT) dig[8 * (uint64_t)sDesc[EVC_DESC * (x / 8)] + x % 8] = sDig[x];
-#ifdef BV_CHAIN_STAMPS
-  for (uint32_t x = t; x < 5 * (nl < EVC_NSTAMP ? nl : EVC_NSTAMP); x += EVC_NT) g_chain_stamps[x] = sStamp[x];
-  if (t == 0) g_chain_stamps[5 * EVC_NSTAMP] = nl;
-#endif
 }
 
 __global__ void __launch_bounds__(256) k_iota(uint64_t n, uint32_t *__restrict__ out) {
@@ -919,37 +571,11 @@ hipError_t ev_build(hipStream_t st, const bv_event_batch &b, uint64_t e0, uint64
   return hipGetLastError();
 }
 
-hipError_t ev_hash(hipStream_t st, uint64_t count, const uint32_t *list, uint64_t e0, const bv_event_batch &b,
-                   const uint32_t *ppos, uint8_t *bodies, const uint64_t *offs, uint32_t *dig) {
+hipError_t ev_hash(hipStream_t st, uint64_t count, uint64_t e0, uint8_t *bodies, const uint64_t *offs, uint32_t *dig) {
   if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ev_hash, grid1(count, 256), dim3(256), 0, st, count, list, e0, b, ppos, bodies, offs, dig);
+  hipLaunchKernelGGL(k_ev_hash, grid1(count, 256), dim3(256), 0, st, count, e0, bodies, offs, dig);
   return hipGetLastError();
 }
-
-hipError_t ev_mid(hipStream_t st, uint64_t count, const uint32_t *list, const uint8_t *bodies, const uint64_t *offs,
-                  const uint32_t *ppos, uint32_t *mid) {
-  if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ev_mid, grid1(count, 256), dim3(256), 0, st, count, list, bodies, offs, ppos, mid);
-  return hipGetLastError();
-}
-
-hipError_t ev_hash_chain(hipStream_t st, uint32_t l0, uint32_t l1, const uint32_t *level_off, const uint32_t *order,
-                         const uint32_t *posin, const bv_event_batch &b, const uint32_t *ppos, uint8_t *bodies,
-                         const uint64_t *offs, const uint32_t *mid, uint32_t *dig) {
-  if (l1 <= l0) return hipSuccess;
-  hipLaunchKernelGGL(k_ev_hash_chain, dim3(1), dim3(EVC_NT), 0, st, l0, l1, level_off, order, posin, b, ppos, bodies,
-                     offs, mid, dig);
-  return hipGetLastError();
-}
-
-#ifdef BV_CHAIN_STAMPS
-}  // namespace bvk
-// the last chain launch's stamps (diagnostic build): out[5 L + k], then nl
-extern "C" int bv_debug_chain_stamps(uint64_t *out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_stamps), sizeof(g_chain_stamps)) == hipSuccess ? 0 : -4;
-}
-namespace bvk {
-#endif
 
 hipError_t iota(hipStream_t st, uint64_t n, uint32_t *out) {
   if (n == 0) return hipSuccess;

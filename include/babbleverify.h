@@ -195,9 +195,12 @@ int bv_sync(bv_ctx *ctx);
  * hashes it and verifies the creator's signature over it.  A parent may be an
  * EARLIER event of the same batch (the in-batch DAG dependency of core.sync,
  * core.go:214-245): its "0X"+hex is spliced into the child's body once the
- * parent's digest is known, level by level on the device (one launch for the
- * narrow levels of a SyncResponse).  ~2-3x fewer bytes cross PCIe than the
- * serialized bodies (64-B tx: ~250 B per event instead of ~530).
+ * parent's digest is known.  Such a batch (a SyncResponse) is built and
+ * hashed in topological order on the host while the device decodes the keys,
+ * builds the key tables and inverts s; then only the digests cross PCIe and
+ * the device verifies.  Batches without in-batch parents are built and hashed
+ * on the device; ~2-3x fewer bytes cross PCIe than the serialized bodies
+ * (64-B tx: ~250 B per event instead of ~530).
  * Per-event result: msg_hash (the body digest = Event.Hash) and status of the
  * event signature (keys.Verify as composed by Event.Verify, event.go:232-247).
  * InternalTransactions are serialized from the verbatim fragment but their

@@ -258,11 +258,6 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
   return mode;
 }
 
-// s^-1 mod N through the device chain (Montgomery in/out handled here).
-// bv_verify_events' body construction and DAG hashing on the host (the
-// device kernels' per-event code, evjson.h + sha256.h), in event order
-// (parents precede children).  bodies: sum of lengths + 64 bytes; offs:
-// n + 1; digests: 32 * n.  Returns the total body bytes.
 // The product's host DAG hasher (hostdag.cpp) over a batch: levels and order
 // as bv_events.cpp computes them; `threads` > 1 runs the parallel steps on
 // that many threads; `portable` selects the portable SHA-256 compressor.
@@ -306,6 +301,11 @@ void emu_host_sha256(const uint8_t *msg, uint64_t len, uint8_t *out, int portabl
 
 int emu_host_sha_accelerated() { return hsha::accelerated(); }
 
+// bv_verify_events' body construction (the device kernels' per-event code,
+// evjson.h) and hashing (sha256.h), in event order (parents precede
+// children): the in-batch parents' hex spliced in once their digests exist.
+// bodies: sum of lengths + 64 bytes; offs: n + 1; digests: 32 * n.  Returns
+// the total body bytes.
 uint64_t emu_ev_bodies(const bv_event_batch *b, uint8_t *bodies, uint64_t cap, uint64_t *offs, uint8_t *digests) {
   const uint64_t n = b->n_events;
   std::vector<uint32_t> ppos(2 * n);
@@ -314,40 +314,13 @@ uint64_t emu_ev_bodies(const bv_event_batch *b, uint8_t *bodies, uint64_t cap, u
   if (offs[n] + 64 > cap) return 0;
   memset(bodies + offs[n], 0, 64);
   for (uint64_t e = 0; e < n; e++) evj_write(*b, e, bodies + offs[e]);
-  std::vector<uint32_t> dig(8 * n + 8);
-  // as k_ev_mid + k_ev_hash_chain: midstates over the placeholder bodies,
-  // then per event (parents first) the tail staged into a separate buffer
-  // (the LDS slot), the parents' hex spliced into the body and the slot, and
-  // the tail compressed from the slot starting at the midstate
-  std::vector<uint32_t> mid((size_t)EV_MID_U32 * n);
-  for (uint64_t e = 0; e < n; e++) ev_midstate(e, bodies, offs, ppos.data(), mid.data());
-  std::vector<uint32_t> slot;
   for (uint64_t e = 0; e < n; e++) {
-    const uint64_t o = offs[e], len = offs[e + 1] - o;
-    const uint32_t nb = mid[(size_t)EV_MID_U32 * e + 8];
-    const uint64_t a0 = (o + 64ull * nb) >> 2, nd = ((offs[e + 1] + 8 + 3) >> 2) - a0;
-    slot.assign(nd, 0);
-    memcpy(slot.data(), bodies + 4 * a0, 4 * nd);
     for (int p = 0; p < 2; p++)
-      if (ppos[2 * e + p] != EVJ_NOPOS) {
-        const uint32_t *wd = &dig[8 * b->parent_ref[2 * e + p]];
-        evj_hex32(bodies + o + ppos[2 * e + p], (const uint8_t *)wd);
-        uint32_t hx[16];  // the device's LDS splice: SWAR hex words, aligned dword stores
-        evj_hex32_words(hx, wd);
-        evj_put64(slot.data(), (uint32_t)(o + ppos[2 * e + p] - 4 * a0), hx);
-      }
+      if (ppos[2 * e + p] != EVJ_NOPOS) evj_hex32(bodies + offs[e] + ppos[2 * e + p], digests + 32 * b->parent_ref[2 * e + p]);
     uint32_t h[8];
-    for (int k = 0; k < 8; k++) h[k] = mid[(size_t)EV_MID_U32 * e + k];
-    // as the device: per block the W+K schedule, then the rounds
-    for (uint64_t j = nb; j < sha256_nblocks(len); j++) {
-      uint32_t w[16], wk[64 * 3];  // interleaved layout as the device's (stride 12 here)
-      sha256_block_words(w, slot.data(), (uint32_t)(o & 3), len, nb, j);
-      sha256_schedule_wk(wk + 4, w, 12);
-      sha256_rounds_wk(h, wk + 4, 12);
-    }
-    ev_digest_words(&dig[8 * e], h);
+    sha256_msg(h, bodies, offs[e], offs[e + 1] - offs[e]);
+    for (int k = 0; k < 32; k++) digests[32 * e + k] = (uint8_t)(h[k / 4] >> (24 - 8 * (k % 4)));
   }
-  memcpy(digests, dig.data(), 32 * n);
   return offs[n];
 }
 

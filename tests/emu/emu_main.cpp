@@ -12,9 +12,17 @@
 // msg_len, key_len, has_pre; then msg_off[n_msgs+1] u64, msg_bytes,
 // key_off[n_keys+1] u64, key_bytes, item_msg u32[n], item_key u32[n],
 // r_be[32n], s_be[32n], pre[n] (if has_pre).
+//
+// `emu_asan dag <seed> [n]`: a random event wire batch (keys of 0 / 33 / 65 /
+// 70 bytes, nil and empty transaction lists, nil transactions, ITX and
+// BlockSignature fragments, no / known-hash / in-batch parents) in
+// exactly-sized heap buffers; the product's host DAG hasher (hostdag.cpp,
+// hostsha.cpp) on 1 and 4 threads and with the portable compressor must give
+// the digests of the plain in-order build (emu_ev_bodies).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include "../../include/babbleverify.h"
@@ -25,6 +33,8 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
 int oracle_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint64_t *accept_bits,
                         int n_threads);
 void oracle_init(void);
+void emu_host_dag_hash(const bv_event_batch *b, uint8_t *digests, int threads, int portable);
+uint64_t emu_ev_bodies(const bv_event_batch *b, uint8_t *bodies, uint64_t cap, uint64_t *offs, uint8_t *digests);
 }
 
 namespace {
@@ -35,9 +45,114 @@ bool rd(FILE *f, std::vector<T> &v, uint64_t n) {
   return n == 0 || fread(v.data(), sizeof(T), n, f) == n;
 }
 
+struct Rng {
+  uint64_t x;
+  uint64_t next() {
+    x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+    return x;
+  }
+  uint64_t below(uint64_t n) { return next() % n; }
+};
+
+// every array in its own exactly-sized heap block (ASan sees any over-read)
+template <class T>
+T *exact(const std::vector<T> &v, std::vector<std::unique_ptr<char[]>> &keep) {
+  if (v.empty()) return nullptr;
+  keep.emplace_back(new char[v.size() * sizeof(T)]);
+  memcpy(keep.back().get(), v.data(), v.size() * sizeof(T));
+  return (T *)keep.back().get();
+}
+
+int dag_main(uint64_t seed, uint64_t n) {
+  Rng r{seed * 0x9E3779B97F4A7C15ull + 1};
+  std::vector<uint64_t> key_off{0};
+  std::vector<uint8_t> keys;
+  const int lens[4] = {0, 33, 65, 70};
+  for (int k = 0; k < 6; k++) {
+    const int L = lens[r.below(4)];
+    for (int i = 0; i < L; i++) keys.push_back((uint8_t)r.next());
+    key_off.push_back(keys.size());
+  }
+  std::vector<uint32_t> creator(n);
+  std::vector<int64_t> index(n), ts(n);
+  std::vector<uint8_t> pkind(2 * n), tx_list_nil(n), tx_nil, tx_bytes, phash, itx, bsig;
+  std::vector<uint64_t> pref(2 * n), tx_start{0}, tx_off{0}, itx_off{0}, bsig_off{0};
+  for (uint64_t e = 0; e < n; e++) {
+    creator[e] = (uint32_t)r.below(6);
+    index[e] = (int64_t)r.next() >> r.below(64);
+    ts[e] = (int64_t)r.next() >> r.below(64);
+    for (int p = 0; p < 2; p++) {
+      const uint64_t c = r.below(10);
+      if (c < 2 || e == 0) {
+        pkind[2 * e + p] = BV_PARENT_NONE;
+      } else if (c < 5) {
+        pkind[2 * e + p] = BV_PARENT_HASH;
+        pref[2 * e + p] = phash.size() / 32;
+        for (int i = 0; i < 32; i++) phash.push_back((uint8_t)r.next());
+      } else {
+        pkind[2 * e + p] = BV_PARENT_EVENT;
+        pref[2 * e + p] = e - 1 - r.below(e < 8 ? e : 8);
+      }
+    }
+    tx_list_nil[e] = r.below(8) == 0;
+    const uint64_t ntx = tx_list_nil[e] ? 0 : r.below(4);
+    for (uint64_t t = 0; t < ntx; t++) {
+      tx_nil.push_back(r.below(10) == 0);
+      const uint64_t L = r.below(200);
+      for (uint64_t i = 0; i < L; i++) tx_bytes.push_back((uint8_t)r.next());
+      tx_off.push_back(tx_bytes.size());
+    }
+    tx_start.push_back(tx_off.size() - 1);
+    const uint64_t il = r.below(6) == 0 ? 1 + r.below(90) : 0, bl = r.below(6) == 0 ? 1 + r.below(90) : 0;
+    for (uint64_t i = 0; i < il; i++) itx.push_back((uint8_t)(' ' + r.below(90)));
+    for (uint64_t i = 0; i < bl; i++) bsig.push_back((uint8_t)(' ' + r.below(90)));
+    itx_off.push_back(itx.size());
+    bsig_off.push_back(bsig.size());
+  }
+  std::vector<std::unique_ptr<char[]>> keep;
+  bv_event_batch b{};
+  b.n_events = n;
+  b.n_keys = 6;
+  b.key_bytes = exact(keys, keep);
+  b.key_off = exact(key_off, keep);
+  b.creator = exact(creator, keep);
+  b.index = exact(index, keep);
+  b.timestamp = exact(ts, keep);
+  b.parent_kind = exact(pkind, keep);
+  b.parent_ref = exact(pref, keep);
+  b.n_parent_hashes = phash.size() / 32;
+  b.parent_hashes = exact(phash, keep);
+  b.tx_start = exact(tx_start, keep);
+  b.tx_off = exact(tx_off, keep);
+  b.tx_bytes = exact(tx_bytes, keep);
+  b.tx_list_nil = exact(tx_list_nil, keep);
+  b.tx_nil = exact(tx_nil, keep);
+  b.itx_off = exact(itx_off, keep);
+  b.itx_json = exact(itx, keep);
+  b.bsig_off = exact(bsig_off, keep);
+  b.bsig_json = exact(bsig, keep);
+  const uint64_t cap = 4096 * n + 4 * tx_bytes.size() + itx.size() + bsig.size() + 4096;
+  std::vector<uint8_t> bodies(cap), want(32 * n), got(32 * n);
+  std::vector<uint64_t> offs(n + 1);
+  if (!emu_ev_bodies(&b, bodies.data(), cap, offs.data(), want.data())) return 2;
+  int bad = 0;
+  for (int threads : {1, 4})
+    for (int portable : {0, 1}) {
+      std::fill(got.begin(), got.end(), 0);
+      emu_host_dag_hash(&b, got.data(), threads, portable);
+      const bool eq = memcmp(got.data(), want.data(), 32 * n) == 0;
+      printf("dag threads %d portable %d: %s (%llu events)\n", threads, portable, eq ? "equal" : "MISMATCH",
+             (unsigned long long)n);
+      bad += !eq;
+    }
+  return bad ? 1 : 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
+  if (argc >= 3 && strcmp(argv[1], "dag") == 0)
+    return dag_main(strtoull(argv[2], nullptr, 10), argc > 3 ? strtoull(argv[3], nullptr, 10) : 700);
   if (argc < 2) {
     fprintf(stderr, "usage: %s batch.bin [threads]\n", argv[0]);
     return 2;

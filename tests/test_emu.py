@@ -156,3 +156,10 @@ def test_asan_ubsan_emulator(tmp_path):
                            env={"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "PATH": "/usr/bin:/bin"})
         assert r.returncode == 0, r.stdout + r.stderr
         assert r.stdout.count("equal") == 3 and "MISMATCH" not in r.stdout, r.stdout
+    # the product's host DAG hasher (hostdag.cpp + hostsha.cpp) under the
+    # sanitizers on random wire batches in exactly-sized buffers
+    for seed in (1, 2, 3):
+        r = subprocess.run([exe, "dag", str(seed), "700"], capture_output=True, text=True, timeout=600,
+                           env={"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "PATH": "/usr/bin:/bin"})
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert r.stdout.count("equal") == 4 and "MISMATCH" not in r.stdout, r.stdout

@@ -183,8 +183,10 @@ def test_verify_events_chunk_boundaries(monkeypatch):
 
 @pytest.mark.gpu
 def test_verify_events_sync_sized_dag_depth():
-    """A SyncLimit-sized batch (config.go:44) from 4 creators: ~250 DAG
-    levels hashed on the device (narrow levels in one launch)."""
+    """A SyncLimit-sized batch (config.go:44) from 4 creators: 333 DAG levels
+    of 3, bodies built and hashed in topological order on the host
+    (hostdag.cpp) while the device verifies: digests and statuses equal the
+    oracle's over the generator's bodies."""
     from babble_amd.verifier import Verifier
     from oracle import coracle
 

