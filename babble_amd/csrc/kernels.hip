@@ -1,20 +1,23 @@
 // kernels.hip — gfx950 kernels of the batch verifier (per-unit work lives in
-// verify_core.h).
+// verify_core.h; bv_api.cpp drives them).
 //
-// Pipeline for one batch (bv_api.cpp drives it; two streams):
-//   main stream                               keys stream
-//   k_key_decode  (Unmarshal, public_key.go:14)   sinv stream
-//        |--------- fork ------------------>  k_table_bases  B_j = 2^(8j) Q
-//   k_sha256      (crypto.SHA256, hash.go:8)  k_table_fill<8> d * B_j, affine
-//        |<-- join -- k_sinv (batched s^-1,         |
-//                     needs only s)                 |
-//   k_verify_g    (u1, u2, GLV split; R_G = u1 G,   |
-//                  16 adds from the G table)        |
-//        |<-------- join ------------------------- -+
-//   k_verify_q    (R = R_G + u2 Q, 32 adds from the key's table; decision
-//                  table; x(R) mod N == r; status + __ballot accept bits)
-// k_verify_generic replaces g/q when keys carry too few items for a table.
-// The G table (k_table_bases + k_table_fill<16>) is built once per context.
+// One batch (streams owned by the library, one set per device):
+//   lane (the call's)            s^-1 stream                keys stream (high priority)
+//   k_sha256 (hash.go:8)         k_key_decode (Unmarshal,
+//        |                         public_key.go:14)  ---> k_table_bases  2^(L k) Q, serial
+//        |                       k_sinv (batched s^-1)      k_table_fill   sub-tables
+//        |<------ join ---------------'                     k_table_pair   chord sums
+//   k_verify_g   u1, u2, GLV split; R_G = u1 G: 9 XYZZ adds from the    |
+//                26-bit signed G table (10 windows)                      |
+//        |<------ join ----------------------------------------------------'
+//   k_verify_q   R = R_G + k1 Q + k2 phi(Q): 22 adds from the key's K12
+//                (12-bit signed, GLV) tables; decision table; X == r ZZ;
+//                status + __ballot accept bits
+// Key cache (BV_F_KEY_CACHE): the validator's KC tables (22-bit signed
+// windows, built once by k_table_pair_kc) replace the keys stream and
+// k_verify_gq does g + q in one pass.  k_verify_generic covers keys with too
+// few items for a table.  The G table (k_table_pair_g, 21.5 GB) is built once
+// per process and device.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

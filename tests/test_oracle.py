@@ -118,3 +118,17 @@ def test_btcec_port_equals_oracle():
     _, st, _ = coracle.verify_batch(d, n_threads=4)
     assert np.array_equal(coracle.port_verify_batch(d, n_threads=4), st)
     assert len(set(st.tolist())) == 4
+
+
+def test_reference_usage_keys_are_off_curve():
+    """docs/usage.rst:166-181 of the reference: four
+    "0x"-prefixed PubKeyHex values; DecodeFromString gives 65 bytes with
+    prefix 0x04, but no point of secp256k1 — both oracles and the product's
+    host hex decoder agree."""
+    from babble_amd import native
+
+    for pk in load("reference_usage_peers.json")["peers"]:
+        b = gs.DecodeFromString(pk["PubKeyHex"])
+        assert len(b) == 65 and b[0] == 4 and gs.Unmarshal(b) is None
+        assert coracle.lib().oracle_unmarshal(b, 65, None) == 0
+        assert native.hex_decode(pk["PubKeyHex"]) == b

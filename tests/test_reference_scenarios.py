@@ -259,3 +259,39 @@ def test_decode_signature_error_passes_through_unchanged(v):
         ev.Signature = sig
         ev._hash = None
         assert H.insert_event_verify(ev, verifier=v) == "wrong number of values in signature: got %d, want 2" % parts
+
+
+def test_reference_usage_peers_keys_panic_on_device(v):
+    """the four PubKeyHex values of the reference's own
+    docs/usage.rst:166-181 (lowercase "0x" prefix) are reference-held
+    vectors for common.DecodeFromString -> keys.ToPublicKey: each decodes
+    (bv_hex_decode) to 65 bytes with prefix 0x04 but lies off the curve, so
+    elliptic.Unmarshal leaves X nil and ecdsa.Verify panics in ScalarMult
+    for any item whose r and s pass the range checks (REF_PANIC); items
+    stopped earlier keep their earlier outcome (r = 0: REJECT; parts != 2:
+    REJECT_ERR).  Statuses equal the C oracle's."""
+    from babble_amd.batch import BatchBuilder
+    from oracle import coracle
+    from tests.helpers import load
+
+    peers = load("reference_usage_peers.json")["peers"]
+    sg = Signer(181)
+    bb = BatchBuilder()
+    want = []
+    for p in peers:
+        pub = native.hex_decode(p["PubKeyHex"])
+        assert pub == gs.DecodeFromString(p["PubKeyHex"]) and len(pub) == 65 and pub[0] == 4
+        assert gs.Unmarshal(pub) is None
+        k = bb.add_key(pub)
+        msg = p["Moniker"].encode()
+        d, _ = sg.key()
+        sig = sg.sign(d, hashlib.sha256(msg).digest())
+        m = bb.add_msg(msg)
+        for s, st in ((sig, native.REF_PANIC), ("0|" + sig.split("|")[1], native.REJECT), ("abc", native.REJECT_ERR)):
+            bb.add_item(m, k, s)
+            want.append(st)
+    b = bb.pack()
+    res = v.verify(b)
+    assert res.status.tolist() == want
+    _, st, _ = coracle.verify_batch(b.as_dict())
+    assert st.tolist() == want
