@@ -221,6 +221,11 @@ int bv_slot_begin(bv_ctx *ctx, hipStream_t st, const bv_batch *b, const bv_resul
   return BV_OK;
 }
 
+hipError_t bv_host_wait(bv_ctx *ctx, hipStream_t st) {
+  hipError_t e = hipEventRecord(ctx->ev_host, st);
+  return e != hipSuccess ? e : hipEventSynchronize(ctx->ev_host);
+}
+
 int bv_mark_done(bv_ctx *ctx, hipStream_t st) {
   HIPCHK(hipEventRecord(ctx->S().done, st), BV_E_LAUNCH, "event");
   HIPCHK(hipEventRecord(ctx->ev_done, st), BV_E_LAUNCH, "event");
@@ -383,6 +388,7 @@ static int create_impl(bv_ctx *ctx) {
   for (auto &sl : ctx->slot)
     for (auto &e : sl.ev) HIPCHK(hipEventCreate(&e), BV_E_NODEVICE, "hipEventCreate");
   HIPCHK(hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming), BV_E_NODEVICE, "hipEventCreate");
+  HIPCHK(hipEventCreateWithFlags(&ctx->ev_host, hipEventDisableTiming), BV_E_NODEVICE, "hipEventCreate");
   for (auto &sl : ctx->slot)
     HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), BV_E_NODEVICE, "hipEventCreate");
   ctx->chunk_ev.resize(64);
@@ -457,6 +463,7 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   for (auto &e : ctx->chunk_ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
+  if (ctx->ev_host) (void)hipEventDestroy(ctx->ev_host);
   streams_release(ctx);
   delete ctx->pool;
   delete ctx;
@@ -736,7 +743,7 @@ static int verify_device_impl(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dr
     std::vector<uint64_t> hko(nk + 1);
     HIPCHK(hipMemcpyAsync(hko.data(), dbatch->key_off, (nk + 1) * 8ull, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
            "d2h key_off");
-    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+    HIPCHK(bv_host_wait(ctx, st), BV_E_LAUNCH, "sync");
     if (hko[0] != 0) return bv_fail(ctx, BV_E_ARGS, "key_off[0] != 0");
     for (uint32_t k = 0; k < nk; k++)
       if (hko[k] > hko[k + 1]) return bv_fail(ctx, BV_E_ARGS, "key_off not monotone");
@@ -744,7 +751,7 @@ static int verify_device_impl(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dr
     if (hko[nk]) {
       HIPCHK(hipMemcpyAsync(hkb.data(), dbatch->key_bytes, hko[nk], hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
              "d2h key bytes");
-      HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+      HIPCHK(bv_host_wait(ctx, st), BV_E_LAUNCH, "sync");
     }
     int rc = bv_kc_prepare(ctx, nk, hkb.data(), hko.data(), dbatch->key_bytes, dbatch->key_off, st, &kc);
     if (rc != BV_OK) return rc;

@@ -89,6 +89,7 @@ struct bv_group {
   std::vector<nccl_comm> comms;
   bool logical = false;  // every entry of `devices` is the same device: no RCCL
   std::vector<DevBuf> send, recv;  // per device: shard bits, gathered bits
+  std::vector<hipEvent_t> sent;    // per device: its send buffer is written (recorded on its ctx's stream)
   std::vector<std::vector<uint64_t>> sub_off, sub_msg;
   std::string err;
   std::mutex mu;
@@ -109,6 +110,7 @@ extern "C" void bv_group_destroy(bv_group *g) {
       g_rccl.destroy(g->comms[i]);
     }
     (void)hipSetDevice(g->devices[i]);
+    if (i < g->sent.size() && g->sent[i]) (void)hipEventDestroy(g->sent[i]);
     if (i < g->send.size()) g->send[i].release();
     if (i < g->recv.size()) g->recv[i].release();
     bv_destroy(g->ctx[i]);
@@ -136,6 +138,12 @@ extern "C" int bv_group_create(bv_group **out, const int *devices, int n_devices
     }
     if (g->logical) c->kc_budget /= (uint64_t)n_devices;  // the shards share the device's HBM
     g->ctx.push_back(c);
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      bv_group_destroy(g);
+      return BV_E_NODEVICE;
+    }
+    g->sent.push_back(e);
   }
   g->send.resize(n_devices);
   g->recv.resize(n_devices);
@@ -187,6 +195,8 @@ extern "C" int bv_group_verify_batch(bv_group *g, const bv_batch *b, bv_result *
 
 static int group_verify(bv_group *g, const bv_batch *b, bv_result *res, GroupPlan &p) {
   const int D = (int)g->ctx.size();
+  if (b->n_items > UINT32_MAX || b->n_msgs > UINT32_MAX)  // the group plan indexes items and messages with u32
+    return gfail(g, BV_E_ARGS, "more than 2^32 items or messages in one group call");
   int rc = bv_validate_host_batch(g->ctx[0], b);
   if (rc != BV_OK) return gfail(g, rc, g->ctx[0]->err);
   bv_batch sorted;
@@ -245,7 +255,8 @@ static int group_verify(bv_group *g, const bv_batch *b, bv_result *res, GroupPla
       }
       const uint64_t sw = (sb[d].n_items + 63) / 64;
       if (hipMemsetAsync(g->send[d].p, 0, words * 8, c->stream) != hipSuccess ||
-          (sw && hipMemcpyAsync(g->send[d].p, c->S().bits.p, sw * 8, hipMemcpyDeviceToDevice, c->stream) != hipSuccess))
+          (sw && hipMemcpyAsync(g->send[d].p, c->S().bits.p, sw * 8, hipMemcpyDeviceToDevice, c->stream) != hipSuccess) ||
+          hipEventRecord(g->sent[d], c->stream) != hipSuccess)
         rcs[d] = BV_E_LAUNCH;
     });
   for (auto &t : th) t.join();
@@ -254,11 +265,12 @@ static int group_verify(bv_group *g, const bv_batch *b, bv_result *res, GroupPla
 
   if (g->logical) {
     // logical shards of one device: the gather is D copies into shard 0's
-    // buffer, on the device's lane 0 (every shard's ctx->stream), so each
-    // copy is ordered after that shard's bits
+    // buffer on shard 0's stream, each ordered after that shard's send
+    // buffer by its event (whatever stream the shard ran on)
     (void)hipSetDevice(g->devices[0]);
     for (int d = 0; d < D; d++)
-      if (hipMemcpyAsync((uint8_t *)g->recv[0].p + (size_t)d * words * 8, g->send[d].p, words * 8,
+      if (hipStreamWaitEvent(g->ctx[0]->stream, g->sent[d], 0) != hipSuccess ||
+          hipMemcpyAsync((uint8_t *)g->recv[0].p + (size_t)d * words * 8, g->send[d].p, words * 8,
                          hipMemcpyDeviceToDevice, g->ctx[0]->stream) != hipSuccess)
         return gfail(g, BV_E_LAUNCH, "gather shard bits");
   } else {

@@ -251,6 +251,7 @@ struct bv_ctx {
   Slot &S() { return slot[cur]; }
   std::vector<hipEvent_t> chunk_ev;
   hipEvent_t ev_done = nullptr;  // end of the last call's device work (both slots: bv_wait_all)
+  hipEvent_t ev_host = nullptr;  // host waits on this ctx's own work on a shared lane (bv_host_wait)
   bool has_done = false;
   bool table_mode = false;
   int key_w = 0;  // 8, 12 or 20 (KC) in table mode
@@ -296,6 +297,9 @@ hipStream_t bv_copy_stream(bv_ctx *ctx);   // the device's copy stream (created 
 int bv_drain(bv_ctx *ctx, hipStream_t st, int rc);
 int bv_wait_all(bv_ctx *ctx);              // host: every call's device work has finished
 int bv_mark_done(bv_ctx *ctx, hipStream_t st);
+// Wait on the host for the work this ctx has enqueued on `st` so far (an
+// event, not hipStreamSynchronize: the lanes are shared with other contexts)
+hipError_t bv_host_wait(bv_ctx *ctx, hipStream_t st);
 // Next slot for a device call writing `res`: st waits for the slot's last
 // call, and for the other slot's last call when their result ranges overlap.
 int bv_slot_begin(bv_ctx *ctx, hipStream_t st, const bv_batch *b, const bv_result *res);  // record the end of this call (its slot and ev_done)

@@ -140,7 +140,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
            BV_E_LAUNCH, "k_key_decode");
     std::vector<uint8_t> kst(n_keys);
     HIPCHK(hipMemcpyAsync(kst.data(), ctx->S().kstatus.p, n_keys, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h kst");
-    HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+    HIPCHK(bv_host_wait(ctx, st), BV_E_LAUNCH, "sync");
     ctx->S().kc_decoded = true;  // this batch's statuses and points are in the slot (bv_run_keys reuses them)
     for (uint32_t k : unknown) {
       const std::string key = key_of(k);
@@ -199,7 +199,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
     std::vector<int> fresh;
     bool launched = false;
     auto rollback = [&]() {
-      if (launched) (void)hipStreamSynchronize(st);  // enqueued builds may still write the tables
+      if (launched) (void)bv_host_wait(ctx, st);  // enqueued builds may still write the tables
       for (int si : fresh) {
         auto &s = ctx->kc_slots[si];
         if (s.table) {
@@ -252,7 +252,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
     for (size_t g0 = 0; g0 < admit.size(); g0 += G) {
       const uint32_t n = (uint32_t)std::min<size_t>(G, admit.size() - g0);
       uint64_t *tabs = (uint64_t *)ctx->S().pin_small.p;
-      if (launched && (e = hipStreamSynchronize(st)) != hipSuccess) return fail(BV_E_LAUNCH, "sync", e);  // pin_small reuse
+      if (launched && (e = bv_host_wait(ctx, st)) != hipSuccess) return fail(BV_E_LAUNCH, "sync", e);  // pin_small reuse
       for (uint32_t i = 0; i < n; i++) {
         const uint32_t k = admit[g0 + i];
         if ((e = hipMemcpyAsync(ctx->kc_kxy.as<uint8_t>() + 64ull * i, ctx->S().kxy.as<uint8_t>() + 64ull * k, 64,
@@ -277,7 +277,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
       ctx->kc_index[ctx->kc_slots[si].bytes] = si;
       ctx->kc_seen.erase(ctx->kc_slots[si].bytes);
     }
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return bv_fail(ctx, BV_E_LAUNCH, "sync", e);  // pin_small
+    if ((e = bv_host_wait(ctx, st)) != hipSuccess) return bv_fail(ctx, BV_E_LAUNCH, "sync", e);  // pin_small
   }
   for (uint32_t k = 0; k < n_keys; k++)
     if (alias[k] != k) slot_of[k] = slot_of[alias[k]];
@@ -331,6 +331,6 @@ extern "C" int bv_kc_register(bv_ctx *ctx, uint32_t n_keys, const uint8_t *key_b
   if (rc != BV_OK) return bv_drain(ctx, st, rc);
   rc = bv_mark_done(ctx, st);
   if (rc != BV_OK) return bv_drain(ctx, st, rc);
-  HIPCHK(hipStreamSynchronize(st), BV_E_LAUNCH, "sync");
+  HIPCHK(bv_host_wait(ctx, st), BV_E_LAUNCH, "sync");
   return BV_OK;
 }

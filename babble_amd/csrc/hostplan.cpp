@@ -121,6 +121,8 @@ void plan_group(const bv_batch *b, int D, GroupPlan &p, bv_batch &sorted) {
 extern "C" int bv_plan_group(const bv_batch *b, int n_shards, uint64_t *item_bounds, uint64_t *msg_bounds,
                              uint32_t *perm) {
   if (!b || n_shards <= 0 || !item_bounds || !msg_bounds) return BV_E_ARGS;
+  // the plan's permutation and sorted indices are u32 (item_msg is u32 too)
+  if (b->n_items > UINT32_MAX || b->n_msgs > UINT32_MAX) return BV_E_ARGS;
   if (b->n_items && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be)) return BV_E_ARGS;
   for (uint64_t i = 0; i < b->n_items; i++)
     if (b->item_msg[i] >= b->n_msgs) return BV_E_ARGS;

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../babble_amd/csrc/field.h"
+#include "../../babble_amd/csrc/point.h"
 
 // OP_ZSSM + k: component k of the zipped (x^2, y^2, x y) program;
 // OP_ZSSS + k: component k of the zipped (x^2, y^2, (x ^ y)^2) program
@@ -78,6 +79,52 @@ extern "C" int fc_run(int op, uint32_t n, const uint32_t *a, const uint32_t *b, 
   if (e == hipSuccess && n) e = hipMemcpy(r, dr, bytes, hipMemcpyDeviceToHost);
   (void)hipFree(da);
   (void)hipFree(db);
+  (void)hipFree(dr);
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
+// XYZZ mixed additions of the verify kernels (point.h gexz_add_ge and the
+// zipped gexz_add_ge_lat), exceptional cases included: acc = 33 words per
+// lane (X, Y, ZZ, ZZZ, inf flag), pts = 16 words (affine x2, y2); out = the
+// accumulator after acc += pt (P == Q doubles, P == -Q gives the
+// identity, the identity takes the point).
+__global__ void __launch_bounds__(256) k_xyzz(int lat, uint32_t n, const uint32_t *__restrict__ acc,
+                                              const uint32_t *__restrict__ pts, uint32_t *__restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  gexz R;
+  fe x, y;
+  const uint32_t *a = acc + 33 * (uint64_t)i, *q = pts + 16 * (uint64_t)i;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    R.X.v[k] = a[k], R.Y.v[k] = a[8 + k], R.ZZ.v[k] = a[16 + k], R.ZZZ.v[k] = a[24 + k];
+    x.v[k] = q[k], y.v[k] = q[8 + k];
+  }
+  bool inf = a[32] != 0;
+  if (lat) gexz_add_ge_lat(R, inf, x, y);
+  else gexz_add_ge(R, inf, x, y);
+  uint32_t *o = out + 33 * (uint64_t)i;
+#pragma unroll
+  for (int k = 0; k < 8; k++) o[k] = R.X.v[k], o[8 + k] = R.Y.v[k], o[16 + k] = R.ZZ.v[k], o[24 + k] = R.ZZZ.v[k];
+  o[32] = inf ? 1u : 0u;
+}
+
+extern "C" int fc_xyzz(int lat, uint32_t n, const uint32_t *acc, const uint32_t *pts, uint32_t *out) {
+  uint32_t *da = nullptr, *dp = nullptr, *dr = nullptr;
+  const size_t ab = (size_t)(n ? n : 1) * 33 * 4, pb = (size_t)(n ? n : 1) * 16 * 4;
+  hipError_t e = hipMalloc(&da, ab);
+  if (e == hipSuccess) e = hipMalloc(&dp, pb);
+  if (e == hipSuccess) e = hipMalloc(&dr, ab);
+  if (e == hipSuccess && n) e = hipMemcpy(da, acc, ab, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) e = hipMemcpy(dp, pts, pb, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) {
+    hipLaunchKernelGGL(k_xyzz, dim3((n + 255) / 256), dim3(256), 0, 0, lat, n, da, dp, dr);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess && n) e = hipMemcpy(out, dr, ab, hipMemcpyDeviceToHost);
+  (void)hipFree(da);
+  (void)hipFree(dp);
   (void)hipFree(dr);
   return e == hipSuccess ? 0 : -(int)e;
 }

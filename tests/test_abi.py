@@ -171,3 +171,25 @@ def test_host_alloc_fails_loudly_or_frees():
     buf = ctypes.create_string_buffer(16)
     L.bv_host_free(ctypes.cast(buf, ctypes.c_void_p))  # not ours: ignored
     assert native.lib().bv_last_stream(None) is None
+
+
+def test_plan_group_rejects_more_than_2_32_items():
+    """the group plan keeps its permutation and sorted indices in
+    u32; a batch claiming more than 2^32 items (or messages) is BV_E_ARGS
+    before any array is read (the arrays here are tiny on purpose)."""
+    import numpy as np
+
+    L = native.lib()
+    im = np.zeros(8, np.uint32)
+    rs = np.zeros((8, 32), np.uint8)
+    b = native.BvBatch()
+    b.n_msgs = 1
+    b.n_items = 2**32 + 5
+    b.item_msg = b.item_key = im.ctypes.data
+    b.r_be = b.s_be = rs.ctypes.data
+    ib = np.zeros(3, np.uint64)
+    mb = np.zeros(3, np.uint64)
+    assert L.bv_plan_group(ctypes.byref(b), 2, ib.ctypes.data, mb.ctypes.data, None) == native.BV_E_ARGS
+    b.n_items = 4
+    b.n_msgs = 2**32 + 1
+    assert L.bv_plan_group(ctypes.byref(b), 2, ib.ctypes.data, mb.ctypes.data, None) == native.BV_E_ARGS

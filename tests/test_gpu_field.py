@@ -181,3 +181,76 @@ def test_zipped_programs_match_python_ints(combo):
         r = _run(f"{combo}{k}", a, b)
         bad = [(hex(x), hex(y), hex(z)) for x, y, z in zip(a, b, r) if z >= 2**256 or (z - want[k](x, y)) % P]
         assert not bad, (k, bad[:5])
+
+
+def _ec_add(p1, p2):
+    """Affine secp256k1 addition over Python ints (None = identity)."""
+    if p1 is None:
+        return p2
+    if p2 is None:
+        return p1
+    (x1, y1), (x2, y2) = p1, p2
+    if x1 == x2 and (y1 + y2) % P == 0:
+        return None
+    if p1 == p2:
+        lam = 3 * x1 * x1 * pow(2 * y1, -1, P) % P
+    else:
+        lam = (y2 - y1) * pow(x2 - x1, -1, P) % P
+    x3 = (lam * lam - x1 - x2) % P
+    return x3, (lam * (x1 - x3) - y1) % P
+
+
+def _ec_mul(k, pt):
+    acc = None
+    for bit in bin(k)[2:]:
+        acc = _ec_add(acc, acc)
+        if bit == "1":
+            acc = _ec_add(acc, pt)
+    return acc
+
+
+@pytest.mark.parametrize("lat", [0, 1], ids=["gexz_add_ge", "gexz_add_ge_lat"])
+def test_xyzz_mixed_add_exceptional_cases(lat):
+    """the XYZZ mixed addition of the verify kernels (point.h,
+    madd-2008-s; the zipped latency variant too) on the device, against
+    Python integers, with the accumulator in random projective form (X = x
+    z^2, Y = y z^3, ZZ = z^2, ZZZ = z^3): generic sums, P + P (the
+    dbl-2008-s-1 doubling branch), P + (-P) (the identity) and the identity
+    plus a point.  Results compared as affine points (X / ZZ, Y / ZZZ)."""
+    G = (0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798,
+         0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8)
+    rng = random.Random(17 + lat)
+    accs, pts, want = [], [], []
+    for i in range(256):
+        a = _ec_mul(rng.randrange(1, N), G)
+        kind = i % 4
+        b = a if kind == 1 else ((a[0], P - a[1]) if kind == 2 else _ec_mul(rng.randrange(1, N), G))
+        z = rng.randrange(1, P)
+        zz, zzz = z * z % P, z * z * z % P
+        if kind == 3:
+            accs.append([0, 0, 0, 0, 1])
+            want.append(b)
+        else:
+            accs.append([a[0] * zz % P, a[1] * zzz % P, zz, zzz, 0])
+            want.append(_ec_add(a, b))
+        pts.append(b)
+    A = np.zeros((len(accs), 33), np.uint32)
+    Q = np.zeros((len(pts), 16), np.uint32)
+    for i, (acc, pt) in enumerate(zip(accs, pts)):
+        for j in range(4):
+            A[i, 8 * j:8 * j + 8] = _pack([acc[j]])[0]
+        A[i, 32] = acc[4]
+        Q[i, :8], Q[i, 8:] = _pack([pt[0]])[0], _pack([pt[1]])[0]
+    R = np.zeros_like(A)
+    L = _lib()
+    L.fc_xyzz.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.fc_xyzz.restype = ctypes.c_int
+    assert L.fc_xyzz(lat, len(accs), A.ctypes.data, Q.ctypes.data, R.ctypes.data) == 0
+    for i, w in enumerate(want):
+        X, Y, ZZ, ZZZ = (_unpack(R[i:i + 1, 8 * j:8 * j + 8])[0] % P for j in range(4))
+        if w is None:
+            assert R[i, 32] == 1, (i, "expected the identity")
+            continue
+        assert R[i, 32] == 0, i
+        assert ZZ and pow(ZZ, 3, P) == pow(ZZZ, 2, P), i
+        assert (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P) == w, (i, i % 4)
