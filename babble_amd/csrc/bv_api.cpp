@@ -405,6 +405,7 @@ static int create_impl(bv_ctx *ctx) {
     ctx->ev_chunk = mb <= 0 ? 0 : std::max<uint64_t>(1, (uint64_t)(mb * (1 << 20)));  // >= 256 events a chunk anyway
   }
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
+  if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
   return BV_OK;
 }
 
@@ -1059,10 +1060,111 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
   return BV_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Small batches (addSelfEvent's own event, core.go:292; processJoinRequest's
+// ITX, node_rpc.go:250-260; a short SyncResponse): latency, not throughput.
+// ONE copy in, ONE k_small launch (every step of an item in one workgroup,
+// kernels.hip), ONE copy out; key-cache tables are resolved on the host
+// without a device round trip.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kSmallItems = 256;       // items (and messages) per small batch
+constexpr uint64_t kSmallMsgLen = 16 << 10;  // longest message: one lane hashes it
+
+static bool small_batch(const bv_batch *b) {
+  if (b->n_items == 0 || b->n_items > kSmallItems || b->n_msgs > kSmallItems) return false;
+  for (uint64_t m = 0; m < b->n_msgs; m++)
+    if (b->msg_off[m + 1] - b->msg_off[m] > kSmallMsgLen) return false;
+  return true;
+}
+
+static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
+  const uint32_t n_keys = b->n_keys;
+  const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0, key_len = n_keys ? b->key_off[n_keys] : 0;
+  hipStream_t st = ctx->stream;
+  ctx->last = st;
+  ctx->timing = bv_timing{};
+  size_t total = 0;
+  auto at = [&](size_t bytes) {
+    const size_t o = total;
+    total += align256(bytes);
+    return o;
+  };
+  const size_t o_msg = at(msg_len + 64), o_moff = at((n_msgs + 1) * 8), o_key = at(key_len + 64),
+               o_koff = at((n_keys + 1) * 8ull), o_im = at(n_items * 4), o_ik = at(n_items * 4),
+               o_r = at(n_items * 32), o_s = at(n_items * 32), o_pre = at(n_items), o_tab = at(n_keys * 8ull),
+               in_end = total;
+  const size_t o_dig = at(n_msgs * 32), o_st = at(n_items), out_end = total;
+  if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // previous calls' staging
+  HIPCHK(ctx->pin_in.ensure(in_end), BV_E_OOM, "alloc pinned staging");
+  HIPCHK(ctx->pin_out.ensure(out_end - o_dig), BV_E_OOM, "alloc pinned results");
+  HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
+  uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
+  auto put = [&](size_t o, const void *src, size_t n) {
+    if (n) memcpy(pin + o, src, n);
+  };
+  put(o_msg, b->msg_bytes, msg_len);
+  memset(pin + o_msg + msg_len, 0, 64);  // the SHA kernels read the last dword's neighbours
+  put(o_moff, b->msg_off, (n_msgs + 1) * 8);
+  put(o_key, b->key_bytes, key_len);
+  memset(pin + o_key + key_len, 0, 64);
+  put(o_koff, b->key_off, (n_keys + 1) * 8ull);
+  put(o_im, b->item_msg, n_items * 4);
+  put(o_ik, b->item_key, n_items * 4);
+  put(o_r, b->r_be, n_items * 32);
+  put(o_s, b->s_be, n_items * 32);
+  if (b->pre) put(o_pre, b->pre, n_items);
+  const bool kc = (ctx->flags & BV_F_KEY_CACHE) && n_keys;
+  uint32_t hits = 0;
+  if (kc) hits = bv_kc_lookup(ctx, n_keys, b->key_bytes, b->key_off, (uint64_t *)(pin + o_tab));
+  hipEvent_t *ev = ctx->S().ev;
+  HIPCHK(hipEventRecord(ev[E_CALL], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipMemcpyAsync(dev, pin, in_end, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d (small batch)");
+  HIPCHK(hipEventRecord(ev[E_START], st), BV_E_LAUNCH, "event");
+  HIPCHK(bvk::verify_small(st, (uint32_t)n_items, (uint32_t)n_msgs, dev + o_msg, (const uint64_t *)(dev + o_moff),
+                           dev + o_key, (const uint64_t *)(dev + o_koff), (const uint32_t *)(dev + o_im),
+                           (const uint32_t *)(dev + o_ik), dev + o_r, dev + o_s, b->pre ? dev + o_pre : nullptr,
+                           kc ? (const uint64_t *)(dev + o_tab) : nullptr, ctx->g_table, (uint32_t *)(dev + o_dig),
+                           dev + o_st),
+         BV_E_LAUNCH, "k_small");
+  HIPCHK(hipEventRecord(ev[E_END], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipMemcpyAsync(ctx->pin_out.p, dev + o_dig, out_end - o_dig, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
+         "d2h (small batch)");
+  HIPCHK(hipEventRecord(ev[E_OUT], st), BV_E_LAUNCH, "event");
+  int rc = bv_mark_done(ctx, st);
+  if (rc != BV_OK) return rc;
+  HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "small batch sync");
+  const uint8_t *out = (const uint8_t *)ctx->pin_out.p;
+  if (res->msg_hash && n_msgs) memcpy(res->msg_hash, out, n_msgs * 32);
+  const uint8_t *stv = out + (o_st - o_dig);
+  if (res->status) memcpy(res->status, stv, n_items);
+  if (res->accept_bits) {
+    memset(res->accept_bits, 0, (n_items + 63) / 64 * 8);
+    for (uint64_t i = 0; i < n_items; i++)
+      if (stv[i] == BV_ACCEPT) res->accept_bits[i / 64] |= 1ull << (i % 64);
+  }
+  bv_timing &t = ctx->timing;
+  t.ms_total = t.ms_verify = elapsed(ev[E_START], ev[E_END]);
+  t.ms_h2d = elapsed(ev[E_CALL], ev[E_START]);
+  t.ms_d2h = elapsed(ev[E_END], ev[E_OUT]);
+  t.key_path = kc && hits ? BV_KCW : 0;
+  t.kc_hits = hits;
+  t.kc_keys = (uint32_t)ctx->kc_index.size();
+  t.ms_host = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return BV_OK;
+}
+
 extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   if (!ctx || !b || !res) return BV_E_ARGS;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
+  if (ctx->small_path && small_batch(b)) {
+    int rc = bv_validate_host_batch(ctx, b);
+    if (rc != BV_OK) return rc;
+    rc = small_verify(ctx, b, res);
+    return rc == BV_OK ? rc : bv_drain(ctx, ctx->stream, rc);
+  }
   bv_host_call call;
   int rc = bv_host_launch(ctx, b, &call, res);
   if (rc != BV_OK) return bv_drain(ctx, ctx->stream, rc);

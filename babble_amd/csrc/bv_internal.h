@@ -51,6 +51,9 @@ hipError_t verify_g(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *,
 hipError_t verify_q(hipStream_t, int, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
                     const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
                     const uint64_t *, const uint32_t *, uint8_t *, uint64_t *);
+hipError_t verify_small(hipStream_t, uint32_t, uint32_t, const uint8_t *, const uint64_t *, const uint8_t *,
+                        const uint64_t *, const uint32_t *, const uint32_t *, const uint8_t *, const uint8_t *,
+                        const uint8_t *, const uint64_t *, const uint32_t *, uint32_t *, uint8_t *);
 hipError_t verify_generic(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
@@ -274,8 +277,9 @@ struct bv_ctx {
   // chunk (BV_HOST_CHUNK_MB, >= 1 MB), event staging chunk (BV_EV_CHUNK_MB,
   // 0 = one chunk; chunks hold >= 256 events), bulk events' verify beside the next chunk
   // (BV_EV_VERIFY_STREAM=0: on the main stream)
+  // small host batches through k_small (BV_SMALL=0: the bulk pipeline)
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
-  bool ev_split_verify = true;
+  bool ev_split_verify = true, small_path = true;
 };
 
 // one in-flight host-entry call (bv_host_launch -> bv_host_finish)
@@ -334,6 +338,7 @@ int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
                   hipStream_t st, bool hashed, bool kc);
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
                   const uint64_t *dko, hipStream_t st, bool *use, bool force_build = false);
+uint32_t bv_kc_lookup(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, uint64_t *tabs);
 void bv_kc_init(bv_ctx *ctx);     // budget, admission and fault-injection settings (bv_create)
 void bv_kc_release(bv_ctx *ctx);  // free every cached table (bv_destroy, after all calls finished)
 // `res` (may be null): the caller's result buffers, written by DMA directly

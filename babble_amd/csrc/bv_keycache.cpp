@@ -297,6 +297,24 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
   return BV_OK;
 }
 
+// Host-only lookup for the small-batch path (no device work, no sync): the
+// table of every batch key that has one built, else 0.  Small batches never
+// build tables (registration and bulk batches do).  Returns the hits.
+uint32_t bv_kc_lookup(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, uint64_t *tabs) {
+  uint32_t hits = 0;
+  const uint64_t clock = ++ctx->kc_clock;
+  for (uint32_t k = 0; k < n_keys; k++) {
+    tabs[k] = 0;
+    if (!key_form_ok(hkb + hko[k], hko[k + 1] - hko[k])) continue;
+    auto it = ctx->kc_index.find(std::string((const char *)hkb + hko[k], (size_t)(hko[k + 1] - hko[k])));
+    if (it == ctx->kc_index.end()) continue;
+    ctx->kc_slots[it->second].last_use = clock;
+    tabs[k] = (uint64_t)(uintptr_t)ctx->kc_slots[it->second].table;
+    hits++;
+  }
+  return hits;
+}
+
 extern "C" int bv_kc_register(bv_ctx *ctx, uint32_t n_keys, const uint8_t *key_bytes, const uint64_t *key_off) {
   if (!ctx || (n_keys && !key_off)) return BV_E_ARGS;
   std::lock_guard<std::mutex> lk(ctx->mu);

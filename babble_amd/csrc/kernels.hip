@@ -525,6 +525,162 @@ __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, uint64
 }
 
 // ---------------------------------------------------------------------------
+// Small batches: k_small, ONE launch per batch, one 256-thread workgroup per
+// item (workgroup b also hashes message b for the digest output).  A small
+// batch is bound by its longest serial chain, not by throughput, so the work
+// of one item is spread over the workgroup's four waves (lanes of different
+// waves run different code at the same time; lanes of one wave only when
+// they run the same code):
+//   phase 1  wave 0: SHA-256 of the item's message (e)
+//            wave 1: s^-1 (one Bernstein-Yang inversion)
+//            wave 2: elliptic.Unmarshal of the item's key (Q)
+//            wave 3: SHA-256 of message b -> msg_hash[b]
+//   phase 2  thread 0: decision table, u1 = e w, u2 = r w, GLV split
+//   phase 3  wave 1 lanes 0, 1: u1 G over G windows 0-4 / 5-9
+//            wave 2: k1 Q;  wave 3: k2 phi(Q) — from the key's cached KC
+//            table when it has one (6 lookups each), else a NAF double-and-
+//            add chain (129 doublings) on the affine point
+//   phase 4  wave 0 lanes 0, 1: two XYZZ sums; thread 0: the last sum and
+//            x(R) mod N == r
+// Statuses only; the host packs a small batch's accept bits.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs,
+                                               const uint8_t *__restrict__ msg_bytes,
+                                               const uint64_t *__restrict__ msg_off,
+                                               const uint8_t *__restrict__ key_bytes,
+                                               const uint64_t *__restrict__ key_off,
+                                               const uint32_t *__restrict__ item_msg,
+                                               const uint32_t *__restrict__ item_key,
+                                               const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
+                                               const uint8_t *__restrict__ pre, const uint64_t *__restrict__ kc_tabs,
+                                               const uint32_t *__restrict__ g_table,
+                                               uint32_t *__restrict__ digest_words, uint8_t *__restrict__ status) {
+  const uint32_t b = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  __shared__ uint32_t sh_e[8], sh_w[8], sh_q[16], sh_u1[8], sh_k[8];
+  __shared__ uint32_t sh_part[4][33];
+  __shared__ uint32_t sh_ks, sh_go;
+  const bool item = b < n_items;
+  // ---- phase 1
+  if (item && lane == 0) {
+    if (wave == 0) {
+      uint32_t h[8];
+      const uint32_t m = item_msg[b];
+      sha256_msg(h, msg_bytes, msg_off[m], msg_off[m + 1] - msg_off[m]);
+#pragma unroll
+      for (int k = 0; k < 8; k++) sh_e[k] = bswap32(h[k]);  // the digest's big-endian bytes (as k_sha256)
+    } else if (wave == 1) {
+      sc s, w;
+      sc_load_be_words(s, s_be + 8 * (uint64_t)b);
+      if (s_usable(pre, b, s)) {
+        sinv_one(w, s);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) w.v[k] = 0;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) sh_w[k] = w.v[k];
+    } else if (wave == 2) {
+      const uint32_t k = item_key[b];
+      uint8_t st;
+      fe x, y;
+      key_decode_point(key_bytes, key_off[k], key_off[k + 1] - key_off[k], st, x, y);
+#pragma unroll
+      for (int c = 0; c < 8; c++) sh_q[c] = x.v[c], sh_q[8 + c] = y.v[c];
+      sh_ks = st;
+    }
+  }
+  if (wave == 3 && lane == 0 && b < n_msgs) sha256_one(b, msg_bytes, msg_off, digest_words);
+  __syncthreads();
+  if (!item) return;  // uniform per workgroup
+  // ---- phase 2
+  if (t == 0) {
+    fe r, sv;
+    fe_load_be_words(r, r_be + 8 * (uint64_t)b);
+    fe_load_be_words(sv, s_be + 8 * (uint64_t)b);
+    const uint8_t cls = classify(pre ? pre[b] : 0, (uint8_t)sh_ks, r, sv);
+    sh_go = cls == 0xFF;
+    if (cls != 0xFF) {
+      status[b] = cls;
+    } else {
+      sc w, e, rs;
+#pragma unroll
+      for (int k = 0; k < 8; k++) w.v[k] = sh_w[k], rs.v[k] = r.v[k];
+      sc_load_be_words(e, sh_e);
+      uint32_t u1[8], k1[4], k2[4], signs;
+      scalars_from(w, e, rs, u1, k1, k2, signs);
+#pragma unroll
+      for (int k = 0; k < 8; k++) sh_u1[k] = u1[k];
+#pragma unroll
+      for (int k = 0; k < 4; k++) sh_k[k] = k1[k], sh_k[4 + k] = k2[k];
+      sh_go = 1u | (signs << 1);
+    }
+  }
+  __syncthreads();
+  const uint32_t go = sh_go;
+  if (!go) return;  // decided by the table (uniform)
+  // ---- phase 3: four partial sums
+  if (lane < 2 && wave == 1) {  // u1 G, windows [5 lane, 5 lane + 5)
+    uint32_t u[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) u[k] = sh_u1[k];
+    gexz R;
+    bool inf = true;
+    fe_set(R.X, 0), fe_set(R.Y, 0), fe_set(R.ZZ, 0), fe_set(R.ZZZ, 0);
+    g_table_add_range<BV_GW, BV_GNWIN, true>(R, inf, g_table, u, (BV_GNWIN / 2) * (int)lane,
+                                              lane ? BV_GNWIN : BV_GNWIN / 2);
+    part_store(sh_part[lane], R, inf);
+  } else if (lane == 0 && wave >= 2) {  // k1 Q (wave 2) / k2 phi(Q) (wave 3)
+    const uint32_t h = wave - 2;
+    uint32_t kk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) kk[k] = sh_k[4 * h + k];
+    const bool neg = (go >> (1 + h)) & 1u;
+    const uint64_t tab = kc_tabs ? kc_tabs[item_key[b]] : 0;
+    gexz R;
+    bool inf = true;
+    fe_set(R.X, 0), fe_set(R.Y, 0), fe_set(R.ZZ, 0), fe_set(R.ZZZ, 0);
+    if (tab) {
+      key_table_add<BV_KCW, BV_KCNWIN, true, true>(R, inf, (const uint32_t *)tab, kk, neg, h != 0);
+    } else {
+      fe qx, qy;
+#pragma unroll
+      for (int c = 0; c < 8; c++) qx.v[c] = sh_q[c], qy.v[c] = sh_q[8 + c];
+      if (h) {
+        fe beta;
+        fe_load(beta, FE_BETA);
+        fe_mul(qx, qx, beta);  // phi(Q) = (beta x, y)
+      }
+      if (neg) fe_neg(qy, qy);
+      gej J;
+      naf_mul<true>(J, inf, qx, qy, kk);
+      if (!inf) gexz_from_gej(R, J);
+    }
+    part_store(sh_part[2 + h], R, inf);
+  }
+  __syncthreads();
+  // ---- phase 4
+  if (wave == 0 && lane < 2) {
+    gexz A, B;
+    bool ia, ib;
+    part_load(sh_part[2 * lane], A, ia);
+    part_load(sh_part[2 * lane + 1], B, ib);
+    gexz_add(A, ia, B, ib);
+    part_store(sh_part[2 * lane], A, ia);
+  }
+  __syncthreads();
+  if (t == 0) {
+    gexz A, B;
+    bool ia, ib;
+    part_load(sh_part[0], A, ia);
+    part_load(sh_part[2], B, ib);
+    gexz_add(A, ia, B, ib);
+    fe r;
+    fe_load_be_words(r, r_be + 8 * (uint64_t)b);
+    status[b] = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Launch wrappers (called from bv_api.cpp)
 // ---------------------------------------------------------------------------
 namespace bvk {
@@ -753,6 +909,19 @@ hipError_t build_kc(hipStream_t st, uint32_t n, const uint32_t *kxy, const uint8
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_table_pair_kc<BV_KCW, BV_KCL, BV_KCNWIN>),
                      dim3(BV_KCNWIN * (BV_KCENT / BV_KCPAIR_ENT), n), dim3(256), 0, st, sub, kst, tabs, (uint4 *)pscr);
+  return hipGetLastError();
+}
+
+hipError_t verify_small(hipStream_t st, uint32_t n_items, uint32_t n_msgs, const uint8_t *msg_bytes,
+                        const uint64_t *msg_off, const uint8_t *key_bytes, const uint64_t *key_off,
+                        const uint32_t *item_msg, const uint32_t *item_key, const uint8_t *r_be, const uint8_t *s_be,
+                        const uint8_t *pre, const uint64_t *kc_tabs, const uint32_t *g_table, uint32_t *dig,
+                        uint8_t *status) {
+  const uint32_t grid = std::max(n_items, n_msgs);
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_small, dim3(grid), dim3(256), 0, st, n_items, n_msgs, msg_bytes, msg_off, key_bytes, key_off,
+                     item_msg, item_key, (const uint32_t *)r_be, (const uint32_t *)s_be, pre, kc_tabs, g_table, dig,
+                     status);
   return hipGetLastError();
 }
 

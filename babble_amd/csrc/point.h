@@ -348,6 +348,58 @@ DEV void gexz_add_ge_lat(gexz &r, bool &inf, const fe &x2, const fe &y2) {
 #endif
 }
 
+// r += b, both XYZZ (add-2008-s: 12M + 2S) with the exceptional cases:
+// either operand the identity, P + P (doubles), P + (-P) (the identity).
+// Combines the partial sums of the small-batch kernel (k_small).
+DEV void gexz_add(gexz &r, bool &rinf, const gexz &b, bool binf) {
+  if (binf) return;
+  if (rinf) {
+    r = b;
+    rinf = false;
+    return;
+  }
+  fe U1, U2, S1, S2, P, R, PP, PPP, Q, t;
+  fe_mul(U1, r.X, b.ZZ);
+  fe_mul(U2, b.X, r.ZZ);
+  fe_mul(S1, r.Y, b.ZZZ);
+  fe_mul(S2, b.Y, r.ZZZ);
+  fe_sub(P, U2, U1);
+  fe_sub(R, S2, S1);
+  if (fe_is_zero(P)) {
+    if (fe_is_zero(R)) {
+      gexz d;
+      gexz_double(d, r);
+      r = d;
+    } else {
+      rinf = true;
+    }
+    return;
+  }
+  fe_sqr(PP, P);
+  fe_mul(PPP, P, PP);
+  fe_mul(Q, U1, PP);
+  fe_sqr(t, R);
+  fe_sub(t, t, PPP);
+  fe_sub(t, t, Q);
+  fe_sub(r.X, t, Q);          // X3 = R^2 - PPP - 2Q
+  fe_sub(t, Q, r.X);
+  fe_mul(t, R, t);
+  fe_mul(S1, S1, PPP);
+  fe_sub(r.Y, t, S1);         // Y3 = R (Q - X3) - S1 PPP
+  fe_mul(r.ZZ, r.ZZ, b.ZZ);
+  fe_mul(r.ZZ, r.ZZ, PP);     // ZZ3 = ZZ1 ZZ2 PP
+  fe_mul(r.ZZZ, r.ZZZ, b.ZZZ);
+  fe_mul(r.ZZZ, r.ZZZ, PPP);  // ZZZ3 = ZZZ1 ZZZ2 PPP
+}
+
+// Jacobian (X, Y, Z) -> XYZZ (X, Y, Z^2, Z^3): the same point
+DEV void gexz_from_gej(gexz &r, const gej &a) {
+  r.X = a.X;
+  r.Y = a.Y;
+  fe_sqr(r.ZZ, a.Z);
+  fe_mul(r.ZZZ, r.ZZ, a.Z);
+}
+
 template <bool LAT>
 DEV void pt_add_ge(gexz &r, bool &inf, const fe &x2, const fe &y2) {
   if (LAT) gexz_add_ge_lat(r, inf, x2, y2);

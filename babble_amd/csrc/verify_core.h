@@ -100,11 +100,8 @@ DEV void sha256_one(uint64_t m, const uint8_t *bytes, const uint64_t *off, uint3
 // len 65, prefix 0x04, x < p, y < p, y^2 == x^3 + 7.  len 0 -> ToPublicKey
 // returns nil (KS_EMPTY: ecdsa.Verify panics at pub.Curve).
 // ---------------------------------------------------------------------------
-DEV void key_decode_one(uint32_t k, const uint8_t *kbytes, const uint64_t *koff, uint8_t *kstatus, uint32_t *kxy) {
-  const uint64_t o = koff[k];
-  const uint64_t len = koff[k + 1] - o;
-  uint8_t st = KS_BAD;
-  fe x, y;
+DEV void key_decode_point(const uint8_t *kbytes, uint64_t o, uint64_t len, uint8_t &st, fe &x, fe &y) {
+  st = KS_BAD;
   fe_set(x, 0);
   fe_set(y, 0);
   if (len == 0) {
@@ -139,6 +136,12 @@ DEV void key_decode_one(uint32_t k, const uint8_t *kbytes, const uint64_t *koff,
       if (fe_eq(y2, x3)) st = KS_OK;
     }
   }
+}
+
+DEV void key_decode_one(uint32_t k, const uint8_t *kbytes, const uint64_t *koff, uint8_t *kstatus, uint32_t *kxy) {
+  uint8_t st;
+  fe x, y;
+  key_decode_point(kbytes, koff[k], koff[k + 1] - koff[k], st, x, y);
   kstatus[k] = st;
   fe_store(kxy + 16 * k, x);
   fe_store(kxy + 16 * k + 8, y);
@@ -698,4 +701,110 @@ DEV uint8_t verify_item_generic(uint64_t i, const uint32_t *item_key, const uint
   }
   g_table_add<BV_GW, BV_GNWIN, LAT>(R, inf, g_table, u1);
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
+}
+
+// ---------------------------------------------------------------------------
+// Small batches (k_small: one workgroup per item, every step of one item's
+// verification in one launch).  The pieces below are the
+// per-lane work of its roles.
+// ---------------------------------------------------------------------------
+// w = s^-1 R (Montgomery form, as k_sinv makes it) for one item: the plain
+// inverse R^2 / s of s (taken as (s/R) R), times 1.
+DEV void sinv_one(sc &w, const sc &s) {
+  sc t, one;
+#pragma unroll
+  for (int k = 0; k < 8; k++) one.v[k] = k == 0 ? 1u : 0u;
+  sc_inverse_var(t, s);
+  sc_mont(w, t, one);
+}
+
+// u1 = e w and the GLV split of u2 = r w (item_scalars over values)
+DEV void scalars_from(const sc &w, const sc &e, const sc &r, uint32_t u1[8], uint32_t k1[4], uint32_t k2[4],
+                      uint32_t &signs) {
+  sc a, b;
+  sc_mont(a, e, w);
+  sc_mont(b, r, w);
+#pragma unroll
+  for (int k = 0; k < 8; k++) u1[k] = a.v[k];
+  glv_split(k1, k2, signs, b);
+}
+
+// g_table_add over windows [j0, j1) only: the signed recoding runs over
+// every window (a digit depends on the carry out of the window below), the
+// table additions only in the range — so lanes can sum disjoint ranges.
+template <int W, int NWIN, bool LAT = false, class PT = gexz>
+DEV void g_table_add_range(PT &R, bool &inf, const uint32_t *tab, uint32_t u[8], int j0, int j1) {
+  constexpr uint32_t ENT = 1u << (W - 1);
+  uint32_t carry = 0;
+  for (int j = 0; j < NWIN; j++) {
+    uint32_t d = (u[0] & ((1u << W) - 1u)) + carry;
+#pragma unroll
+    for (int c = 0; c < 7; c++) u[c] = (u[c] >> W) | (u[c + 1] << (32 - W));
+    u[7] >>= W;
+    carry = d > ENT ? 1u : 0u;
+    const bool dneg = carry != 0;
+    if (dneg) d = (1u << W) - d;
+    if (j < j0 || j >= j1) continue;
+    const uint32_t *e = tab + ((uint64_t)j * ENT + d) * BV_ENTRY_U32;
+    fe x, y;
+    fe_load4(x, e);
+    fe_load4(y, e + 8);
+    fe_cneg_canon(y, dneg);
+    pt_add_ge_step<LAT>(R, inf, x, y, d != 0);
+  }
+}
+
+// R = k P for an affine P and a 128-bit k (4 limbs), MSB-first over the
+// non-adjacent form of k (digits in {-1, 0, 1}, ~k/3 additions): a key
+// without a table (the small-batch kernel's cold path).  pos / neg digit
+// masks: c = 3k ^ k, pos = (c & 3k) >> 1, neg = (c & k) >> 1.
+template <bool LAT = false>
+DEV void naf_mul(gej &R, bool &inf, const fe &px, const fe &py, const uint32_t k[4]) {
+  uint32_t h[5], kk[5], pos[5], neg[5];
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) kk[i] = k[i];
+  kk[4] = 0;
+  // h = 3k = k + 2k
+  uint32_t prev = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint32_t k2 = (kk[i] << 1) | (prev >> 31);
+    prev = kk[i];
+    h[i] = addc32(kk[i], k2, c);
+  }
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint32_t x = h[i] ^ kk[i];
+    pos[i] = x & h[i];
+    neg[i] = x & kk[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 5; i++) {  // >> 1
+    pos[i] = (pos[i] >> 1) | (i < 4 ? pos[i + 1] << 31 : 0u);
+    neg[i] = (neg[i] >> 1) | (i < 4 ? neg[i + 1] << 31 : 0u);
+  }
+  fe ny;
+  fe_neg(ny, py);
+  inf = true;
+  fe_set(R.X, 0);
+  fe_set(R.Y, 0);
+  fe_set(R.Z, 0);
+  for (int bit = 129; bit >= 0; bit--) {
+    if (!inf) gej_double_sel<LAT>(R, R);
+    const uint32_t p = (pos[bit >> 5] >> (bit & 31)) & 1u, n = (neg[bit >> 5] >> (bit & 31)) & 1u;
+    if (p | n) gej_add_ge_sel<LAT>(R, inf, px, n ? ny : py);
+  }
+}
+
+// One XYZZ partial sum (+ identity flag) in 33 words (LDS hand-off)
+DEV void part_store(uint32_t *p, const gexz &R, bool inf) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) p[k] = R.X.v[k], p[8 + k] = R.Y.v[k], p[16 + k] = R.ZZ.v[k], p[24 + k] = R.ZZZ.v[k];
+  p[32] = inf ? 1u : 0u;
+}
+DEV void part_load(const uint32_t *p, gexz &R, bool &inf) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) R.X.v[k] = p[k], R.Y.v[k] = p[8 + k], R.ZZ.v[k] = p[16 + k], R.ZZZ.v[k] = p[24 + k];
+  inf = p[32] != 0;
 }

@@ -178,6 +178,60 @@ const uint32_t *emu_g_table(int nt) {
   return gt;
 }
 
+// k_small's per-item steps (kernels.hip) run one after another: the same
+// verify_core.h / point.h pieces the workgroup's waves run concurrently
+// (SHA-256, s^-1, key decode, decision table, u1 / u2 + GLV, the two G
+// window ranges, the NAF chains of k1 Q and k2 phi(Q), the XYZZ sums and
+// the final check).  The key cache's table lookups are exercised on the GPU.
+uint8_t small_item(uint64_t i, const bv_batch *b, const uint8_t *msg, const uint32_t *r, const uint32_t *s,
+                   const uint32_t *gt) {
+  const uint32_t m = b->item_msg[i], k = b->item_key[i];
+  uint32_t h[8], e_words[8];
+  sha256_msg(h, msg, b->msg_off[m], b->msg_off[m + 1] - b->msg_off[m]);
+  for (int c = 0; c < 8; c++) e_words[c] = bswap32(h[c]);
+  sc sv, w;
+  sc_load_be_words(sv, s + 8 * i);
+  if (s_usable(b->pre, i, sv)) sinv_one(w, sv);
+  else for (int c = 0; c < 8; c++) w.v[c] = 0;
+  uint8_t ks;
+  fe qx, qy;
+  key_decode_point(b->key_bytes, b->key_off[k], b->key_off[k + 1] - b->key_off[k], ks, qx, qy);
+  fe rf, sf;
+  fe_load_be_words(rf, r + 8 * i);
+  fe_load_be_words(sf, s + 8 * i);
+  const uint8_t cls = classify(b->pre ? b->pre[i] : 0, ks, rf, sf);
+  if (cls != 0xFF) return cls;
+  sc e, rs;
+  sc_load_be_words(e, e_words);
+  for (int c = 0; c < 8; c++) rs.v[c] = rf.v[c];
+  uint32_t u1[8], k1[4], k2[4], signs;
+  scalars_from(w, e, rs, u1, k1, k2, signs);
+  gexz P[4];
+  bool inf[4];
+  for (int q = 0; q < 2; q++) {
+    uint32_t u[8];
+    for (int c = 0; c < 8; c++) u[c] = u1[c];
+    inf[q] = true;
+    g_table_add_range<BV_GW, BV_GNWIN>(P[q], inf[q], gt, u, (BV_GNWIN / 2) * q, q ? BV_GNWIN : BV_GNWIN / 2);
+  }
+  for (int hh = 0; hh < 2; hh++) {
+    fe px = qx, py = qy;
+    if (hh) {
+      fe beta;
+      fe_load(beta, FE_BETA);
+      fe_mul(px, px, beta);
+    }
+    if ((signs >> hh) & 1u) fe_neg(py, py);
+    gej J;
+    naf_mul<false>(J, inf[2 + hh], px, py, hh ? k2 : k1);
+    if (!inf[2 + hh]) gexz_from_gej(P[2 + hh], J);
+  }
+  gexz_add(P[0], inf[0], P[1], inf[1]);
+  gexz_add(P[2], inf[2], P[3], inf[3]);
+  gexz_add(P[0], inf[0], P[2], inf[2]);
+  return final_check(P[0], inf[0], rf) ? BV_ACCEPT : BV_REJECT;
+}
+
 template <class T>
 T *aligned(std::vector<uint8_t> &store, size_t bytes) {
   store.assign(bytes + 64, 0);
@@ -191,7 +245,8 @@ extern "C" {
 
 // Same pipeline and mode choice as bv_api.cpp run_device, on the host.
 // force_mode: -1 = same rule as the library, 0 = generic, 1 = K8 tables,
-// 2 = K12 tables.  Returns the mode used (0, 1 or 2).
+// 2 = K12 tables, 3 = the small-batch kernel's steps (k_small).  Returns the
+// mode used.
 int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint64_t *bits, int n_threads,
                      int force_mode) {
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
@@ -219,7 +274,7 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
     mode = (n_keys <= 8192 && n_items >= 16ull * n_keys) ? 1 : 0;
     if (mode == 1 && n_keys <= 1024 && n_items >= 2048ull * n_keys) mode = 2;
   }
-  const bool table_mode = mode != 0;
+  const bool table_mode = mode == 1 || mode == 2;
   const uint32_t *gt = emu_g_table(n_threads);
   uint32_t *kt = nullptr;
   if (table_mode) {
@@ -233,7 +288,9 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
   const uint64_t T = ((n_items + M - 1) / M + 255) / 256 * 256;  // kernel grid size
   parallel_for(T, n_threads, [&](uint64_t t) { sinv_thread(t, T, n_items, M, s, b->pre, scratch); });
   std::vector<uint8_t> st(n_items + 1);
-  if (table_mode) {
+  if (mode == 3) {
+    parallel_for(n_items, n_threads, [&](uint64_t i) { st[i] = small_item(i, b, msg, r, s, gt); });
+  } else if (table_mode) {
     parallel_for(n_items, n_threads,
                  [&](uint64_t i) {
                    verify_item_g(i, n_items, b->item_key, r, s, b->pre, kst, b->item_msg, dig, scratch, u12, gt, rg);

@@ -202,7 +202,7 @@ int main(int argc, char **argv) {
   oracle_verify_batch(&b, h0.data(), st0.data(), b0.data(), nt);
 
   int bad = 0;
-  for (int mode = 0; mode <= 2; mode++) {
+  for (int mode = 0; mode <= 3; mode++) {
     std::vector<uint8_t> h(32 * n_msgs + 1), st(n_items + 1);
     std::vector<uint64_t> bits(nw + 1);
     const int m = emu_verify_batch(&b, h.data(), st.data(), bits.data(), nt, mode);

@@ -89,7 +89,7 @@ def test_glv_constants_and_split():
         assert (k1 + k2 * LAMBDA - k) % N == 0, hex(k)
 
 
-@pytest.mark.parametrize("mode", [2, 1, 0])
+@pytest.mark.parametrize("mode", [2, 1, 0, 3])
 def test_golden_items(mode):
     batch, expected, _ = golden_items_batch()
     h, st, bits, m = emu.verify_batch(batch.as_dict(), force_mode=mode)
@@ -97,7 +97,7 @@ def test_golden_items(mode):
     assert np.array_equal(st, expected)
 
 
-@pytest.mark.parametrize("mode", [2, 1, 0])
+@pytest.mark.parametrize("mode", [2, 1, 0, 3])
 def test_adversarial_mix(mode):
     b = synth.adversarial(2500, seed=21, n_creators=4, scale_per_million=dict(
         rflip=20000, sflip=20000, body=10000, highs=10000, range=8000, fmt=8000, key=12000))
@@ -155,7 +155,7 @@ def test_asan_ubsan_emulator(tmp_path):
         r = subprocess.run([exe, path, "4"], capture_output=True, text=True, timeout=600,
                            env={"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "PATH": "/usr/bin:/bin"})
         assert r.returncode == 0, r.stdout + r.stderr
-        assert r.stdout.count("equal") == 3 and "MISMATCH" not in r.stdout, r.stdout
+        assert r.stdout.count("equal") == 4 and "MISMATCH" not in r.stdout, r.stdout
     # the product's host DAG hasher (hostdag.cpp + hostsha.cpp) under the
     # sanitizers on random wire batches in exactly-sized buffers
     for seed in (1, 2, 3):

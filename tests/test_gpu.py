@@ -200,18 +200,77 @@ def test_generic_path_few_items_per_key(verifier):
     assert verifier.timing()["key_path"] == 0
 
 
-def test_small_batch_latency_rule_takes_k8_tables(verifier):
-    """Batches of <= 16 keys and <= 4096 items take the K8 tables even below
-    16 items per key (the per-lane generic path's 128 doublings + ~128
-    additions in one lane are the longer chain): a single event, and 40
-    events from 8 keys with adversarial items, both equal to the oracle."""
-    b1 = synth.events(1, n_creators=1, seed=901)
-    check_against_oracle(verifier, b1)
-    assert verifier.timing()["key_path"] == 8
-    b40 = synth.adversarial(40, seed=902, n_creators=8, scale_per_million=MIX)
-    assert b40.n_keys <= 16 and b40.n_items < 16 * b40.n_keys
-    check_against_oracle(verifier, b40)
-    assert verifier.timing()["key_path"] == 8
+def test_small_batch_latency_rule_takes_k8_tables(monkeypatch):
+    """With the small-batch kernel off (BV_SMALL=0), batches of <= 16 keys
+    and <= 4096 items take the K8 tables even below 16 items per key (the
+    per-lane generic path's 128 doublings + ~128 additions in one lane are
+    the longer chain): a single event, and 40 events from 8 keys with
+    adversarial items, both equal to the oracle."""
+    from babble_amd.verifier import Verifier
+
+    monkeypatch.setenv("BV_SMALL", "0")  # read at bv_create
+    v = Verifier(device=0)
+    try:
+        b1 = synth.events(1, n_creators=1, seed=901)
+        check_against_oracle(v, b1)
+        assert v.timing()["key_path"] == 8
+        b40 = synth.adversarial(40, seed=902, n_creators=8, scale_per_million=MIX)
+        assert b40.n_keys <= 16 and b40.n_items < 16 * b40.n_keys
+        check_against_oracle(v, b40)
+        assert v.timing()["key_path"] == 8
+    finally:
+        v.close()
+
+
+def test_small_batch_kernel_equals_oracle(verifier, monkeypatch):
+    """k_small: a host batch of <= 256 items is one copy in,
+    ONE launch (hash, s^-1, key decode, u1 G, k1 Q + k2 phi(Q) by NAF chains
+    on keys without a table, the decision table) and one copy out.  The
+    golden items (every decision-table class, R = infinity, doubling cases)
+    in chunks of <= 256 items, a 40-item adversarial batch, single events and
+    one BlockBody with 100 signatures: digests, statuses and bits equal the
+    oracle's, and equal the bulk pipeline's (BV_SMALL=0)."""
+    from babble_amd import shard
+    from babble_amd.verifier import Verifier
+
+    golden, expected, _ = golden_items_batch()
+    batches = [shard.slice_batch(golden, lo, min(lo + 256, golden.n_items)) for lo in range(0, golden.n_items, 256)]
+    batches += [synth.adversarial(40, seed=903, n_creators=8, scale_per_million=MIX),
+                synth.events(1, n_creators=1, seed=904), synth.events(7, n_creators=3, seed=905),
+                synth.blocks(1, n_validators=100, seed=906).batch]
+    monkeypatch.setenv("BV_SMALL", "0")
+    bulk = Verifier(device=0)
+    try:
+        got = []
+        for b in batches:
+            assert b.n_items <= 256
+            res = check_against_oracle(verifier, b)
+            t = verifier.timing()
+            assert t["key_path"] == 0 and t["ms_total"] > 0  # the small kernel ran (no per-batch tables)
+            ref = bulk.verify(b)
+            assert np.array_equal(ref.status, res.status) and np.array_equal(ref.msg_hash, res.msg_hash)
+            got.append(res.status)
+        assert np.array_equal(np.concatenate(got[:len(got) - 4]), expected)
+    finally:
+        bulk.close()
+
+
+def test_small_batch_kernel_key_cache(monkeypatch):
+    """k_small with registered keys: the items of cached keys take their KC
+    tables (6 lookups per GLV half), the others the NAF chains, in the same
+    launch; equal to the oracle."""
+    from babble_amd.verifier import Verifier
+
+    v = Verifier(device=0, flags=native.F_KEY_CACHE)
+    try:
+        b = synth.adversarial(200, seed=907, n_creators=6, scale_per_million=MIX)
+        good = [b.key(k) for k in range(b.n_keys) if gs.Unmarshal(b.key(k)) is not None]
+        v.register_keys(good[:3])
+        check_against_oracle(v, b)
+        t = v.timing()
+        assert t["key_path"] == 22 and 0 < t["kc_hits"] < b.n_keys
+    finally:
+        v.close()
 
 
 def test_c5_blocks_check_block(verifier):
