@@ -461,6 +461,7 @@ def main():
         line["latency_ms"] = latency_leg(args)
         line["events_entry"] = events_entry_leg(args)
         line["tx_sweep"] = tx_sweep_leg(args, v, local)
+        line["c5_fast_sync"] = guarded(c5_leg, args, local)
     if rank == 0:
         if world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(batch, args.cpu_seconds)
@@ -471,30 +472,163 @@ def main():
         dist.destroy_process_group()
 
 
+def guarded(fn, *a):
+    """An extra leg's failure is recorded in the line instead of losing it."""
+    try:
+        return fn(*a)
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        traceback.print_exc()
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def warm_leg(args, devs, world, dist, local, step_with):
-    """Same device-resident batches with BV_F_KEY_CACHE: the first call
-    builds the 64 creators' tables (reported as cold_ms), the timed steps
-    reuse them; hashing, s^-1, u1 G, u2 Q and the decision run every step."""
+    """Same device-resident batches with BV_F_KEY_CACHE: the 64 creators are
+    registered first (bv_kc_register builds their tables: register_ms), the
+    timed steps reuse them; hashing, s^-1, u1 G, u2 Q and the decision run
+    every step."""
     import numpy as np
 
-    from babble_amd import native
+    from babble_amd import native, synth
     from babble_amd.verifier import Verifier
 
     vc = Verifier(device=local, flags=native.F_KEY_CACHE)
+    kb = synth.events(1, n_creators=args.creators, seed=2)  # the same seeded creator keys
+    t0 = time.perf_counter()
+    vc.register_keys([kb.key(k) for k in range(kb.n_keys)])
+    reg_ms = (time.perf_counter() - t0) * 1e3
+    builds = vc.timing()["kc_builds"]
     t0 = time.perf_counter()
     vc.verify_device(devs[0])
     cold_ms = (time.perf_counter() - t0) * 1e3
-    builds = vc.timing()["kc_builds"]
     elapsed, tms = timed_steps(step_with(vc), args.steps, 1, 1, None, local, vc)
     for j, dev in enumerate(devs):
         assert np.array_equal(dev.result().accept_bits, expected_words(0, args.events, j))
     out = {"value": args.events * args.steps / elapsed, "unit": "verifies/s",
-           "ms_per_step": elapsed / args.steps * 1e3, "first_call_ms": cold_ms, "tables_built_first_call": builds,
+           "ms_per_step": elapsed / args.steps * 1e3, "register_ms": reg_ms, "tables_built_by_register": builds,
+           "first_call_ms": cold_ms,
            "key_path": int(tms[-1]["key_path"]),
            "breakdown_ms": {"k_sha256": mean(tms, "ms_sha256"), "k_sinv": mean(tms, "ms_scalar"),
                             "k_verify_g": mean(tms, "ms_verify_g"), "k_verify_q": mean(tms, "ms_verify"),
                             "device_total": mean(tms, "ms_total")}}
     vc.close()
+    return out
+
+
+# C5 roofline (key-cache path, k_verify_gq): 9 XYZZ adds from the G table +
+# 12 from the validator's KC table (6 per GLV half) at 10 modmuls each, the
+# 6 beta x products of the phi half, ~7 for u1 / u2, the GLV split and the
+# check: 223 modmuls x 80 IMUL32 per signature.
+C5_MODMUL_PER_ITEM = 223
+
+
+def c5_leg(args, local, reps=5):
+    """SURVEY §8d C5 / BASELINE configs[4], fast-sync replay: 10^4 BlockBodies
+    x 100 validators (seed 5, 16 x 64-B transactions, ~1.77 KB bodies), 5 %
+    of the signatures corrupted.  One step = PeerSet.Hash of the 100
+    validators (one device launch, the serial SHA chain of
+    peer_set.go:104-115), then ONE bv_verify_batch from host buffers with
+    every BlockBody (hashed once each, block.go:29-55) + the anchor Frame's
+    canonical JSON (frame.go:35-46, an item-less message) and the 10^6
+    signature items, then the host fold of CheckBlock (hashgraph.go:1599-1630:
+    valid count > TrustCount per block) and the frame-hash comparison.  The
+    validator set is registered with the key cache first (Babble knows its
+    PeerSet before replaying).  Beside it: the C port on a bounded sample of
+    the same items, all cores; and the device-resident rate of the same batch
+    (bv_verify_batch_device, inputs in HBM) with its own roofline line."""
+    import hashlib
+
+    import numpy as np
+
+    from babble_amd import frame as F
+    from babble_amd import hashgraph as H
+    from babble_amd import native, synth
+    from babble_amd.batch import PackedBatch
+    from babble_amd.verifier import Verifier
+
+    wb = synth.blocks(10_000, n_validators=100, seed=5)
+    b = wb.batch
+    rng = np.random.default_rng(5)
+    bad = rng.choice(b.n_items, size=b.n_items // 20, replace=False)
+    b.s_be[bad, 7] ^= 0x40
+    keys = [b.key(k) for k in range(b.n_keys)]
+    peers = [H.Peer("172.77.%d.%d:1337" % (i // 250, i % 250 + 1), "0X" + k.hex().upper(), "node%d" % i)
+             for i, k in enumerate(keys)]
+    frame = F.Frame(Round=10_000, Peers=peers, Roots={p.PubKeyString(): F.Root(Events=None) for p in peers},
+                    Events=None, PeerSets={0: peers}, Timestamp=1_600_000_000)
+    fjson = frame.Marshal()
+    fhash = hashlib.sha256(fjson).digest()
+    off = np.concatenate([b.msg_off, [b.msg_off[-1] + len(fjson)]]).astype(np.uint64)
+    rb = PackedBatch(np.concatenate([b.msg_bytes, np.frombuffer(fjson, np.uint8)]), off, b.key_bytes, b.key_off,
+                     b.item_msg, b.item_key, b.r_be, b.s_be, b.pre)
+    v = Verifier(device=local, flags=native.F_KEY_CACHE)
+    t0 = time.perf_counter()
+    v.register_keys(keys)
+    reg_ms = (time.perf_counter() - t0) * 1e3
+    tc = H.PeerSet(peers).TrustCount()
+
+    def step():
+        ph = v.peer_set_hash(keys)
+        res = v.verify(rb)
+        counts = (res.status == 1).reshape(wb.n_blocks, wb.n_validators).sum(axis=1)
+        return ph, res, counts
+
+    step()
+    ts = []
+    for _ in range(reps):
+        t1 = time.perf_counter()
+        ph, res, counts = step()
+        ts.append(time.perf_counter() - t1)
+    tm = v.timing()
+    ok_blocks = int((counts > tc).sum())
+    assert ph == wb.peers_hash, "PeerSet.Hash differs from the generator's chain"
+    assert res.msg_hash[-1].tobytes() == fhash, "frame hash differs"
+    want = np.ones(b.n_items, np.uint8)
+    want[bad] = 0
+    assert np.array_equal(res.status, want), "C5 statuses differ from the seeded corruption"
+    el = float(np.median(ts))
+    # device-resident: the same batch in HBM, bv_verify_batch_device
+    d = v.to_device(rb)
+    v.verify_device(d, sync=True)
+    dts = []
+    for _ in range(reps):
+        t1 = time.perf_counter()
+        v.verify_device(d, sync=True)
+        dts.append(time.perf_counter() - t1)
+    td = v.timing()
+    assert np.array_equal(d.result().status, want)
+    kv = td["ms_verify"] * 1e-3
+    ach = b.n_items * C5_MODMUL_PER_ITEM * IMUL32_PER_MODMUL / kv if kv > 0 else 0.0
+    out = {"value": b.n_items / el, "unit": "verifies/s", "ms_per_replay": el * 1e3, "blocks": wb.n_blocks,
+           "validators": wb.n_validators, "items": b.n_items, "bytes_bodies": int(b.msg_off[-1]),
+           "frame_json_bytes": len(fjson), "register_ms": reg_ms, "key_path": int(tm["key_path"]),
+           "blocks_passing_check_block": ok_blocks, "trust_count": tc,
+           "host_breakdown_ms": host_breakdown([tm]),
+           "device_resident": {"value": b.n_items / float(np.median(dts)), "unit": "verifies/s",
+                               "ms_per_call": float(np.median(dts)) * 1e3,
+                               "breakdown_ms": {"k_sha256": td["ms_sha256"], "k_sinv": td["ms_scalar"],
+                                                "k_verify_gq": td["ms_verify"], "device_total": td["ms_total"]}},
+           "roofline": {"bound": "valu-int", "kernel": "k_verify_gq<false> (key cache)",
+                        "achieved": ach / 1e12, "peak": PEAK_IMUL32_PER_S / 1e12,
+                        "unit": f"T IMUL32/s ({C5_MODMUL_PER_ITEM} modmuls x 80 IMUL32 per signature)",
+                        "frac": ach / PEAK_IMUL32_PER_S}}
+    v.close()
+    if not args.no_cpu:
+        from oracle import coracle  # CPU baseline leg only
+
+        from babble_amd import shard
+
+        n = 20_000  # 200 blocks: their 200 bodies and 20,000 signatures
+        prep = coracle.Prepared(shard.slice_batch(b, 0, n).as_dict())
+        cores = cpu_threads()
+        prep.port(cores)
+        t1 = time.perf_counter()
+        st = prep.port(cores)
+        dt = time.perf_counter() - t1
+        assert np.array_equal(st, want[:n])
+        out["cpu"] = {"value": n / dt, "unit": "verifies/s", "cores": cores, "sample": f"first {n} items (200 blocks)",
+                      "what": "oracle.c port_verify_batch (SHA-256 per item's body + decode + ECDSA), all cores"}
     return out
 
 
@@ -637,6 +771,7 @@ def events_entry_leg(args):
     v.close()
     dag_packed, dag = synth.event_fields(1000, n_creators=4, seed=31, parents="event")
     vc = Verifier(device=local, flags=native.F_KEY_CACHE)
+    vc.register_keys([dag_packed.key(k) for k in range(dag_packed.n_keys)])
     vc.verify_events(dag)
     ts = []
     for _ in range(15):
@@ -774,7 +909,9 @@ def latency_leg(args):
                     tc.append((time.perf_counter() - t0) * 1e3)
                 row[name] = float(np.median(tc))
         for name, ver in (("cold", v0), ("warm_key_cache", vc)):
-            ver.verify(b)  # warm-up (and, for the cache, the table build)
+            if ver is vc:  # the creators are registered validators (their tables built here)
+                ver.register_keys([b.key(k) for k in range(b.n_keys)])
+            ver.verify(b)  # warm-up
             ts = []
             for _ in range(15):
                 t0 = time.perf_counter()
