@@ -405,7 +405,7 @@ static int create_impl(bv_ctx *ctx) {
     ctx->ev_chunk = mb <= 0 ? 0 : std::max<uint64_t>(1, (uint64_t)(mb * (1 << 20)));  // >= 256 events a chunk anyway
   }
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
-  if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
+  if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0, ctx->small_force = atoi(s) == 2;
   return BV_OK;
 }
 
@@ -1077,6 +1077,22 @@ static bool small_batch(const bv_batch *b) {
   return true;
 }
 
+// k_small's per-item NAF chain (129 doublings on one lane) is no faster than
+// the per-batch K8 tables' base chain (1 cold event: 1.09 vs 1.01 ms,
+// profiles/r04_small_lat.log), so a small batch takes k_small when every
+// well-formed key has a key-cache table (malformed keys need none), or when
+// BV_SMALL=2 forces it (tests).
+static bool small_keys_ready(bv_ctx *ctx, const bv_batch *b) {
+  if (ctx->small_force) return true;
+  if (!(ctx->flags & BV_F_KEY_CACHE)) return false;
+  for (uint32_t k = 0; k < b->n_keys; k++) {
+    const uint64_t len = b->key_off[k + 1] - b->key_off[k];
+    if (len != 65 || b->key_bytes[b->key_off[k]] != 4) continue;
+    if (!ctx->kc_index.count(std::string((const char *)b->key_bytes + b->key_off[k], 65))) return false;
+  }
+  return true;
+}
+
 static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   const auto t0 = std::chrono::steady_clock::now();
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
@@ -1162,9 +1178,11 @@ extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   if (ctx->small_path && small_batch(b)) {
     int rc = bv_validate_host_batch(ctx, b);
     if (rc != BV_OK) return rc;
+    if (!small_keys_ready(ctx, b)) goto bulk;
     rc = small_verify(ctx, b, res);
     return rc == BV_OK ? rc : bv_drain(ctx, ctx->stream, rc);
   }
+bulk:
   bv_host_call call;
   int rc = bv_host_launch(ctx, b, &call, res);
   if (rc != BV_OK) return bv_drain(ctx, ctx->stream, rc);

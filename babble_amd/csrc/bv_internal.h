@@ -277,9 +277,10 @@ struct bv_ctx {
   // chunk (BV_HOST_CHUNK_MB, >= 1 MB), event staging chunk (BV_EV_CHUNK_MB,
   // 0 = one chunk; chunks hold >= 256 events), bulk events' verify beside the next chunk
   // (BV_EV_VERIFY_STREAM=0: on the main stream)
-  // small host batches through k_small (BV_SMALL=0: the bulk pipeline)
+  // small host batches through k_small (BV_SMALL=0: the bulk pipeline; 2:
+  // also keys without a key-cache table)
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
-  bool ev_split_verify = true, small_path = true;
+  bool ev_split_verify = true, small_path = true, small_force = false;
 };
 
 // one in-flight host-entry call (bv_host_launch -> bv_host_finish)
