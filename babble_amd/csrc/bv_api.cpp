@@ -1080,17 +1080,11 @@ static bool small_batch(const bv_batch *b) {
 // k_small's per-item NAF chain (129 doublings on one lane) is no faster than
 // the per-batch K8 tables' base chain (1 cold event: 1.09 vs 1.01 ms,
 // profiles/r04_small_lat.log), so a small batch takes k_small when every
-// well-formed key has a key-cache table (malformed keys need none), or when
-// BV_SMALL=2 forces it (tests).
+// well-formed key has a key-cache table or is known to be off the curve
+// (malformed keys need none), or when BV_SMALL=2 forces it (tests).
 static bool small_keys_ready(bv_ctx *ctx, const bv_batch *b) {
   if (ctx->small_force) return true;
-  if (!(ctx->flags & BV_F_KEY_CACHE)) return false;
-  for (uint32_t k = 0; k < b->n_keys; k++) {
-    const uint64_t len = b->key_off[k + 1] - b->key_off[k];
-    if (len != 65 || b->key_bytes[b->key_off[k]] != 4) continue;
-    if (!ctx->kc_index.count(std::string((const char *)b->key_bytes + b->key_off[k], 65))) return false;
-  }
-  return true;
+  return (ctx->flags & BV_F_KEY_CACHE) && bv_kc_covers(ctx, b->n_keys, b->key_bytes, b->key_off);
 }
 
 static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {

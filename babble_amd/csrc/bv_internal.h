@@ -340,6 +340,7 @@ int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
                   const uint64_t *dko, hipStream_t st, bool *use, bool force_build = false);
 uint32_t bv_kc_lookup(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, uint64_t *tabs);
+bool bv_kc_covers(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko);
 void bv_kc_init(bv_ctx *ctx);     // budget, admission and fault-injection settings (bv_create)
 void bv_kc_release(bv_ctx *ctx);  // free every cached table (bv_destroy, after all calls finished)
 // `res` (may be null): the caller's result buffers, written by DMA directly

@@ -301,18 +301,30 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
 // table of every batch key that has one built, else 0.  Small batches never
 // build tables (registration and bulk batches do).  Returns the hits.
 uint32_t bv_kc_lookup(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, uint64_t *tabs) {
-  uint32_t hits = 0;
+  uint32_t hits = 0;  // distinct keys, as bv_kc_prepare counts them
   const uint64_t clock = ++ctx->kc_clock;
   for (uint32_t k = 0; k < n_keys; k++) {
     tabs[k] = 0;
     if (!key_form_ok(hkb + hko[k], hko[k + 1] - hko[k])) continue;
     auto it = ctx->kc_index.find(std::string((const char *)hkb + hko[k], (size_t)(hko[k + 1] - hko[k])));
     if (it == ctx->kc_index.end()) continue;
-    ctx->kc_slots[it->second].last_use = clock;
-    tabs[k] = (uint64_t)(uintptr_t)ctx->kc_slots[it->second].table;
-    hits++;
+    auto &slot = ctx->kc_slots[it->second];
+    hits += slot.last_use != clock;
+    slot.last_use = clock;
+    tabs[k] = (uint64_t)(uintptr_t)slot.table;
   }
   return hits;
+}
+
+// Every well-formed key of the batch has a table or is known to be off the
+// curve (k_small then needs no per-batch table build).
+bool bv_kc_covers(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko) {
+  for (uint32_t k = 0; k < n_keys; k++) {
+    if (!key_form_ok(hkb + hko[k], hko[k + 1] - hko[k])) continue;
+    const std::string key((const char *)hkb + hko[k], (size_t)(hko[k + 1] - hko[k]));
+    if (!ctx->kc_index.count(key) && !ctx->kc_bad.count(key)) return false;
+  }
+  return true;
 }
 
 extern "C" int bv_kc_register(bv_ctx *ctx, uint32_t n_keys, const uint8_t *key_bytes, const uint64_t *key_off) {

@@ -1,0 +1,241 @@
+// coop.h — wave-cooperative field arithmetic mod p for latency-bound chains
+// (the north star's "wavefront-cooperative carry propagation").
+//
+// A lone wave that walks a serial chain (the key tables' base chain
+// 2^(L j) Q: ~120 doublings per key) is bound by the dependent-instruction
+// latency of ONE lane's field multiply (~440 ns, profiles/r03_ubench_coop.txt),
+// not by issue slots: 63 lanes idle.  Here a field element lives in a 16-lane
+// DPP row — limb k (32 bits) in lane k < 8 of the row, zeros in lanes 8..15 —
+// so one multiply is ~8 short column steps per lane instead of ~160
+// instructions, and the wave's four rows run up to four DIFFERENT multiplies
+// at once (the independent products of one doubling level).
+//
+// Carries between limbs are resolved with a carry-lookahead over wave-wide
+// lane masks: G = lanes whose digit carries out, P = lanes whose digit is
+// 0xFFFFFFFF; the carries INTO the lanes are ((G << 1) + P) ^ P.
+//
+// Forms:  NORMAL  lanes 0..7 hold the limbs of a value < 2^256 (weakly
+//                 reduced mod p), lanes 8..15 hold 0 — what mul() takes and
+//                 returns;
+//         WIDE    a 64-bit value per lane (lanes 0..8), value =
+//                 sum w_k 2^(32 k), w_k < 2^40 — sums and differences of
+//                 normal values without carry handling; norm() brings them
+//                 back (one carry pass + the 2^256 = 2^32 + 977 fold).
+// Subtraction adds a multiple of p whose redundant limbs are all >= 2^32
+// (M4 = 4p below), so every lane stays non-negative.
+//
+// Every step is exact for all inputs: the rare carry out of limb 7 after a
+// fold is taken by a wave-uniform branch.  gfx950 only (DPP row controls).
+#pragma once
+#include "field.h"
+
+#if defined(__HIPCC__)
+namespace coop {
+
+__device__ __forceinline__ uint32_t pos() { return __lane_id() & 15u; }
+__device__ __forceinline__ uint32_t row() { return __lane_id() >> 4; }
+
+// DPP (gfx9 encoding): row_shl:n 0x100+n (lane k reads lane k+n of its row),
+// row_shr:n 0x110+n (lane k reads lane k-n), row_newbcast:n 0x150+n (every
+// lane reads lane n of its row); lanes without a source read 0 (bound_ctrl)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+}
+
+// v + (carry into this lane), carries generated where `gen` and rippling
+// through lanes holding 0xFFFFFFFF.  A row's top lane never generates here
+// (every caller keeps its values below the row's width), so rows stay
+// independent.
+__device__ __forceinline__ uint32_t resolve(uint32_t v, bool gen) {
+  const uint64_t G = __ballot(gen), P = __ballot(v == 0xFFFFFFFFu);
+  const uint64_t C = ((G << 1) + P) ^ P;
+  return v + (uint32_t)((C >> __lane_id()) & 1u);
+}
+
+// lanes 0..8 digits d (d_8 = a multiple of 2^256, small): fold d_8 (2^256 =
+// 2^32 + 977) into lanes 0 and 1 and resolve; a carry out of lane 7 (the
+// value was within ~2^45 of 2^256) folds once more.  Returns NORMAL.
+__device__ __forceinline__ uint32_t fold(uint32_t d) {
+  const uint32_t k = pos();
+  uint32_t o = dpp<0x158>(d);
+  uint64_t z = k == 0 ? (uint64_t)d + (uint64_t)o * 977u : k == 1 ? (uint64_t)d + o : (k < 8 ? (uint64_t)d : 0u);
+  uint64_t y = (uint64_t)(uint32_t)z + dpp<0x111>((uint32_t)(z >> 32));
+  d = resolve((uint32_t)y, (y >> 32) != 0);  // lane 8: the carry out of limb 7
+  if (__ballot(k == 8 && d != 0)) {        // rare, wave-uniform
+    o = dpp<0x158>(d);
+    z = k == 0 ? (uint64_t)d + (uint64_t)o * 977u : k == 1 ? (uint64_t)d + o : (k < 8 ? (uint64_t)d : 0u);
+    y = (uint64_t)(uint32_t)z + dpp<0x111>((uint32_t)(z >> 32));
+    d = resolve((uint32_t)y, (y >> 32) != 0);  // the value is now < 2^46: no carry out
+  }
+  return k < 8 ? d : 0u;
+}
+
+// WIDE -> NORMAL
+__device__ __forceinline__ uint32_t norm(uint64_t w) {
+  const uint64_t v = (uint64_t)(uint32_t)w + dpp<0x111>((uint32_t)(w >> 32));
+  return fold(resolve((uint32_t)v, (v >> 32) != 0));
+}
+
+// a b mod p; a, b NORMAL (row-local), result NORMAL
+__device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) {
+  const uint32_t k = pos();
+  uint64_t acc = 0;
+  uint32_t cnt = 0, bs = b;
+  // lane k accumulates column k = sum_s a_s b_(k-s) (b shifts up one lane a step)
+#define COOP_STEP(s)                                 \
+  {                                                  \
+    const uint32_t as = dpp<0x150 + (s)>(a);         \
+    if (s) bs = dpp<0x111>(bs);                      \
+    const uint64_t p = (uint64_t)as * bs;            \
+    const uint64_t n = acc + p;                      \
+    cnt += n < p ? 1u : 0u;                          \
+    acc = n;                                         \
+  }
+  COOP_STEP(0) COOP_STEP(1) COOP_STEP(2) COOP_STEP(3) COOP_STEP(4) COOP_STEP(5) COOP_STEP(6) COOP_STEP(7)
+#undef COOP_STEP
+  // column k = lo_k + 2^32 hi_k + 2^64 cnt_k -> digit k of the 512-bit product
+  const uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
+  const uint64_t u = (uint64_t)lo + dpp<0x111>(hi) + dpp<0x112>(cnt);  // < 2^34
+  const uint64_t v = (uint64_t)(uint32_t)u + dpp<0x111>((uint32_t)(u >> 32));
+  uint32_t d = resolve((uint32_t)v, (v >> 32) != 0);  // d_0 .. d_15
+  // 2^256 = 2^32 + 977: lane k < 8 gets d_k + 977 d_(k+8) + d_(k+7) (k >= 1), lane 8 gets d_15
+  const uint32_t x8 = dpp<0x108>(d), x7 = dpp<0x107>(d);
+  const uint64_t t = k < 8 ? (uint64_t)x8 * 977u + d + (k >= 1 ? x7 : 0u) : (k == 8 ? (uint64_t)x7 : 0u);
+  const uint64_t w = (uint64_t)(uint32_t)t + dpp<0x111>((uint32_t)(t >> 32));  // < 2^32 + 2^10
+  d = resolve((uint32_t)w, (w >> 32) != 0);  // lanes 0..8, lane 9 in {0, 1}
+  // second fold: r_8 + 2^32 r_9 at 2^256 -> limbs 0..2
+  const uint32_t r8 = dpp<0x158>(d), r9 = dpp<0x159>(d);
+  const uint64_t z = k == 0   ? (uint64_t)d + (uint64_t)r8 * 977u
+                     : k == 1 ? (uint64_t)d + r8 + (uint64_t)r9 * 977u
+                     : k == 2 ? (uint64_t)d + r9
+                              : (k < 8 ? (uint64_t)d : 0u);
+  const uint64_t y = (uint64_t)(uint32_t)z + dpp<0x111>((uint32_t)(z >> 32));
+  d = resolve((uint32_t)y, (y >> 32) != 0);  // lane 8: the carry out of limb 7
+  if (__ballot(k == 8 && d != 0)) {        // rare, wave-uniform
+    const uint32_t o = dpp<0x158>(d);
+    const uint64_t z2 = k == 0 ? (uint64_t)d + (uint64_t)o * 977u : k == 1 ? (uint64_t)d + o : (k < 8 ? (uint64_t)d : 0u);
+    const uint64_t y2 = (uint64_t)(uint32_t)z2 + dpp<0x111>((uint32_t)(z2 >> 32));
+    d = resolve((uint32_t)y2, (y2 >> 32) != 0);
+  }
+  return k < 8 ? d : 0u;
+}
+
+// 4p in redundant limbs all >= 2^32 (lane k's limb; lane 8: 2): a + M4 - b
+// keeps every lane non-negative for NORMAL b.  sum M4_k 2^(32 k) = 4p.
+__device__ __forceinline__ uint64_t m4() {
+  const uint32_t k = pos();
+  return k == 0 ? 0x1FFFFF0BCull : k == 1 ? 0x1FFFFFFFAull : k < 8 ? 0x1FFFFFFFEull : (k == 8 ? 2ull : 0ull);
+}
+// WIDE multiples: a + (M4 - b) for NORMAL b
+__device__ __forceinline__ uint64_t negw(uint32_t b) { return m4() - b; }
+
+// the value of row `r` in every row (one ds_bpermute)
+__device__ __forceinline__ uint32_t from_row(uint32_t x, uint32_t r) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((r << 4) | pos()) << 2), (int)x);
+}
+
+// Jacobian doubling dbl-2009-l (a = 0; the same formulas, hence the same
+// representative, as point.h gej_double) with the state (X, Y, Z, NORMAL)
+// replicated in every row: its seven products form three levels,
+// {X^2, Y^2, Y Z} -> {B^2, E^2, (X + B)^2} -> E (D - X3), and the products of
+// a level run in rows 0..2 at once.  The input is not the identity.
+__device__ __forceinline__ void dbl(uint32_t &X, uint32_t &Y, uint32_t &Z) {
+  const uint32_t r = row();
+  // level 1: A = X^2 (row 0), B = Y^2 (row 1), YZ (row 2)
+  uint32_t m = mul(r == 0 || r == 3 ? X : Y, r == 1 ? Y : r == 2 ? Z : X);
+  const uint32_t A = from_row(m, 0), B = from_row(m, 1), YZ = from_row(m, 2);
+  const uint32_t E = norm(3ull * A);
+  const uint32_t XB = norm((uint64_t)X + B);
+  // level 2: C = B^2 (row 0), F = E^2 (row 1), W = (X + B)^2 (row 2)
+  const uint32_t s = r == 1 ? E : r == 2 ? XB : B;
+  m = mul(s, s);
+  const uint32_t C = from_row(m, 0), F = from_row(m, 1), W = from_row(m, 2);
+  const uint32_t D = norm(2ull * ((uint64_t)W + negw(A) + negw(C)));  // 2 ((X + B)^2 - A - C)
+  X = norm((uint64_t)F + 2ull * negw(D));                             // F - 2 D
+  const uint32_t t = norm((uint64_t)D + negw(X));                     // D - X3
+  // level 3: E (D - X3), every row
+  m = mul(E, t);
+  Y = norm((uint64_t)m + 8ull * negw(C));  // E (D - X3) - 8 C
+  Z = norm(2ull * YZ);
+}
+
+// a NORMAL value (replicated in every row) is 0 mod p: 0 or p itself
+__device__ __forceinline__ bool is_zero(uint32_t a) {
+  const uint32_t k = __lane_id();
+  const uint64_t z = __ballot(k < 8 && a == 0u), pp = __ballot(k < 8 && a == (k == 0 ? 0xFFFFFC2Fu : k == 1 ? 0xFFFFFFFEu : 0xFFFFFFFFu));
+  return (z & 0xFFu) == 0xFFu || (pp & 0xFFu) == 0xFFu;
+}
+
+// r += (x2, y2) affine (NORMAL), the same formulas and exceptional cases as
+// point.h gej_add_ge (Z3 = Z1 H): its products form five levels
+// {Z1^2} -> {x2 Z1Z1, Z1 Z1Z1} -> {y2 t, H^2} -> {H HH, X1 HH, Z1 H, R^2} ->
+// {R (V - X3), Y1 HHH}, each level's products in rows 0..3 at once.  `inf`
+// (wave-uniform) is r's identity flag.
+__device__ __forceinline__ void madd(uint32_t &X, uint32_t &Y, uint32_t &Z, bool &inf, uint32_t x2, uint32_t y2) {
+  if (inf) {
+    X = x2;
+    Y = y2;
+    Z = pos() == 0 ? 1u : 0u;
+    inf = false;
+    return;
+  }
+  const uint32_t r = row();
+  const uint32_t ZZ = mul(Z, Z);
+  uint32_t m = mul(r == 1 ? Z : x2, ZZ);  // row 0: U2 = x2 Z1Z1, row 1: Z1 Z1Z1
+  const uint32_t U2 = from_row(m, 0), t = from_row(m, 1);
+  const uint32_t H = norm((uint64_t)U2 + negw(X));
+  m = mul(r == 1 ? H : y2, r == 1 ? H : t);  // row 0: S2 = y2 Z1^3, row 1: HH = H^2
+  const uint32_t S2 = from_row(m, 0), HH = from_row(m, 1);
+  const uint32_t R = norm((uint64_t)S2 + negw(Y));
+  if (is_zero(H)) {  // wave-uniform
+    if (is_zero(R)) dbl(X, Y, Z);
+    else inf = true;
+    return;
+  }
+  // row 0: HHH = H HH, row 1: V = X1 HH, row 2: Z3 = Z1 H, row 3: R^2
+  m = mul(r == 0 ? H : r == 1 ? X : r == 2 ? Z : R, r == 2 ? H : r == 3 ? R : HH);
+  const uint32_t HHH = from_row(m, 0), V = from_row(m, 1), Z3 = from_row(m, 2), RR = from_row(m, 3);
+  const uint32_t X3 = norm((uint64_t)RR + negw(HHH) + 2ull * negw(V));  // R^2 - HHH - 2V
+  const uint32_t t2 = norm((uint64_t)V + negw(X3));                      // V - X3
+  m = mul(r == 1 ? Y : R, r == 1 ? HHH : t2);  // row 0: R (V - X3), row 1: Y1 HHH
+  const uint32_t a = from_row(m, 0), b = from_row(m, 1);
+  Y = norm((uint64_t)a + negw(b));
+  X = X3;
+  Z = Z3;
+}
+
+// (X, Y, Z) = k P for an affine P (NORMAL, replicated) and a 128-bit k
+// (4 limbs, wave-uniform): MSB-first over the non-adjacent form of k (~k/3
+// additions; verify_core.h naf_mul, per lane), every step cooperative.
+__device__ __forceinline__ void naf_mul(uint32_t &X, uint32_t &Y, uint32_t &Z, bool &inf, uint32_t px, uint32_t py,
+                                        const uint32_t k[4]) {
+  uint32_t h[5], kk[5], pos_[5], neg_[5], c = 0, prev = 0;
+  for (int i = 0; i < 4; i++) kk[i] = k[i];
+  kk[4] = 0;
+  for (int i = 0; i < 5; i++) {  // h = 3k
+    const uint32_t k2 = (kk[i] << 1) | (prev >> 31);
+    prev = kk[i];
+    h[i] = addc32(kk[i], k2, c);
+  }
+  for (int i = 0; i < 5; i++) {
+    const uint32_t x = h[i] ^ kk[i];
+    pos_[i] = x & h[i];
+    neg_[i] = x & kk[i];
+  }
+  for (int i = 0; i < 5; i++) {
+    pos_[i] = (pos_[i] >> 1) | (i < 4 ? pos_[i + 1] << 31 : 0u);
+    neg_[i] = (neg_[i] >> 1) | (i < 4 ? neg_[i + 1] << 31 : 0u);
+  }
+  const uint32_t ny = norm(negw(py));
+  inf = true;
+  X = Y = Z = 0;
+  for (int bit = 129; bit >= 0; bit--) {
+    if (!inf) dbl(X, Y, Z);
+    const uint32_t p = (pos_[bit >> 5] >> (bit & 31)) & 1u, n = (neg_[bit >> 5] >> (bit & 31)) & 1u;
+    if (p | n) madd(X, Y, Z, inf, px, n ? ny : py);
+  }
+}
+
+}  // namespace coop
+#endif

@@ -149,6 +149,17 @@ __global__ void __launch_bounds__(64) k_table_bases(uint32_t n_bases, const uint
   table_bases_one<LAT>(b, bxy, bases_jac, w, nwin);
 }
 
+// The same chain, one wave per base, wave-cooperative (coop.h): 126
+// doublings of 64 keys 0.46 -> 0.28 ms (profiles/r04_coop_chain.log).
+__global__ void __launch_bounds__(64) k_table_bases_coop(uint32_t n_bases, const uint32_t *__restrict__ bxy,
+                                                         const uint8_t *__restrict__ bstatus,
+                                                         uint32_t *__restrict__ bases_jac, int w, int nwin) {
+  const uint32_t b = blockIdx.x;
+  if (b >= n_bases) return;
+  if (bstatus && bstatus[b] != KS_OK) return;  // wave-uniform
+  coop_bases_one(b, bxy, bases_jac, w, nwin);
+}
+
 // blockDim = BLOCK (<= 2^W), grid (NWIN * 2^W/BLOCK, n_bases).  Block (j, c)
 // computes entries d = BLOCK c + t of window j and normalises them to
 // affine with one field inversion (prefix/suffix products in LDS).  PHI:
@@ -539,7 +550,8 @@ __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, uint64
 //   phase 3  wave 1 lanes 0, 1: u1 G over G windows 0-4 / 5-9
 //            wave 2: k1 Q;  wave 3: k2 phi(Q) — from the key's cached KC
 //            table when it has one (6 lookups each), else a NAF double-and-
-//            add chain (129 doublings) on the affine point
+//            add chain (129 doublings) on the affine point, the whole wave
+//            cooperating on each step (coop.h)
 //   phase 4  wave 0 lanes 0, 1: two XYZZ sums; thread 0: the last sum and
 //            x(R) mod N == r
 // Statuses only; the host packs a small batch's accept bits.
@@ -629,33 +641,42 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
     g_table_add_range<BV_GW, BV_GNWIN, true>(R, inf, g_table, u, (BV_GNWIN / 2) * (int)lane,
                                               lane ? BV_GNWIN : BV_GNWIN / 2);
     part_store(sh_part[lane], R, inf);
-  } else if (lane == 0 && wave >= 2) {  // k1 Q (wave 2) / k2 phi(Q) (wave 3)
+  } else if (wave >= 2) {  // k1 Q (wave 2) / k2 phi(Q) (wave 3)
     const uint32_t h = wave - 2;
     uint32_t kk[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) kk[k] = sh_k[4 * h + k];
     const bool neg = (go >> (1 + h)) & 1u;
-    const uint64_t tab = kc_tabs ? kc_tabs[item_key[b]] : 0;
-    gexz R;
-    bool inf = true;
-    fe_set(R.X, 0), fe_set(R.Y, 0), fe_set(R.ZZ, 0), fe_set(R.ZZZ, 0);
-    if (tab) {
-      key_table_add<BV_KCW, BV_KCNWIN, true, true>(R, inf, (const uint32_t *)tab, kk, neg, h != 0);
-    } else {
-      fe qx, qy;
-#pragma unroll
-      for (int c = 0; c < 8; c++) qx.v[c] = sh_q[c], qy.v[c] = sh_q[8 + c];
-      if (h) {
-        fe beta;
-        fe_load(beta, FE_BETA);
-        fe_mul(qx, qx, beta);  // phi(Q) = (beta x, y)
+    const uint64_t tab = kc_tabs ? kc_tabs[item_key[b]] : 0;  // wave-uniform
+    if (tab) {  // the key's cached KC table: 6 lookups on lane 0
+      if (lane == 0) {
+        gexz R;
+        bool inf = true;
+        fe_set(R.X, 0), fe_set(R.Y, 0), fe_set(R.ZZ, 0), fe_set(R.ZZZ, 0);
+        key_table_add<BV_KCW, BV_KCNWIN, true, true>(R, inf, (const uint32_t *)tab, kk, neg, h != 0);
+        part_store(sh_part[2 + h], R, inf);
       }
-      if (neg) fe_neg(qy, qy);
-      gej J;
-      naf_mul<true>(J, inf, qx, qy, kk);
-      if (!inf) gexz_from_gej(R, J);
+    } else {  // no table: the NAF chain, wave-cooperative (coop.h)
+      const uint32_t c = coop::pos();
+      uint32_t px = c < 8 ? sh_q[c] : 0u, py = c < 8 ? sh_q[8 + c] : 0u;
+      if (h) px = coop::mul(px, c < 8 ? FE_BETA[c] : 0u);  // phi(Q) = (beta x, y)
+      if (neg) py = coop::norm(coop::negw(py));
+      uint32_t X, Y, Z;
+      bool inf;
+      coop::naf_mul(X, Y, Z, inf, px, py, kk);
+      uint32_t ZZ = 0, ZZZ = 0;
+      if (!inf) {
+        ZZ = coop::mul(Z, Z);
+        ZZZ = coop::mul(ZZ, Z);
+      }
+      if (lane < 8) {
+        sh_part[2 + h][lane] = X;
+        sh_part[2 + h][8 + lane] = Y;
+        sh_part[2 + h][16 + lane] = ZZ;
+        sh_part[2 + h][24 + lane] = ZZZ;
+      }
+      if (lane == 0) sh_part[2 + h][32] = inf ? 1u : 0u;
     }
-    part_store(sh_part[2 + h], R, inf);
   }
   __syncthreads();
   // ---- phase 4
@@ -773,6 +794,13 @@ static int k12_lat_mask(bool busy) {
 // GLV key tables (verify_core.h).  `sub`
 // is the K12 sub-table scratch (n_bases * BV_K12SUB_U32 words), `pscr` the
 // K12 prefix-product scratch (n_bases * BV_K12HALF_U32 / 2 words).
+// the base chains run wave-cooperative (BV_COOP_BASES=0 at process start:
+// the per-lane chain, for A/B)
+static const bool g_coop_bases = [] {
+  const char *s = getenv("BV_COOP_BASES");
+  return s == nullptr || atoi(s) != 0;
+}();
+
 hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
                         uint32_t *bases_jac, uint32_t *sub, uint32_t *pscr, uint32_t *table, uint64_t n_items) {
   if (n_bases == 0) return hipSuccess;
@@ -782,7 +810,9 @@ hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t
   // a kernel's VGPR footprint decides when its waves get a SIMD: there the
   // throughput point ops (fewer VGPRs) win; elsewhere the zipped ones.
   const int lat = kw == 12 ? k12_lat_mask(!lat_variant(n_items)) : 3;
-  if (lat & 1)
+  if (g_coop_bases)
+    hipLaunchKernelGGL(k_table_bases_coop, dim3(n_bases), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w, nwin);
+  else if (lat & 1)
     hipLaunchKernelGGL(k_table_bases<true>, grid1(n_bases, 64), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w,
                        nwin);
   else
@@ -900,7 +930,10 @@ size_t kc_pscr_bytes() {
 hipError_t build_kc(hipStream_t st, uint32_t n, const uint32_t *kxy, const uint8_t *kst, uint32_t *bases_jac,
                     uint32_t *sub, uint32_t *pscr, const uint64_t *tabs) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_table_bases<true>, grid1(n, 64), dim3(64), 0, st, n, kxy, kst, bases_jac, BV_KCL, BV_KCNSUB);
+  if (g_coop_bases)
+    hipLaunchKernelGGL(k_table_bases_coop, dim3(n), dim3(64), 0, st, n, kxy, kst, bases_jac, BV_KCL, BV_KCNSUB);
+  else
+    hipLaunchKernelGGL(k_table_bases<true>, grid1(n, 64), dim3(64), 0, st, n, kxy, kst, bases_jac, BV_KCL, BV_KCNSUB);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_table_fill<BV_KCL, BV_KCNSUB, false>), dim3(BV_KCNSUB * ((1u << BV_KCL) / 256u), n),

@@ -8,6 +8,7 @@
 
 #include "../../include/babbleverify.h"
 #include "geometry.h"
+#include "coop.h"
 #include "point.h"
 #include "sha256.h"
 
@@ -168,6 +169,28 @@ DEV void table_bases_one(uint32_t b, const uint32_t *bxy, uint32_t *bases_jac, i
     }
   }
 }
+
+#if defined(__HIPCC__)
+// The same chain, wave-cooperative (coop.h): ONE wave per base, the
+// doubling's three product levels spread over the wave's DPP rows; lanes
+// 0..7 (row 0) store.  Same formulas, so the same Jacobian representatives
+// as table_bases_one.
+__device__ __forceinline__ void coop_bases_one(uint32_t b, const uint32_t *bxy, uint32_t *bases_jac, int w, int nwin) {
+  const uint32_t k = coop::pos(), lane = __lane_id();
+  uint32_t X = k < 8 ? bxy[16 * (uint64_t)b + k] : 0u, Y = k < 8 ? bxy[16 * (uint64_t)b + 8 + k] : 0u;
+  uint32_t Z = k == 0 ? 1u : 0u;
+  uint32_t *out = bases_jac + (uint64_t)b * nwin * 24;
+  for (int j = 0; j < nwin; j++) {
+    if (lane < 8) {
+      out[24 * j + lane] = X;
+      out[24 * j + 8 + lane] = Y;
+      out[24 * j + 16 + lane] = Z;
+    }
+    if (j + 1 < nwin)
+      for (int i = 0; i < w; i++) coop::dbl(X, Y, Z);
+  }
+}
+#endif
 
 // d * B (B affine), MSB-first double-and-add over `bits` bits of d.  The
 // returned Z is 1 for d == 0 so it can join a batch inversion.

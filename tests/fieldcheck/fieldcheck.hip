@@ -9,6 +9,8 @@
 #include <stdint.h>
 #include "../../babble_amd/csrc/field.h"
 #include "../../babble_amd/csrc/point.h"
+#include "../../babble_amd/csrc/verify_core.h"
+#include "../../babble_amd/csrc/coop.h"
 
 // OP_ZSSM + k: component k of the zipped (x^2, y^2, x y) program;
 // OP_ZSSS + k: component k of the zipped (x^2, y^2, (x ^ y)^2) program
@@ -126,5 +128,50 @@ extern "C" int fc_xyzz(int lat, uint32_t n, const uint32_t *acc, const uint32_t 
   (void)hipFree(da);
   (void)hipFree(dp);
   (void)hipFree(dr);
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
+// Key-table base chains B_j = 2^(w j) Q (j < nwin) of n affine points
+// (16 words each: x, y limbs), per lane (verify_core.h table_bases_one, the
+// zipped doubling) or wave-cooperative (coop.h: one wave per point, the
+// doubling's products spread over the DPP rows); out: n x nwin x 24 words
+// (X, Y, Z).  Both must agree mod p (same formulas).
+__global__ void __launch_bounds__(64) k_bases_lane(uint32_t n, const uint32_t *xy, uint32_t *out, int w, int nwin) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < n) table_bases_one<true>(b, xy, out, w, nwin);
+}
+__global__ void __launch_bounds__(64) k_bases_coop(uint32_t n, const uint32_t *xy, uint32_t *out, int w, int nwin) {
+  const uint32_t b = blockIdx.x;
+  if (b >= n) return;
+#if defined(__HIP_DEVICE_COMPILE__)
+  coop_bases_one(b, xy, out, w, nwin);
+#endif
+}
+
+extern "C" int fc_bases(int coop, uint32_t n, const uint32_t *xy, uint32_t *out, int w, int nwin, float *ms) {
+  uint32_t *dxy = nullptr, *dout = nullptr;
+  const size_t ob = (size_t)n * nwin * 24 * 4;
+  hipError_t e = hipMalloc(&dxy, (size_t)n * 64 + 64);
+  if (e == hipSuccess) e = hipMalloc(&dout, ob + 64);
+  if (e == hipSuccess) e = hipMemcpy(dxy, xy, (size_t)n * 64, hipMemcpyHostToDevice);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  for (int rep = 0; rep < 2 && e == hipSuccess; rep++) {  // the second run is timed
+    (void)hipEventRecord(e0, 0);
+    if (coop)
+      hipLaunchKernelGGL(k_bases_coop, dim3(n), dim3(64), 0, 0, n, dxy, dout, w, nwin);
+    else
+      hipLaunchKernelGGL(k_bases_lane, dim3((n + 63) / 64), dim3(64), 0, 0, n, dxy, dout, w, nwin);
+    e = hipGetLastError();
+    (void)hipEventRecord(e1, 0);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+  }
+  if (e == hipSuccess && ms) e = hipEventElapsedTime(ms, e0, e1);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, ob, hipMemcpyDeviceToHost);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(dxy);
+  (void)hipFree(dout);
   return e == hipSuccess ? 0 : -(int)e;
 }

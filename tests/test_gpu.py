@@ -271,10 +271,12 @@ def test_small_batch_kernel_key_cache(monkeypatch):
 
     b = synth.adversarial(200, seed=907, n_creators=6, scale_per_million=MIX)
     good = sorted({b.key(k) for k in range(b.n_keys) if gs.Unmarshal(b.key(k)) is not None})
+
     v = Verifier(device=0, flags=native.F_KEY_CACHE)
     try:
         v.register_keys(good)
-        check_against_oracle(v, b)
+        check_against_oracle(v, b)  # bulk: the 65-byte off-curve keys are new (decoded and remembered)
+        check_against_oracle(v, b)  # now every well-formed key is cached or known bad: k_small
         t = v.timing()
         assert t["key_path"] == 22 and t["kc_hits"] == len(good) and t["ms_h2d"] > 0
         v.register_keys(good[:3])  # still cached (registration only protects); a fresh key is not:

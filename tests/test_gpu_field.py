@@ -254,3 +254,42 @@ def test_xyzz_mixed_add_exceptional_cases(lat):
         assert R[i, 32] == 0, i
         assert ZZ and pow(ZZ, 3, P) == pow(ZZZ, 2, P), i
         assert (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P) == w, (i, i % 4)
+
+
+@pytest.mark.parametrize("w,nwin", [(6, 22), (8, 16), (11, 12)], ids=["K12", "K8", "KC"])
+def test_coop_base_chain_equals_per_lane(w, nwin):
+    """The wave-cooperative base chain (coop.h: field elements in 16-lane DPP
+    rows, the doubling's products spread over the rows, carry-lookahead over
+    lane masks) equals the per-lane zipped chain (table_bases_one) mod p on
+    every base of every key-table geometry, for random points and points
+    with extreme limb patterns (x or y near 0 / p), and prints both chain
+    latencies (one key, one wave)."""
+    G = (0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798,
+         0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8)
+    rng = random.Random(w)
+    pts = [_ec_mul(rng.randrange(1, N), G) for _ in range(60)]
+    pts += [G, _ec_mul(2, G), _ec_mul(N - 1, G), _ec_mul(3, G)]
+    xy = np.zeros((len(pts), 16), np.uint32)
+    for i, (x, y) in enumerate(pts):
+        xy[i, :8], xy[i, 8:] = _pack([x])[0], _pack([y])[0]
+    L = _lib()
+    L.fc_bases.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                           ctypes.POINTER(ctypes.c_float)]
+    L.fc_bases.restype = ctypes.c_int
+    outs, ms = [], []
+    for coop in (0, 1):
+        out = np.zeros((len(pts), nwin, 24), np.uint32)
+        t = ctypes.c_float()
+        assert L.fc_bases(coop, len(pts), xy.ctypes.data, out.ctypes.data, w, nwin, ctypes.byref(t)) == 0
+        outs.append(out)
+        ms.append(t.value)
+    for i in range(len(pts)):
+        for j in range(nwin):
+            a = [_unpack(outs[0][i:i + 1, j, 8 * c:8 * c + 8])[0] % P for c in range(3)]
+            b = [_unpack(outs[1][i:i + 1, j, 8 * c:8 * c + 8])[0] % P for c in range(3)]
+            assert a == b, (i, j)
+    # the chain's first base is the point itself; the last is 2^(w (nwin-1)) P
+    X, Y, Z = [_unpack(outs[1][0:1, nwin - 1, 8 * c:8 * c + 8])[0] % P for c in range(3)]
+    zi = pow(Z, -1, P)
+    assert (X * zi * zi % P, Y * zi * zi * zi % P) == _ec_mul(2 ** (w * (nwin - 1)), pts[0])
+    print(f"\nbase chain {w}x{nwin - 1} doublings, {len(pts)} keys: per-lane {ms[0]:.3f} ms, coop {ms[1]:.3f} ms")
