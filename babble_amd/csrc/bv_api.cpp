@@ -405,7 +405,7 @@ static int create_impl(bv_ctx *ctx) {
     ctx->ev_chunk = mb <= 0 ? 0 : std::max<uint64_t>(1, (uint64_t)(mb * (1 << 20)));  // >= 256 events a chunk anyway
   }
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
-  if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0, ctx->small_force = atoi(s) == 2;
+  if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
   return BV_OK;
 }
 
@@ -1065,7 +1065,10 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
 // ITX, node_rpc.go:250-260; a short SyncResponse): latency, not throughput.
 // ONE copy in, ONE k_small launch (every step of an item in one workgroup,
 // kernels.hip), ONE copy out; key-cache tables are resolved on the host
-// without a device round trip.
+// without a device round trip, keys without one take k_small's cooperative
+// NAF chain (1 cold event 0.55 ms against 0.78 ms through the per-batch K8
+// tables; with the key cache 0.18 ms against 0.47 ms,
+// profiles/r04_small_lat.log).
 // ---------------------------------------------------------------------------
 constexpr uint64_t kSmallItems = 256;       // items (and messages) per small batch
 constexpr uint64_t kSmallMsgLen = 16 << 10;  // longest message: one lane hashes it
@@ -1075,16 +1078,6 @@ static bool small_batch(const bv_batch *b) {
   for (uint64_t m = 0; m < b->n_msgs; m++)
     if (b->msg_off[m + 1] - b->msg_off[m] > kSmallMsgLen) return false;
   return true;
-}
-
-// k_small's per-item NAF chain (129 doublings on one lane) is no faster than
-// the per-batch K8 tables' base chain (1 cold event: 1.09 vs 1.01 ms,
-// profiles/r04_small_lat.log), so a small batch takes k_small when every
-// well-formed key has a key-cache table or is known to be off the curve
-// (malformed keys need none), or when BV_SMALL=2 forces it (tests).
-static bool small_keys_ready(bv_ctx *ctx, const bv_batch *b) {
-  if (ctx->small_force) return true;
-  return (ctx->flags & BV_F_KEY_CACHE) && bv_kc_covers(ctx, b->n_keys, b->key_bytes, b->key_off);
 }
 
 static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
@@ -1172,11 +1165,9 @@ extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   if (ctx->small_path && small_batch(b)) {
     int rc = bv_validate_host_batch(ctx, b);
     if (rc != BV_OK) return rc;
-    if (!small_keys_ready(ctx, b)) goto bulk;
     rc = small_verify(ctx, b, res);
     return rc == BV_OK ? rc : bv_drain(ctx, ctx->stream, rc);
   }
-bulk:
   bv_host_call call;
   int rc = bv_host_launch(ctx, b, &call, res);
   if (rc != BV_OK) return bv_drain(ctx, ctx->stream, rc);

@@ -277,10 +277,9 @@ struct bv_ctx {
   // chunk (BV_HOST_CHUNK_MB, >= 1 MB), event staging chunk (BV_EV_CHUNK_MB,
   // 0 = one chunk; chunks hold >= 256 events), bulk events' verify beside the next chunk
   // (BV_EV_VERIFY_STREAM=0: on the main stream)
-  // small host batches through k_small (BV_SMALL=0: the bulk pipeline; 2:
-  // also keys without a key-cache table)
+  // small host batches through k_small (BV_SMALL=0: the bulk pipeline)
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
-  bool ev_split_verify = true, small_path = true, small_force = false;
+  bool ev_split_verify = true, small_path = true;
 };
 
 // one in-flight host-entry call (bv_host_launch -> bv_host_finish)
@@ -340,7 +339,6 @@ int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
                   const uint64_t *dko, hipStream_t st, bool *use, bool force_build = false);
 uint32_t bv_kc_lookup(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, uint64_t *tabs);
-bool bv_kc_covers(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko);
 void bv_kc_init(bv_ctx *ctx);     // budget, admission and fault-injection settings (bv_create)
 void bv_kc_release(bv_ctx *ctx);  // free every cached table (bv_destroy, after all calls finished)
 // `res` (may be null): the caller's result buffers, written by DMA directly

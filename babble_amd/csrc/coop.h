@@ -34,6 +34,10 @@ namespace coop {
 
 __device__ __forceinline__ uint32_t pos() { return __lane_id() & 15u; }
 __device__ __forceinline__ uint32_t row() { return __lane_id() >> 4; }
+// per-lane masks and multipliers (lane-constant, so the compiler keeps
+// them in registers instead of branching on the lane index)
+__device__ __forceinline__ uint32_t lo8() { return pos() < 8 ? 0xFFFFFFFFu : 0u; }  // limb lanes
+__device__ __forceinline__ uint32_t f977() { return pos() == 0 ? 977u : (pos() == 1 ? 1u : 0u); }
 
 // DPP (gfx9 encoding): row_shl:n 0x100+n (lane k reads lane k+n of its row),
 // row_shr:n 0x110+n (lane k reads lane k-n), row_newbcast:n 0x150+n (every
@@ -57,18 +61,18 @@ __device__ __forceinline__ uint32_t resolve(uint32_t v, bool gen) {
 // 2^32 + 977) into lanes 0 and 1 and resolve; a carry out of lane 7 (the
 // value was within ~2^45 of 2^256) folds once more.  Returns NORMAL.
 __device__ __forceinline__ uint32_t fold(uint32_t d) {
-  const uint32_t k = pos();
+  const uint32_t m = lo8(), f = f977();
   uint32_t o = dpp<0x158>(d);
-  uint64_t z = k == 0 ? (uint64_t)d + (uint64_t)o * 977u : k == 1 ? (uint64_t)d + o : (k < 8 ? (uint64_t)d : 0u);
+  uint64_t z = (uint64_t)(d & m) + (uint64_t)o * f;  // lane 0: + 977 o, lane 1: + o
   uint64_t y = (uint64_t)(uint32_t)z + dpp<0x111>((uint32_t)(z >> 32));
   d = resolve((uint32_t)y, (y >> 32) != 0);  // lane 8: the carry out of limb 7
-  if (__ballot(k == 8 && d != 0)) {        // rare, wave-uniform
+  if (__ballot(pos() == 8 && d != 0)) {    // rare, wave-uniform
     o = dpp<0x158>(d);
-    z = k == 0 ? (uint64_t)d + (uint64_t)o * 977u : k == 1 ? (uint64_t)d + o : (k < 8 ? (uint64_t)d : 0u);
+    z = (uint64_t)(d & m) + (uint64_t)o * f;
     y = (uint64_t)(uint32_t)z + dpp<0x111>((uint32_t)(z >> 32));
     d = resolve((uint32_t)y, (y >> 32) != 0);  // the value is now < 2^46: no carry out
   }
-  return k < 8 ? d : 0u;
+  return d & m;
 }
 
 // WIDE -> NORMAL
@@ -83,14 +87,17 @@ __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) {
   uint64_t acc = 0;
   uint32_t cnt = 0, bs = b;
   // lane k accumulates column k = sum_s a_s b_(k-s) (b shifts up one lane a step)
-#define COOP_STEP(s)                                 \
-  {                                                  \
-    const uint32_t as = dpp<0x150 + (s)>(a);         \
-    if (s) bs = dpp<0x111>(bs);                      \
-    const uint64_t p = (uint64_t)as * bs;            \
-    const uint64_t n = acc + p;                      \
-    cnt += n < p ? 1u : 0u;                          \
-    acc = n;                                         \
+  // acc += as bs, cnt += the carry out: one v_mad_u64_u32 (its carry-out
+  // SGPR pair) and one v_addc (gfx950 wants 2 wait states between the VALU
+  // write of an SGPR and a VALU carry-in read of it: the s_nop)
+#define COOP_STEP(s)                                                                            \
+  {                                                                                             \
+    const uint32_t as = dpp<0x150 + (s)>(a);                                                    \
+    if (s) bs = dpp<0x111>(bs);                                                                 \
+    asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" \
+                 : "+v"(acc), "+v"(cnt)                                                         \
+                 : "v"(as), "v"(bs)                                                             \
+                 : "vcc");                                                                      \
   }
   COOP_STEP(0) COOP_STEP(1) COOP_STEP(2) COOP_STEP(3) COOP_STEP(4) COOP_STEP(5) COOP_STEP(6) COOP_STEP(7)
 #undef COOP_STEP
@@ -99,33 +106,34 @@ __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) {
   const uint64_t u = (uint64_t)lo + dpp<0x111>(hi) + dpp<0x112>(cnt);  // < 2^34
   const uint64_t v = (uint64_t)(uint32_t)u + dpp<0x111>((uint32_t)(u >> 32));
   uint32_t d = resolve((uint32_t)v, (v >> 32) != 0);  // d_0 .. d_15
-  // 2^256 = 2^32 + 977: lane k < 8 gets d_k + 977 d_(k+8) + d_(k+7) (k >= 1), lane 8 gets d_15
-  const uint32_t x8 = dpp<0x108>(d), x7 = dpp<0x107>(d);
-  const uint64_t t = k < 8 ? (uint64_t)x8 * 977u + d + (k >= 1 ? x7 : 0u) : (k == 8 ? (uint64_t)x7 : 0u);
+  // 2^256 = 2^32 + 977: lane k < 8 gets d_k + 977 d_(k+8) + d_(k+7) (k >= 1),
+  // lane 8 gets d_15 (row_shl:8 / :7 read zeros past the row's end)
+  const uint32_t m = lo8();
+  const uint32_t x8 = dpp<0x108>(d) & m, x7 = dpp<0x107>(d) & (k == 0 ? 0u : (k <= 8 ? 0xFFFFFFFFu : 0u));
+  const uint64_t t = (uint64_t)x8 * 977u + (d & m) + x7;
   const uint64_t w = (uint64_t)(uint32_t)t + dpp<0x111>((uint32_t)(t >> 32));  // < 2^32 + 2^10
   d = resolve((uint32_t)w, (w >> 32) != 0);  // lanes 0..8, lane 9 in {0, 1}
-  // second fold: r_8 + 2^32 r_9 at 2^256 -> limbs 0..2
+  // second fold: r_8 + 2^32 r_9 at 2^256 -> limbs 0..2 (977 r_8 | r_8 + 977 r_9 | r_9)
   const uint32_t r8 = dpp<0x158>(d), r9 = dpp<0x159>(d);
-  const uint64_t z = k == 0   ? (uint64_t)d + (uint64_t)r8 * 977u
-                     : k == 1 ? (uint64_t)d + r8 + (uint64_t)r9 * 977u
-                     : k == 2 ? (uint64_t)d + r9
-                              : (k < 8 ? (uint64_t)d : 0u);
+  const uint32_t a8 = k == 0 ? 977u : (k == 1 ? 1u : 0u), a9 = k == 1 ? 977u : (k == 2 ? 1u : 0u);
+  const uint64_t z = (uint64_t)(d & m) + (uint64_t)r8 * a8 + (uint64_t)r9 * a9;
   const uint64_t y = (uint64_t)(uint32_t)z + dpp<0x111>((uint32_t)(z >> 32));
   d = resolve((uint32_t)y, (y >> 32) != 0);  // lane 8: the carry out of limb 7
   if (__ballot(k == 8 && d != 0)) {        // rare, wave-uniform
     const uint32_t o = dpp<0x158>(d);
-    const uint64_t z2 = k == 0 ? (uint64_t)d + (uint64_t)o * 977u : k == 1 ? (uint64_t)d + o : (k < 8 ? (uint64_t)d : 0u);
+    const uint64_t z2 = (uint64_t)(d & m) + (uint64_t)o * f977();
     const uint64_t y2 = (uint64_t)(uint32_t)z2 + dpp<0x111>((uint32_t)(z2 >> 32));
     d = resolve((uint32_t)y2, (y2 >> 32) != 0);
   }
-  return k < 8 ? d : 0u;
+  return d & m;
 }
 
 // 4p in redundant limbs all >= 2^32 (lane k's limb; lane 8: 2): a + M4 - b
 // keeps every lane non-negative for NORMAL b.  sum M4_k 2^(32 k) = 4p.
 __device__ __forceinline__ uint64_t m4() {
   const uint32_t k = pos();
-  return k == 0 ? 0x1FFFFF0BCull : k == 1 ? 0x1FFFFFFFAull : k < 8 ? 0x1FFFFFFFEull : (k == 8 ? 2ull : 0ull);
+  const uint32_t lo = k == 0 ? 0xFFFFF0BCu : k == 1 ? 0xFFFFFFFAu : k < 8 ? 0xFFFFFFFEu : (k == 8 ? 2u : 0u);
+  return ((uint64_t)(k < 8 ? 1u : 0u) << 32) | lo;
 }
 // WIDE multiples: a + (M4 - b) for NORMAL b
 __device__ __forceinline__ uint64_t negw(uint32_t b) { return m4() - b; }

@@ -224,10 +224,9 @@ def test_small_batch_latency_rule_takes_k8_tables(monkeypatch):
 
 def test_small_batch_kernel_equals_oracle(monkeypatch):
     """k_small: a host batch of <= 256 items is one copy in,
-    ONE launch (hash, s^-1, key decode, u1 G, k1 Q + k2 phi(Q) by NAF chains
-    on keys without a table, the decision table) and one copy out (forced
-    here with BV_SMALL=2 for keys without a cached table, which the library
-    otherwise sends through the per-batch tables).  The golden items (every
+    ONE launch (hash, s^-1, key decode, u1 G, k1 Q + k2 phi(Q) by
+    wave-cooperative NAF chains on keys without a table, the decision table)
+    and one copy out.  The golden items (every
     decision-table class, R = infinity, doubling cases) in chunks of <= 256
     items, a 40-item adversarial batch, single events and one BlockBody with
     100 signatures: digests, statuses and bits equal the oracle's, and equal
@@ -235,7 +234,6 @@ def test_small_batch_kernel_equals_oracle(monkeypatch):
     from babble_amd import shard
     from babble_amd.verifier import Verifier
 
-    monkeypatch.setenv("BV_SMALL", "2")
     verifier = Verifier(device=0)
 
     golden, expected, _ = golden_items_batch()
@@ -262,11 +260,10 @@ def test_small_batch_kernel_equals_oracle(monkeypatch):
 
 
 def test_small_batch_kernel_key_cache(monkeypatch):
-    """k_small with registered keys: every valid key registered -> the small
-    kernel with the KC tables (6 lookups per GLV half; malformed keys need no
-    table); a batch with an unregistered valid key -> the per-batch tables;
-    with BV_SMALL=2, cached and uncached keys (NAF chains) in one launch.
-    All equal to the oracle."""
+    """k_small with registered keys: every valid key registered -> the KC
+    tables (6 lookups per GLV half; malformed keys need none); some keys
+    registered -> cached and uncached keys (cooperative NAF chains) in one
+    launch.  All equal to the oracle."""
     from babble_amd.verifier import Verifier
 
     b = synth.adversarial(200, seed=907, n_creators=6, scale_per_million=MIX)
@@ -275,17 +272,14 @@ def test_small_batch_kernel_key_cache(monkeypatch):
     v = Verifier(device=0, flags=native.F_KEY_CACHE)
     try:
         v.register_keys(good)
-        check_against_oracle(v, b)  # bulk: the 65-byte off-curve keys are new (decoded and remembered)
-        check_against_oracle(v, b)  # now every well-formed key is cached or known bad: k_small
+        check_against_oracle(v, b)
         t = v.timing()
         assert t["key_path"] == 22 and t["kc_hits"] == len(good) and t["ms_h2d"] > 0
-        v.register_keys(good[:3])  # still cached (registration only protects); a fresh key is not:
-        fresh = synth.events(30, n_creators=2, seed=908)
+        fresh = synth.events(30, n_creators=2, seed=908)  # unregistered: no table, the NAF chains
         check_against_oracle(v, fresh)
-        assert v.timing()["key_path"] == 8
+        assert v.timing()["key_path"] == 0
     finally:
         v.close()
-    monkeypatch.setenv("BV_SMALL", "2")
     v = Verifier(device=0, flags=native.F_KEY_CACHE)
     try:
         v.register_keys(good[:3])
