@@ -17,6 +17,7 @@
 // chunk.  Digests are copied back as soon as hashing ends (overlapping the
 // verify kernels), statuses and bits after the last kernel.
 #include "bv_internal.h"
+#include "hostsha.h"
 
 #include <algorithm>
 #include <chrono>
@@ -68,6 +69,12 @@ constexpr size_t kChunk = 16ull << 20;         // host-entry staging / PCIe chun
 // host batches whose whole staging layout is at most this cross PCIe as ONE
 // copy: each extra small H2D costs ~20 us of DMA latency on a lone call
 constexpr size_t kSmallStage = 1ull << 20;
+// Host entry: a message longer than this is hashed on the host (hostsha.cpp,
+// the SHA extensions) instead of by one GPU lane — SHA-256 of one message is
+// a serial chain, ~3.2 us a block on a lone lane against ~40 ns on a CPU
+// core: the 54 KB anchor Frame of C5 (853 blocks) took 2.8 ms of device time
+// on its lane (profiles/r04_bench_midround.json c5_fast_sync).
+constexpr uint64_t kHostHashLen = 16 << 10;
 
 }  // namespace
 
@@ -458,6 +465,8 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   bv_kc_release(ctx);
   ctx->pin_in.release();
   ctx->pin_out.release();
+  ctx->pin_long.release();
+  ctx->d_long.release();
   for (auto &sl : ctx->slot)
     for (auto &e : sl.ev)
       if (e) (void)hipEventDestroy(e);
@@ -824,6 +833,15 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   const uint32_t n_keys = b->n_keys;
   const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
   const uint64_t key_len = n_keys ? b->key_off[n_keys] : 0;
+  // long messages (hashed on the host, below)
+  std::vector<uint64_t> longm;
+  if (n_msgs && !ctx->pool->parallel_for(n_msgs, 1 << 17, [b](uint64_t lo, uint64_t hi) {
+        for (uint64_t m = lo; m < hi; m++)
+          if (b->msg_off[m + 1] - b->msg_off[m] > kHostHashLen) return false;
+        return true;
+      }))
+    for (uint64_t m = 0; m < n_msgs; m++)
+      if (b->msg_off[m + 1] - b->msg_off[m] > kHostHashLen) longm.push_back(m);
 
   // one staging layout, identical in pinned host memory and in HBM
   struct Seg {
@@ -954,11 +972,12 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   // Items in message order (item_msg non-decreasing: events, blocks) are
   // verified chunk by chunk as their messages are hashed, so the verify
   // kernels also run under the PCIe transfer; otherwise after the last chunk.
-  const bool in_order = ctx->pool->parallel_for(n_items > 0 ? n_items - 1 : 0, 1 << 17, [b](uint64_t lo, uint64_t hi) {
-    for (uint64_t i = lo; i < hi; i++)
-      if (b->item_msg[i] > b->item_msg[i + 1]) return false;
-    return true;
-  });
+  const bool in_order = longm.empty() &&  // (long messages' digests land after the last chunk)
+                        ctx->pool->parallel_for(n_items > 0 ? n_items - 1 : 0, 1 << 17, [b](uint64_t lo, uint64_t hi) {
+                          for (uint64_t i = lo; i < hi; i++)
+                            if (b->item_msg[i] > b->item_msg[i + 1]) return false;
+                          return true;
+                        });
   bv_item_pipe pipe{ctx, &d, {}, st, kc};
   rc = bv_out_bufs(ctx, &d, nullptr, nullptr, nullptr, true, &pipe.o);
   if (rc != BV_OK) return rc;
@@ -990,7 +1009,8 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
     HIPCHK(hipEventRecord(e, cs), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, e, 0), BV_E_LAUNCH, "join chunk");
     if (m0 == 0) HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SMALL], 0), BV_E_LAUNCH, "join offsets");
-    HIPCHK(bvk::sha256(st, m1 - m0, d.msg_bytes, d.msg_off + m0, pipe.o.dig + 8 * m0), BV_E_LAUNCH, "k_sha256");
+    HIPCHK(bvk::sha256(st, m1 - m0, d.msg_bytes, d.msg_off + m0, pipe.o.dig + 8 * m0, kHostHashLen), BV_E_LAUNCH,
+           "k_sha256");
     HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is the one used
     if (in_order) {  // items up to the first one of a message >= m1, in whole 64-item words
       const uint64_t i_end = m1 == n_msgs ? n_items
@@ -1000,6 +1020,31 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
       if (rc != BV_OK) return rc;
     }
     m0 = m1;
+  }
+  if (!longm.empty()) {
+    // the long messages on the host (pool threads, SHA extensions) while the
+    // device hashes the rest; then their digests cross and are put in place
+    const uint64_t nl = longm.size();
+    HIPCHK(ctx->pin_long.ensure(nl * 40), BV_E_OOM, "alloc pinned long digests");
+    HIPCHK(ctx->d_long.ensure(nl * 40), BV_E_OOM, "alloc long digests");
+    uint64_t *lidx = (uint64_t *)ctx->pin_long.p;
+    uint8_t *ldig = (uint8_t *)(lidx + nl);
+    memcpy(lidx, longm.data(), nl * 8);
+    ctx->pool->parallel_for(nl, 1, [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; i++) {
+        const uint64_t m = longm[i];
+        hsha::digest(b->msg_bytes + b->msg_off[m], b->msg_off[m + 1] - b->msg_off[m], ldig + 32 * i);
+      }
+      return true;
+    });
+    HIPCHK(hipMemcpyAsync(ctx->d_long.p, lidx, nl * 40, hipMemcpyHostToDevice, cs), BV_E_LAUNCH, "h2d long digests");
+    hipEvent_t e = chunk_event();
+    HIPCHK(hipEventRecord(e, cs), BV_E_LAUNCH, "event");
+    HIPCHK(hipStreamWaitEvent(st, e, 0), BV_E_LAUNCH, "join long digests");
+    HIPCHK(bvk::put_digests(st, nl, ctx->d_long.as<uint64_t>(), (const uint32_t *)(ctx->d_long.as<uint8_t>() + nl * 8),
+                            pipe.o.dig),
+           BV_E_LAUNCH, "k_put_digests");
+    HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");
   }
   HIPCHK(hipEventRecord(ctx->S().ev[E_STAGED], cs), BV_E_LAUNCH, "event");
   call->ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -28,7 +28,8 @@
 #define KS_OK 0  // k_key_decode statuses (verify_core.h)
 
 namespace bvk {
-hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *);
+hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint32_t *, uint64_t max_len = ~0ull);
+hipError_t put_digests(hipStream_t, uint64_t, const uint64_t *, const uint32_t *, uint32_t *);
 hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
 hipError_t sha256_chain(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
 hipError_t ev_build(hipStream_t, const bv_event_batch &, uint64_t, uint64_t, uint64_t *, uint32_t *, uint64_t *,
@@ -231,6 +232,10 @@ struct bv_ctx {
   // host-entry staging: one layout in pinned memory and in HBM
   PinnedBuf pin_in, pin_out;
   DevBuf d_in;
+  // host entry: messages longer than kHostHashLen hashed on the host (their
+  // index and digest), uploaded beside the device hashing
+  PinnedBuf pin_long;
+  DevBuf d_long;
   // work buffers
   // Per-call work buffers in kSlots slots: device-resident calls rotate
   // through them, so a call waits only for the last user of its slot and

@@ -32,11 +32,21 @@
 #ifndef BV_SHA_WAVES
 #define BV_SHA_WAVES 1
 #endif
+// one message per lane; messages longer than max_len are left to the host
+// (their digests arrive by k_put_digests)
 __global__ void __launch_bounds__(256, BV_SHA_WAVES) k_sha256(uint64_t n_msgs, const uint8_t *__restrict__ bytes,
                                                 const uint64_t *__restrict__ off,
-                                                uint32_t *__restrict__ digest_words) {
+                                                uint32_t *__restrict__ digest_words, uint64_t max_len) {
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m < n_msgs) sha256_one(m, bytes, off, digest_words);
+  if (m < n_msgs && off[m + 1] - off[m] <= max_len) sha256_one(m, bytes, off, digest_words);
+}
+
+// digests computed elsewhere (the host, for long messages): message idx[i]
+// gets the 8 words vals[8 i ..]
+__global__ void __launch_bounds__(256) k_put_digests(uint64_t n, const uint64_t *__restrict__ idx,
+                                                     const uint32_t *__restrict__ vals, uint32_t *__restrict__ dig) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < 8 * n) dig[8 * idx[t / 8] + t % 8] = vals[t];
 }
 
 // PeerSet.Hash (src/peers/peer_set.go:104-115): h = [] then, for each peer
@@ -717,9 +727,16 @@ static inline dim3 grid1(uint64_t n, uint32_t block) { return dim3((uint32_t)((n
 #endif
 static inline bool lat_variant(uint64_t n) { return n <= BV_LAT_MAX_ITEMS; }
 
-hipError_t sha256(hipStream_t st, uint64_t n, const uint8_t *bytes, const uint64_t *off, uint32_t *dig) {
+hipError_t sha256(hipStream_t st, uint64_t n, const uint8_t *bytes, const uint64_t *off, uint32_t *dig,
+                  uint64_t max_len) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sha256, grid1(n, 256), dim3(256), 0, st, n, bytes, off, dig);
+  hipLaunchKernelGGL(k_sha256, grid1(n, 256), dim3(256), 0, st, n, bytes, off, dig, max_len);
+  return hipGetLastError();
+}
+
+hipError_t put_digests(hipStream_t st, uint64_t n, const uint64_t *idx, const uint32_t *vals, uint32_t *dig) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_put_digests, grid1(8 * n, 256), dim3(256), 0, st, n, idx, vals, dig);
   return hipGetLastError();
 }
 

@@ -417,3 +417,31 @@ def test_bench_gpus_beyond_the_box_fails():
                        capture_output=True, text=True, timeout=180)
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_long_messages_hashed_on_host(verifier):
+    """Host entry: messages longer than 16 KB (e.g. a Frame's JSON) are hashed
+    on the host (SHA extensions) beside the device's hashing of the rest, and
+    their digests put in place before the verify kernels: a batch mixing
+    C2 bodies with 16 KB + 1, 20 KB and 100 KB messages (some signed, some
+    item-less), in order and shuffled — digests, statuses and bits equal the
+    oracle's."""
+    import dataclasses
+
+    from babble_amd.batch import PackedBatch
+
+    b = synth.adversarial(3000, seed=31, n_creators=8, scale_per_million=MIX)
+    rng = np.random.default_rng(31)
+    msgs = [b.message(m) for m in range(b.n_msgs)]
+    for pos_, size in ((5, 16 * 1024 + 1), (700, 20_000), (2999, 100_000), (1500, 64)):
+        msgs[pos_] = rng.integers(0, 256, size, dtype=np.uint8).tobytes()  # signatures over them now fail
+    msgs += [rng.integers(0, 256, 50_000, dtype=np.uint8).tobytes()]  # an item-less long message
+    off = np.zeros(len(msgs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in msgs])
+    lb = PackedBatch(np.frombuffer(b"".join(msgs), np.uint8).copy(), off, b.key_bytes, b.key_off, b.item_msg,
+                     b.item_key, b.r_be, b.s_be, b.pre)
+    res = check_against_oracle(verifier, lb)
+    assert res.msg_hash[-1].tobytes() == hashlib.sha256(msgs[-1]).digest()
+    perm = rng.permutation(lb.n_items)
+    check_against_oracle(verifier, dataclasses.replace(lb, item_msg=lb.item_msg[perm], item_key=lb.item_key[perm],
+                                                       r_be=lb.r_be[perm], s_be=lb.s_be[perm], pre=lb.pre[perm]))
