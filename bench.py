@@ -588,8 +588,10 @@ def c5_leg(args, local, reps=5):
     want[bad] = 0
     assert np.array_equal(res.status, want), "C5 statuses differ from the seeded corruption"
     el = float(np.median(ts))
-    # device-resident: the same batch in HBM, bv_verify_batch_device
-    d = v.to_device(rb)
+    # device-resident: the blocks' batch in HBM, bv_verify_batch_device (the
+    # 54 KB Frame left out: in HBM it would be one GPU lane's serial SHA chain,
+    # which the host entry above hashes on the CPU instead)
+    d = v.to_device(b)
     v.verify_device(d, sync=True)
     dts = []
     for _ in range(reps):
