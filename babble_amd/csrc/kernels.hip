@@ -818,14 +818,12 @@ static const bool g_coop_bases = [] {
   return s == nullptr || atoi(s) != 0;
 }();
 
-hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
-                        uint32_t *bases_jac, uint32_t *sub, uint32_t *pscr, uint32_t *table, uint64_t n_items) {
+// The serial base chains 2^(w k)·Q of a table build (its first launch).
+hipError_t table_bases(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
+                       uint32_t *bases_jac, uint64_t n_items) {
   if (n_bases == 0) return hipSuccess;
   const int w = kw == 0 ? BV_GL : kw == 8 ? BV_KW : BV_K12L;
   const int nwin = kw == 0 ? BV_GNSUB : kw == 8 ? BV_KNWIN : BV_K12NSUB;
-  // K12 (large batches) builds beside the bulk kernels on a busy chip, where
-  // a kernel's VGPR footprint decides when its waves get a SIMD: there the
-  // throughput point ops (fewer VGPRs) win; elsewhere the zipped ones.
   const int lat = kw == 12 ? k12_lat_mask(!lat_variant(n_items)) : 3;
   if (g_coop_bases)
     hipLaunchKernelGGL(k_table_bases_coop, dim3(n_bases), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w, nwin);
@@ -835,8 +833,18 @@ hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t
   else
     hipLaunchKernelGGL(k_table_bases<false>, grid1(n_bases, 64), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w,
                        nwin);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+// The sub-tables and chord sums over the bases table_bases wrote.
+hipError_t table_fill(hipStream_t st, int kw, uint32_t n_bases, const uint8_t *bstatus, uint32_t *bases_jac,
+                      uint32_t *sub, uint32_t *pscr, uint32_t *table, uint64_t n_items) {
+  if (n_bases == 0) return hipSuccess;
+  // K12 (large batches) builds beside the bulk kernels on a busy chip, where
+  // a kernel's VGPR footprint decides when its waves get a SIMD: there the
+  // throughput point ops (fewer VGPRs) win; elsewhere the zipped ones.
+  const int lat = kw == 12 ? k12_lat_mask(!lat_variant(n_items)) : 3;
+  hipError_t e = hipSuccess;
   if (kw == 0) {  // n_bases == 1 (G); `pscr` holds BV_GPAIR_BLOCKS blocks x 4096 fe
     hipLaunchKernelGGL((k_table_fill<BV_GL, BV_GNSUB, false>), dim3(BV_GNSUB * ((1u << BV_GL) / 256u), 1), dim3(256),
                        0, st, bases_jac, bstatus, sub);
@@ -872,6 +880,12 @@ hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t
                        bstatus, table, (uint4 *)pscr);
   }
   return hipGetLastError();
+}
+
+hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
+                        uint32_t *bases_jac, uint32_t *sub, uint32_t *pscr, uint32_t *table, uint64_t n_items) {
+  hipError_t e = table_bases(st, kw, n_bases, bxy, bstatus, bases_jac, n_items);
+  return e != hipSuccess ? e : table_fill(st, kw, n_bases, bstatus, bases_jac, sub, pscr, table, n_items);
 }
 
 hipError_t sinv(hipStream_t st, uint64_t n, uint32_t M, const uint32_t *s_be, const uint8_t *pre, uint32_t *w) {
