@@ -345,9 +345,7 @@ static int streams_acquire(bv_ctx *ctx) {
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
     bool ok = true;
     for (hipStream_t &s : d.lane) ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
-    const char *sp = getenv("BV_SPRIO");
-    const bool s_hi = sp ? atoi(sp) != 0 : BV_SPRIO;
-    ok = ok && hipStreamCreateWithPriority(&d.sstream, hipStreamNonBlocking, s_hi ? hi : lo) == hipSuccess;
+    ok = ok && hipStreamCreateWithPriority(&d.sstream, hipStreamNonBlocking, BV_SPRIO ? hi : lo) == hipSuccess;
     ok = ok && hipStreamCreateWithPriority(&d.kstream, hipStreamNonBlocking, BV_KPRIO ? hi : lo) == hipSuccess;
     if (!ok) {
       (void)hipGetLastError();
@@ -408,7 +406,6 @@ static int create_impl(bv_ctx *ctx) {
   ctx->pool = new CopyPool((int)std::min<unsigned>(hw ? hw - 1 : 0, 7));
   if (ctx->flags & BV_F_KEY_CACHE) bv_kc_init(ctx);
   // A/B knobs (bv_internal.h), read once here
-  if (const char *s = getenv("BV_KPLACE")) ctx->kplace = atoi(s);
   if (const char *s = getenv("BV_HOST_CHUNK_MB")) ctx->host_msg_chunk = (uint64_t)(std::max(1.0, atof(s)) * (1 << 20));
   if (const char *s = getenv("BV_EV_CHUNK_MB")) {
     const double mb = atof(s);
@@ -557,15 +554,6 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
                            ctx->S().kxy.as<uint32_t>()),
            BV_E_LAUNCH, "k_key_decode");
   HIPCHK(hipEventRecord(ev[E_KDEC], ctx->sstream), BV_E_LAUNCH, "event");
-  const bool split = !kc && table_mode && ctx->kplace != 0;
-  auto bases_on_s = [&]() -> int {
-    HIPCHK(bvk::table_bases(ctx->sstream, key_w, n_keys, ctx->S().kxy.as<uint32_t>(), ctx->S().kstatus.as<uint8_t>(),
-                            ctx->S().bases_jac.as<uint32_t>(), n_items),
-           BV_E_LAUNCH, "key bases");
-    HIPCHK(hipEventRecord(ev[E_BASES], ctx->sstream), BV_E_LAUNCH, "event");
-    return BV_OK;
-  };
-  if (split && ctx->kplace == 1 && bases_on_s() != BV_OK) return BV_E_LAUNCH;
   // s^-1 needs only s: concurrent with everything up to k_verify_g
   HIPCHK(hipStreamWaitEvent(ctx->sstream, s_ready, 0), BV_E_LAUNCH, "fork");
   // items per lane: kPrepM amortises the inversion in large batches; a small
@@ -575,14 +563,8 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   HIPCHK(bvk::sinv(ctx->sstream, n_items, M, (const uint32_t *)b->s_be, b->pre, ctx->S().scratch.as<uint32_t>()),
          BV_E_LAUNCH, "k_sinv");
   HIPCHK(hipEventRecord(ev[E_SINV], ctx->sstream), BV_E_LAUNCH, "event");
-  if (split && ctx->kplace == 2 && bases_on_s() != BV_OK) return BV_E_LAUNCH;
-  HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[split ? E_BASES : E_KDEC], 0), BV_E_LAUNCH, "fork");
-  if (split) {
-    HIPCHK(bvk::table_fill(ctx->kstream, key_w, n_keys, ctx->S().kstatus.as<uint8_t>(), ctx->S().bases_jac.as<uint32_t>(),
-                           ctx->S().key_sub.as<uint32_t>(), ctx->S().key_pscr.as<uint32_t>(),
-                           ctx->S().key_table.as<uint32_t>(), n_items),
-           BV_E_LAUNCH, "key tables");
-  } else if (!kc) {
+  HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_KDEC], 0), BV_E_LAUNCH, "fork");
+  if (!kc) {
     if (table_mode)
       HIPCHK(bvk::build_tables(ctx->kstream, key_w, n_keys, ctx->S().kxy.as<uint32_t>(), ctx->S().kstatus.as<uint8_t>(),
                                ctx->S().bases_jac.as<uint32_t>(), ctx->S().key_sub.as<uint32_t>(),

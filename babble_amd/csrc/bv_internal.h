@@ -36,9 +36,6 @@ hipError_t ev_build(hipStream_t, const bv_event_batch &, uint64_t, uint64_t, uin
                     uint8_t *, void *, size_t *);
 hipError_t ev_hash(hipStream_t, uint64_t, uint64_t, uint8_t *, const uint64_t *, uint32_t *);
 hipError_t iota(hipStream_t, uint64_t, uint32_t *);
-hipError_t table_bases(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint64_t);
-hipError_t table_fill(hipStream_t, int, uint32_t, const uint8_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t *,
-                      uint64_t);
 hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
                         uint32_t *, uint32_t *, uint64_t n_items);
 hipError_t build_kc(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *, uint32_t *,
@@ -198,7 +195,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // timing / ordering events (see bv_read_timing)
 enum {
   E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_SINV,
-  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_KDEC, E_BASES, E_COUNT
+  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_KDEC, E_COUNT
 };
 
 constexpr uint32_t kKcMaxBatchKeys = 4096;  // key cache: batches with more keys use per-batch tables
@@ -260,7 +257,6 @@ struct bv_ctx {
   Slot slot[kSlots];
   int cur = 0;
   Slot &S() { return slot[cur]; }
-  int kplace = 0;  // BV_KPLACE A/B: 0 bases+fills on kstream; 1 bases on sstream before s^-1; 2 after s^-1
   std::vector<hipEvent_t> chunk_ev;
   hipEvent_t ev_done = nullptr;  // end of the last call's device work (both slots: bv_wait_all)
   hipEvent_t ev_host = nullptr;  // host waits on this ctx's own work on a shared lane (bv_host_wait)

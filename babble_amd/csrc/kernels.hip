@@ -173,13 +173,8 @@ __global__ void __launch_bounds__(64) k_table_bases_coop(uint32_t n_bases, const
 // blockDim = BLOCK (<= 2^W), grid (NWIN * 2^W/BLOCK, n_bases).  Block (j, c)
 // computes entries d = BLOCK c + t of window j and normalises them to
 // affine with one field inversion (prefix/suffix products in LDS).  PHI:
-// also write the phi(T) half of a GLV key table.  SPLIT (one block per
-// window, BLOCK == 2^W): the 2^(W/2) low multiples l B and the 2^(W - W/2)
-// high multiples (h 2^(W/2)) B are built once by the block's first threads
-// and each entry is one Jacobian addition of a low and a high multiple
-// (0 < l < 2^(W/2) <= h 2^(W/2): never equal or opposite), instead of every
-// thread's own double-and-add over W bits (K8: ~3.4x fewer multiplies).
-template <int W, int NWIN, bool PHI, int BLOCK = 256, bool LAT = true, bool SPLIT = false>
+// also write the phi(T) half of a GLV key table.
+template <int W, int NWIN, bool PHI, int BLOCK = 256, bool LAT = true>
 __global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict__ bases_jac,
                                                       const uint8_t *__restrict__ bstatus,
                                                       uint32_t *__restrict__ table) {
@@ -205,25 +200,7 @@ __global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict
   gej R;
   bool inf;
   fe Z;
-  if constexpr (SPLIT) {
-    static_assert(BLOCK == (1 << W), "split fill: one block per window");
-    constexpr int LO = W / 2;
-    constexpr uint32_t NLO = 1u << LO, NHI = 1u << (W - LO);
-    __shared__ gej sP[NLO + NHI];
-    __shared__ uint32_t sInf[NLO + NHI];
-    if (t < NLO + NHI) {
-      gej P;
-      bool pinf;
-      fe pz;
-      table_point<LAT>(P, pinf, pz, bx, by, table_split_multiple(t, LO), W);
-      sP[t] = P;
-      sInf[t] = pinf;
-    }
-    __syncthreads();
-    table_point_join(R, inf, Z, sP, sInf, d, LO);
-  } else {
-    table_point<LAT>(R, inf, Z, bx, by, d, W);
-  }
+  table_point<LAT>(R, inf, Z, bx, by, d, W);
   if (!inf) fe_mul(Z, Z, bz);
   sPre[t] = Z;
   sSuf[t] = Z;
@@ -840,19 +817,15 @@ static const bool g_coop_bases = [] {
   const char *s = getenv("BV_COOP_BASES");
   return s == nullptr || atoi(s) != 0;
 }();
-// per-batch K8 / K12 fills from shared low / high multiples (k_table_fill
-// SPLIT; BV_SPLIT_FILL=0 at process start: every entry's own double-and-add)
-static const bool g_split_fill = [] {
-  const char *s = getenv("BV_SPLIT_FILL");
-  return s == nullptr || atoi(s) != 0;
-}();
 
-// The serial base chains 2^(w k)·Q of a table build (its first launch).
-hipError_t table_bases(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
-                       uint32_t *bases_jac, uint64_t n_items) {
+hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
+                        uint32_t *bases_jac, uint32_t *sub, uint32_t *pscr, uint32_t *table, uint64_t n_items) {
   if (n_bases == 0) return hipSuccess;
   const int w = kw == 0 ? BV_GL : kw == 8 ? BV_KW : BV_K12L;
   const int nwin = kw == 0 ? BV_GNSUB : kw == 8 ? BV_KNWIN : BV_K12NSUB;
+  // K12 (large batches) builds beside the bulk kernels on a busy chip, where
+  // a kernel's VGPR footprint decides when its waves get a SIMD: there the
+  // throughput point ops (fewer VGPRs) win; elsewhere the zipped ones.
   const int lat = kw == 12 ? k12_lat_mask(!lat_variant(n_items)) : 3;
   if (g_coop_bases)
     hipLaunchKernelGGL(k_table_bases_coop, dim3(n_bases), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w, nwin);
@@ -862,18 +835,8 @@ hipError_t table_bases(hipStream_t st, int kw, uint32_t n_bases, const uint32_t 
   else
     hipLaunchKernelGGL(k_table_bases<false>, grid1(n_bases, 64), dim3(64), 0, st, n_bases, bxy, bstatus, bases_jac, w,
                        nwin);
-  return hipGetLastError();
-}
-
-// The sub-tables and chord sums over the bases table_bases wrote.
-hipError_t table_fill(hipStream_t st, int kw, uint32_t n_bases, const uint8_t *bstatus, uint32_t *bases_jac,
-                      uint32_t *sub, uint32_t *pscr, uint32_t *table, uint64_t n_items) {
-  if (n_bases == 0) return hipSuccess;
-  // K12 (large batches) builds beside the bulk kernels on a busy chip, where
-  // a kernel's VGPR footprint decides when its waves get a SIMD: there the
-  // throughput point ops (fewer VGPRs) win; elsewhere the zipped ones.
-  const int lat = kw == 12 ? k12_lat_mask(!lat_variant(n_items)) : 3;
-  hipError_t e = hipSuccess;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   if (kw == 0) {  // n_bases == 1 (G); `pscr` holds BV_GPAIR_BLOCKS blocks x 4096 fe
     hipLaunchKernelGGL((k_table_fill<BV_GL, BV_GNSUB, false>), dim3(BV_GNSUB * ((1u << BV_GL) / 256u), 1), dim3(256),
                        0, st, bases_jac, bstatus, sub);
@@ -894,20 +857,10 @@ hipError_t table_fill(hipStream_t st, int kw, uint32_t n_bases, const uint8_t *b
       }
     }
   } else if (kw == 8) {
-    if (g_split_fill)
-      hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true, 256, true, true>), dim3(BV_KNWIN, n_bases), dim3(256), 0,
-                         st, bases_jac, bstatus, table);
-    else
-      hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
-                         dim3(256), 0, st, bases_jac, bstatus, table);
+    hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
+                       dim3(256), 0, st, bases_jac, bstatus, table);
   } else {
-    if (g_split_fill && (lat & 2))
-      hipLaunchKernelGGL((k_table_fill<BV_K12L, BV_K12NSUB, false, 1 << BV_K12L, true, true>), dim3(BV_K12NSUB, n_bases),
-                         dim3(1 << BV_K12L), 0, st, bases_jac, bstatus, sub);
-    else if (g_split_fill)
-      hipLaunchKernelGGL((k_table_fill<BV_K12L, BV_K12NSUB, false, 1 << BV_K12L, false, true>),
-                         dim3(BV_K12NSUB, n_bases), dim3(1 << BV_K12L), 0, st, bases_jac, bstatus, sub);
-    else if (lat & 2)
+    if (lat & 2)
       hipLaunchKernelGGL((k_table_fill<BV_K12L, BV_K12NSUB, false, 1 << BV_K12L, true>), dim3(BV_K12NSUB, n_bases),
                          dim3(1 << BV_K12L), 0, st, bases_jac, bstatus, sub);
     else
@@ -919,12 +872,6 @@ hipError_t table_fill(hipStream_t st, int kw, uint32_t n_bases, const uint8_t *b
                        bstatus, table, (uint4 *)pscr);
   }
   return hipGetLastError();
-}
-
-hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
-                        uint32_t *bases_jac, uint32_t *sub, uint32_t *pscr, uint32_t *table, uint64_t n_items) {
-  hipError_t e = table_bases(st, kw, n_bases, bxy, bstatus, bases_jac, n_items);
-  return e != hipSuccess ? e : table_fill(st, kw, n_bases, bstatus, bases_jac, sub, pscr, table, n_items);
 }
 
 hipError_t sinv(hipStream_t st, uint64_t n, uint32_t M, const uint32_t *s_be, const uint8_t *pre, uint32_t *w) {

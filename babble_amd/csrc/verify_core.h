@@ -208,24 +208,6 @@ DEV void table_point(gej &R, bool &inf, fe &Z, const fe &bx, const fe &by, uint3
   else Z = R.Z;
 }
 
-// Split fill (k_table_fill SPLIT): the block's 2^lo low multiples l B and
-// 2^(w - lo) high multiples (h 2^lo) B are P[0, 2^lo) and P[2^lo, ...);
-// thread t < 2^lo + 2^(w - lo) builds P[t] = table_split_multiple(t) B.
-DEV uint32_t table_split_multiple(uint32_t t, int lo) {
-  return t < (1u << lo) ? t : (t - (1u << lo)) << lo;
-}
-
-// d B = l B + (h 2^lo) B, l = d mod 2^lo, h = d >> lo: one Jacobian addition
-// (0 < l < 2^lo <= h 2^lo < 2^w << N: the two are never equal or opposite).
-DEV void table_point_join(gej &R, bool &inf, fe &Z, const gej *P, const uint32_t *pinf, uint32_t d, int lo) {
-  const uint32_t nlo = 1u << lo, l = d & (nlo - 1), h = d >> lo;
-  R = P[l];
-  inf = pinf[l] != 0;
-  gej_add(R, inf, P[nlo + h], pinf[nlo + h] != 0);
-  if (inf) fe_set(Z, 1);
-  else Z = R.Z;
-}
-
 // Store one entry given Z^-1 (canonical affine; d == 0 stored as zeros).
 // With `phi` != null also store phi(entry) = (beta x, y) there.
 DEV void table_store(uint32_t *entry, uint32_t *phi, uint32_t d, const gej &R, bool inf, const fe &zi) {

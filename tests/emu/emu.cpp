@@ -32,11 +32,10 @@ void parallel_for(uint64_t n, int nt, F f) {
   for (auto &x : th) x.join();
 }
 
-// k_table_bases + k_table_fill<w, nwin, phi, block, LAT, split>: one (b,
-// window, chunk) block per task; the block's prefix/suffix scans run
-// serially.
+// k_table_bases + k_table_fill<w, nwin, phi, block>: one (b, window, chunk)
+// block per task; the block's prefix/suffix scans run serially.
 void emu_fill(uint32_t n_bases, const uint8_t *bstatus, const uint32_t *bases, int w, uint32_t nwin, bool phi,
-              uint32_t block, uint32_t *table, int nt, bool split = false) {
+              uint32_t block, uint32_t *table, int nt) {
   const uint32_t chunks = (1u << w) / block;
   const uint64_t half_u32 = (uint64_t)nwin * (1ull << w) * BV_ENTRY_U32;
   parallel_for((uint64_t)n_bases * nwin * chunks, nt, [&](uint64_t task) {
@@ -54,19 +53,9 @@ void emu_fill(uint32_t n_bases, const uint8_t *bstatus, const uint32_t *bases, i
     std::vector<gej> R(block);
     std::vector<fe> Z(block), pre(block), suf(block);
     std::vector<char> inf(block);
-    const int lo = w / 2;
-    std::vector<gej> P(split ? (1u << lo) + (1u << (w - lo)) : 0);
-    std::vector<uint32_t> pinf(P.size());
-    for (uint32_t t = 0; t < P.size(); t++) {
-      bool f;
-      fe pz;
-      table_point(P[t], f, pz, bx, by, table_split_multiple(t, lo), w);
-      pinf[t] = f;
-    }
     for (uint32_t t = 0; t < block; t++) {
       bool f;
-      if (split) table_point_join(R[t], f, Z[t], P.data(), pinf.data(), c * block + t, lo);
-      else table_point(R[t], f, Z[t], bx, by, c * block + t, w);
+      table_point(R[t], f, Z[t], bx, by, c * block + t, w);
       if (!f) fe_mul(Z[t], Z[t], bz);
       inf[t] = f;
     }
@@ -133,7 +122,7 @@ void emu_build_tables(int kw, uint32_t n_bases, const uint32_t *bxy, const uint8
   std::vector<uint32_t> bases;
   if (kw == 8) {
     emu_bases(n_bases, bxy, bstatus, bases, BV_KW, BV_KNWIN, nt);
-    emu_fill(n_bases, bstatus, bases.data(), BV_KW, BV_KNWIN, true, 256, table, nt, true);
+    emu_fill(n_bases, bstatus, bases.data(), BV_KW, BV_KNWIN, true, 256, table, nt);
     return;
   }
   if (kw == 0) {
@@ -155,7 +144,7 @@ void emu_build_tables(int kw, uint32_t n_bases, const uint32_t *bxy, const uint8
   constexpr uint32_t W = BV_K12W, L = BV_K12L, NWIN = BV_K12NWIN, NS = 1u << L;
   emu_bases(n_bases, bxy, bstatus, bases, L, BV_K12NSUB, nt);
   std::vector<uint32_t> sub((size_t)n_bases * BV_K12SUB_U32 + 16);
-  emu_fill(n_bases, bstatus, bases.data(), L, BV_K12NSUB, false, NS, sub.data(), nt, true);
+  emu_fill(n_bases, bstatus, bases.data(), L, BV_K12NSUB, false, NS, sub.data(), nt);
   const uint64_t half_u32 = BV_K12HALF_U32;
   // k_table_pair: one block per (window, key); the top window stops after
   // its live digits.  Entry order within the block does not change results.
