@@ -42,15 +42,12 @@ constexpr uint32_t kBasesPerKey = 22;       // max(K8 16, K12 22, KC 14) bases p
 constexpr uint64_t kK12MinItemsPerKey = 2048;  // K12 pays for its 11x larger build above this
 constexpr uint32_t kMaxTableKeys = 8192;       // K8: 4 GiB of key tables
 constexpr uint32_t kMaxK12Keys = 1024;         // K12: 2.8 GiB
-// Latency rule: a small batch from a few keys is bound by its longest serial
-// chain, not by total work.  The per-lane generic path runs 128 doublings
-// AND ~128 additions in one lane per item; the K8 tables cost one lane's 120
-// doublings per key plus wide fills, so they finish first even at one item
-// per key (a single event: 1.66 -> see profiles/r03_bench.json latency_ms).
-#ifndef BV_LAT_TABLE_KEYS
-#define BV_LAT_TABLE_KEYS 16
-#endif
-constexpr uint32_t kLatTableKeys = BV_LAT_TABLE_KEYS;
+// Latency rule: a small batch is bound by its longest serial chain, not by
+// total work.  The per-lane generic path runs 128 doublings AND ~128
+// additions in one lane per item (~2.6 ms); the K8 tables cost one wave's
+// 120 doublings per key plus the fills, so they finish first even at one
+// item per key: up to 256 keys (1.85 ms; 0.8 ms at 32 keys), measured in
+// profiles/r04_ab_lat_keys.log.  ctx->lat_table_keys (BV_LAT_TABLE_KEYS).
 constexpr uint64_t kLatTableItems = 4096;
 #ifndef BV_PREP_M
 #define BV_PREP_M 16
@@ -413,6 +410,7 @@ static int create_impl(bv_ctx *ctx) {
   }
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
   if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
+  if (const char *s = getenv("BV_LAT_TABLE_KEYS")) ctx->lat_table_keys = (uint32_t)atoi(s);
   return BV_OK;
 }
 
@@ -520,7 +518,7 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   // tables once a key signs enough items (K12 for large batches, K8 for
   // mid-size), else the generic per-lane path.
   const bool table_mode = kc || (n_keys <= kMaxTableKeys && n_items >= 16ull * n_keys) ||
-                          (n_keys <= kLatTableKeys && n_items <= kLatTableItems && n_items > 0);
+                          (n_keys <= ctx->lat_table_keys && n_items <= kLatTableItems && n_items > 0);
   const int key_w = kc ? BV_KCW
                     : !table_mode ? 0
                     : (n_keys <= kMaxK12Keys && n_items >= kK12MinItemsPerKey * n_keys && !(ctx->flags & BV_F_K8))

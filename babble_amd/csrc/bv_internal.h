@@ -285,6 +285,7 @@ struct bv_ctx {
   // small host batches through k_small (BV_SMALL=0: the bulk pipeline)
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
   bool ev_split_verify = true, small_path = true;
+  uint32_t lat_table_keys = 256;  // latency rule: K8 tables for batches of <= 4096 items from up to this many keys (BV_LAT_TABLE_KEYS)
 };
 
 // one in-flight host-entry call (bv_host_launch -> bv_host_finish)

@@ -193,11 +193,22 @@ def test_k8_tables_forced_by_flag():
 
 
 def test_generic_path_few_items_per_key(verifier):
-    """Keys with fewer than 16 items each take the per-lane path."""
-    b = synth.adversarial(640, seed=9, n_creators=64, scale_per_million=MIX)
-    assert b.n_items < 16 * b.n_keys
+    """Keys with fewer than 16 items each take the per-lane path once the
+    batch is past the latency rule (> 4096 items or > 256 keys)."""
+    b = synth.adversarial(6000, seed=9, n_creators=512, scale_per_million=MIX)
+    assert 4096 < b.n_items < 16 * b.n_keys
     check_against_oracle(verifier, b)
     assert verifier.timing()["key_path"] == 0
+
+
+def test_latency_rule_k8_for_small_many_key_batches(verifier):
+    """A SyncResponse-sized batch from many creators (1000 events, 64 keys:
+    < 16 items per key) takes per-batch K8 tables under the latency rule
+    (2.6 -> 1.0 ms, profiles/r04_ab_lat_keys.log), bit-exact."""
+    b = synth.adversarial(1000, seed=19, n_creators=64, scale_per_million=MIX)
+    assert b.n_items < 16 * b.n_keys and b.n_keys <= 256
+    check_against_oracle(verifier, b)
+    assert verifier.timing()["key_path"] == 8
 
 
 def test_small_batch_latency_rule_takes_k8_tables(monkeypatch):
