@@ -449,8 +449,7 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
     if (ctx->has_done) (void)hipEventSynchronize(ctx->ev_done);
   }
   if (ctx->g_table) gtable_release(ctx->device);
-  DevBuf *bufs[] = {&ctx->d_in, &ctx->kc_kxy,  &ctx->kc_btabs, &ctx->ev_lens,
-                    &ctx->ev_ppos,   &ctx->ev_offs, &ctx->ev_bodies, &ctx->ev_tmp, &ctx->ev_iota};
+  DevBuf *bufs[] = {&ctx->d_in, &ctx->kc_kxy, &ctx->kc_btabs, &ctx->ev_iota};
   for (auto *b : bufs) b->release();
   for (auto &sl : ctx->slot) {
     DevBuf *sb[] = {&sl.digests,   &sl.kstatus, &sl.kxy, &sl.bases_jac, &sl.key_sub, &sl.key_pscr,

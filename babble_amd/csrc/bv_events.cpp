@@ -3,10 +3,10 @@
 //
 // Bulk batches (no in-batch parent: a store / bootstrap replay, parents by
 // known hash): host work is validation and the staging of the compact wire
-// arrays; the bodies are built and hashed on the device chunk by chunk
-// (k_ev_len -> inclusive scan (hipcub) -> k_ev_write -> k_ev_hash) while the
+// arrays; each chunk's bodies are serialised straight into SHA-256 on the
+// device (k_ev_body_hash, one lane per event: no body ever stored) while the
 // next chunk crosses PCIe, and each chunk's items are verified beside the
-// next chunk's build.  Batches with in-batch parents (a SyncResponse's DAG:
+// next chunk's hashing.  Batches with in-batch parents (a SyncResponse's DAG:
 // each body embeds its parents' hashes) are built and hashed on the host in
 // topological order instead (hostdag.cpp; the serial chain is ~50x faster on
 // one CPU core than on one GPU wave: 0.8 vs 5.5 ms per 1000-event
@@ -271,20 +271,21 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
     total += align256(bytes + pad);
     return o;
   };
-  // keys first (the key tables start once they land), then s and pre (s^-1),
-  // r, creators and the parent hashes; the per-event fields follow chunk by
-  // chunk (each chunk's bodies are built, hashed and verified while the next
-  // one crosses PCIe)
+  // keys first (the key tables start once they land), then s and pre (s^-1)
+  // and the parent hashes (any event may name any of them); the per-event
+  // fields, r and the creators among them, follow chunk by chunk (each
+  // chunk's bodies are hashed and its items verified while the next one
+  // crosses PCIe)
   const size_t o_koff = add(eb->key_off, (eb->n_keys + 1) * 8ull, ALL);
   const size_t o_kb = add(eb->key_bytes, key_len, ALL, 1, 64);
   const size_t keys_end = total;
   const size_t o_s = add(eb->s_be, n * 32, ALL);
   const size_t o_pre = add(eb->pre, eb->pre ? n : 0, ALL);
   const size_t s_end = total;
-  const size_t o_r = add(eb->r_be, n * 32, ALL);
-  const size_t o_cr = add(eb->creator, n * 4, ALL);
   const size_t o_ph = add(eb->parent_hashes, eb->parent_hashes ? eb->n_parent_hashes * 32 : 0, ALL);
   const size_t small_end = total;
+  const size_t o_r = add(eb->r_be, n * 32, EV, 32);
+  const size_t o_cr = add(eb->creator, n * 4, EV, 4);
   const size_t o_ix = add(eb->index, n * 8, EV, 8);
   const size_t o_ts = add(eb->timestamp, n * 8, EV, 8);
   const size_t o_pk = add(eb->parent_kind, n * 2, EV, 2);
@@ -324,8 +325,6 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
     for (uint64_t e = per; e < n; e += per) cb.push_back(e);
   }
   cb.push_back(n);
-  uint64_t max_chunk = 0;
-  for (size_t c = 0; c + 1 < cb.size(); c++) max_chunk = std::max(max_chunk, cb[c + 1] - cb[c]);
 
   if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // previous calls' work buffers / staging
   HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
@@ -356,28 +355,10 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   d.s_be = dev + o_s;
   d.pre = eb->pre ? dev + o_pre : nullptr;
 
-  // bodies: an upper bound on their size (exact lengths are on the device)
-  uint64_t kmax = 0;
-  for (uint32_t k = 0; k < eb->n_keys; k++) kmax = std::max<uint64_t>(kmax, eb->key_off[k + 1] - eb->key_off[k]);
-  const uint64_t bound = n * (160 + 2 * 68 + 2 * 20 + 4 * (kmax / 3 + 1) + 16) + 4 * (tx_len / 3 + n_tx) +
-                         8 * n_tx + itx_len + bsig_len + 64;
-  size_t tmp_bytes = 0;
-  HIPCHK(bvk::ev_build(st, d, 0, max_chunk, nullptr, nullptr, nullptr, nullptr, nullptr, &tmp_bytes), BV_E_LAUNCH,
-         "scan size");
-  HIPCHK(ctx->ev_lens.ensure(n * 8), BV_E_OOM, "alloc lens");
-  HIPCHK(ctx->ev_ppos.ensure(n * 8), BV_E_OOM, "alloc ppos");
-  HIPCHK(ctx->ev_offs.ensure((n + 1) * 8), BV_E_OOM, "alloc offs");
-  HIPCHK(ctx->ev_bodies.ensure(bound), BV_E_OOM, "alloc bodies");
-  HIPCHK(ctx->ev_tmp.ensure(std::max<size_t>(tmp_bytes, 256)), BV_E_OOM, "alloc scan scratch");
-  uint64_t *offs = ctx->ev_offs.as<uint64_t>();
-  uint32_t *ppos = ctx->ev_ppos.as<uint32_t>();
-  uint8_t *bodies = ctx->ev_bodies.as<uint8_t>();
-
-  // verification items: item e = (body e, creator key, r, s)
+  // verification items: item e = (body e, creator key, r, s); the bodies
+  // are never stored (k_ev_body_hash writes their digests only)
   bv_batch vb = {};
   vb.n_msgs = n;
-  vb.msg_bytes = bodies;
-  vb.msg_off = offs;
   vb.n_keys = eb->n_keys;
   vb.key_bytes = d.key_bytes;
   vb.key_off = d.key_off;
@@ -453,7 +434,7 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   pipe.kc = kc;
   rc = bv_run_keys(ctx, &vb, ctx->S().ev[E_KREADY], ctx->S().ev[E_SREADY], kc);
   if (rc != BV_OK) return rc;
-  rc = stage(s_end, small_end);  // r, creators, parent hashes (, the DAG order)
+  rc = stage(s_end, small_end);  // the parent hashes
   if (rc != BV_OK) return rc;
   HIPCHK(hipEventRecord(ctx->S().ev[E_SMALL], cs), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SMALL], 0), BV_E_LAUNCH, "join");
@@ -461,7 +442,7 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   HIPCHK(hipEventRecord(ctx->S().ev[E_FORK], st), BV_E_LAUNCH, "event");
 
   // per chunk: its fields cross PCIe on the copy stream; on the main stream
-  // the chunk's bodies are built and (bulk) hashed and its items verified
+  // the chunk's bodies are hashed (k_ev_body_hash) and its items verified
   for (size_t c = 0; c + 1 < cb.size(); c++) {
     const uint64_t e0 = cb[c], e1 = cb[c + 1];
     std::vector<CopyPool::Piece> pieces;
@@ -485,9 +466,7 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
     hipEvent_t landed = ctx->chunk_ev[c % ctx->chunk_ev.size()];
     HIPCHK(hipEventRecord(landed, cs), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, landed, 0), BV_E_LAUNCH, "join chunk");
-    HIPCHK(bvk::ev_build(st, d, e0, e1, ctx->ev_lens.as<uint64_t>(), ppos, offs, bodies, ctx->ev_tmp.p, &tmp_bytes),
-           BV_E_LAUNCH, "event bodies");
-    HIPCHK(bvk::ev_hash(st, e1 - e0, e0, bodies, offs, dig), BV_E_LAUNCH, "k_ev_hash");
+    HIPCHK(bvk::ev_body_hash(st, d, e0, e1, dig), BV_E_LAUNCH, "k_ev_body_hash");
     HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is used
     if (split_verify) {
       hipEvent_t hashed = ctx->chunk_ev[(c + 32) % ctx->chunk_ev.size()];  // waited on at once: reuse is safe

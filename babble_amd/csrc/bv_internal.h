@@ -32,9 +32,7 @@ hipError_t sha256(hipStream_t, uint64_t, const uint8_t *, const uint64_t *, uint
 hipError_t put_digests(hipStream_t, uint64_t, const uint64_t *, const uint32_t *, uint32_t *);
 hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
 hipError_t sha256_chain(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
-hipError_t ev_build(hipStream_t, const bv_event_batch &, uint64_t, uint64_t, uint64_t *, uint32_t *, uint64_t *,
-                    uint8_t *, void *, size_t *);
-hipError_t ev_hash(hipStream_t, uint64_t, uint64_t, uint8_t *, const uint64_t *, uint32_t *);
+hipError_t ev_body_hash(hipStream_t st, const bv_event_batch &b, uint64_t e0, uint64_t e1, uint32_t *dig);
 hipError_t iota(hipStream_t, uint64_t, uint32_t *);
 hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
                         uint32_t *, uint32_t *, uint64_t n_items);
@@ -276,7 +274,7 @@ struct bv_ctx {
   uint64_t kc_clock = 0, kc_bytes = 0, kc_budget = 0;
   DevBuf kc_kxy, kc_btabs;
   // bv_verify_events: body lengths, parent-hex positions, offsets, bodies
-  DevBuf ev_lens, ev_ppos, ev_offs, ev_bodies, ev_tmp, ev_iota;
+  DevBuf ev_iota;
   HostDagScratch dag_scratch;  // in-batch DAG batches: bodies built and hashed on the host (hostdag.cpp)
   // A/B knobs, read once at bv_create (never per call): host-entry message
   // chunk (BV_HOST_CHUNK_MB, >= 1 MB), event staging chunk (BV_EV_CHUNK_MB,

@@ -41,60 +41,73 @@ DEV uint32_t evj_dec_len(int64_t v) {
   return n;
 }
 
-DEV uint8_t *evj_lit(uint8_t *o, const char *s) {
-  while (*s) *o++ = (uint8_t)*s++;
-  return o;
+// Output sinks: anything with put(uint8_t), bytes in order.  EvjMem writes
+// them to memory (the host DAG path and the emulator); the device's bulk
+// path feeds them straight into SHA-256 (kernels.hip EvjShaSink).
+struct EvjMem {
+  uint8_t *p;
+  DEV void put(uint8_t c) { *p++ = c; }
+};
+
+template <class O>
+DEV void evj_lit(O &o, const char *s) {
+  while (*s) o.put((uint8_t)*s++);
 }
 
-DEV uint8_t *evj_dec(uint8_t *o, int64_t v) {
-  const uint32_t n = evj_dec_len(v);
+// decimal, most significant digit first: the digits (<= 20) are collected
+// least significant first as nibbles of lo (16) and hi (4), then emitted
+template <class O>
+DEV void evj_dec(O &o, int64_t v) {
   uint64_t m = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
-  if (v < 0) o[0] = '-';
-  for (uint32_t i = n; i > (v < 0 ? 1u : 0u); i--) {
-    o[i - 1] = (uint8_t)('0' + m % 10);
+  if (v < 0) o.put('-');
+  uint64_t lo = 0, hi = 0;
+  int n = 0;
+  do {
+    const uint64_t d = m % 10;
     m /= 10;
-  }
-  return o + n;
+    if (n < 16) lo |= d << (4 * n);
+    else hi |= d << (4 * (n - 16));
+    n++;
+  } while (m);
+  for (int i = n - 1; i >= 0; i--) o.put((uint8_t)('0' + ((i < 16 ? lo >> (4 * i) : hi >> (4 * (i - 16))) & 15)));
 }
 
 DEV uint8_t evj_b64c(uint32_t x) {
   return (uint8_t)(x < 26 ? 'A' + x : x < 52 ? 'a' + (x - 26) : x < 62 ? '0' + (x - 52) : x == 62 ? '+' : '/');
 }
 
-DEV uint8_t *evj_b64(uint8_t *o, const uint8_t *src, uint64_t n) {
+template <class O>
+DEV void evj_b64(O &o, const uint8_t *src, uint64_t n) {
   uint64_t i = 0;
   for (; i + 3 <= n; i += 3) {
     const uint32_t v = ((uint32_t)src[i] << 16) | ((uint32_t)src[i + 1] << 8) | src[i + 2];
-    o[0] = evj_b64c(v >> 18);
-    o[1] = evj_b64c((v >> 12) & 63);
-    o[2] = evj_b64c((v >> 6) & 63);
-    o[3] = evj_b64c(v & 63);
-    o += 4;
+    o.put(evj_b64c(v >> 18));
+    o.put(evj_b64c((v >> 12) & 63));
+    o.put(evj_b64c((v >> 6) & 63));
+    o.put(evj_b64c(v & 63));
   }
   if (n - i == 1) {
     const uint32_t v = (uint32_t)src[i] << 16;
-    o[0] = evj_b64c(v >> 18);
-    o[1] = evj_b64c((v >> 12) & 63);
-    o[2] = '=';
-    o[3] = '=';
-    o += 4;
+    o.put(evj_b64c(v >> 18));
+    o.put(evj_b64c((v >> 12) & 63));
+    o.put('=');
+    o.put('=');
   } else if (n - i == 2) {
     const uint32_t v = ((uint32_t)src[i] << 16) | ((uint32_t)src[i + 1] << 8);
-    o[0] = evj_b64c(v >> 18);
-    o[1] = evj_b64c((v >> 12) & 63);
-    o[2] = evj_b64c((v >> 6) & 63);
-    o[3] = '=';
-    o += 4;
+    o.put(evj_b64c(v >> 18));
+    o.put(evj_b64c((v >> 12) & 63));
+    o.put(evj_b64c((v >> 6) & 63));
+    o.put('=');
   }
-  return o;
 }
 
-// 32 digest bytes -> 64 uppercase hex chars
+DEV uint8_t evj_hexc(uint32_t x) { return (uint8_t)(x < 10 ? '0' + x : 'A' + x - 10); }
+
+// 32 digest bytes -> 64 uppercase hex chars (in place: the host DAG splice)
 DEV void evj_hex32(uint8_t *o, const uint8_t *d) {
   for (int i = 0; i < 32; i++) {
-    const uint32_t hi = d[i] >> 4, lo = d[i] & 15;
-    o[2 * i] = (uint8_t)(hi < 10 ? '0' + hi : 'A' + hi - 10);
-    o[2 * i + 1] = (uint8_t)(lo < 10 ? '0' + lo : 'A' + lo - 10);
+    o[2 * i] = evj_hexc(d[i] >> 4);
+    o[2 * i + 1] = evj_hexc(d[i] & 15);
   }
 }
 
@@ -146,69 +159,124 @@ DEV uint64_t evj_len(const bv_event_batch &b, uint64_t e, uint32_t ppos[2]) {
   return n;
 }
 
-// Write event e's body at `o` (evj_len bytes).  In-batch parents get 64 '0'
+// Event e's body into sink `o` (evj_len bytes).  In-batch parents get 64 '0'
 // placeholders, overwritten by evj_hex32 once the parent's digest exists.
-DEV void evj_write(const bv_event_batch &b, uint64_t e, uint8_t *o) {
-  o = evj_lit(o, EVJ_L0);
+template <class O>
+DEV void evj_emit(const bv_event_batch &b, uint64_t e, O &o) {
+  evj_lit(o, EVJ_L0);
   if (b.tx_list_nil && b.tx_list_nil[e]) {
-    o = evj_lit(o, "null");
+    evj_lit(o, "null");
   } else {
     const uint64_t t0 = b.tx_start[e], t1 = b.tx_start[e + 1];
-    *o++ = '[';
+    o.put('[');
     for (uint64_t t = t0; t < t1; t++) {
-      if (t > t0) *o++ = ',';
+      if (t > t0) o.put(',');
       if (b.tx_nil && b.tx_nil[t]) {
-        o = evj_lit(o, "null");
+        evj_lit(o, "null");
       } else {
-        *o++ = '"';
-        o = evj_b64(o, b.tx_bytes + b.tx_off[t], b.tx_off[t + 1] - b.tx_off[t]);
-        *o++ = '"';
+        o.put('"');
+        evj_b64(o, b.tx_bytes + b.tx_off[t], b.tx_off[t + 1] - b.tx_off[t]);
+        o.put('"');
       }
     }
-    *o++ = ']';
+    o.put(']');
   }
-  o = evj_lit(o, EVJ_L1);
+  evj_lit(o, EVJ_L1);
   const uint64_t il = evj_frag_len(b.itx_off, e);
   if (il) {
-    for (uint64_t i = 0; i < il; i++) o[i] = b.itx_json[b.itx_off[e] + i];
-    o += il;
+    for (uint64_t i = 0; i < il; i++) o.put(b.itx_json[b.itx_off[e] + i]);
   } else {
-    o = evj_lit(o, "null");
+    evj_lit(o, "null");
   }
-  o = evj_lit(o, EVJ_L2);
+  evj_lit(o, EVJ_L2);
   for (int p = 0; p < 2; p++) {
     const uint8_t k = b.parent_kind[2 * e + p];
-    if (p == 1) *o++ = ',';
+    if (p == 1) o.put(',');
     if (k == BV_PARENT_NONE) {
-      o = evj_lit(o, "\"\"");
+      evj_lit(o, "\"\"");
       continue;
     }
-    o = evj_lit(o, "\"0X");
-    if (k == BV_PARENT_HASH)
-      evj_hex32(o, b.parent_hashes + 32 * b.parent_ref[2 * e + p]);
-    else
-      for (int i = 0; i < 64; i++) o[i] = '0';
-    o += 64;
-    *o++ = '"';
+    evj_lit(o, "\"0X");
+    if (k == BV_PARENT_HASH) {
+      const uint8_t *d = b.parent_hashes + 32 * b.parent_ref[2 * e + p];
+      for (int i = 0; i < 32; i++) {
+        o.put(evj_hexc(d[i] >> 4));
+        o.put(evj_hexc(d[i] & 15));
+      }
+    } else {
+      for (int i = 0; i < 64; i++) o.put('0');
+    }
+    o.put('"');
   }
-  *o++ = ']';
-  o = evj_lit(o, EVJ_L3);
+  o.put(']');
+  evj_lit(o, EVJ_L3);
   const uint32_t c = b.creator[e];
-  o = evj_b64(o, b.key_bytes + b.key_off[c], b.key_off[c + 1] - b.key_off[c]);
-  o = evj_lit(o, EVJ_L4);
-  o = evj_dec(o, b.index[e]);
-  o = evj_lit(o, EVJ_L5);
+  evj_b64(o, b.key_bytes + b.key_off[c], b.key_off[c + 1] - b.key_off[c]);
+  evj_lit(o, EVJ_L4);
+  evj_dec(o, b.index[e]);
+  evj_lit(o, EVJ_L5);
   const uint64_t bl = evj_frag_len(b.bsig_off, e);
   if (bl) {
-    for (uint64_t i = 0; i < bl; i++) o[i] = b.bsig_json[b.bsig_off[e] + i];
-    o += bl;
+    for (uint64_t i = 0; i < bl; i++) o.put(b.bsig_json[b.bsig_off[e] + i]);
   } else {
-    o = evj_lit(o, "null");
+    evj_lit(o, "null");
   }
-  o = evj_lit(o, EVJ_L6);
-  o = evj_dec(o, b.timestamp[e]);
-  o[0] = '}';
-  o[1] = '\n';
+  evj_lit(o, EVJ_L6);
+  evj_dec(o, b.timestamp[e]);
+  o.put('}');
+  o.put('\n');
+}
+
+// Streaming SHA-256 sink (k_ev_body_hash: the body is never stored).
+// `row` holds the chaining value (8 words) and the current block (16 words,
+// big-endian); bytes are packed into `w` and stored a word at a time.  The
+// compression is out of line: one copy of the rounds, not one per put()
+// call site of evj_emit.
+__host__ __device__ __attribute__((noinline)) inline void evj_sha_block(uint32_t *row) {
+  uint32_t h[8], w[16];
+  for (int i = 0; i < 8; i++) h[i] = row[i];
+  for (int i = 0; i < 16; i++) w[i] = row[8 + i];
+  sha256_compress(h, w);
+  for (int i = 0; i < 8; i++) row[i] = h[i];
+}
+
+struct EvjSha {
+  uint32_t *row;
+  uint32_t w, n, nblk;  // pending word, bytes in the current block, full blocks
+  DEV void put(uint8_t c) {
+    w = (w << 8) | c;
+    if ((++n & 3) == 0) {
+      row[8 + (n >> 2) - 1] = w;
+      if (n == 64) {
+        evj_sha_block(row);
+        n = 0;
+        nblk++;
+      }
+    }
+  }
+};
+
+DEV EvjSha evj_sha_begin(uint32_t *row) {
+  uint32_t h[8];
+  sha256_init(h);
+  for (int i = 0; i < 8; i++) row[i] = h[i];
+  return EvjSha{row, 0, 0, 0};
+}
+
+// FIPS 180-4 padding, then the digest as big-endian bytes packed in words
+// (the layout of sha256_one's digest words)
+DEV void evj_sha_finish(EvjSha &o, uint32_t be[8]) {
+  const uint64_t bits = ((uint64_t)o.nblk * 64 + o.n) * 8;
+  o.put(0x80);
+  while (o.n != 56) o.put(0);
+  for (int i = 7; i >= 0; i--) o.put((uint8_t)(bits >> (8 * i)));
+  for (int i = 0; i < 8; i++) be[i] = bswap32(o.row[i]);
+}
+
+// Event e's body written at `o` (evj_len bytes).
+DEV void evj_write(const bv_event_batch &b, uint64_t e, uint8_t *o) {
+  EvjMem m{o};
+  evj_emit(b, e, m);
 }
 
 // ---------------------------------------------------------------------------

@@ -17,7 +17,9 @@
 // windows, built once by k_table_pair_kc) replace the keys stream and
 // k_verify_gq does g + q in one pass.  k_verify_generic covers keys with too
 // few items for a table.  The G table (k_table_pair_g, 21.5 GB) is built once
-// per process and device.
+// per process and device.  Host batches of <= 256 items take k_small (one
+// workgroup per item, one launch).  bv_verify_events' bulk batches hash each
+// body as it is serialised from wire fields (k_ev_body_hash: no body stored).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,7 +29,6 @@
 
 #include "verify_core.h"
 
-#include <hipcub/hipcub.hpp>
 
 #ifndef BV_SHA_WAVES
 #define BV_SHA_WAVES 1
@@ -77,64 +78,28 @@ __global__ void __launch_bounds__(64) k_sha256_chain(uint32_t n, const uint8_t *
 // ---------------------------------------------------------------------------
 // Events from wire fields (evjson.h): body lengths, bodies, level hashing
 // ---------------------------------------------------------------------------
-// Events [e0, e1) of the batch in every kernel below (a staging chunk).
-__global__ void __launch_bounds__(256) k_ev_len(bv_event_batch b, uint64_t e0, uint64_t e1,
-                                                uint64_t *__restrict__ lens, uint32_t *__restrict__ ppos) {
-  const uint64_t e = e0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= e1) return;
-  uint32_t pp[2];
-  lens[e] = evj_len(b, e, pp);
-  ppos[2 * e] = pp[0];
-  ppos[2 * e + 1] = pp[1];
-}
-
-// Bodies of EV_WRITE_NT consecutive events are contiguous in the output:
-// each thread writes its body byte by byte into LDS, then the block stores
-// the whole range with coalesced dword stores (the partial dwords at either
-// end, shared with the neighbouring blocks' bodies, byte by byte).  Blocks
-// whose bodies exceed the LDS buffer write straight to global memory.
-#define EV_WRITE_NT 64
-#define EV_WRITE_CAP (32 * 1024)
-__global__ void __launch_bounds__(EV_WRITE_NT) k_ev_write(bv_event_batch b, uint64_t c0, uint64_t c1,
-                                                          const uint64_t *__restrict__ offs,
-                                                          uint8_t *__restrict__ bodies) {
-  __shared__ uint32_t lds[EV_WRITE_CAP / 4 + 4];
-  const uint64_t n = c1;
-  const uint64_t e0 = c0 + (uint64_t)blockIdx.x * EV_WRITE_NT, e = e0 + threadIdx.x;
-  const uint64_t e1 = e0 + EV_WRITE_NT < n ? e0 + EV_WRITE_NT : n;
-  const uint64_t base = offs[e0], end = offs[e1], a0 = base & ~(uint64_t)3;
-  if (end - a0 > EV_WRITE_CAP) {  // uniform per block
-    if (e < n) evj_write(b, e, bodies + offs[e]);
-    return;
-  }
-  uint8_t *l = (uint8_t *)lds;
-  if (e < e1) evj_write(b, e, l + (offs[e] - a0));
-  __syncthreads();
-  const uint64_t d0 = (base + 3) & ~(uint64_t)3, d1 = end & ~(uint64_t)3;
-  if (d0 <= d1) {
-    for (uint64_t q = base + threadIdx.x; q < d0; q += EV_WRITE_NT) bodies[q] = l[q - a0];
-    for (uint64_t q = d1 + threadIdx.x; q < end; q += EV_WRITE_NT) bodies[q] = l[q - a0];
-    for (uint64_t q = d0 + 4 * threadIdx.x; q < d1; q += 4 * EV_WRITE_NT)
-      *(uint32_t *)(bodies + q) = lds[(q - a0) >> 2];
-  } else {  // the range lies inside one dword
-    for (uint64_t q = base + threadIdx.x; q < end; q += EV_WRITE_NT) bodies[q] = l[q - a0];
-  }
-}
-
-// Events e0 .. e0 + count - 1 of a batch without in-batch parents (their
-// bodies are complete): SHA-256 of each, one lane per event.  Batches WITH
-// in-batch parents are hashed on the host (hostdag.cpp).
-__global__ void __launch_bounds__(256) k_ev_hash(uint64_t count, uint64_t e0, uint8_t *__restrict__ bodies,
-                                                 const uint64_t *__restrict__ offs, uint32_t *__restrict__ dig) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) sha256_one(e0 + i, bodies, offs, dig);
-}
-
-// offs[0, count) += *base (the end of the previous chunk's bodies)
-__global__ void __launch_bounds__(256) k_add_base(uint64_t count, uint64_t *__restrict__ offs,
-                                                  const uint64_t *__restrict__ base) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) offs[i] += *base;
+// Bodies serialised straight into SHA-256, one lane per event (batches
+// without in-batch parents; those are hashed on the host, hostdag.cpp): no
+// body, length or offset array in HBM.  Each lane keeps its chaining value
+// and current block in a 25-word LDS row (odd stride: the 64 lanes' rows
+// start in distinct banks); bytes are packed big-endian into a register and
+// stored a word at a time; a full block is compressed by evh_block, one
+// out-of-line copy of the rounds for every put() call site of the
+// serialiser.
+#define EVH_NT 256
+#define EVH_ROW 25
+__global__ void __launch_bounds__(EVH_NT) k_ev_body_hash(bv_event_batch b, uint64_t e0, uint64_t e1,
+                                                         uint32_t *__restrict__ dig) {
+  __shared__ uint32_t rows[EVH_NT * EVH_ROW];
+  const uint64_t e = e0 + (uint64_t)blockIdx.x * EVH_NT + threadIdx.x;
+  if (e >= e1) return;  // no barriers below
+  EvjSha o = evj_sha_begin(rows + threadIdx.x * EVH_ROW);
+  evj_emit(b, e, o);
+  uint32_t be[8];
+  evj_sha_finish(o, be);
+  uint4 *dst = (uint4 *)(dig + 8 * e);
+  dst[0] = make_uint4(be[0], be[1], be[2], be[3]);
+  dst[1] = make_uint4(be[4], be[5], be[6], be[7]);
 }
 
 __global__ void __launch_bounds__(256) k_iota(uint64_t n, uint32_t *__restrict__ out) {
@@ -740,37 +705,9 @@ hipError_t put_digests(hipStream_t st, uint64_t n, const uint64_t *idx, const ui
   return hipGetLastError();
 }
 
-// Bodies of events [e0, e1) of `b` (device pointers): lengths, offsets
-// (offs: n + 1; an inclusive scan of the chunk's lengths into
-// offs + e0 + 1, shifted by offs[e0], the end of the previous chunk's bodies;
-// offs[0] = 0), then the JSON.  `tmp` / `tmp_bytes`: scan scratch (query with
-// tmp == null for chunks of up to e1 - e0 events).
-hipError_t ev_build(hipStream_t st, const bv_event_batch &b, uint64_t e0, uint64_t e1, uint64_t *lens,
-                    uint32_t *ppos, uint64_t *offs, uint8_t *bodies, void *tmp, size_t *tmp_bytes) {
-  const uint64_t m = e1 - e0;
-  if (!tmp) return hipcub::DeviceScan::InclusiveSum(nullptr, *tmp_bytes, lens, offs + 1, (int)m, st);
-  if (m == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ev_len, grid1(m, 256), dim3(256), 0, st, b, e0, e1, lens, ppos);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (e0 == 0) {
-    e = hipMemsetAsync(offs, 0, 8, st);
-    if (e != hipSuccess) return e;
-  }
-  e = hipcub::DeviceScan::InclusiveSum(tmp, *tmp_bytes, lens + e0, offs + e0 + 1, (int)m, st);
-  if (e != hipSuccess) return e;
-  if (e0 > 0) {
-    hipLaunchKernelGGL(k_add_base, grid1(m, 256), dim3(256), 0, st, m, offs + e0 + 1, offs + e0);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(k_ev_write, grid1(m, EV_WRITE_NT), dim3(EV_WRITE_NT), 0, st, b, e0, e1, offs, bodies);
-  return hipGetLastError();
-}
-
-hipError_t ev_hash(hipStream_t st, uint64_t count, uint64_t e0, uint8_t *bodies, const uint64_t *offs, uint32_t *dig) {
-  if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ev_hash, grid1(count, 256), dim3(256), 0, st, count, e0, bodies, offs, dig);
+hipError_t ev_body_hash(hipStream_t st, const bv_event_batch &b, uint64_t e0, uint64_t e1, uint32_t *dig) {
+  if (e1 <= e0) return hipSuccess;
+  hipLaunchKernelGGL(k_ev_body_hash, grid1(e1 - e0, EVH_NT), dim3(EVH_NT), 0, st, b, e0, e1, dig);
   return hipGetLastError();
 }
 

@@ -381,6 +381,19 @@ uint64_t emu_ev_bodies(const bv_event_batch *b, uint8_t *bodies, uint64_t cap, u
   return offs[n];
 }
 
+// k_ev_body_hash: each body serialised straight into the streaming SHA-256
+// sink (batches without in-batch parents); digests[n, 32].
+void emu_ev_body_hash(const bv_event_batch *b, uint8_t *digests) {
+  for (uint64_t e = 0; e < b->n_events; e++) {
+    uint32_t row[25];
+    EvjSha o = evj_sha_begin(row);
+    evj_emit(*b, e, o);
+    uint32_t be[8];
+    evj_sha_finish(o, be);
+    memcpy(digests + 32 * e, be, 32);
+  }
+}
+
 void emu_sc_inverse(const uint32_t s_le[8], uint32_t out_le[8]) {
   sc s, sM, R2, inv, one, r;
   for (int i = 0; i < 8; i++) s.v[i] = s_le[i];

@@ -134,6 +134,19 @@ def ev_bodies(eb):
     return [bodies[offs[i]:offs[i + 1]].tobytes() for i in range(n)], dig[:n]
 
 
+def ev_body_hash(eb) -> np.ndarray:
+    """emu_ev_body_hash: the device's streaming serialise-and-hash
+    (k_ev_body_hash) on the host: digests[n, 32]."""
+    L = lib()
+    L.emu_ev_body_hash.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.emu_ev_body_hash.restype = None
+    keep: list = []
+    cb = eb.c_struct(keep)
+    dig = np.zeros((max(eb.n_events, 1), 32), np.uint8)
+    L.emu_ev_body_hash(ctypes.byref(cb), dig.ctypes.data)
+    return dig[: eb.n_events]
+
+
 def host_dag_hash(eb, threads: int = 1, portable: bool = False) -> np.ndarray:
     """The product's host DAG hasher (babble_amd/csrc/hostdag.cpp, linked
     into the emulator library): digests[n, 32] of an events.EventWireBatch."""

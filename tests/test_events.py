@@ -93,6 +93,23 @@ def test_emu_bodies_equal_oracle_edge_cases():
         assert [d.tobytes() for d in dig] == wd
 
 
+def test_emu_streaming_body_hash_equals_hashlib():
+    """k_ev_body_hash's streaming serialise-and-hash (no body in memory), run
+    by the emulator: equal to hashlib over the oracle's bodies for batches
+    without in-batch parents, over bodies of every length mod 64 (the
+    padding's block-boundary cases) and the edge cases of random_wire."""
+    seen = set()
+    for seed in (4, 5, 6, 7):
+        wire, want, wd = random_wire(seed, n=160, in_batch=False)
+        assert emu.ev_body_hash(wire).tolist() == [list(d) for d in wd]
+        seen |= {len(x) % 64 for x in want}
+    assert len(seen) == 64
+    packed, wire = synth.event_fields(300, n_creators=5, seed=8, parents="hash")
+    dig = emu.ev_body_hash(wire)
+    for i in range(packed.n_items):
+        assert dig[i].tobytes() == hashlib.sha256(packed.message(i)).digest(), i
+
+
 def test_no_transactions_and_wire_bytes():
     packed, wire = synth.event_fields(50, n_creators=3, seed=9, n_tx=0)
     bodies, _ = emu.ev_bodies(wire)

@@ -35,7 +35,7 @@ for _ in range(7):
     ts.append((time.perf_counter() - t0) * 1e3)
 assert np.all(res.status == 1)
 tm = v.timing()
-print("chunk_mb", os.environ.get("BV_EV_CHUNK_MB", "16"), "pinned", pinned, "median call ms", round(float(np.median(ts)), 3),
+print("chunk_mb", os.environ.get("BV_EV_CHUNK_MB", "64"), "pinned", pinned, "median call ms", round(float(np.median(ts)), 3),
       {k: round(tm[k], 3) for k in ("ms_h2d", "ms_host_prep", "ms_sha256", "ms_verify")}, flush=True)
 v.close()
 arena.close()
