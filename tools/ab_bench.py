@@ -14,7 +14,7 @@ from babble_amd import native, synth  # noqa: E402
 libs = sys.argv[1:]
 n = int(os.environ.get("AB_N", "1000000"))
 b = synth.events(n, n_creators=64, seed=2)
-res = {l: {"cold": [], "warm": []} for l in libs}
+res = {l: {"cold": [], "warm": [], "sha": []} for l in libs}
 from babble_amd import verifier as V  # noqa: E402
 
 for rnd in range(3):
@@ -34,7 +34,9 @@ for rnd in range(3):
             st = d.result().status
             assert np.count_nonzero(st == 1) == n, np.bincount(st)
             res[l][mode].append(min(ts) * 1e3)
+            if mode == "cold":
+                res[l]["sha"].append(v.timing()["ms_sha256"])
             v.close()
         print(rnd, l, {m: round(res[l][m][-1], 4) for m in res[l]}, flush=True)
 for l in libs:
-    print(f"{l}: cold {min(res[l]['cold']):.4f} ms  warm {min(res[l]['warm']):.4f} ms")
+    print(f"{l}: cold {min(res[l]['cold']):.4f} ms  warm {min(res[l]['warm']):.4f} ms  k_sha256 {min(res[l]['sha']):.4f} ms")

@@ -1,20 +1,19 @@
 # Build libbabbleverify.so with extra -D flags into $1 (A/B experiments on
 # one GPU box): tools/build_variant.sh gpurun_var/x.so -DFOO=0
-# With BV_REV=<git revision> the sources of that revision are built instead.
+# The sources are copied to a scratch directory and built by their own
+# Makefile (host-only files with the host compiler), the extra flags added to
+# the device compile.  With BV_REV=<git revision> that revision is built.
 set -e
 out=$(realpath -m "$1"); shift
+root="$(cd "$(dirname "$0")/.." && pwd)"
 d=$(mktemp -d)
-src="$(dirname "$0")/../babble_amd/csrc"
 if [ -n "$BV_REV" ]; then
-  git -C "$(dirname "$0")/.." archive "$BV_REV" babble_amd/csrc include | tar -x -C $d
-  src=$d/babble_amd/csrc
+  git -C "$root" archive "$BV_REV" babble_amd/csrc include | tar -x -C $d
+else
+  mkdir -p $d/babble_amd && cp -r "$root/babble_amd/csrc" $d/babble_amd/ && cp -r "$root/include" $d/
+  rm -rf $d/babble_amd/csrc/obj
 fi
-cd "$src"
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-unused-variable $*"
-/opt/rocm/bin/hipcc $F -c kernels.hip -o $d/k.o &
-for f in *.cpp; do /opt/rocm/bin/hipcc $F -x hip -c $f -o $d/${f%.cpp}.o & done
-wait
-cd - > /dev/null
 mkdir -p "$(dirname "$out")"
-/opt/rocm/bin/hipcc $F -shared -o "$out" $d/*.o -ldl -lpthread
+make -s -C $d/babble_amd/csrc -j8 OUT="$out" \
+  HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-variable $*"
 rm -rf $d
