@@ -462,6 +462,7 @@ def main():
         line["events_entry"] = events_entry_leg(args)
         line["tx_sweep"] = tx_sweep_leg(args, v, local)
         line["c5_fast_sync"] = guarded(c5_leg, args, local)
+        line["c1_insert"] = guarded(c1_leg, args, local)
     if rank == 0:
         if world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(batch, args.cpu_seconds)
@@ -784,6 +785,42 @@ def events_entry_leg(args):
     vc.close()
     out["sync_dag_1000"] = {"ms_median": float(np.median(ts)), "creators": 4, "dag_levels": dag_levels(dag),
                             "cpu": None if args.no_cpu else cpu_sync_dag(dag_packed)}
+    return out
+
+
+def c1_leg(args, local) -> dict:
+    """SURVEY §8d C1 / BASELINE configs[0]: 4 peers, 10k signed events in the
+    hashgraph play order (each event's parents are earlier events of the
+    batch: the in-batch DAG), through bv_verify_events as one batch, cold and
+    with the 4 peers registered; beside the CPU ingesting the same events the
+    way InsertEvent does (SHA-256 of every body in order, then ecdsa.Verify:
+    the C port on one core, as the reference's serial InsertEvent, and on
+    all cores)."""
+    import numpy as np
+
+    from babble_amd import native, synth
+    from babble_amd.verifier import Verifier
+
+    import hashlib
+
+    packed, dag = synth.event_fields(10_000, n_creators=4, seed=1, parents="event")
+    out = {"events": 10_000, "creators": 4, "dag_levels": dag_levels(dag)}
+    for name, flags in (("cold", 0), ("warm", native.F_KEY_CACHE)):
+        v = Verifier(device=local, flags=flags)
+        if flags:
+            v.register_keys([packed.key(k) for k in range(packed.n_keys)])
+        v.verify_events(dag)
+        ts = []
+        for _ in range(9):
+            t0 = time.perf_counter()
+            res = v.verify_events(dag)
+            ts.append((time.perf_counter() - t0) * 1e3)
+        assert np.all(res.status == 1)
+        assert res.msg_hash[-1].tobytes() == hashlib.sha256(packed.message(packed.n_msgs - 1)).digest()
+        v.close()
+        out[name] = {"ms_median": float(np.median(ts)), "value": 10_000 / (float(np.median(ts)) * 1e-3),
+                     "unit": "verifies/s"}
+    out["cpu"] = None if args.no_cpu else cpu_sync_dag(packed)
     return out
 
 
