@@ -49,16 +49,32 @@ void bv_host_dag_hash(const bv_event_batch &b, const uint32_t *order, const uint
       }
     }
   });
-  // the chain: level L's events need only levels < L
+  // the chain: level L's events need only levels < L; a level's events are
+  // finished in pairs whose compressions interleave (hsha::finish2)
+  auto splice = [&](uint32_t e) {
+    uint8_t *body = bodies + off[e];
+    for (int p = 0; p < 2; p++)
+      if (ppos[2 * e + p] != EVJ_NOPOS) evj_hex32(body + ppos[2 * e + p], digests + 32ull * b.parent_ref[2 * e + p]);
+  };
   auto finish = [&](uint64_t lo, uint64_t hi) {
-    for (uint64_t i = lo; i < hi; i++) {
+    uint64_t i = lo;
+    for (; i + 1 < hi; i += 2) {
+      const uint32_t e = order[i], f = order[i + 1];
+      splice(e);
+      splice(f);
+      uint32_t he[8], hf[8];
+      memcpy(he, mid + 8ull * e, sizeof he);
+      memcpy(hf, mid + 8ull * f, sizeof hf);
+      hsha::finish2(he, bodies + off[e], 64ull * ev_mid_blocks(ppos + 2 * e), off[e + 1] - off[e],
+                    digests + 32ull * e, hf, bodies + off[f], 64ull * ev_mid_blocks(ppos + 2 * f),
+                    off[f + 1] - off[f], digests + 32ull * f);
+    }
+    if (i < hi) {
       const uint32_t e = order[i];
-      uint8_t *body = bodies + off[e];
-      for (int p = 0; p < 2; p++)
-        if (ppos[2 * e + p] != EVJ_NOPOS) evj_hex32(body + ppos[2 * e + p], digests + 32ull * b.parent_ref[2 * e + p]);
+      splice(e);
       uint32_t h[8];
       memcpy(h, mid + 8ull * e, sizeof h);
-      hsha::finish(h, body, 64ull * ev_mid_blocks(ppos + 2 * e), off[e + 1] - off[e], digests + 32ull * e);
+      hsha::finish(h, bodies + off[e], 64ull * ev_mid_blocks(ppos + 2 * e), off[e + 1] - off[e], digests + 32ull * e);
     }
   };
   for (uint32_t L = 1; L < n_levels; L++) {

@@ -87,6 +87,60 @@ __attribute__((target("sha,sse4.1,ssse3"))) void compress_shani(uint32_t h[8], c
   _mm_storeu_si128((__m128i *)&h[4], _mm_alignr_epi8(s1, t, 8));      // HGFE
 }
 
+// Two independent single-block compressions, their rounds interleaved: the
+// sha256rnds2 chain of one block is latency-bound, so a second message's
+// rounds fill the gaps (the serial DAG levels of a SyncResponse hash their
+// 2-3 events this way, hostdag.cpp).
+__attribute__((target("sha,sse4.1,ssse3"))) void compress2_shani(uint32_t ha[8], const uint8_t *pa, uint32_t hb[8],
+                                                                 const uint8_t *pb) {
+  const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+  __m128i ta = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)&ha[0]), 0xB1);
+  __m128i a1 = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)&ha[4]), 0x1B);
+  __m128i a0 = _mm_alignr_epi8(ta, a1, 8);
+  a1 = _mm_blend_epi16(a1, ta, 0xF0);
+  __m128i tb = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)&hb[0]), 0xB1);
+  __m128i b1 = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)&hb[4]), 0x1B);
+  __m128i b0 = _mm_alignr_epi8(tb, b1, 8);
+  b1 = _mm_blend_epi16(b1, tb, 0xF0);
+  const __m128i abef_a = a0, cdgh_a = a1, abef_b = b0, cdgh_b = b1;
+  __m128i wa[4], wb[4];
+#define HSHA_SCHED(w, p, i)                                                                                  \
+  if ((i) < 4)                                                                                               \
+    w[(i) & 3] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)((p) + 16 * (i))), bswap);               \
+  else                                                                                                       \
+    w[(i) & 3] = _mm_sha256msg2_epu32(_mm_add_epi32(_mm_sha256msg1_epu32(w[(i) & 3], w[((i) + 1) & 3]),    \
+                                                    _mm_alignr_epi8(w[((i) + 3) & 3], w[((i) + 2) & 3], 4)), \
+                                      w[((i) + 3) & 3]);
+#define HSHA_RND4X2(i)                                                                 \
+  {                                                                                    \
+    HSHA_SCHED(wa, pa, i)                                                              \
+    HSHA_SCHED(wb, pb, i)                                                              \
+    const __m128i k = _mm_load_si128((const __m128i *)&K[4 * (i)]);                   \
+    const __m128i ma = _mm_add_epi32(wa[(i) & 3], k), mb = _mm_add_epi32(wb[(i) & 3], k); \
+    a1 = _mm_sha256rnds2_epu32(a1, a0, ma);                                            \
+    b1 = _mm_sha256rnds2_epu32(b1, b0, mb);                                            \
+    a0 = _mm_sha256rnds2_epu32(a0, a1, _mm_shuffle_epi32(ma, 0x0E));                   \
+    b0 = _mm_sha256rnds2_epu32(b0, b1, _mm_shuffle_epi32(mb, 0x0E));                   \
+  }
+  HSHA_RND4X2(0) HSHA_RND4X2(1) HSHA_RND4X2(2) HSHA_RND4X2(3) HSHA_RND4X2(4) HSHA_RND4X2(5) HSHA_RND4X2(6)
+  HSHA_RND4X2(7) HSHA_RND4X2(8) HSHA_RND4X2(9) HSHA_RND4X2(10) HSHA_RND4X2(11) HSHA_RND4X2(12) HSHA_RND4X2(13)
+  HSHA_RND4X2(14) HSHA_RND4X2(15)
+#undef HSHA_RND4X2
+#undef HSHA_SCHED
+  a0 = _mm_add_epi32(a0, abef_a);
+  a1 = _mm_add_epi32(a1, cdgh_a);
+  b0 = _mm_add_epi32(b0, abef_b);
+  b1 = _mm_add_epi32(b1, cdgh_b);
+  ta = _mm_shuffle_epi32(a0, 0x1B);
+  a1 = _mm_shuffle_epi32(a1, 0xB1);
+  _mm_storeu_si128((__m128i *)&ha[0], _mm_blend_epi16(ta, a1, 0xF0));
+  _mm_storeu_si128((__m128i *)&ha[4], _mm_alignr_epi8(a1, ta, 8));
+  tb = _mm_shuffle_epi32(b0, 0x1B);
+  b1 = _mm_shuffle_epi32(b1, 0xB1);
+  _mm_storeu_si128((__m128i *)&hb[0], _mm_blend_epi16(tb, b1, 0xF0));
+  _mm_storeu_si128((__m128i *)&hb[4], _mm_alignr_epi8(b1, tb, 8));
+}
+
 bool cpu_has_sha() {
   __builtin_cpu_init();
   return __builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1");
@@ -131,6 +185,56 @@ void finish(uint32_t h[8], const uint8_t *msg, size_t from, size_t len, uint8_t 
     out[4 * i + 2] = (uint8_t)(h[i] >> 8);
     out[4 * i + 3] = (uint8_t)h[i];
   }
+}
+
+namespace {
+// The blocks still to compress for one message after `from`: its whole data
+// blocks in place, then the FIPS tail (padding and length) in `tail`.
+struct Pending {
+  const uint8_t *msg;
+  size_t whole, nb;  // whole data blocks, all blocks
+  uint8_t tail[128];
+  void set(const uint8_t *m, size_t from, size_t len) {
+    msg = m + from;
+    whole = (len - from) / 64;
+    const size_t rest = len - from - whole * 64;
+    memset(tail, 0, sizeof tail);
+    memcpy(tail, msg + whole * 64, rest);
+    tail[rest] = 0x80;
+    const size_t tb = rest + 9 <= 64 ? 1 : 2;
+    const uint64_t bits = (uint64_t)len * 8;
+    for (int i = 0; i < 8; i++) tail[tb * 64 - 1 - i] = (uint8_t)(bits >> (8 * i));
+    nb = whole + tb;
+  }
+  const uint8_t *block(size_t j) const { return j < whole ? msg + 64 * j : tail + 64 * (j - whole); }
+};
+
+void put_digest(const uint32_t h[8], uint8_t out[32]) {
+  for (int i = 0; i < 8; i++) {
+    out[4 * i] = (uint8_t)(h[i] >> 24);
+    out[4 * i + 1] = (uint8_t)(h[i] >> 16);
+    out[4 * i + 2] = (uint8_t)(h[i] >> 8);
+    out[4 * i + 3] = (uint8_t)h[i];
+  }
+}
+}  // namespace
+
+void finish2(uint32_t ha[8], const uint8_t *ma, size_t from_a, size_t len_a, uint8_t out_a[32], uint32_t hb[8],
+             const uint8_t *mb, size_t from_b, size_t len_b, uint8_t out_b[32]) {
+  if (!accelerated()) {
+    finish(ha, ma, from_a, len_a, out_a);
+    finish(hb, mb, from_b, len_b, out_b);
+    return;
+  }
+  Pending a, b;
+  a.set(ma, from_a, len_a);
+  b.set(mb, from_b, len_b);
+  const size_t both = a.nb < b.nb ? a.nb : b.nb;
+  for (size_t j = 0; j < both; j++) compress2_shani(ha, a.block(j), hb, b.block(j));
+  for (size_t j = both; j < a.nb; j++) compress_shani(ha, a.block(j), 1);
+  for (size_t j = both; j < b.nb; j++) compress_shani(hb, b.block(j), 1);
+  put_digest(ha, out_a);
+  put_digest(hb, out_b);
 }
 
 void digest(const uint8_t *msg, size_t len, uint8_t out[32]) {

@@ -16,6 +16,10 @@ void compress(uint32_t h[8], const uint8_t *blocks, size_t nblocks);
 // bytes (from a multiple of 64): the remaining whole blocks, the FIPS
 // padding, and the 32 big-endian digest bytes into `out`.
 void finish(uint32_t h[8], const uint8_t *msg, size_t from, size_t len, uint8_t out[32]);
+// finish() of two independent messages, their compressions interleaved
+// (SHA extensions; the portable code runs them one after the other)
+void finish2(uint32_t ha[8], const uint8_t *ma, size_t from_a, size_t len_a, uint8_t out_a[32], uint32_t hb[8],
+             const uint8_t *mb, size_t from_b, size_t len_b, uint8_t out_b[32]);
 void digest(const uint8_t *msg, size_t len, uint8_t out[32]);
 // 1 when the SHA extensions are used; force_portable(true) selects the
 // portable code (tests exercise both)
