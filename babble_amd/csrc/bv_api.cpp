@@ -410,6 +410,7 @@ static int create_impl(bv_ctx *ctx) {
   }
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
   if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
+  if (const char *s = getenv("BV_SMALL_WARM_MAX")) ctx->small_warm_max = (uint64_t)std::max(0, atoi(s));
   if (const char *s = getenv("BV_LAT_TABLE_KEYS")) ctx->lat_table_keys = (uint32_t)atoi(s);
   return BV_OK;
 }
@@ -1115,8 +1116,24 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
 constexpr uint64_t kSmallItems = 256;       // items (and messages) per small batch
 constexpr uint64_t kSmallMsgLen = 16 << 10;  // longest message: one lane hashes it
 
-static bool small_batch(const bv_batch *b) {
-  if (b->n_items == 0 || b->n_items > kSmallItems || b->n_msgs > kSmallItems) return false;
+// Small batches: <= 256 items, or up to ctx->small_warm_max (512) items when
+// every well-formed key already has a key-cache table (no item needs the
+// cooperative NAF chain).  k_small costs ~0.18 ms + ~0.6 us per item, the
+// bulk pipeline ~0.5 ms from 512 to 4096 warm items: 512 items 0.34 against
+// 0.48-0.63 ms, 1000 items equal, 2000 items 0.92 against 0.67
+// (profiles/r04_ab_small_warm.log).
+static bool small_batch(bv_ctx *ctx, const bv_batch *b) {
+  if (b->n_items == 0) return false;
+  const uint64_t n = std::max<uint64_t>(b->n_items, b->n_msgs);
+  if (n > kSmallItems) {
+    if (n > ctx->small_warm_max || !(ctx->flags & BV_F_KEY_CACHE) || b->n_keys == 0 || b->n_keys > kKcMaxBatchKeys)
+      return false;
+    // the key bytes are read below: only a well-formed batch (the bulk path
+    // reports a malformed one through its own validation)
+    if (bv_validate_host_batch(ctx, b) != BV_OK || !bv_kc_all_cached(ctx, b->n_keys, b->key_bytes, b->key_off))
+      return false;
+  }
+  if (b->n_msgs && !b->msg_off) return false;  // (validation reports it)
   for (uint64_t m = 0; m < b->n_msgs; m++)
     if (b->msg_off[m + 1] - b->msg_off[m] > kSmallMsgLen) return false;
   return true;
@@ -1204,7 +1221,7 @@ extern "C" int bv_verify_batch(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   if (!ctx || !b || !res) return BV_E_ARGS;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device), BV_E_NODEVICE, "hipSetDevice");
-  if (ctx->small_path && small_batch(b)) {
+  if (ctx->small_path && small_batch(ctx, b)) {
     int rc = bv_validate_host_batch(ctx, b);
     if (rc != BV_OK) return rc;
     rc = small_verify(ctx, b, res);

@@ -283,6 +283,7 @@ struct bv_ctx {
   // small host batches through k_small (BV_SMALL=0: the bulk pipeline)
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
   bool ev_split_verify = true, small_path = true;
+  uint64_t small_warm_max = 512;  // k_small for batches whose keys are all cached (BV_SMALL_WARM_MAX)
   uint32_t lat_table_keys = 256;  // latency rule: K8 tables for batches of <= 4096 items from up to this many keys (BV_LAT_TABLE_KEYS)
 };
 
@@ -343,6 +344,7 @@ int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
                   const uint64_t *dko, hipStream_t st, bool *use, bool force_build = false);
 uint32_t bv_kc_lookup(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, uint64_t *tabs);
+bool bv_kc_all_cached(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko);
 void bv_kc_init(bv_ctx *ctx);     // budget, admission and fault-injection settings (bv_create)
 void bv_kc_release(bv_ctx *ctx);  // free every cached table (bv_destroy, after all calls finished)
 // `res` (may be null): the caller's result buffers, written by DMA directly

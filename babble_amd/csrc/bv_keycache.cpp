@@ -316,6 +316,15 @@ uint32_t bv_kc_lookup(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const ui
   return hits;
 }
 
+// Every well-formed key of the batch has a built table (host-only).
+bool bv_kc_all_cached(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko) {
+  for (uint32_t k = 0; k < n_keys; k++) {
+    if (!key_form_ok(hkb + hko[k], hko[k + 1] - hko[k])) continue;
+    if (!ctx->kc_index.count(std::string((const char *)hkb + hko[k], (size_t)(hko[k + 1] - hko[k])))) return false;
+  }
+  return true;
+}
+
 extern "C" int bv_kc_register(bv_ctx *ctx, uint32_t n_keys, const uint8_t *key_bytes, const uint64_t *key_off) {
   if (!ctx || (n_keys && !key_off)) return BV_E_ARGS;
   std::lock_guard<std::mutex> lk(ctx->mu);
