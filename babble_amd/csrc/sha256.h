@@ -163,173 +163,14 @@ DEV void sha256_block_words(uint32_t w[16], const uint32_t *src0, uint32_t sh, u
   }
 }
 
-// The 16 message words of a block whose padding (if any) is already in
-// the buffer: 17 aligned dwords at `src`, realigned by `sh` bytes.
-DEV void sha256_block_words_padded(uint32_t w[16], const uint32_t *src, uint32_t sh) {
-  uint32_t d[17];
-#pragma unroll
-  for (int i = 0; i < 17; i++) d[i] = src[i];
-#pragma unroll
-  for (int i = 0; i < 16; i++) w[i] = be_word_at(d[i + 1], d[i], sh);
-}
-
 // Compress blocks [blk0, blk1) of a len-byte message into h (see
-// sha256_block_words for src0 / sh).  Lets a caller hash a message in
-// pieces: a midstate over leading blocks, then the rest from another buffer
-// (k_ev_hash_chain).
+// sha256_block_words for src0 / sh).
 DEV void sha256_blocks(uint32_t h[8], const uint32_t *src0, uint32_t sh, uint64_t len, uint64_t blk0,
                        uint64_t blk1) {
   for (uint64_t blk = blk0; blk < blk1; blk++) {
     uint32_t w[16];
     sha256_block_words(w, src0, sh, len, blk0, blk);
     sha256_compress(h, w);
-  }
-}
-
-// The message schedule with the round constants folded in: wk[i] = W_i + K_i,
-// element i stored at wk[(i / 4) * stride + i % 4] (stride 4: contiguous; a
-// wider stride interleaves several lanes' schedules in 16-byte chunks, so
-// lanes reading their own schedule in lockstep hit distinct LDS banks).
-// Independent of the chaining state, so another lane can compute it while
-// the previous block's rounds run (k_ev_hash_chain).
-// `wk` may live in LDS: the 48 expansion steps run as a 3-trip loop of 16
-// (the ring indices stay static), which keeps the chain kernel's code small.
-DEV void sha256_schedule_wk(uint32_t *wk, const uint32_t w[16], uint32_t stride = 4) {
-  uint32_t x[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    x[i] = w[i];
-    wk[(i >> 2) * stride + (i & 3)] = w[i] + SHA_K[i];
-  }
-#pragma unroll 1
-  for (int r = 16; r < 64; r += 16) {
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const uint32_t w15 = x[(u + 1) & 15], w2 = x[(u + 14) & 15];
-      const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
-      const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
-      x[u] = x[u] + s0 + x[(u + 9) & 15] + s1;
-      wk[((r + u) >> 2) * stride + (u & 3)] = x[u] + SHA_K[r + u];
-    }
-  }
-}
-
-// The 64 rounds of one block from a precomputed W + K schedule, for a
-// latency-bound single wave (k_ev_hash_chain).  Fully unrolled, and round
-// i + 1's h + K + W (its h is round i's g) is formed during round i, off the
-// e -> e' chain: e' = d + (hkw + S1(e) + Ch(e, f, g)).  One wave, 4 lanes:
-// 1.66 us per block against 2.51 us for an 8-trip loop of 8 rounds
-// (tools/ubench_sha.hip, profiles/r02_ubench_sha_lat.txt).
-// Round forms (BV_SHA_RW, A/B in tools/chain_stamps.py): 0 plain (t1 = h +
-// S1 + Ch + WK, the compiler schedules), 1 h + K + W formed one round early,
-// 2 also d + (h + K + W) one round early (e' = add3(dhkw, S1(e), Ch)).
-#ifndef BV_SHA_RW
-#define BV_SHA_RW 0
-#endif
-DEV void sha256_rounds_wk(uint32_t h[8], const uint32_t *wk, uint32_t stride = 4) {
-  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#if BV_SHA_RW == 0
-#pragma unroll
-  for (int i = 0; i < 64; i++) {
-    const uint32_t t1 = hh + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g)) +
-                        wk[(i >> 2) * stride + (i & 3)];
-    const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, b, c);
-    hh = g;
-    g = f;
-    f = e;
-    e = d + t1;
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + t2;
-  }
-#else
-  uint32_t hkw = hh + wk[0];
-#if BV_SHA_RW == 2
-  // d + (h + K + W) one round early too (round i+1's d is round i's c):
-  // e' = add3(dhkw, S1(e), Ch) — one dependent add fewer on the e chain
-  uint32_t dhkw = d + hkw;
-#endif
-#pragma unroll
-  for (int i = 0; i < 64; i++) {
-#if BV_SHA_RW == 2
-    const uint32_t s1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)), ch = (e & f) ^ (~e & g);
-    const uint32_t ne = dhkw + s1 + ch;
-    const uint32_t t1 = hkw + s1 + ch;
-#else
-    const uint32_t t1 = hkw + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & f) ^ (~e & g));
-#endif
-    if (i < 63) hkw = g + wk[((i + 1) >> 2) * stride + ((i + 1) & 3)];
-    const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, b, c);
-    hh = g;
-    g = f;
-    f = e;
-#if BV_SHA_RW == 2
-    e = ne;
-    if (i < 63) dhkw = c + hkw;
-#else
-    e = d + t1;
-#endif
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + t2;
-  }
-#endif
-  h[0] += a;
-  h[1] += b;
-  h[2] += c;
-  h[3] += d;
-  h[4] += e;
-  h[5] += f;
-  h[6] += g;
-  h[7] += hh;
-}
-
-// A block's rounds in two pieces on the working state s = (a, ..., h):
-// rounds 0-15 straight from the 16 message words (no schedule needed yet),
-// then rounds 16-63, 16 at a time, from a W + K schedule other lanes expand
-// meanwhile (wk laid out as in sha256_schedule_wk); the caller adds s into the
-// chaining state afterwards (k_ev_hash_chain's first tail block).
-DEV void sha256_round(uint32_t s[8], uint32_t kw) {
-  const uint32_t a = s[0], e = s[4];
-  const uint32_t t1 = s[7] + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + ((e & s[5]) ^ (~e & s[6])) + kw;
-  const uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + maj3(a, s[1], s[2]);
-  s[7] = s[6];
-  s[6] = s[5];
-  s[5] = e;
-  s[4] = s[3] + t1;
-  s[3] = s[2];
-  s[2] = s[1];
-  s[1] = a;
-  s[0] = t1 + t2;
-}
-DEV void sha256_rounds_first16(uint32_t s[8], const uint32_t w[16]) {
-#pragma unroll
-  for (int i = 0; i < 16; i++) sha256_round(s, w[i] + SHA_K[i]);
-}
-// rounds r0 .. r0 + 15 from the W + K schedule
-DEV void sha256_rounds16_wk(uint32_t s[8], const uint32_t *wk, uint32_t stride, int r0) {
-#pragma unroll
-  for (int u = 0; u < 16; u++) sha256_round(s, wk[((r0 + u) >> 2) * stride + (u & 3)]);
-}
-// The schedule in chunks of 16 (x: the 16-word ring, initially the block's
-// message words): chunk 0 stores W_0..15 + K, chunk c (1..3) expands and
-// stores W_16c..16c+15 + K, so a consumer can run 16 rounds per chunk
-// while the next chunk is expanded (k_ev_hash_chain's first tail block).
-DEV void sha256_schedule_chunk(uint32_t x[16], uint32_t *wk, uint32_t stride, int c) {
-  if (c == 0) {
-#pragma unroll
-    for (int i = 0; i < 16; i++) wk[(i >> 2) * stride + (i & 3)] = x[i] + SHA_K[i];
-    return;
-  }
-#pragma unroll
-  for (int u = 0; u < 16; u++) {
-    const uint32_t w15 = x[(u + 1) & 15], w2 = x[(u + 14) & 15];
-    const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
-    const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
-    x[u] = x[u] + s0 + x[(u + 9) & 15] + s1;
-    wk[((16 * c + u) >> 2) * stride + (u & 3)] = x[u] + SHA_K[16 * c + u];
   }
 }
 
