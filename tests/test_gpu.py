@@ -294,6 +294,30 @@ def test_small_batch_kernel_warm_up_to_512(monkeypatch):
             v.close()
 
 
+def test_small_batch_randomized_against_oracle():
+    """k_small over randomized small adversarial batches (1..500 items, 1..9
+    creators, the C4 mix of malformed keys and signatures), cold and with
+    part of the valid keys registered (cached and uncached keys in one
+    launch; batches above 256 items take k_small only when every key is
+    cached): every status, digest and bit equal to the C oracle."""
+    from babble_amd.verifier import Verifier
+
+    rng = np.random.default_rng(2024)
+    cold = Verifier(device=0)
+    warm = Verifier(device=0, flags=native.F_KEY_CACHE)
+    try:
+        for it in range(14):
+            n = int(rng.integers(1, 500))
+            b = synth.adversarial(n, seed=3000 + it, n_creators=int(rng.integers(1, 10)), scale_per_million=MIX)
+            good = sorted({b.key(k) for k in range(b.n_keys) if gs.Unmarshal(b.key(k)) is not None})
+            warm.register_keys(good[: max(1, len(good) // 2)] if it % 2 else good)
+            check_against_oracle(cold, b)
+            check_against_oracle(warm, b)
+    finally:
+        cold.close()
+        warm.close()
+
+
 def test_small_batch_kernel_key_cache(monkeypatch):
     """k_small with registered keys: every valid key registered -> the KC
     tables (6 lookups per GLV half; malformed keys need none); some keys
