@@ -78,8 +78,11 @@ N_SIMD = 256 * 4
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 300 timed steps (~0.6 s of device time, two batches in flight) after 20
+    # warm-up steps: sustained throughput; 30 steps (60 ms) read 1-4 % low and
+    # noisier on the same box (profiles/r04_ab_bench_steps.log)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--events", type=int, default=1_000_000, help="events per GPU per step")
     ap.add_argument("--creators", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=9.0, help="target CPU-baseline sample duration (each leg)")
