@@ -378,9 +378,13 @@ hipStream_t bv_copy_stream(bv_ctx *ctx) {
   return ctx->cstream;
 }
 
+// After a failed call: wait for everything this ctx enqueued.  The streams
+// are shared with the process's other contexts, so each wait is an event of
+// the ctx's own recorded behind its work (bv_host_wait), not a stream
+// synchronize that would also wait for other contexts' later work.
 int bv_drain(bv_ctx *ctx, hipStream_t st, int rc) {
   for (hipStream_t s : {st, ctx->sstream, ctx->kstream, ctx->cstream})
-    if (s) (void)hipStreamSynchronize(s);
+    if (s && bv_host_wait(ctx, s) != hipSuccess) (void)hipStreamSynchronize(s);
   for (auto &sl : ctx->slot) sl.uncovered.clear();
   (void)hipGetLastError();
   return rc;
