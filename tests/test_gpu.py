@@ -99,8 +99,18 @@ def test_c4_adversarial_mix(verifier, device_api):
 
 
 def test_c4_adversarial_full_rate(verifier):
-    """C4 at 10^5 items with the exact per-million corruption mix."""
+    """C4 at 10^5 items with the exact per-million corruption mix (~70 keys,
+    ~1.4k items per key: the K12 tables under the few-keys rule)."""
     b = synth.adversarial(100_000, seed=44)
+    check_against_oracle(verifier, b)
+    assert verifier.timing()["key_path"] == 12
+
+
+def test_k8_tables_many_keys(verifier):
+    """More than 128 keys with fewer than 2048 items each: the 8-bit key
+    tables (their build is the cheaper one when many keys share the chip)."""
+    b = synth.adversarial(60_000, seed=45, n_creators=200, scale_per_million=MIX)
+    assert b.n_keys > 128 and b.n_items < 2048 * b.n_keys
     check_against_oracle(verifier, b)
     assert verifier.timing()["key_path"] == 8
 
