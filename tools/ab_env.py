@@ -3,7 +3,7 @@ runs in its own child process (the library reads the knobs once per process)
 over cold device-resident C2 batches from 64 creators at several sizes, two
 batches in flight as bench.py; variants interleaved, median of 3 rounds.
 
-  python tools/ab_env.py "base:" "ks2:BV_KSTREAMS=2" [--sizes 250000,1000000]
+  python tools/ab_env.py "base:" "var:AB_LIB=gpurun_var/x.so" [--sizes=250000,1000000]
 """
 import json
 import os
@@ -19,7 +19,11 @@ def child(sizes):
     import numpy as np
     import torch
 
-    from babble_amd import synth
+    from babble_amd import native, synth
+
+    if os.environ.get("AB_LIB"):  # a library variant (tools/build_variant.sh)
+        native.LIB_PATH = os.path.abspath(os.environ["AB_LIB"])
+        native._lib = None
     from babble_amd.verifier import Verifier
 
     out = {}
