@@ -39,16 +39,16 @@ constexpr uint64_t kK12TableBytes = BV_K12TABLE_U32 * 4;
 constexpr uint64_t kK12SubBytes = BV_K12SUB_U32 * 4;
 constexpr uint64_t kK12PrefixBytes = (uint64_t)BV_K12NWIN * BV_K12ENT * 32;  // one fe per entry
 constexpr uint32_t kBasesPerKey = 22;       // max(K8 16, K12 22, KC 14) bases per key
-// K12 pays for its 11x larger build above ctx->k12_min_items items per key
-// (BV_K12_MIN_ITEMS, default 2048) when the chip is busy building many keys'
-// tables; with few keys (<= kK12FewKeys) the build is a latency chain beside
-// an idle chip, and K12's 22 lookups per item (against K8's 32) win from
-// kK12FewMinItems items per key on: 64 creators, 16k / 32k / 62.5k / 125k
-// events 25.2 -> 30.5, 49.4 -> 60.0, 94.8 -> 104.8, 178.5 -> 205.0 M/s
-// (profiles/r04_ab_k12min.log).  Batches in the latency rule's range keep
-// K8 (its chain is one launch shorter: 1000-4000 cold events 0.03-0.05 ms).
-constexpr uint32_t kK12FewKeys = 128;
-constexpr uint64_t kK12FewMinItems = 128;
+// Per-batch K12 (22 lookups per item) or K8 (32) tables: K12 for every
+// table-mode batch above the latency rule's size (kLatTableItems) with at
+// most kMaxK12Keys keys, and for smaller ones from ctx->k12_min_items (2048,
+// BV_K12_MIN_ITEMS) items per key; K8 otherwise (the latency rule's small
+// batches: K8's chain is one launch shorter, 1000-4000 cold events
+// 0.03-0.05 ms).  The cheaper lookups win over K12's larger build at every
+// measured key count, two batches in flight (profiles/r04_ab_k12min*.log):
+// 64 keys, 16k / 125k events 25.2 -> 30.5, 178.5 -> 205.0 M/s; 200 keys,
+// 50k / 200k 39.4 -> 51.0, 136.7 -> 208.0; 1000 keys, 64k / 1M 13.1 -> 19.1
+// (32 items per key), 143.1 -> 217.2.
 constexpr uint32_t kMaxTableKeys = 8192;       // K8: 4 GiB of key tables
 constexpr uint32_t kMaxK12Keys = 1024;         // K12: 2.8 GiB
 // Latency rule: a small batch is bound by its longest serial chain, not by
@@ -423,6 +423,7 @@ static int create_impl(bv_ctx *ctx) {
   }
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
   if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
+  if (const char *s = getenv("BV_TABLE_MIN_ITEMS")) ctx->table_min_items = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_K12_MIN_ITEMS")) ctx->k12_min_items = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_SMALL_WARM_MAX")) ctx->small_warm_max = (uint64_t)std::max(0, atoi(s));
   if (const char *s = getenv("BV_LAT_TABLE_KEYS")) ctx->lat_table_keys = (uint32_t)atoi(s);
@@ -531,13 +532,11 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   // Key path: the key cache when prepared; otherwise per-batch fixed-base
   // tables once a key signs enough items (K12 for large batches, K8 for
   // mid-size), else the generic per-lane path.
-  const bool table_mode = kc || (n_keys <= kMaxTableKeys && n_items >= 16ull * n_keys) ||
+  const bool table_mode = kc || (n_keys <= kMaxTableKeys && n_items >= ctx->table_min_items * n_keys) ||
                           (n_keys <= ctx->lat_table_keys && n_items <= kLatTableItems && n_items > 0);
   const int key_w = kc ? BV_KCW
                     : !table_mode ? 0
-                    : (n_keys <= kMaxK12Keys && (n_items >= ctx->k12_min_items * n_keys ||
-                                                  (n_keys <= kK12FewKeys && n_items > kLatTableItems &&
-                                                   n_items >= kK12FewMinItems * n_keys)) &&
+                    : (n_keys <= kMaxK12Keys && (n_items >= ctx->k12_min_items * n_keys || n_items > kLatTableItems) &&
                        !(ctx->flags & BV_F_K8))
                         ? 12
                         : 8;

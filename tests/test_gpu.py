@@ -100,19 +100,27 @@ def test_c4_adversarial_mix(verifier, device_api):
 
 def test_c4_adversarial_full_rate(verifier):
     """C4 at 10^5 items with the exact per-million corruption mix (~70 keys,
-    ~1.4k items per key: the K12 tables under the few-keys rule)."""
+    ~1.4k items per key: the K12 tables)."""
     b = synth.adversarial(100_000, seed=44)
     check_against_oracle(verifier, b)
     assert verifier.timing()["key_path"] == 12
 
 
 def test_k8_tables_many_keys(verifier):
-    """More than 128 keys with fewer than 2048 items each: the 8-bit key
-    tables (their build is the cheaper one when many keys share the chip)."""
-    b = synth.adversarial(60_000, seed=45, n_creators=200, scale_per_million=MIX)
-    assert b.n_keys > 128 and b.n_items < 2048 * b.n_keys
+    """More than 1024 keys (kMaxK12Keys) with >= 16 items each: the 8-bit
+    key tables."""
+    b = synth.adversarial(25_000, seed=45, n_creators=1100, scale_per_million=MIX)
+    assert b.n_keys > 1024 and 16 * b.n_keys <= b.n_items < 2048 * b.n_keys
     check_against_oracle(verifier, b)
     assert verifier.timing()["key_path"] == 8
+
+
+def test_k12_tables_many_keys_few_items(verifier):
+    """200 keys with ~300 items each (above the latency rule's size): K12."""
+    b = synth.adversarial(60_000, seed=46, n_creators=200, scale_per_million=MIX)
+    assert b.n_items > 4096 and b.n_items < 2048 * b.n_keys
+    check_against_oracle(verifier, b)
+    assert verifier.timing()["key_path"] == 12
 
 
 def test_c4_adversarial_1m(verifier):

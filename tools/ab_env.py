@@ -28,7 +28,7 @@ def child(sizes):
 
     out = {}
     for n in sizes:
-        b = synth.events(n, n_creators=64, seed=2)
+        b = synth.events(n, n_creators=int(os.environ.get("AB_CREATORS", "64")), seed=2)
         v = Verifier(0)
         ds = [v.to_device(b) for _ in range(2)]
         for k in range(4):
