@@ -51,6 +51,15 @@ constexpr uint32_t kBasesPerKey = 22;       // max(K8 16, K12 22, KC 14) bases p
 // (32 items per key), 143.1 -> 217.2.
 constexpr uint32_t kMaxTableKeys = 8192;       // K8: 4 GiB of key tables
 constexpr uint32_t kMaxK12Keys = 1024;         // K12: 2.8 GiB
+// Table or generic: the per-batch build costs ~3.3 us per key (K12 and K8,
+// two batches in flight) but serves each item ~8x cheaper than the generic
+// path (~16.5 ns per item, floor ~1.2 ms per batch).  Up to kManyKeys keys
+// the build is inside that floor and tables win from 16 items per key
+// (ctx->table_min_items); above it from 192 (ctx->table_min_items_many):
+// 1000 keys, 64k / 128k events generic 45.9 / 59.1 M/s against K12 19.0 /
+// 37.7; 3000 keys at 192 per key K8 64.5 against 62.6
+// (profiles/r04_ab_generic_vs_tables.log, r04_ab_generic_lat.log).
+constexpr uint32_t kManyKeys = 256;
 // Latency rule: a small batch is bound by its longest serial chain, not by
 // total work.  The per-lane generic path runs 128 doublings AND ~128
 // additions in one lane per item (~2.6 ms); the K8 tables cost one wave's
@@ -424,6 +433,7 @@ static int create_impl(bv_ctx *ctx) {
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
   if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS")) ctx->table_min_items = (uint64_t)std::max(1, atoi(s));
+  if (const char *s = getenv("BV_TABLE_MIN_ITEMS_MANY")) ctx->table_min_items_many = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_K12_MIN_ITEMS")) ctx->k12_min_items = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_SMALL_WARM_MAX")) ctx->small_warm_max = (uint64_t)std::max(0, atoi(s));
   if (const char *s = getenv("BV_LAT_TABLE_KEYS")) ctx->lat_table_keys = (uint32_t)atoi(s);
@@ -532,7 +542,8 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   // Key path: the key cache when prepared; otherwise per-batch fixed-base
   // tables once a key signs enough items (K12 for large batches, K8 for
   // mid-size), else the generic per-lane path.
-  const bool table_mode = kc || (n_keys <= kMaxTableKeys && n_items >= ctx->table_min_items * n_keys) ||
+  const uint64_t min_items = n_keys <= kManyKeys ? ctx->table_min_items : ctx->table_min_items_many;
+  const bool table_mode = kc || (n_keys <= kMaxTableKeys && n_items >= min_items * n_keys) ||
                           (n_keys <= ctx->lat_table_keys && n_items <= kLatTableItems && n_items > 0);
   const int key_w = kc ? BV_KCW
                     : !table_mode ? 0

@@ -284,6 +284,7 @@ struct bv_ctx {
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
   bool ev_split_verify = true, small_path = true;
   uint64_t table_min_items = 16;   // per-batch tables (not the generic path) from this many items per key
+  uint64_t table_min_items_many = 192;  // the same above kManyKeys keys
   uint64_t k12_min_items = 2048;  // per-batch K12 (not K8) tables from this many items per key
   uint64_t small_warm_max = 512;  // k_small for batches whose keys are all cached (BV_SMALL_WARM_MAX)
   uint32_t lat_table_keys = 256;  // latency rule: K8 tables for batches of <= 4096 items from up to this many keys (BV_LAT_TABLE_KEYS)

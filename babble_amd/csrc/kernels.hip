@@ -691,6 +691,13 @@ static inline dim3 grid1(uint64_t n, uint32_t block) { return dim3((uint32_t)((n
 #define BV_LAT_MAX_ITEMS 131072
 #endif
 static inline bool lat_variant(uint64_t n) { return n <= BV_LAT_MAX_ITEMS; }
+// The generic per-lane kernel's latency variant pays only up to 32k items:
+// with two batches in flight its larger VGPR footprint halves the rate at
+// 64k-128k items (1000 keys: 28.2 -> 45.9 / 28.6 -> 59.1 M/s without it),
+// while single calls at <= 32k keep its 2.6-3.2 ms (r04_ab_generic_lat.log).
+#ifndef BV_GEN_LAT_MAX_ITEMS
+#define BV_GEN_LAT_MAX_ITEMS 32768
+#endif
 
 hipError_t sha256(hipStream_t st, uint64_t n, const uint8_t *bytes, const uint64_t *off, uint32_t *dig,
                   uint64_t max_len) {
@@ -794,8 +801,14 @@ hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t
       }
     }
   } else if (kw == 8) {
-    hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
-                       dim3(256), 0, st, bases_jac, bstatus, table);
+    // (as K12: the throughput point ops above the latency range; 3000 keys,
+    // 144k-576k events 10.3 -> 17.9, 38.4 -> 64.5 M/s, r04_ab_k8_fill.log)
+    if (lat_variant(n_items))
+      hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
+                         dim3(256), 0, st, bases_jac, bstatus, table);
+    else
+      hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true, 256, false>),
+                         dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases), dim3(256), 0, st, bases_jac, bstatus, table);
   } else {
     if (lat & 2)
       hipLaunchKernelGGL((k_table_fill<BV_K12L, BV_K12NSUB, false, 1 << BV_K12L, true>), dim3(BV_K12NSUB, n_bases),
@@ -917,7 +930,7 @@ hipError_t verify_generic(hipStream_t st, uint64_t n, uint64_t lo, uint64_t hi, 
                           const uint32_t *kxy, const uint32_t *item_msg, const uint32_t *dig, const uint32_t *w,
                           const uint32_t *g_table, uint8_t *status, uint64_t *bits) {
   if (hi <= lo) return hipSuccess;
-  if (lat_variant(n))
+  if (n <= BV_GEN_LAT_MAX_ITEMS)
     hipLaunchKernelGGL(k_verify_generic<true>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be,
                        pre, kst, kxy, item_msg, dig, w, g_table, status, bits);
   else

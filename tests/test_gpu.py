@@ -106,13 +106,30 @@ def test_c4_adversarial_full_rate(verifier):
     assert verifier.timing()["key_path"] == 12
 
 
-def test_k8_tables_many_keys(verifier):
-    """More than 1024 keys (kMaxK12Keys) with >= 16 items each: the 8-bit
-    key tables."""
-    b = synth.adversarial(25_000, seed=45, n_creators=1100, scale_per_million=MIX)
-    assert b.n_keys > 1024 and 16 * b.n_keys <= b.n_items < 2048 * b.n_keys
+def test_k8_tables_many_keys(monkeypatch):
+    """More than 1024 keys (kMaxK12Keys): the 8-bit key tables, filled with
+    the throughput point ops above 131072 items.  The many-key table
+    threshold (192 items per key) is lowered to 16 so the oracle check stays
+    at 140k items."""
+    from babble_amd.verifier import Verifier
+
+    monkeypatch.setenv("BV_TABLE_MIN_ITEMS_MANY", "16")  # read at bv_create
+    verifier = Verifier(device=0)
+    b = synth.adversarial(140_000, seed=45, n_creators=1100, scale_per_million=MIX)
+    assert b.n_keys > 1024 and 16 * b.n_keys <= b.n_items < 2048 * b.n_keys and b.n_items > 131072
     check_against_oracle(verifier, b)
     assert verifier.timing()["key_path"] == 8
+    verifier.close()
+
+
+def test_generic_path_many_keys_few_items(verifier):
+    """More than 256 keys with fewer than 192 items each: the generic
+    per-lane path, at 40k items (throughput variant) and 20k (latency)."""
+    for n in (40_000, 20_000):
+        b = synth.adversarial(n, seed=47, n_creators=1100, scale_per_million=MIX)
+        assert b.n_keys > 256 and b.n_items < 192 * b.n_keys
+        check_against_oracle(verifier, b)
+        assert verifier.timing()["key_path"] == 0
 
 
 def test_k12_tables_many_keys_few_items(verifier):
