@@ -574,7 +574,9 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   HIPCHK(hipEventRecord(ev[E_START], ctx->sstream), BV_E_LAUNCH, "event");
   // (key cache: every batch decodes its keys too — statuses never come from
   // the cache — unless bv_kc_prepare already did on the call's stream)
-  if (!(kc && ctx->S().kc_decoded))
+  if (kc && ctx->S().kc_decoded)  // its statuses are read on this stream too (k_verify_g)
+    HIPCHK(hipStreamWaitEvent(ctx->sstream, ctx->S().ev[E_KCDEC], 0), BV_E_LAUNCH, "join");
+  else
     HIPCHK(bvk::key_decode(ctx->sstream, n_keys, b->key_bytes, b->key_off, ctx->S().kstatus.as<uint8_t>(),
                            ctx->S().kxy.as<uint32_t>()),
            BV_E_LAUNCH, "k_key_decode");

@@ -193,7 +193,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // timing / ordering events (see bv_read_timing)
 enum {
   E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_SINV,
-  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_KDEC, E_COUNT
+  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_KDEC, E_KCDEC, E_COUNT
 };
 
 constexpr uint32_t kKcMaxBatchKeys = 4096;  // key cache: batches with more keys use per-batch tables

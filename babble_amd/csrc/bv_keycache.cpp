@@ -138,6 +138,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
     HIPCHK(ctx->S().kxy.ensure((uint64_t)n_keys * 64), BV_E_OOM, "alloc kxy");
     HIPCHK(bvk::key_decode(st, n_keys, dkb, dko, ctx->S().kstatus.as<uint8_t>(), ctx->S().kxy.as<uint32_t>()),
            BV_E_LAUNCH, "k_key_decode");
+    HIPCHK(hipEventRecord(ctx->S().ev[E_KCDEC], st), BV_E_LAUNCH, "event");
     std::vector<uint8_t> kst(n_keys);
     HIPCHK(hipMemcpyAsync(kst.data(), ctx->S().kstatus.p, n_keys, hipMemcpyDeviceToHost, st), BV_E_LAUNCH, "d2h kst");
     HIPCHK(bv_host_wait(ctx, st), BV_E_LAUNCH, "sync");
@@ -154,8 +155,26 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
       else blocked = true;
     }
   }
-  if (blocked && !force_build) return BV_OK;  // a valid key without a table: per-batch path
+  // Every return below that leaves *use false after this call's k_key_decode
+  // was launched on `st` waits for it first: the per-batch path then decodes
+  // the batch again on the s^-1 stream into the same buffers.
+  auto bail = [&]() -> int {
+    if (ctx->S().kc_decoded) {
+      ctx->S().kc_decoded = false;
+      if (bv_host_wait(ctx, st) != hipSuccess) return bv_fail(ctx, BV_E_LAUNCH, "sync", hipGetLastError());
+    }
+    return BV_OK;
+  };
+  if (blocked && !force_build) return bail();  // a valid key without a table: per-batch path
 
+  // Registration builds as many registered keys as the budget holds (in the
+  // caller's order); the rest stay uncached (timing.kc_keys tells).  A
+  // batch whose own keys alone exceed the budget takes the per-batch path.
+  const uint64_t fit = ctx->kc_budget / kKcTableBytes;
+  if (admit.size() > fit) {
+    if (!force_build) return bail();
+    admit.resize(fit);
+  }
   uint32_t builds = 0;
   if (!admit.empty()) {
     if (!ctx->S().kc_decoded) {  // the admitted keys' points: decode the batch now
@@ -163,10 +182,10 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
       HIPCHK(ctx->S().kxy.ensure((uint64_t)n_keys * 64), BV_E_OOM, "alloc kxy");
       HIPCHK(bvk::key_decode(st, n_keys, dkb, dko, ctx->S().kstatus.as<uint8_t>(), ctx->S().kxy.as<uint32_t>()),
              BV_E_LAUNCH, "k_key_decode");
+      HIPCHK(hipEventRecord(ctx->S().ev[E_KCDEC], st), BV_E_LAUNCH, "event");
       ctx->S().kc_decoded = true;  // ordered before the builds and the verify on `st`; sstream waits (bv_run_keys)
     }
     const uint64_t need = (uint64_t)admit.size() * kKcTableBytes;
-    if (need > ctx->kc_budget) return BV_OK;  // this batch's keys alone exceed the budget
     bool all_registered = true;
     for (uint32_t k : admit) all_registered = all_registered && ctx->kc_registered.count(key_of(k));
     // evict least-recently-used tables this batch does not use: unregistered
@@ -185,7 +204,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
           victim_reg = reg;
         }
       }
-      if (victim < 0) return BV_OK;
+      if (victim < 0) return bail();
       if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // no call in flight may still read it
       auto &s = ctx->kc_slots[victim];
       HIPCHK(hipFree(s.table), BV_E_LAUNCH, "free cached table");
@@ -230,7 +249,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
       if (kc_table_alloc(ctx, &s.table) != hipSuccess) {
         s.table = nullptr;
         rollback();
-        return BV_OK;  // HBM exhausted: per-batch path for this call, nothing indexed
+        return bail();  // HBM exhausted: per-batch path for this call, nothing indexed
       }
       ctx->kc_bytes += kKcTableBytes;
       slot_of[k] = si;

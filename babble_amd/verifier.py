@@ -302,6 +302,17 @@ class Group:
             raise native.BvError(rc, self._L.bv_group_last_error(self._g).decode(errors="replace"))
         return VerifyResult(h[: b.n_msgs], st[: b.n_items], bits[: (b.n_items + 63) // 64])
 
+    def verify_into(self, b: PackedBatch, res: VerifyResult) -> VerifyResult:
+        """bv_group_verify_batch into caller-owned result arrays (PinnedArena
+        arrays: a batch built there is DMA'd to every device in place)."""
+        keep: list = []
+        cb = _cbatch(b, keep)
+        r = native.BvResult(_p(res.msg_hash), _p(res.status), _p(res.accept_bits))
+        rc = self._L.bv_group_verify_batch(self._g, ctypes.byref(cb), ctypes.byref(r))
+        if rc != native.BV_OK:
+            raise native.BvError(rc, self._L.bv_group_last_error(self._g).decode(errors="replace"))
+        return res
+
     def timing(self, i: int = 0) -> dict:
         t = native.BvTiming()
         rc = self._L.bv_group_get_timing(self._g, i, ctypes.byref(t))

@@ -92,6 +92,9 @@ def parse():
                     help="batches in flight: consecutive steps rotate over this many streams and result buffers")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rank plumbing only, on CPU over gloo: no GPU, no verification (tests)")
+    ap.add_argument("--group-logical", type=int, default=0,
+                    help="N=1 rehearsal of the N-GPU group leg: bv_group over this many logical shards of GPU 0")
+    ap.add_argument("--group-reps", type=int, default=5, help="timed bv_group_verify_batch calls per group leg")
     return ap.parse_args()
 
 
@@ -128,10 +131,11 @@ def check_rank_env(args) -> int:
     return world
 
 
-def dry_run(args, world: int, rank: int) -> None:
+def dry_run(args, world: int, rank: int, worker) -> None:
     """The N-rank plumbing on CPU (gloo): each rank's expected accept bitmask
-    of its shard, all-gathered and checked as the GPU run checks its own;
-    rank 0 prints a line with value null."""
+    of its shard, all-gathered and checked as the GPU run checks its own; the
+    N-GPU legs' barriers, max-over-ranks and group worker (bench_multi) with
+    CPU stand-ins; rank 0 prints a line with value null."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -150,15 +154,39 @@ def dry_run(args, world: int, rank: int) -> None:
         if not np.array_equal(got[q].numpy().view(np.uint64), expected_words(q, args.events)):
             raise SystemExit(f"rank {rank}: gathered bitmask of rank {q} differs")
     el = time.perf_counter() - t0
+    extras = multi_gpu_legs(args, world, rank, worker, None, 0) if world > 1 or args.group_logical else {}
     if rank == 0:
-        print(json.dumps({"metric": "ECDSA event verifies/sec", "value": None, "unit": "verifies/s", "n_gpus": world,
-                          "steps": 0, "warmup": 0, "ms_per_step": el * 1e3, "higher_is_better": True,
-                          "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "dry run (no GPU)",
-                          "dry_run": True, "config": {"workload": "launcher plumbing only",
-                                                      "parallelism": f"shard{world}" if world > 1 else "single"}}),
+        print(json.dumps(dict({"metric": "ECDSA event verifies/sec", "value": None, "unit": "verifies/s",
+                               "n_gpus": world, "steps": 0, "warmup": 0, "ms_per_step": el * 1e3,
+                               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+                               "data": "dry run (no GPU)", "dry_run": True,
+                               "config": {"workload": "launcher plumbing only",
+                                          "parallelism": f"shard{world}" if world > 1 else "single"}}, **extras)),
               flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def multi_gpu_legs(args, world: int, rank: int, worker, batch, local: int) -> dict:
+    """bench_multi's legs after the headline (VERDICT r4 #1): every rank's
+    pinned host entries at once, then the library's own multi-GPU entry
+    (bv_group_verify_batch over all N devices from rank 0's worker process)
+    while the other ranks wait at a store barrier.  Every rank runs the same
+    barrier sequence whatever fails, so no rank waits for one that gave up."""
+    import bench_multi as M
+
+    fence = M.StoreFence(rank, world) if world > 1 else M.LocalFence()
+    out = {}
+    if world > 1:
+        try:
+            out["concurrent"] = M.concurrent_legs(fence, rank, world, batch, local, dry_run=args.dry_run)
+        except Exception as e:  # noqa: BLE001 (the fences inside have all run: see concurrent_legs)
+            out["concurrent"] = {"error": f"{type(e).__name__}: {e}"}
+    fence.barrier("group")
+    if rank == 0:
+        out["group"] = M.run_group_worker(worker) if worker is not None else {"error": "no group worker"}
+    fence.barrier("group-done")
+    return out
 
 
 def cpu_threads() -> int:
@@ -306,8 +334,25 @@ def main():
     world = check_rank_env(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.dry_run:
-        return dry_run(args, world, rank)
+    worker = None
+    if rank == 0 and not args.no_extras and (world > 1 or args.group_logical > 1):
+        import bench_multi
+
+        # started before this process touches a GPU; it waits on its stdin
+        devices = list(range(world)) if world > 1 else [0] * args.group_logical
+        worker = bench_multi.start_group_worker(devices, args.events, args.group_reps, args.dry_run)
+    try:
+        if args.dry_run:
+            return dry_run(args, world, rank, worker)
+        return run(args, world, rank, local, worker)
+    finally:
+        if worker is not None:
+            import bench_multi
+
+            bench_multi.stop_group_worker(worker)
+
+
+def run(args, world: int, rank: int, local: int, worker) -> None:
     import numpy as np
     import torch
 
@@ -466,6 +511,10 @@ def main():
         line["tx_sweep"] = tx_sweep_leg(args, v, local)
         line["c5_fast_sync"] = guarded(c5_leg, args, local)
         line["c1_insert"] = guarded(c1_leg, args, local)
+    if not args.no_extras and (world > 1 or args.group_logical > 1):
+        extras = multi_gpu_legs(args, world, rank, worker, batch, local)
+        if rank == 0:
+            line.update(extras)
     if rank == 0:
         if world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(batch, args.cpu_seconds)

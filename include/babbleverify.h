@@ -141,8 +141,11 @@ const char *bv_last_error(const bv_ctx *ctx);
  * peer set changes) — replacing the previous set, and build the tables of the
  * registered valid keys that have none, before returning.  Registered tables
  * are never evicted for unregistered keys.  BV_E_ARGS on a ctx without the
- * cache or more than 4096 keys.  bv_get_timing's kc_builds / kc_keys report
- * what was built. */
+ * cache or more than 4096 keys.  Cap: the budget holds floor(BV_KEY_CACHE_GB
+ * / 0.805) tables (119 at the default 96 GB); past it, the first registered
+ * keys in the caller's order that fit get tables and the rest none (their
+ * batches take the per-batch path), still BV_OK.  bv_get_timing's kc_builds
+ * / kc_keys report what was built and what the cache holds. */
 int bv_kc_register(bv_ctx *ctx, uint32_t n_keys, const uint8_t *key_bytes, const uint64_t *key_off);
 
 /* Synchronous batch verify from host buffers (the cgo entry point).  Any

@@ -188,6 +188,44 @@ def test_bench_launcher_starts_n_ranks_dry_run():
     assert len(lines) == 1, p.stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["dry_run"] and line["config"]["parallelism"] == "shard2"
+    # the N-GPU legs' plumbing — every rank's concurrent legs
+    # passed the store barriers and max-over-ranks, rank 0's group worker
+    # merged the shard words exactly while rank 1 waited
+    conc = line["concurrent"]
+    for leg in ("host_entry_pinned", "events_bulk_pinned"):
+        assert conc[leg]["ranks"] == 2 and conc[leg]["ms_per_call_slowest_rank"] > 0, conc
+    grp = line["group"]
+    assert grp["devices"] == [0, 1] and grp["bitmask_check"].startswith("exact"), grp
+
+
+def test_bench_group_logical_dry_run():
+    """`--group-logical 2` at N = 1 (the one-GPU rehearsal of the group leg):
+    the worker is started before any GPU use and released after the
+    headline; in dry-run mode it merges two logical shards' words."""
+    p = _bench(["--dry-run", "--group-logical", "2", "--events", "3000"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and "concurrent" not in line
+    assert line["group"]["devices"] == [0, 0] and line["group"]["events_per_call"] == 6000
+
+
+def test_group_input_concatenates_c3_chunks():
+    """bench_multi.c3_group_input: N consecutive C3 chunks as one batch —
+    messages, items and the seeded rejections re-based chunk by chunk."""
+    import bench_multi
+
+    b, bad = bench_multi.c3_group_input(2, 300)
+    c0, bad0 = synth.c3_chunk(0, 300)
+    c1, bad1 = synth.c3_chunk(1, 300)
+    assert b.n_items == 600 and b.n_msgs == 600 and b.n_keys == 64
+    assert np.array_equal(bad, np.concatenate([bad0, bad1 + 300]))
+    for j in (0, 299, 300, 599):
+        src, k = (c0, j) if j < 300 else (c1, j - 300)
+        assert b.message(int(b.item_msg[j])) == src.message(int(src.item_msg[k]))
+        assert b.key(int(b.item_key[j])) == src.key(int(src.item_key[k]))
+        assert bytes(b.r_be[j]) == bytes(src.r_be[k]) and bytes(b.s_be[j]) == bytes(src.s_be[k])
 
 
 def test_bench_rank_refuses_world_mismatch():

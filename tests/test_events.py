@@ -312,3 +312,131 @@ def test_host_dag_hash_wide_levels():
     packed, wire = synth.event_fields(3000, n_creators=300, seed=33, parents="event")
     dig = emu.host_dag_hash(wire, threads=6)
     assert all(dig[i].tobytes() == hashlib.sha256(packed.message(i)).digest() for i in range(3000))
+
+
+KCW = 22  # timing key_path of a batch served by key-cache tables (geometry.h BV_KCW)
+
+
+def _oracle_bodies(wire):
+    """The canonical bodies of a synth-shaped wire batch (one list of
+    non-nil transactions, no ITX / BlockSignature fragments) restated by the
+    oracle (gosemantics.EventBody.Marshal, event.go:38-45), parents resolved
+    in order as ReadWireInfo does (hashgraph.go:1555-1578)."""
+    n = wire.n_events
+    kind = np.asarray(wire.parent_kind).reshape(n, 2)
+    ref = np.asarray(wire.parent_ref).reshape(n, 2)
+    ph = np.asarray(wire.parent_hashes).reshape(-1, 32)
+    ko = np.asarray(wire.key_off, np.int64)
+    bodies, digests = [], []
+    for i in range(n):
+        ps = []
+        for k in range(2):
+            if kind[i, k] == E.PARENT_HASH:
+                ps.append(gs.EncodeToString(ph[int(ref[i, k])].tobytes()))
+            elif kind[i, k] == E.PARENT_EVENT:
+                ps.append(gs.EncodeToString(digests[int(ref[i, k])]))
+            else:
+                ps.append("")
+        t0, t1 = int(wire.tx_start[i]), int(wire.tx_start[i + 1])
+        txs = [wire.tx_bytes[int(wire.tx_off[t]):int(wire.tx_off[t + 1])].tobytes() for t in range(t0, t1)]
+        c = int(wire.creator[i])
+        body = gs.EventBody(Transactions=txs, InternalTransactions=None, Parents=ps,
+                            Creator=wire.key_bytes[ko[c]:ko[c + 1]].tobytes(), Index=int(wire.index[i]),
+                            BlockSignatures=None, Timestamp=int(wire.timestamp[i])).Marshal()
+        bodies.append(body)
+        digests.append(hashlib.sha256(body).digest())
+    return bodies, digests
+
+
+def _adversarial_kc_wire(parents, n, seed, fresh_key=None):
+    """A signed synth wire batch (6 creators) with every key class the key
+    cache must keep apart: 2 % corrupted s; events re-assigned to a 65-byte
+    key off the curve (a creator's key with y changed), to its compressed
+    33-byte form and to an empty key; optionally to a `fresh_key` (valid,
+    never seen by the cache).  Returns (wire, oracle statuses, digests, bits,
+    the valid creator keys)."""
+    from babble_amd.batch import PackedBatch
+    from oracle import coracle
+
+    _, wire = synth.event_fields(n, n_creators=6, seed=seed, parents=parents)
+    ko = np.asarray(wire.key_off, np.int64)
+    keys = [wire.key_bytes[ko[k]:ko[k + 1]].tobytes() for k in range(len(ko) - 1)]
+    off_curve = bytearray(keys[0])
+    off_curve[64] ^= 1
+    extra = [bytes(off_curve), bytes([2 + (keys[1][64] & 1)]) + keys[1][1:33], b""]
+    if fresh_key is not None:
+        extra.append(fresh_key)
+    allk = keys + extra
+    wire.key_bytes = np.frombuffer(b"".join(allk), np.uint8).copy()
+    wire.key_off = np.concatenate([[0], np.cumsum([len(k) for k in allk])]).astype(np.uint64)
+    rng = np.random.default_rng(seed)
+    # re-assigned events come from the batch's tail: a re-assigned body's
+    # in-batch descendants no longer match their signatures
+    rows = n - 1 - rng.choice(n // 8, size=4 * len(extra) * max(1, n // 400), replace=False)
+    wire.creator = np.asarray(wire.creator, np.uint32).copy()
+    wire.creator[rows] = len(keys) + np.arange(len(rows)) % len(extra)
+    bad = rng.choice(np.setdiff1d(np.arange(n), rows), size=max(1, n // 50), replace=False)
+    wire.s_be = np.asarray(wire.s_be).copy()
+    wire.s_be[bad, 11] ^= 0x02
+    bodies, digests = _oracle_bodies(wire)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum([len(b) for b in bodies])
+    packed = PackedBatch(np.frombuffer(b"".join(bodies), np.uint8).copy(), off, wire.key_bytes, wire.key_off,
+                         np.arange(n, dtype=np.uint32), wire.creator, wire.r_be, wire.s_be,
+                         wire.pre if wire.pre is not None else np.zeros(n, np.uint8))
+    h, st, bits = coracle.verify_batch(packed.as_dict())
+    assert [d.tobytes() for d in h] == digests
+    assert {0, 1, 3} <= set(np.unique(st).tolist())  # rejects, accepts and the empty / malformed-key panics
+    return wire, st, h, bits, keys
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parents,n", [("event", 1500), ("hash", 6000)])
+def test_verify_events_key_cache_matches_oracle(parents, n):
+    """bv_verify_events on a BV_F_KEY_CACHE context, with
+    in-batch parents (host-hashed DAG path) and without (bulk path), through
+    every cache state — cold (unknown keys decoded, valid ones remembered:
+    per-batch tables), admitted on the second batch (KC tables built, then
+    used), warm (hits), registered (tables from bv_kc_register before the
+    first batch) and blocked (a fresh valid key keeps the batch on the
+    per-batch path) — over corrupted s, an off-curve key, a compressed and an
+    empty key: digests, statuses and bits equal to the C oracle's over the
+    oracle-serialized bodies and to a Verifier without the cache."""
+    from babble_amd import native
+    from babble_amd.verifier import Verifier
+
+    wire, st, h, bits, keys = _adversarial_kc_wire(parents, n, seed=61)
+
+    def check(res, what):
+        assert np.array_equal(res.msg_hash, h), what
+        assert np.array_equal(res.status, st), what
+        assert np.array_equal(res.accept_bits, bits), what
+
+    v0 = Verifier(0)
+    vc = Verifier(0, flags=native.F_KEY_CACHE)
+    vr = Verifier(0, flags=native.F_KEY_CACHE)
+    try:
+        check(v0.verify_events(wire), "no cache")
+        check(vc.verify_events(wire), "cold")
+        assert vc.timing()["key_path"] != KCW, "first sight: keys not admitted yet"
+        check(vc.verify_events(wire), "admitted")
+        t = vc.timing()
+        assert t["key_path"] == KCW and t["kc_builds"] == len(keys), t
+        check(vc.verify_events(wire), "warm")
+        t = vc.timing()
+        assert t["key_path"] == KCW and t["kc_builds"] == 0 and t["kc_hits"] == len(keys), t
+        vr.register_keys(keys)
+        check(vr.verify_events(wire), "registered")
+        assert vr.timing()["key_path"] == KCW
+        # a fresh valid key (never seen): the batch takes the per-batch path
+        # on the warm ctx, statuses still exact
+        fresh = synth.events(1, n_creators=1, seed=62).key(0)
+        w2, st2, h2, bits2, _ = _adversarial_kc_wire(parents, n, seed=61, fresh_key=fresh)
+        res = vc.verify_events(w2)
+        assert np.array_equal(res.msg_hash, h2) and np.array_equal(res.status, st2)
+        assert np.array_equal(res.accept_bits, bits2)
+        assert vc.timing()["key_path"] != KCW, "blocked by the fresh key"
+    finally:
+        v0.close()
+        vc.close()
+        vr.close()

@@ -110,6 +110,43 @@ def test_key_cache_eviction(monkeypatch):
         v.close()
 
 
+def test_key_cache_register_beyond_budget(monkeypatch):
+    """registering more validators than the budget holds
+    builds the first ones that fit (2.5 GB: 3 tables of 805 MB) and returns
+    BV_OK; the 2 left over never evict a registered table, so batches naming
+    them take the per-batch path after their (already launched) key decode —
+    the bail-out waits for that decode before the s^-1 stream decodes again —
+    on the host entry, the device entry and the events entry, every result
+    exact."""
+    from babble_amd.verifier import Verifier
+
+    monkeypatch.setenv("BV_KEY_CACHE_GB", "2.5")
+    monkeypatch.setenv("BV_KC_ADMIT", "1")
+    b = synth.adversarial(20_000, seed=46, n_creators=5, scale_per_million=MIX)
+    keys = [b.key(k) for k in range(b.n_keys)]
+    n_valid = len(set(valid_keys(b)))
+    assert n_valid == 5
+    v = Verifier(device=0, flags=native.F_KEY_CACHE)
+    try:
+        v.register_keys(keys)
+        t = v.timing()
+        assert t["kc_builds"] == 3 and t["kc_keys"] == 3, t
+        for _ in range(2):
+            oracle_check(v.verify(b), b)
+            t = v.timing()
+            assert t["key_path"] in (8, 12) and t["kc_keys"] == 3 and t["kc_builds"] == 0, t
+        d = v.to_device(b)
+        v.verify_device(d)
+        oracle_check(d.result(), b)
+        packed, wire = synth.event_fields(4000, n_creators=5, seed=46, parents="hash")
+        res = v.verify_events(wire)
+        h, st, bits = coracle.verify_batch(packed.as_dict())
+        assert np.array_equal(res.msg_hash, h) and np.array_equal(res.status, st)
+        assert np.array_equal(res.accept_bits, bits)
+    finally:
+        v.close()
+
+
 @pytest.mark.parametrize("fail", ["alloc:3", "build:2"])
 def test_key_cache_failure_leaves_no_unbuilt_slot(monkeypatch, fail):
     """a KC table allocation (the 3rd of a 64-key miss batch)
