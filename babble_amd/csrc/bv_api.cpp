@@ -432,6 +432,7 @@ static int create_impl(bv_ctx *ctx) {
   }
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
   if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
+  if (const char *s = getenv("BV_SMALL_STAMPS")) ctx->small_stamps = atoi(s) != 0;
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS")) ctx->table_min_items = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS_MANY")) ctx->table_min_items_many = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_K12_MIN_ITEMS")) ctx->k12_min_items = (uint64_t)std::max(1, atoi(s));
@@ -1210,6 +1211,12 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   uint32_t hits = 0;
   if (kc) hits = bv_kc_lookup(ctx, n_keys, b->key_bytes, b->key_off, (uint64_t *)(pin + o_tab));
   hipEvent_t *ev = ctx->S().ev;
+  uint64_t *stamps = nullptr;
+  if (ctx->small_stamps) {
+    HIPCHK(ctx->d_stamps.ensure(16 * 8), BV_E_OOM, "alloc stamps");
+    HIPCHK(hipMemsetAsync(ctx->d_stamps.p, 0, 16 * 8, st), BV_E_LAUNCH, "memset stamps");
+    stamps = ctx->d_stamps.as<uint64_t>();
+  }
   HIPCHK(hipEventRecord(ev[E_CALL], st), BV_E_LAUNCH, "event");
   HIPCHK(hipMemcpyAsync(dev, pin, in_end, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d (small batch)");
   HIPCHK(hipEventRecord(ev[E_START], st), BV_E_LAUNCH, "event");
@@ -1217,7 +1224,7 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
                            dev + o_key, (const uint64_t *)(dev + o_koff), (const uint32_t *)(dev + o_im),
                            (const uint32_t *)(dev + o_ik), dev + o_r, dev + o_s, b->pre ? dev + o_pre : nullptr,
                            kc ? (const uint64_t *)(dev + o_tab) : nullptr, ctx->g_table, (uint32_t *)(dev + o_dig),
-                           dev + o_st),
+                           dev + o_st, stamps),
          BV_E_LAUNCH, "k_small");
   HIPCHK(hipEventRecord(ev[E_END], st), BV_E_LAUNCH, "event");
   HIPCHK(hipMemcpyAsync(ctx->pin_out.p, dev + o_dig, out_end - o_dig, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
@@ -1243,6 +1250,13 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   t.kc_hits = hits;
   t.kc_keys = (uint32_t)ctx->kc_index.size();
   t.ms_host = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (stamps) {  // diagnostics: workgroup 0's phase clocks, relative to its start
+    uint64_t h[16];
+    HIPCHK(hipMemcpy(h, stamps, sizeof h, hipMemcpyDeviceToHost), BV_E_LAUNCH, "d2h stamps");
+    fprintf(stderr, "k_small stamps n=%llu kernel_ms=%.4f:", (unsigned long long)n_items, t.ms_total);
+    for (int k = 1; k < 14; k++) fprintf(stderr, " %d:%lld", k, h[k] ? (long long)(h[k] - h[0]) : -1ll);
+    fprintf(stderr, "\n");
+  }
   return BV_OK;
 }
 

@@ -52,7 +52,8 @@ hipError_t verify_q(hipStream_t, int, uint64_t, uint64_t, uint64_t, const uint32
                     const uint64_t *, const uint32_t *, uint8_t *, uint64_t *);
 hipError_t verify_small(hipStream_t, uint32_t, uint32_t, const uint8_t *, const uint64_t *, const uint8_t *,
                         const uint64_t *, const uint32_t *, const uint32_t *, const uint8_t *, const uint8_t *,
-                        const uint8_t *, const uint64_t *, const uint32_t *, uint32_t *, uint8_t *);
+                        const uint8_t *, const uint64_t *, const uint32_t *, uint32_t *, uint8_t *,
+                        uint64_t *stamps = nullptr);
 hipError_t verify_generic(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
@@ -230,6 +231,7 @@ struct bv_ctx {
   // host-entry staging: one layout in pinned memory and in HBM
   PinnedBuf pin_in, pin_out;
   DevBuf d_in;
+  DevBuf d_stamps;  // BV_SMALL_STAMPS: k_small phase clocks (diagnostics)
   // host entry: messages longer than kHostHashLen hashed on the host (their
   // index and digest), uploaded beside the device hashing
   PinnedBuf pin_long;
@@ -286,6 +288,7 @@ struct bv_ctx {
   uint64_t table_min_items = 16;   // per-batch tables (not the generic path) from this many items per key
   uint64_t table_min_items_many = 192;  // the same above kManyKeys keys
   uint64_t k12_min_items = 2048;  // per-batch K12 (not K8) tables from this many items per key
+  bool small_stamps = false;      // BV_SMALL_STAMPS=1: print k_small's phase clocks to stderr
   uint64_t small_warm_max = 512;  // k_small for batches whose keys are all cached (BV_SMALL_WARM_MAX)
   uint32_t lat_table_keys = 256;  // latency rule: K8 tables for batches of <= 4096 items from up to this many keys (BV_LAT_TABLE_KEYS)
 };

@@ -159,6 +159,9 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
   // was launched on `st` waits for it first: the per-batch path then decodes
   // the batch again on the s^-1 stream into the same buffers.
   auto bail = [&]() -> int {
+    ctx->timing.kc_hits = hits;
+    ctx->timing.kc_builds = 0;
+    ctx->timing.kc_keys = (uint32_t)ctx->kc_index.size();
     if (ctx->S().kc_decoded) {
       ctx->S().kc_decoded = false;
       if (bv_host_wait(ctx, st) != hipSuccess) return bv_fail(ctx, BV_E_LAUNCH, "sync", hipGetLastError());

@@ -541,8 +541,15 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
                                                const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                const uint8_t *__restrict__ pre, const uint64_t *__restrict__ kc_tabs,
                                                const uint32_t *__restrict__ g_table,
-                                               uint32_t *__restrict__ digest_words, uint8_t *__restrict__ status) {
+                                               uint32_t *__restrict__ digest_words, uint8_t *__restrict__ status,
+                                               uint64_t *__restrict__ stamps) {
   const uint32_t b = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  // diagnostics (BV_SMALL_STAMPS): shader clocks of workgroup 0's phases
+#define SMALL_STAMP(k)                                                     \
+  do {                                                                     \
+    if (stamps && b == 0) stamps[k] = __builtin_amdgcn_s_memtime();        \
+  } while (0)
+  if (t == 0) SMALL_STAMP(0);
   __shared__ uint32_t sh_e[8], sh_w[8], sh_q[16], sh_u1[8], sh_k[8];
   __shared__ uint32_t sh_part[4][33];
   __shared__ uint32_t sh_ks, sh_go;
@@ -555,6 +562,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
       sha256_msg(h, msg_bytes, msg_off[m], msg_off[m + 1] - msg_off[m]);
 #pragma unroll
       for (int k = 0; k < 8; k++) sh_e[k] = bswap32(h[k]);  // the digest's big-endian bytes (as k_sha256)
+      SMALL_STAMP(1);
     } else if (wave == 1) {
       sc s, w;
       sc_load_be_words(s, s_be + 8 * (uint64_t)b);
@@ -566,6 +574,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
       }
 #pragma unroll
       for (int k = 0; k < 8; k++) sh_w[k] = w.v[k];
+      SMALL_STAMP(2);
     } else if (wave == 2) {
       const uint32_t k = item_key[b];
       uint8_t st;
@@ -574,10 +583,15 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
 #pragma unroll
       for (int c = 0; c < 8; c++) sh_q[c] = x.v[c], sh_q[8 + c] = y.v[c];
       sh_ks = st;
+      SMALL_STAMP(3);
     }
   }
-  if (wave == 3 && lane == 0 && b < n_msgs) sha256_one(b, msg_bytes, msg_off, digest_words);
+  if (wave == 3 && lane == 0 && b < n_msgs) {
+    sha256_one(b, msg_bytes, msg_off, digest_words);
+    SMALL_STAMP(4);
+  }
   __syncthreads();
+  if (t == 0) SMALL_STAMP(5);
   if (!item) return;  // uniform per workgroup
   // ---- phase 2
   if (t == 0) {
@@ -603,6 +617,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
     }
   }
   __syncthreads();
+  if (t == 0) SMALL_STAMP(6);
   const uint32_t go = sh_go;
   if (!go) return;  // decided by the table (uniform)
   // ---- phase 3: four partial sums
@@ -616,6 +631,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
     g_table_add_range<BV_GW, BV_GNWIN, true>(R, inf, g_table, u, (BV_GNWIN / 2) * (int)lane,
                                               lane ? BV_GNWIN : BV_GNWIN / 2);
     part_store(sh_part[lane], R, inf);
+    SMALL_STAMP(7 + lane);
   } else if (wave >= 2) {  // k1 Q (wave 2) / k2 phi(Q) (wave 3)
     const uint32_t h = wave - 2;
     uint32_t kk[4];
@@ -630,6 +646,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
         fe_set(R.X, 0), fe_set(R.Y, 0), fe_set(R.ZZ, 0), fe_set(R.ZZZ, 0);
         key_table_add<BV_KCW, BV_KCNWIN, true, true>(R, inf, (const uint32_t *)tab, kk, neg, h != 0);
         part_store(sh_part[2 + h], R, inf);
+        SMALL_STAMP(9 + h);
       }
     } else {  // no table: the NAF chain, wave-cooperative (coop.h)
       const uint32_t c = coop::pos();
@@ -650,10 +667,14 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
         sh_part[2 + h][16 + lane] = ZZ;
         sh_part[2 + h][24 + lane] = ZZZ;
       }
-      if (lane == 0) sh_part[2 + h][32] = inf ? 1u : 0u;
+      if (lane == 0) {
+        sh_part[2 + h][32] = inf ? 1u : 0u;
+        SMALL_STAMP(9 + h);
+      }
     }
   }
   __syncthreads();
+  if (t == 0) SMALL_STAMP(11);
   // ---- phase 4
   if (wave == 0 && lane < 2) {
     gexz A, B;
@@ -664,6 +685,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
     part_store(sh_part[2 * lane], A, ia);
   }
   __syncthreads();
+  if (t == 0) SMALL_STAMP(12);
   if (t == 0) {
     gexz A, B;
     bool ia, ib;
@@ -673,7 +695,9 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
     fe r;
     fe_load_be_words(r, r_be + 8 * (uint64_t)b);
     status[b] = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
+    SMALL_STAMP(13);
   }
+#undef SMALL_STAMP
 }
 
 // ---------------------------------------------------------------------------
@@ -916,12 +940,12 @@ hipError_t verify_small(hipStream_t st, uint32_t n_items, uint32_t n_msgs, const
                         const uint64_t *msg_off, const uint8_t *key_bytes, const uint64_t *key_off,
                         const uint32_t *item_msg, const uint32_t *item_key, const uint8_t *r_be, const uint8_t *s_be,
                         const uint8_t *pre, const uint64_t *kc_tabs, const uint32_t *g_table, uint32_t *dig,
-                        uint8_t *status) {
+                        uint8_t *status, uint64_t *stamps) {
   const uint32_t grid = std::max(n_items, n_msgs);
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(k_small, dim3(grid), dim3(256), 0, st, n_items, n_msgs, msg_bytes, msg_off, key_bytes, key_off,
                      item_msg, item_key, (const uint32_t *)r_be, (const uint32_t *)s_be, pre, kc_tabs, g_table, dig,
-                     status);
+                     status, stamps);
   return hipGetLastError();
 }
 
