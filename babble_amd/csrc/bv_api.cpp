@@ -130,7 +130,7 @@ hipError_t PinnedBuf::ensure(size_t bytes) {
   }
   size_t want = std::max(bytes, cap * 3 / 2);
   want = (want + 4095) & ~(size_t)4095;
-  hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+  hipError_t e = hipHostMalloc(&p, want, flags);
   if (e != hipSuccess) {
     p = nullptr;
     (void)hipGetLastError();
@@ -489,6 +489,7 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
   bv_kc_release(ctx);
   ctx->pin_in.release();
   ctx->pin_out.release();
+  ctx->small_io.release();
   ctx->pin_long.release();
   ctx->d_long.release();
   for (auto &sl : ctx->slot)
@@ -1144,7 +1145,7 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
 // profiles/r04_small_lat.log).
 // ---------------------------------------------------------------------------
 constexpr uint64_t kSmallItems = 256;       // items (and messages) per small batch
-constexpr uint64_t kSmallMsgLen = 16 << 10;  // longest message: one lane hashes it
+constexpr uint64_t kSmallMsgLen = 16 << 10;  // longest message (hashed on the host, inside the call)
 
 // Small batches: <= 256 items, or up to ctx->small_warm_max (512) items when
 // every well-formed key already has a key-cache table (no item needs the
@@ -1173,7 +1174,7 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   const auto t0 = std::chrono::steady_clock::now();
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
-  const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0, key_len = n_keys ? b->key_off[n_keys] : 0;
+  const uint64_t key_len = n_keys ? b->key_off[n_keys] : 0;
   hipStream_t st = ctx->stream;
   ctx->last = st;
   ctx->timing = bv_timing{};
@@ -1183,22 +1184,31 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
     total += align256(bytes);
     return o;
   };
-  const size_t o_msg = at(msg_len + 64), o_moff = at((n_msgs + 1) * 8), o_key = at(key_len + 64),
-               o_koff = at((n_keys + 1) * 8ull), o_im = at(n_items * 4), o_ik = at(n_items * 4),
-               o_r = at(n_items * 32), o_s = at(n_items * 32), o_pre = at(n_items), o_tab = at(n_keys * 8ull),
-               in_end = total;
-  const size_t o_dig = at(n_msgs * 32), o_st = at(n_items), out_end = total;
-  if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // previous calls' staging
-  HIPCHK(ctx->pin_in.ensure(in_end), BV_E_OOM, "alloc pinned staging");
-  HIPCHK(ctx->pin_out.ensure(out_end - o_dig), BV_E_OOM, "alloc pinned results");
-  HIPCHK(ctx->d_in.ensure(total), BV_E_OOM, "alloc device staging");
-  uint8_t *pin = (uint8_t *)ctx->pin_in.p, *dev = ctx->d_in.as<uint8_t>();
+  // ONE mapped, coherent pinned buffer the kernel reads and writes in place
+  // (no copy either way): the digests (hashed here), keys, item arrays, the
+  // key cache's table address per key; then the statuses
+  const size_t o_dig = at(n_msgs * 32), o_key = at(key_len + 64), o_koff = at((n_keys + 1) * 8ull),
+               o_im = at(n_items * 4), o_ik = at(n_items * 4), o_r = at(n_items * 32), o_s = at(n_items * 32),
+               o_pre = at(n_items), o_tab = at(n_keys * 8ull), o_st = at(n_items);
+  if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // the previous call may still read the buffer
+  const auto t_waited = std::chrono::steady_clock::now();
+  ctx->small_io.flags = hipHostMallocMapped | hipHostMallocCoherent;
+  HIPCHK(ctx->small_io.ensure(total), BV_E_OOM, "alloc small-batch buffer");
+  uint8_t *pin = (uint8_t *)ctx->small_io.p, *dev = nullptr;
+  HIPCHK(hipHostGetDevicePointer((void **)&dev, pin, 0), BV_E_LAUNCH, "device pointer (small batch)");
   auto put = [&](size_t o, const void *src, size_t n) {
     if (n) memcpy(pin + o, src, n);
   };
-  put(o_msg, b->msg_bytes, msg_len);
-  memset(pin + o_msg + msg_len, 0, 64);  // the SHA kernels read the last dword's neighbours
-  put(o_moff, b->msg_off, (n_msgs + 1) * 8);
+  // SHA-256 of every message on the host (SHA extensions; the messages are
+  // <= 16 KB, a few hundred at most): the kernel's first phase is s^-1 alone
+  uint8_t *dig = pin + o_dig;
+  auto hash = [b, dig](uint64_t lo, uint64_t hi) {
+    for (uint64_t m = lo; m < hi; m++)
+      hsha::digest(b->msg_bytes + b->msg_off[m], b->msg_off[m + 1] - b->msg_off[m], dig + 32 * m);
+    return true;
+  };
+  if (n_msgs <= 16) hash(0, n_msgs);
+  else ctx->pool->parallel_for(n_msgs, 16, hash);
   put(o_key, b->key_bytes, key_len);
   memset(pin + o_key + key_len, 0, 64);
   put(o_koff, b->key_off, (n_keys + 1) * 8ull);
@@ -1210,6 +1220,7 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   const bool kc = (ctx->flags & BV_F_KEY_CACHE) && n_keys;
   uint32_t hits = 0;
   if (kc) hits = bv_kc_lookup(ctx, n_keys, b->key_bytes, b->key_off, (uint64_t *)(pin + o_tab));
+  const auto t_staged = std::chrono::steady_clock::now();
   hipEvent_t *ev = ctx->S().ev;
   uint64_t *stamps = nullptr;
   if (ctx->small_stamps) {
@@ -1217,25 +1228,20 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
     HIPCHK(hipMemsetAsync(ctx->d_stamps.p, 0, 16 * 8, st), BV_E_LAUNCH, "memset stamps");
     stamps = ctx->d_stamps.as<uint64_t>();
   }
-  HIPCHK(hipEventRecord(ev[E_CALL], st), BV_E_LAUNCH, "event");
-  HIPCHK(hipMemcpyAsync(dev, pin, in_end, hipMemcpyHostToDevice, st), BV_E_LAUNCH, "h2d (small batch)");
   HIPCHK(hipEventRecord(ev[E_START], st), BV_E_LAUNCH, "event");
-  HIPCHK(bvk::verify_small(st, (uint32_t)n_items, (uint32_t)n_msgs, dev + o_msg, (const uint64_t *)(dev + o_moff),
-                           dev + o_key, (const uint64_t *)(dev + o_koff), (const uint32_t *)(dev + o_im),
-                           (const uint32_t *)(dev + o_ik), dev + o_r, dev + o_s, b->pre ? dev + o_pre : nullptr,
-                           kc ? (const uint64_t *)(dev + o_tab) : nullptr, ctx->g_table, (uint32_t *)(dev + o_dig),
-                           dev + o_st, stamps),
+  HIPCHK(bvk::verify_small(st, (uint32_t)n_items, dev + o_dig, dev + o_key, (const uint64_t *)(dev + o_koff),
+                           (const uint32_t *)(dev + o_im), (const uint32_t *)(dev + o_ik), dev + o_r, dev + o_s,
+                           b->pre ? dev + o_pre : nullptr, kc ? (const uint64_t *)(dev + o_tab) : nullptr,
+                           ctx->g_table, dev + o_st, stamps),
          BV_E_LAUNCH, "k_small");
   HIPCHK(hipEventRecord(ev[E_END], st), BV_E_LAUNCH, "event");
-  HIPCHK(hipMemcpyAsync(ctx->pin_out.p, dev + o_dig, out_end - o_dig, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
-         "d2h (small batch)");
-  HIPCHK(hipEventRecord(ev[E_OUT], st), BV_E_LAUNCH, "event");
   int rc = bv_mark_done(ctx, st);
   if (rc != BV_OK) return rc;
+  const auto t_enq = std::chrono::steady_clock::now();
+  if (res->msg_hash && n_msgs) memcpy(res->msg_hash, dig, n_msgs * 32);  // while the device works
   HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "small batch sync");
-  const uint8_t *out = (const uint8_t *)ctx->pin_out.p;
-  if (res->msg_hash && n_msgs) memcpy(res->msg_hash, out, n_msgs * 32);
-  const uint8_t *stv = out + (o_st - o_dig);
+  const auto t_sync = std::chrono::steady_clock::now();
+  const uint8_t *stv = pin + o_st;
   if (res->status) memcpy(res->status, stv, n_items);
   if (res->accept_bits) {
     memset(res->accept_bits, 0, (n_items + 63) / 64 * 8);
@@ -1244,8 +1250,6 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   }
   bv_timing &t = ctx->timing;
   t.ms_total = t.ms_verify = elapsed(ev[E_START], ev[E_END]);
-  t.ms_h2d = elapsed(ev[E_CALL], ev[E_START]);
-  t.ms_d2h = elapsed(ev[E_END], ev[E_OUT]);
   t.key_path = kc && hits ? BV_KCW : 0;
   t.kc_hits = hits;
   t.kc_keys = (uint32_t)ctx->kc_index.size();
@@ -1253,6 +1257,11 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   if (stamps) {  // diagnostics: workgroup 0's phase clocks, relative to its start
     uint64_t h[16];
     HIPCHK(hipMemcpy(h, stamps, sizeof h, hipMemcpyDeviceToHost), BV_E_LAUNCH, "d2h stamps");
+    auto us = [&](std::chrono::steady_clock::time_point a) {
+      return std::chrono::duration<double, std::micro>(a - t0).count();
+    };
+    fprintf(stderr, "k_small host_us waited=%.1f staged=%.1f enqueued=%.1f synced=%.1f\n", us(t_waited),
+            us(t_staged), us(t_enq), us(t_sync));
     fprintf(stderr, "k_small stamps n=%llu kernel_ms=%.4f:", (unsigned long long)n_items, t.ms_total);
     for (int k = 1; k < 14; k++) fprintf(stderr, " %d:%lld", k, h[k] ? (long long)(h[k] - h[0]) : -1ll);
     fprintf(stderr, "\n");

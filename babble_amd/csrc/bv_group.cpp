@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstring>
 #include <thread>
+#include <tuple>
 
 #include "bv_internal.h"
 #include "hostplan.h"
@@ -90,7 +91,11 @@ struct bv_group {
   bool logical = false;  // every entry of `devices` is the same device: no RCCL
   std::vector<DevBuf> send, recv;  // per device: shard bits, gathered bits
   std::vector<hipEvent_t> sent;    // per device: its send buffer is written (recorded on its ctx's stream)
-  std::vector<std::vector<uint64_t>> sub_off, sub_msg;
+  // per device: its shard's re-based message offsets and item -> message
+  // indices, in bv_host_alloc memory so the shard's staging DMAs them in
+  // place (grown on demand, reused across calls)
+  std::vector<void *> sub_off, sub_msg;
+  std::vector<size_t> sub_off_cap, sub_msg_cap;
   std::string err;
   std::mutex mu;
 };
@@ -115,6 +120,8 @@ extern "C" void bv_group_destroy(bv_group *g) {
     if (i < g->recv.size()) g->recv[i].release();
     bv_destroy(g->ctx[i]);
   }
+  for (void *p : g->sub_off) bv_host_free(p);
+  for (void *p : g->sub_msg) bv_host_free(p);
   delete g;
 }
 
@@ -147,8 +154,10 @@ extern "C" int bv_group_create(bv_group **out, const int *devices, int n_devices
   }
   g->send.resize(n_devices);
   g->recv.resize(n_devices);
-  g->sub_off.resize(n_devices);
-  g->sub_msg.resize(n_devices);
+  g->sub_off.assign(n_devices, nullptr);
+  g->sub_msg.assign(n_devices, nullptr);
+  g->sub_off_cap.assign(n_devices, 0);
+  g->sub_msg_cap.assign(n_devices, 0);
   if (g->logical) {
     *out = g;
     return BV_OK;
@@ -197,46 +206,66 @@ static int group_verify(bv_group *g, const bv_batch *b, bv_result *res, GroupPla
   const int D = (int)g->ctx.size();
   if (b->n_items > UINT32_MAX || b->n_msgs > UINT32_MAX)  // the group plan indexes items and messages with u32
     return gfail(g, BV_E_ARGS, "more than 2^32 items or messages in one group call");
-  int rc = bv_validate_host_batch(g->ctx[0], b);
-  if (rc != BV_OK) return gfail(g, rc, g->ctx[0]->err);
+  bv_ctx *c0 = g->ctx[0];
+  int rc = bv_validate_host_batch(c0, b);
+  if (rc != BV_OK) return gfail(g, rc, c0->err);
+  // (the O(n) order check on the copy pool: 8M items ~1 ms instead of ~8)
+  const bool in_order = c0->pool->parallel_for(b->n_items > 0 ? b->n_items - 1 : 0, 1 << 17,
+                                                [b](uint64_t lo, uint64_t hi) {
+                                                  for (uint64_t i = lo; i < hi; i++)
+                                                    if (b->item_msg[i] > b->item_msg[i + 1]) return false;
+                                                  return true;
+                                                });
   bv_batch sorted;
-  plan_group(b, D, p, sorted);
+  plan_group(b, D, p, sorted, in_order ? 1 : 0);
   const std::vector<uint64_t> &bounds = p.bounds;
-
-  // per-device sub-batches: the shard's items and its message range
-  // (re-based offsets and indices); keys are replicated (small)
-  std::vector<bv_batch> sb(D);
-  std::vector<std::vector<uint32_t>> item_msg(D);
+  // per-device pinned buffers for the shards' re-based arrays (allocated
+  // here, on the calling thread: bv_host_alloc is process-wide)
   for (int d = 0; d < D; d++) {
-    const uint64_t a = bounds[d], z = bounds[d + 1], lo = p.mlo[d], hi = p.mhi[d];
-    auto &off = g->sub_off[d];
-    off.resize(hi - lo + 1);
-    for (uint64_t m = lo; m <= hi; m++) off[m - lo] = b->msg_off[m] - b->msg_off[lo];
-    item_msg[d].resize(z - a);
-    for (uint64_t i = a; i < z; i++) item_msg[d][i - a] = (uint32_t)(sorted.item_msg[i] - lo);
-    bv_batch &s = sb[d];
-    s = sorted;
-    s.n_msgs = hi - lo;
-    s.msg_bytes = b->msg_bytes ? b->msg_bytes + (hi > lo ? b->msg_off[lo] : 0) : nullptr;
-    s.msg_off = off.data();
-    s.n_items = z - a;
-    s.item_msg = item_msg[d].data();
-    s.item_key = sorted.item_key ? sorted.item_key + a : nullptr;
-    s.r_be = sorted.r_be ? sorted.r_be + 32 * a : nullptr;
-    s.s_be = sorted.s_be ? sorted.s_be + 32 * a : nullptr;
-    s.pre = sorted.pre ? sorted.pre + a : nullptr;
+    const size_t noff = (p.mhi[d] - p.mlo[d] + 1) * 8, nim = std::max<uint64_t>(bounds[d + 1] - bounds[d], 1) * 4;
+    for (auto [buf, cap, need] : {std::make_tuple(&g->sub_off[d], &g->sub_off_cap[d], noff),
+                                  std::make_tuple(&g->sub_msg[d], &g->sub_msg_cap[d], nim)})
+      if (*cap < need) {
+        bv_host_free(*buf);
+        *buf = nullptr;
+        *cap = 0;
+        if (bv_host_alloc(need + need / 4, buf) != BV_OK) return gfail(g, BV_E_OOM, "pinned shard arrays");
+        *cap = need + need / 4;
+      }
   }
   uint64_t words = 1;
   for (int d = 0; d < D; d++) words = std::max<uint64_t>(words, (bounds[d + 1] - bounds[d] + 63) / 64);
 
   if (p.permuted && res->status) p.s_status.resize(b->n_items);
   uint8_t *st_out = p.permuted ? (res->status ? p.s_status.data() : nullptr) : res->status;
-  // stage + launch every shard concurrently (one host thread per device)
+  // build, stage and launch every shard concurrently (one host thread per
+  // device): the shard's items and its message range with re-based offsets
+  // and indices; keys are replicated (small)
+  std::vector<bv_batch> sb(D);
   std::vector<bv_host_call> calls(D);
   std::vector<int> rcs(D, BV_OK);
   std::vector<std::thread> th;
   for (int d = 0; d < D; d++)
     th.emplace_back([&, d]() {
+      {
+        const uint64_t a = bounds[d], z = bounds[d + 1], lo = p.mlo[d], hi = p.mhi[d];
+        uint64_t *off = (uint64_t *)g->sub_off[d];
+        const uint64_t base = b->msg_off ? b->msg_off[lo] : 0;  // (null only with no messages)
+        for (uint64_t m = lo; m <= hi; m++) off[m - lo] = b->msg_off ? b->msg_off[m] - base : 0;
+        uint32_t *im = (uint32_t *)g->sub_msg[d];
+        for (uint64_t i = a; i < z; i++) im[i - a] = (uint32_t)(sorted.item_msg[i] - lo);
+        bv_batch &s = sb[d];
+        s = sorted;
+        s.n_msgs = hi - lo;
+        s.msg_bytes = b->msg_bytes ? b->msg_bytes + (hi > lo ? base : 0) : nullptr;
+        s.msg_off = off;
+        s.n_items = z - a;
+        s.item_msg = im;
+        s.item_key = sorted.item_key ? sorted.item_key + a : nullptr;
+        s.r_be = sorted.r_be ? sorted.r_be + 32 * a : nullptr;
+        s.s_be = sorted.s_be ? sorted.s_be + 32 * a : nullptr;
+        s.pre = sorted.pre ? sorted.pre + a : nullptr;
+      }
       bv_ctx *c = g->ctx[d];
       std::lock_guard<std::mutex> clk(c->mu);
       if (hipSetDevice(c->device) != hipSuccess) {

@@ -50,10 +50,10 @@ hipError_t verify_g(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *,
 hipError_t verify_q(hipStream_t, int, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
                     const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
                     const uint64_t *, const uint32_t *, uint8_t *, uint64_t *);
-hipError_t verify_small(hipStream_t, uint32_t, uint32_t, const uint8_t *, const uint64_t *, const uint8_t *,
-                        const uint64_t *, const uint32_t *, const uint32_t *, const uint8_t *, const uint8_t *,
-                        const uint8_t *, const uint64_t *, const uint32_t *, uint32_t *, uint8_t *,
-                        uint64_t *stamps = nullptr);
+hipError_t verify_small(hipStream_t, uint32_t n_items, const uint8_t *dig, const uint8_t *key_bytes,
+                        const uint64_t *key_off, const uint32_t *item_msg, const uint32_t *item_key,
+                        const uint8_t *r_be, const uint8_t *s_be, const uint8_t *pre, const uint64_t *kc_tabs,
+                        const uint32_t *g_table, uint8_t *status, uint64_t *stamps = nullptr);
 hipError_t verify_generic(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
@@ -73,6 +73,7 @@ struct DevBuf {
 struct PinnedBuf {
   void *p = nullptr;
   size_t cap = 0;
+  unsigned flags = hipHostMallocDefault;  // hipHostMalloc flags of the next allocation
   hipError_t ensure(size_t bytes);
   void release();
 };
@@ -230,6 +231,7 @@ struct bv_ctx {
   CopyPool *pool = nullptr;
   // host-entry staging: one layout in pinned memory and in HBM
   PinnedBuf pin_in, pin_out;
+  PinnedBuf small_io;  // k_small's inputs and statuses, read / written by the kernel in place (mapped, coherent)
   DevBuf d_in;
   DevBuf d_stamps;  // BV_SMALL_STAMPS: k_small phase clocks (diagnostics)
   // host entry: messages longer than kHostHashLen hashed on the host (their

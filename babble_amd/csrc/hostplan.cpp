@@ -72,9 +72,9 @@ static bool items_in_message_order(const bv_batch *b) {
 // shards, and a PARTITION of the messages [0, n_msgs) into contiguous device
 // ranges — every message is hashed exactly once, including messages no item
 // references (bv_verify_batch writes every digest too).
-void plan_group(const bv_batch *b, int D, GroupPlan &p, bv_batch &sorted) {
+void plan_group(const bv_batch *b, int D, GroupPlan &p, bv_batch &sorted, int in_order) {
   sorted = *b;
-  p.permuted = !items_in_message_order(b);
+  p.permuted = in_order < 0 ? !items_in_message_order(b) : in_order == 0;
   if (p.permuted) {
     const uint64_t n = b->n_items, M = b->n_msgs;
     std::vector<uint64_t> cnt(M + 1, 0);

@@ -18,4 +18,6 @@ struct GroupPlan {
 
 // Fills `p` for `b` over D shards; `sorted` = b with its item arrays in the
 // plan's order (p's own copies when permuted).  b's item_msg must be < n_msgs.
-void plan_group(const bv_batch *b, int D, GroupPlan &p, bv_batch &sorted);
+// `in_order`: whether item_msg is non-decreasing, when the caller already
+// knows (-1: checked here).
+void plan_group(const bv_batch *b, int D, GroupPlan &p, bv_batch &sorted, int in_order = -1);

@@ -512,143 +512,221 @@ __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, uint64
 
 // ---------------------------------------------------------------------------
 // Small batches: k_small, ONE launch per batch, one 256-thread workgroup per
-// item (workgroup b also hashes message b for the digest output).  A small
-// batch is bound by its longest serial chain, not by throughput, so the work
-// of one item is spread over the workgroup's four waves (lanes of different
-// waves run different code at the same time; lanes of one wave only when
-// they run the same code):
-//   phase 1  wave 0: SHA-256 of the item's message (e)
-//            wave 1: s^-1 (one Bernstein-Yang inversion)
+// item.  A small batch is bound by its longest serial chain, not by
+// throughput, so one item's work is spread over the workgroup (lanes of
+// different waves run different code at the same time; lanes of one wave
+// only when they run the same code).  The host has hashed the messages
+// (SHA-NI, hostsha.cpp) and sends the digests.
+//   phase 1  wave 1: s^-1 (one Bernstein-Yang inversion; wave-uniform, so
+//            the compiler runs it on the scalar unit)
 //            wave 2: elliptic.Unmarshal of the item's key (Q)
-//            wave 3: SHA-256 of message b -> msg_hash[b]
-//   phase 2  thread 0: decision table, u1 = e w, u2 = r w, GLV split
-//   phase 3  wave 1 lanes 0, 1: u1 G over G windows 0-4 / 5-9
-//            wave 2: k1 Q;  wave 3: k2 phi(Q) — from the key's cached KC
-//            table when it has one (6 lookups each), else a NAF double-and-
-//            add chain (129 doublings) on the affine point, the whole wave
-//            cooperating on each step (coop.h)
-//   phase 4  wave 0 lanes 0, 1: two XYZZ sums; thread 0: the last sum and
-//            x(R) mod N == r
-// Statuses only; the host packs a small batch's accept bits.
+//   phase 2  wave 0 lane 0: decision table, u1 = e w;  wave 1 lane 0:
+//            u2 = r w and its GLV split (k1, k2, signs)
+//   phase 3  key with a key-cache table: 22 leaves in lanes 0..21 of wave
+//            0, every table entry loaded at once — G windows 0..9 of u1,
+//            KC windows 0..5 of k1 (T) and of k2 (phi(T)) — summed by a
+//            binary tree (affine pairs, then XYZZ sums: 5 levels of zipped
+//            point additions, nodes handed over through LDS);
+//            key without one: waves 2 / 3 run k1 Q / k2 phi(Q) as
+//            wave-cooperative NAF chains (coop.h) while wave 0 sums the 10
+//            G leaves, then wave 0 lane 0 adds the three partial sums
+//   phase 4  wave 0 lane 0: x(R) mod N == r
+// Statuses only; the host packs a small batch's accept bits.  `stamps`
+// (BV_SMALL_STAMPS diagnostics): workgroup 0's shader clocks per phase.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs,
-                                               const uint8_t *__restrict__ msg_bytes,
-                                               const uint64_t *__restrict__ msg_off,
+namespace {
+constexpr int kSmallLeaves = BV_GNWIN + 2 * BV_KCNWIN;  // 22
+struct SmallNode {
+  uint32_t w[33];
+};
+// one level of the wave-0 sum tree: node i <- node 2i + node 2i+1 (the last
+// node of an odd count moves up alone); nodes in `from`, results in `to`
+DEV void small_tree_level(const SmallNode *from, SmallNode *to, int n, uint32_t lane) {
+  if (lane < (uint32_t)(n + 1) / 2) {
+    gexz A, B;
+    bool ia, ib = true;
+    part_load(from[2 * lane].w, A, ia);
+    if (2 * (int)lane + 1 < n) part_load(from[2 * lane + 1].w, B, ib);
+    gexz_add_lat(A, ia, B, ib);
+    part_store(to[lane].w, A, ia);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this wave's LDS writes land before the next level reads
+  __builtin_amdgcn_wave_barrier();
+}
+// the leaves' first level: affine pairs (2i, 2i+1) -> XYZZ node i
+DEV void small_leaf_pairs(const fe &x, const fe &y, bool zero, SmallNode *to, SmallNode *scratch, int n,
+                          uint32_t lane) {
+  if (lane < (uint32_t)n) {  // the leaf, affine: (x, y, zero) in the node's X, Y, identity slots
+#pragma unroll
+    for (int k = 0; k < 8; k++) scratch[lane].w[k] = x.v[k], scratch[lane].w[8 + k] = y.v[k];
+    scratch[lane].w[32] = zero ? 1u : 0u;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  if (lane < (uint32_t)(n + 1) / 2) {
+    fe x1, y1, x2, y2;
+    bool i1, i2 = true;
+#pragma unroll
+    for (int k = 0; k < 8; k++) x1.v[k] = scratch[2 * lane].w[k], y1.v[k] = scratch[2 * lane].w[8 + k];
+    i1 = scratch[2 * lane].w[32] != 0;
+    if (2 * (int)lane + 1 < n) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) x2.v[k] = scratch[2 * lane + 1].w[k], y2.v[k] = scratch[2 * lane + 1].w[8 + k];
+      i2 = scratch[2 * lane + 1].w[32] != 0;
+    }
+    gexz R;
+    bool inf;
+    gexz_sum_ge_lat(R, inf, x1, y1, i1, x2, y2, i2);
+    part_store(to[lane].w, R, inf);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t *__restrict__ digest_words,
                                                const uint8_t *__restrict__ key_bytes,
                                                const uint64_t *__restrict__ key_off,
                                                const uint32_t *__restrict__ item_msg,
                                                const uint32_t *__restrict__ item_key,
                                                const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                const uint8_t *__restrict__ pre, const uint64_t *__restrict__ kc_tabs,
-                                               const uint32_t *__restrict__ g_table,
-                                               uint32_t *__restrict__ digest_words, uint8_t *__restrict__ status,
+                                               const uint32_t *__restrict__ g_table, uint8_t *__restrict__ status,
                                                uint64_t *__restrict__ stamps) {
   const uint32_t b = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  // diagnostics (BV_SMALL_STAMPS): shader clocks of workgroup 0's phases
 #define SMALL_STAMP(k)                                                     \
   do {                                                                     \
     if (stamps && b == 0) stamps[k] = __builtin_amdgcn_s_memtime();        \
   } while (0)
   if (t == 0) SMALL_STAMP(0);
-  __shared__ uint32_t sh_e[8], sh_w[8], sh_q[16], sh_u1[8], sh_k[8];
-  __shared__ uint32_t sh_part[4][33];
-  __shared__ uint32_t sh_ks, sh_go;
-  const bool item = b < n_items;
-  // ---- phase 1
-  if (item && lane == 0) {
-    if (wave == 0) {
-      uint32_t h[8];
-      const uint32_t m = item_msg[b];
-      sha256_msg(h, msg_bytes, msg_off[m], msg_off[m + 1] - msg_off[m]);
+  __shared__ uint32_t sh_w[8], sh_q[16], sh_u1[8], sh_k[8], sh_r[8], sh_s[8], sh_e[8];
+  __shared__ uint32_t sh_ks, sh_go, sh_signs, sh_pre;
+  __shared__ uint64_t sh_tab;
+  __shared__ SmallNode sh_a[kSmallLeaves], sh_b[kSmallLeaves / 2 + 1], sh_c[kSmallLeaves / 4 + 2], sh_d[3];
+  if (b >= n_items) return;  // (the grid is n_items)
+  // ---- phase 1 (the inputs live in host memory, read in place: wave 0
+  // fetches what phases 2-4 need while s^-1 runs)
+  if (lane == 0 && wave == 0) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) sh_e[k] = bswap32(h[k]);  // the digest's big-endian bytes (as k_sha256)
-      SMALL_STAMP(1);
-    } else if (wave == 1) {
-      sc s, w;
-      sc_load_be_words(s, s_be + 8 * (uint64_t)b);
-      if (s_usable(pre, b, s)) {
-        sinv_one(w, s);
-      } else {
+    for (int k = 0; k < 8; k++) sh_r[k] = r_be[8 * (uint64_t)b + k];
+    const uint32_t m = item_msg[b];
 #pragma unroll
-        for (int k = 0; k < 8; k++) w.v[k] = 0;
-      }
+    for (int k = 0; k < 8; k++) sh_e[k] = digest_words[8 * (uint64_t)m + k];
+    sh_pre = pre ? pre[b] : 0u;
+    sh_tab = kc_tabs ? kc_tabs[item_key[b]] : 0;
+  } else if (lane == 0 && wave == 1) {
+    sc s, w;
+    sc_load_be_words(s, s_be + 8 * (uint64_t)b);
 #pragma unroll
-      for (int k = 0; k < 8; k++) sh_w[k] = w.v[k];
-      SMALL_STAMP(2);
-    } else if (wave == 2) {
-      const uint32_t k = item_key[b];
-      uint8_t st;
-      fe x, y;
-      key_decode_point(key_bytes, key_off[k], key_off[k + 1] - key_off[k], st, x, y);
+    for (int k = 0; k < 8; k++) sh_s[k] = s_be[8 * (uint64_t)b + k];
+    if (s_usable(pre, b, s)) {
+      sinv_one(w, s);
+    } else {
 #pragma unroll
-      for (int c = 0; c < 8; c++) sh_q[c] = x.v[c], sh_q[8 + c] = y.v[c];
-      sh_ks = st;
-      SMALL_STAMP(3);
+      for (int k = 0; k < 8; k++) w.v[k] = 0;
     }
-  }
-  if (wave == 3 && lane == 0 && b < n_msgs) {
-    sha256_one(b, msg_bytes, msg_off, digest_words);
-    SMALL_STAMP(4);
+#pragma unroll
+    for (int k = 0; k < 8; k++) sh_w[k] = w.v[k];
+    SMALL_STAMP(2);
+  } else if (lane == 0 && wave == 2) {
+    const uint32_t k = item_key[b];
+    uint8_t st;
+    fe x, y;
+    key_decode_point(key_bytes, key_off[k], key_off[k + 1] - key_off[k], st, x, y);
+#pragma unroll
+    for (int c = 0; c < 8; c++) sh_q[c] = x.v[c], sh_q[8 + c] = y.v[c];
+    sh_ks = st;
+    SMALL_STAMP(3);
   }
   __syncthreads();
   if (t == 0) SMALL_STAMP(5);
-  if (!item) return;  // uniform per workgroup
-  // ---- phase 2
-  if (t == 0) {
+  // ---- phase 2: the decision table and u1 (wave 0), u2 + GLV (wave 1)
+  if (lane == 0 && wave == 0) {
     fe r, sv;
-    fe_load_be_words(r, r_be + 8 * (uint64_t)b);
-    fe_load_be_words(sv, s_be + 8 * (uint64_t)b);
-    const uint8_t cls = classify(pre ? pre[b] : 0, (uint8_t)sh_ks, r, sv);
+    fe_load_be_words(r, sh_r);
+    fe_load_be_words(sv, sh_s);
+    const uint8_t cls = classify((uint8_t)sh_pre, (uint8_t)sh_ks, r, sv);
     sh_go = cls == 0xFF;
     if (cls != 0xFF) {
       status[b] = cls;
     } else {
-      sc w, e, rs;
+      sc w, e, a;
 #pragma unroll
-      for (int k = 0; k < 8; k++) w.v[k] = sh_w[k], rs.v[k] = r.v[k];
+      for (int k = 0; k < 8; k++) w.v[k] = sh_w[k];
       sc_load_be_words(e, sh_e);
-      uint32_t u1[8], k1[4], k2[4], signs;
-      scalars_from(w, e, rs, u1, k1, k2, signs);
+      sc_mont(a, e, w);  // e s^-1 mod N (e unreduced, < 2^256 = R)
 #pragma unroll
-      for (int k = 0; k < 8; k++) sh_u1[k] = u1[k];
-#pragma unroll
-      for (int k = 0; k < 4; k++) sh_k[k] = k1[k], sh_k[4 + k] = k2[k];
-      sh_go = 1u | (signs << 1);
+      for (int k = 0; k < 8; k++) sh_u1[k] = a.v[k];
     }
+  } else if (lane == 0 && wave == 1) {
+    sc w, r, u2;
+#pragma unroll
+    for (int k = 0; k < 8; k++) w.v[k] = sh_w[k];
+    sc_load_be_words(r, sh_r);
+    sc_mont(u2, r, w);  // r s^-1 mod N (only used when the item reaches the math)
+    uint32_t k1[4], k2[4], signs;
+    glv_split(k1, k2, signs, u2);
+#pragma unroll
+    for (int k = 0; k < 4; k++) sh_k[k] = k1[k], sh_k[4 + k] = k2[k];
+    sh_signs = signs;
   }
   __syncthreads();
   if (t == 0) SMALL_STAMP(6);
-  const uint32_t go = sh_go;
-  if (!go) return;  // decided by the table (uniform)
-  // ---- phase 3: four partial sums
-  if (lane < 2 && wave == 1) {  // u1 G, windows [5 lane, 5 lane + 5)
-    uint32_t u[8];
+  if (!sh_go) return;  // decided by the table (uniform)
+  const uint32_t signs = sh_signs;
+  const uint64_t tab = sh_tab;  // wave-uniform
+  // ---- phase 3
+  if (tab) {
+    if (wave == 0) {
+      fe x, y;
+      bool zero = true;
+      if (lane < BV_GNWIN) {  // G window `lane` of u1
+        uint32_t u[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) u[k] = sh_u1[k];
-    gexz R;
-    bool inf = true;
-    fe_set(R.X, 0), fe_set(R.Y, 0), fe_set(R.ZZ, 0), fe_set(R.ZZZ, 0);
-    g_table_add_range<BV_GW, BV_GNWIN, true>(R, inf, g_table, u, (BV_GNWIN / 2) * (int)lane,
-                                              lane ? BV_GNWIN : BV_GNWIN / 2);
-    part_store(sh_part[lane], R, inf);
-    SMALL_STAMP(7 + lane);
-  } else if (wave >= 2) {  // k1 Q (wave 2) / k2 phi(Q) (wave 3)
-    const uint32_t h = wave - 2;
-    uint32_t kk[4];
+        for (int k = 0; k < 8; k++) u[k] = sh_u1[k];
+        table_leaf<BV_GW, 8>(x, y, zero, g_table, u, (int)lane, false, false);
+      } else if (lane < (uint32_t)kSmallLeaves) {  // KC window j of k1 (T) or of k2 (phi(T))
+        const uint32_t q = lane - BV_GNWIN, h = q / BV_KCNWIN;
+        uint32_t kk[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) kk[k] = sh_k[4 * h + k];
-    const bool neg = (go >> (1 + h)) & 1u;
-    const uint64_t tab = kc_tabs ? kc_tabs[item_key[b]] : 0;  // wave-uniform
-    if (tab) {  // the key's cached KC table: 6 lookups on lane 0
-      if (lane == 0) {
-        gexz R;
-        bool inf = true;
-        fe_set(R.X, 0), fe_set(R.Y, 0), fe_set(R.ZZ, 0), fe_set(R.ZZZ, 0);
-        key_table_add<BV_KCW, BV_KCNWIN, true, true>(R, inf, (const uint32_t *)tab, kk, neg, h != 0);
-        part_store(sh_part[2 + h], R, inf);
-        SMALL_STAMP(9 + h);
+        for (int k = 0; k < 4; k++) kk[k] = sh_k[4 * h + k];
+        table_leaf<BV_KCW, 4>(x, y, zero, (const uint32_t *)tab, kk, (int)(q % BV_KCNWIN), (signs >> h) & 1u,
+                              h != 0);
       }
-    } else {  // no table: the NAF chain, wave-cooperative (coop.h)
+      if (lane == 0) SMALL_STAMP(7);
+      small_leaf_pairs(x, y, zero, sh_b, sh_a, kSmallLeaves, lane);  // 22 leaves -> 11 nodes
+      if (lane == 0) SMALL_STAMP(8);
+      small_tree_level(sh_b, sh_c, 11, lane);  // -> 6
+      small_tree_level(sh_c, sh_b, 6, lane);   // -> 3
+      small_tree_level(sh_b, sh_c, 3, lane);   // -> 2
+      small_tree_level(sh_c, sh_b, 2, lane);   // -> 1
+      if (lane == 0) SMALL_STAMP(11);
+    }
+  } else {
+    if (wave == 0) {  // the G leaves and their subtree: 10 -> 5 -> 3 -> 2 -> 1
+      fe x, y;
+      bool zero = true;
+      if (lane < BV_GNWIN) {
+        uint32_t u[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) u[k] = sh_u1[k];
+        table_leaf<BV_GW, 8>(x, y, zero, g_table, u, (int)lane, false, false);
+      }
+      small_leaf_pairs(x, y, zero, sh_b, sh_a, BV_GNWIN, lane);
+      small_tree_level(sh_b, sh_c, 5, lane);
+      small_tree_level(sh_c, sh_b, 3, lane);
+      small_tree_level(sh_b, sh_c, 2, lane);  // the G sum in sh_c[0]
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 33; k++) sh_d[0].w[k] = sh_c[0].w[k];
+        SMALL_STAMP(7);
+      }
+    } else if (wave >= 2) {  // no table: k1 Q (wave 2) / k2 phi(Q) (wave 3), the NAF chain, wave-cooperative
+      const uint32_t h = wave - 2;
+      uint32_t kk[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) kk[k] = sh_k[4 * h + k];
+      const bool neg = (signs >> h) & 1u;
       const uint32_t c = coop::pos();
       uint32_t px = c < 8 ? sh_q[c] : 0u, py = c < 8 ? sh_q[8 + c] : 0u;
       if (h) px = coop::mul(px, c < 8 ? FE_BETA[c] : 0u);  // phi(Q) = (beta x, y)
@@ -662,38 +740,29 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, uint32_t n_msgs
         ZZZ = coop::mul(ZZ, Z);
       }
       if (lane < 8) {
-        sh_part[2 + h][lane] = X;
-        sh_part[2 + h][8 + lane] = Y;
-        sh_part[2 + h][16 + lane] = ZZ;
-        sh_part[2 + h][24 + lane] = ZZZ;
+        sh_d[1 + h].w[lane] = X;
+        sh_d[1 + h].w[8 + lane] = Y;
+        sh_d[1 + h].w[16 + lane] = ZZ;
+        sh_d[1 + h].w[24 + lane] = ZZZ;
       }
       if (lane == 0) {
-        sh_part[2 + h][32] = inf ? 1u : 0u;
+        sh_d[1 + h].w[32] = inf ? 1u : 0u;
         SMALL_STAMP(9 + h);
       }
     }
+    __syncthreads();
+    if (wave == 0) {  // (G + k1 Q) + k2 phi(Q)
+      small_tree_level(sh_d, sh_c, 3, lane);
+      small_tree_level(sh_c, sh_b, 2, lane);
+    }
   }
-  __syncthreads();
-  if (t == 0) SMALL_STAMP(11);
-  // ---- phase 4
-  if (wave == 0 && lane < 2) {
-    gexz A, B;
-    bool ia, ib;
-    part_load(sh_part[2 * lane], A, ia);
-    part_load(sh_part[2 * lane + 1], B, ib);
-    gexz_add(A, ia, B, ib);
-    part_store(sh_part[2 * lane], A, ia);
-  }
-  __syncthreads();
-  if (t == 0) SMALL_STAMP(12);
+  // ---- phase 4: the root (sh_b[0]) -> the decision
   if (t == 0) {
-    gexz A, B;
-    bool ia, ib;
-    part_load(sh_part[0], A, ia);
-    part_load(sh_part[2], B, ib);
-    gexz_add(A, ia, B, ib);
+    gexz A;
+    bool ia;
+    part_load(sh_b[0].w, A, ia);
     fe r;
-    fe_load_be_words(r, r_be + 8 * (uint64_t)b);
+    fe_load_be_words(r, sh_r);
     status[b] = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
     SMALL_STAMP(13);
   }
@@ -936,15 +1005,13 @@ hipError_t build_kc(hipStream_t st, uint32_t n, const uint32_t *kxy, const uint8
   return hipGetLastError();
 }
 
-hipError_t verify_small(hipStream_t st, uint32_t n_items, uint32_t n_msgs, const uint8_t *msg_bytes,
-                        const uint64_t *msg_off, const uint8_t *key_bytes, const uint64_t *key_off,
-                        const uint32_t *item_msg, const uint32_t *item_key, const uint8_t *r_be, const uint8_t *s_be,
-                        const uint8_t *pre, const uint64_t *kc_tabs, const uint32_t *g_table, uint32_t *dig,
-                        uint8_t *status, uint64_t *stamps) {
-  const uint32_t grid = std::max(n_items, n_msgs);
-  if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_small, dim3(grid), dim3(256), 0, st, n_items, n_msgs, msg_bytes, msg_off, key_bytes, key_off,
-                     item_msg, item_key, (const uint32_t *)r_be, (const uint32_t *)s_be, pre, kc_tabs, g_table, dig,
+hipError_t verify_small(hipStream_t st, uint32_t n_items, const uint8_t *dig, const uint8_t *key_bytes,
+                        const uint64_t *key_off, const uint32_t *item_msg, const uint32_t *item_key,
+                        const uint8_t *r_be, const uint8_t *s_be, const uint8_t *pre, const uint64_t *kc_tabs,
+                        const uint32_t *g_table, uint8_t *status, uint64_t *stamps) {
+  if (n_items == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_small, dim3(n_items), dim3(256), 0, st, n_items, (const uint32_t *)dig, key_bytes, key_off,
+                     item_msg, item_key, (const uint32_t *)r_be, (const uint32_t *)s_be, pre, kc_tabs, g_table,
                      status, stamps);
   return hipGetLastError();
 }

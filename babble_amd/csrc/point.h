@@ -392,6 +392,89 @@ DEV void gexz_add(gexz &r, bool &rinf, const gexz &b, bool binf) {
   fe_mul(r.ZZZ, r.ZZZ, PPP);  // ZZZ3 = ZZZ1 ZZZ2 PPP
 }
 
+// gexz_add for latency-bound single lanes (k_small's sum tree): its 14
+// products in five levels of independent multiplies, each level one zipped
+// asm program — {U1, U2, S1} {S2, ZZ1 ZZ2, ZZZ1 ZZZ2} -> {P^2, R^2} ->
+// {P PP, U1 PP, ZZ12 PP} -> {R (Q - X3), S1 PPP, ZZZ12 PPP}.  Same values
+// and exceptional cases.
+DEV void gexz_add_lat(gexz &r, bool &rinf, const gexz &b, bool binf) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (binf) return;
+  if (rinf) {
+    r = b;
+    rinf = false;
+    return;
+  }
+  fe U1, U2, S1, S2, Z12, W12, P, R, PP, RR, PPP, Q, t, u;
+  fe_mul_mul_mul_zip_asm(U1, r.X, b.ZZ, U2, b.X, r.ZZ, S1, r.Y, b.ZZZ);
+  fe_mul_mul_mul_zip_asm(S2, b.Y, r.ZZZ, Z12, r.ZZ, b.ZZ, W12, r.ZZZ, b.ZZZ);
+  fe_sub(P, U2, U1);
+  fe_sub(R, S2, S1);
+  if (fe_is_zero(P)) {
+    if (fe_is_zero(R)) {
+      gexz d;
+      gexz_double(d, r);
+      r = d;
+    } else {
+      rinf = true;
+    }
+    return;
+  }
+  fe_sqr_sqr_zip_asm(PP, P, RR, R);
+  fe_mul_mul_mul_zip_asm(PPP, P, PP, Q, U1, PP, r.ZZ, Z12, PP);
+  fe_sub(t, RR, PPP);
+  fe_sub(t, t, Q);
+  fe_sub(r.X, t, Q);  // X3 = R^2 - PPP - 2Q
+  fe_sub(t, Q, r.X);
+  fe_mul_mul_mul_zip_asm(t, R, t, u, S1, PPP, r.ZZZ, W12, PPP);
+  fe_sub(r.Y, t, u);  // Y3 = R (Q - X3) - S1 PPP
+#else
+  gexz_add(r, rinf, b, binf);
+#endif
+}
+
+// r = (x1, y1) + (x2, y2), two affine points (either may be the identity:
+// i1 / i2) into XYZZ — madd-2008-s with Z1 = 1: 4M + 2S in three zipped
+// levels {P^2, R^2} -> {P PP, x1 PP} -> {R (Q - X3), y1 PPP}.  The first
+// level of k_small's sum tree (table entries are affine).
+DEV void gexz_sum_ge_lat(gexz &r, bool &rinf, const fe &x1, const fe &y1, bool i1, const fe &x2, const fe &y2,
+                         bool i2) {
+  rinf = i1 && i2;
+  if (i1 || i2) {
+    if (!rinf) gexz_set_ge(r, i1 ? x2 : x1, i1 ? y2 : y1);
+    return;
+  }
+  fe P, R;
+  fe_sub(P, x2, x1);
+  fe_sub(R, y2, y1);
+  if (fe_is_zero(P)) {
+    if (fe_is_zero(R)) {
+      gexz a;
+      gexz_set_ge(a, x1, y1);
+      gexz_double(r, a);
+    } else {
+      rinf = true;
+    }
+    return;
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe PP, RR, PPP, Q, t, u;
+  fe_sqr_sqr_zip_asm(PP, P, RR, R);
+  fe_mul_mul_zip_asm(PPP, P, PP, Q, x1, PP);
+  fe_sub(t, RR, PPP);
+  fe_sub(t, t, Q);
+  fe_sub(r.X, t, Q);
+  fe_sub(t, Q, r.X);
+  fe_mul_mul_zip_asm(t, R, t, u, y1, PPP);
+  fe_sub(r.Y, t, u);
+  r.ZZ = PP;
+  r.ZZZ = PPP;
+#else
+  gexz_set_ge(r, x1, y1);
+  gexz_add_ge(r, rinf, x2, y2);
+#endif
+}
+
 // Jacobian (X, Y, Z) -> XYZZ (X, Y, Z^2, Z^3): the same point
 DEV void gexz_from_gej(gexz &r, const gej &a) {
   r.X = a.X;

@@ -820,6 +820,37 @@ DEV void naf_mul(gej &R, bool &inf, const fe &px, const fe &py, const uint32_t k
   }
 }
 
+// One leaf of k_small's sum tree: the entry window j of u (NW limbs of 32
+// bits, consumed; W-bit SIGNED digits by carry recoding, as g_table_add /
+// key_table_add) contributes: (x, y) with y negated for a negative digit,
+// XOR `neg` (the GLV half's sign); `phi`: (beta x, y) of the stored entry;
+// *zero: the digit is 0 (the leaf is the identity).  The recoding runs over
+// windows 0..j (a digit depends on the carry out of the window below).
+template <int W, int NW>
+DEV void table_leaf(fe &x, fe &y, bool &zero, const uint32_t *tab, uint32_t u[NW], int j, bool neg, bool phi) {
+  constexpr uint32_t ENT = 1u << (W - 1);
+  uint32_t carry = 0, d = 0;
+  for (int w = 0; w <= j; w++) {
+    d = (u[0] & ((1u << W) - 1u)) + carry;
+#pragma unroll
+    for (int c = 0; c < NW - 1; c++) u[c] = (u[c] >> W) | (u[c + 1] << (32 - W));
+    u[NW - 1] >>= W;
+    carry = d > ENT ? 1u : 0u;
+  }
+  const bool dneg = carry != 0;
+  if (dneg) d = (1u << W) - d;  // |d - 2^W|, 0 when d == 2^W
+  zero = d == 0;
+  const uint32_t *e = tab + ((uint64_t)j * ENT + d) * BV_ENTRY_U32;  // d == 0: a valid, unused slot
+  fe_load4(x, e);
+  fe_load4(y, e + 8);
+  if (phi) {
+    fe beta;
+    fe_load(beta, FE_BETA);
+    fe_mul(x, x, beta);
+  }
+  fe_cneg_canon(y, dneg != neg);
+}
+
 // One XYZZ partial sum (+ identity flag) in 33 words (LDS hand-off)
 DEV void part_store(uint32_t *p, const gexz &R, bool inf) {
 #pragma unroll

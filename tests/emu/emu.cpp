@@ -180,9 +180,29 @@ const uint32_t *emu_g_table(int nt) {
 
 // k_small's per-item steps (kernels.hip) run one after another: the same
 // verify_core.h / point.h pieces the workgroup's waves run concurrently
-// (SHA-256, s^-1, key decode, decision table, u1 / u2 + GLV, the two G
-// window ranges, the NAF chains of k1 Q and k2 phi(Q), the XYZZ sums and
-// the final check).  The key cache's table lookups are exercised on the GPU.
+// (s^-1, key decode, decision table, u1 / u2 + GLV, the 10 G leaves and
+// their sum tree — affine pairs, then XYZZ sums — the NAF chains of k1 Q and
+// k2 phi(Q), the root sums and the final check).  The digest is SHA-256 of
+// the message (the library hashes small batches on the host).  The key
+// cache's table leaves are exercised on the GPU.
+namespace {
+void tree_sum(std::vector<gexz> &n, std::vector<bool> &inf) {
+  while (n.size() > 1) {  // node i <- node 2i + node 2i+1, an odd last node moves up alone
+    std::vector<gexz> m;
+    std::vector<bool> mi;
+    for (size_t i = 0; i < n.size(); i += 2) {
+      gexz a = n[i];
+      bool ia = inf[i];
+      if (i + 1 < n.size()) gexz_add_lat(a, ia, n[i + 1], inf[i + 1]);
+      m.push_back(a);
+      mi.push_back(ia);
+    }
+    n.swap(m);
+    inf.swap(mi);
+  }
+}
+}  // namespace
+
 uint8_t small_item(uint64_t i, const bv_batch *b, const uint8_t *msg, const uint32_t *r, const uint32_t *s,
                    const uint32_t *gt) {
   const uint32_t m = b->item_msg[i], k = b->item_key[i];
@@ -206,14 +226,25 @@ uint8_t small_item(uint64_t i, const bv_batch *b, const uint8_t *msg, const uint
   for (int c = 0; c < 8; c++) rs.v[c] = rf.v[c];
   uint32_t u1[8], k1[4], k2[4], signs;
   scalars_from(w, e, rs, u1, k1, k2, signs);
-  gexz P[4];
-  bool inf[4];
-  for (int q = 0; q < 2; q++) {
+  fe lx[BV_GNWIN], ly[BV_GNWIN];
+  bool lz[BV_GNWIN];
+  for (int j = 0; j < BV_GNWIN; j++) {
     uint32_t u[8];
     for (int c = 0; c < 8; c++) u[c] = u1[c];
-    inf[q] = true;
-    g_table_add_range<BV_GW, BV_GNWIN>(P[q], inf[q], gt, u, (BV_GNWIN / 2) * q, q ? BV_GNWIN : BV_GNWIN / 2);
+    table_leaf<BV_GW, 8>(lx[j], ly[j], lz[j], gt, u, j, false, false);
   }
+  std::vector<gexz> nodes;
+  std::vector<bool> ninf;
+  for (int j = 0; j < BV_GNWIN; j += 2) {
+    gexz R;
+    bool inf;
+    const bool last = j + 1 >= BV_GNWIN;
+    gexz_sum_ge_lat(R, inf, lx[j], ly[j], lz[j], last ? lx[j] : lx[j + 1], last ? ly[j] : ly[j + 1],
+                    last ? true : lz[j + 1]);
+    nodes.push_back(R);
+    ninf.push_back(inf);
+  }
+  tree_sum(nodes, ninf);
   for (int hh = 0; hh < 2; hh++) {
     fe px = qx, py = qy;
     if (hh) {
@@ -223,13 +254,15 @@ uint8_t small_item(uint64_t i, const bv_batch *b, const uint8_t *msg, const uint
     }
     if ((signs >> hh) & 1u) fe_neg(py, py);
     gej J;
-    naf_mul<false>(J, inf[2 + hh], px, py, hh ? k2 : k1);
-    if (!inf[2 + hh]) gexz_from_gej(P[2 + hh], J);
+    bool inf;
+    gexz Q;
+    naf_mul<false>(J, inf, px, py, hh ? k2 : k1);
+    if (!inf) gexz_from_gej(Q, J);
+    nodes.push_back(Q);
+    ninf.push_back(inf);
   }
-  gexz_add(P[0], inf[0], P[1], inf[1]);
-  gexz_add(P[2], inf[2], P[3], inf[3]);
-  gexz_add(P[0], inf[0], P[2], inf[2]);
-  return final_check(P[0], inf[0], rf) ? BV_ACCEPT : BV_REJECT;
+  tree_sum(nodes, ninf);  // (G + k1 Q) + k2 phi(Q)
+  return final_check(nodes[0], ninf[0], rf) ? BV_ACCEPT : BV_REJECT;
 }
 
 template <class T>
