@@ -20,6 +20,7 @@
 #include "hostsha.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -506,8 +507,26 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
 
 extern "C" void *bv_last_stream(const bv_ctx *ctx) { return ctx ? (void *)ctx->last : nullptr; }
 
+static float elapsed(hipEvent_t a, hipEvent_t b);
+
+// A small batch returns once its statuses have landed, possibly before the
+// kernel's completion signal: its device span is read when asked for.
+void bv_read_small_span(bv_ctx *ctx) {
+  if (!ctx->small_span) return;
+  const auto &sl = ctx->slot[ctx->small_span - 1];
+  if (hipEventSynchronize(sl.ev[E_END]) == hipSuccess)
+    ctx->timing.ms_total = ctx->timing.ms_verify = elapsed(sl.ev[E_START], sl.ev[E_END]);
+  ctx->small_span = 0;
+}
+
 extern "C" int bv_get_timing(const bv_ctx *ctx, bv_timing *out) {
   if (!ctx || !out) return BV_E_ARGS;
+  if (ctx->small_span) {  // (the ctx's own call bookkeeping, not its inputs)
+    bv_ctx *c = const_cast<bv_ctx *>(ctx);
+    std::lock_guard<std::mutex> lk(c->mu);
+    (void)hipSetDevice(c->device);
+    bv_read_small_span(c);
+  }
   *out = ctx->timing;
   return BV_OK;
 }
@@ -762,6 +781,7 @@ extern "C" int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_re
   hipStream_t st = stream ? (hipStream_t)stream : ctx->lane[(ctx->cur + 1) % bv_ctx::kSlots];
   ctx->last = st;
   ctx->timing = bv_timing{};
+  ctx->small_span = 0;
   int rc = verify_device_impl(ctx, dbatch, dresult, st);
   if (rc != BV_OK) return bv_drain(ctx, st, rc);
   if (!async) {
@@ -858,6 +878,7 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   if (!cs) return bv_fail(ctx, BV_E_NODEVICE, "copy stream");
   ctx->last = st;
   ctx->timing = bv_timing{};
+  ctx->small_span = 0;
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
   const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
@@ -1146,6 +1167,7 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
 // ---------------------------------------------------------------------------
 constexpr uint64_t kSmallItems = 256;       // items (and messages) per small batch
 constexpr uint64_t kSmallMsgLen = 16 << 10;  // longest message (hashed on the host, inside the call)
+constexpr uint8_t kSmallPending = 0xFF;      // status sentinel (statuses are 0..3)
 
 // Small batches: <= 256 items, or up to ctx->small_warm_max (512) items when
 // every well-formed key already has a key-cache table (no item needs the
@@ -1178,6 +1200,7 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   hipStream_t st = ctx->stream;
   ctx->last = st;
   ctx->timing = bv_timing{};
+  ctx->small_span = 0;
   size_t total = 0;
   auto at = [&](size_t bytes) {
     const size_t o = total;
@@ -1217,6 +1240,11 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   put(o_r, b->r_be, n_items * 32);
   put(o_s, b->s_be, n_items * 32);
   if (b->pre) put(o_pre, b->pre, n_items);
+  // statuses start as a sentinel no status takes: the host sees each one
+  // land in this (coherent) buffer and returns without waiting for the
+  // kernel's completion signal
+  volatile uint8_t *stv = pin + o_st;
+  memset(pin + o_st, kSmallPending, n_items);
   const bool kc = (ctx->flags & BV_F_KEY_CACHE) && n_keys;
   uint32_t hits = 0;
   if (kc) hits = bv_kc_lookup(ctx, n_keys, b->key_bytes, b->key_off, (uint64_t *)(pin + o_tab));
@@ -1239,17 +1267,38 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   if (rc != BV_OK) return rc;
   const auto t_enq = std::chrono::steady_clock::now();
   if (res->msg_hash && n_msgs) memcpy(res->msg_hash, dig, n_msgs * 32);  // while the device works
-  HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "small batch sync");
+  // Wait for the statuses themselves (each workgroup's one byte, written
+  // last).  The completion event is polled beside them, so a launch that
+  // ends without writing them all (a fault) is an error, never a hang; the
+  // next call on this ctx waits for the event before touching the buffer.
+  uint64_t seen = 0;
+  for (uint64_t spins = 0;; spins++) {
+    while (seen < n_items && stv[seen] != kSmallPending) seen++;
+    if (seen == n_items) break;
+    if ((spins & 255) == 255) {
+      const hipError_t q = hipEventQuery(ctx->ev_done);
+      if (q == hipSuccess) {
+        while (seen < n_items && stv[seen] != kSmallPending) seen++;
+        if (seen < n_items) return bv_fail(ctx, BV_E_LAUNCH, "k_small ended without every status", hipSuccess);
+        break;
+      }
+      if (q != hipErrorNotReady) return bv_fail(ctx, BV_E_LAUNCH, "small batch sync", q);
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
   const auto t_sync = std::chrono::steady_clock::now();
-  const uint8_t *stv = pin + o_st;
-  if (res->status) memcpy(res->status, stv, n_items);
+  if (res->status) memcpy(res->status, (const uint8_t *)stv, n_items);
   if (res->accept_bits) {
     memset(res->accept_bits, 0, (n_items + 63) / 64 * 8);
     for (uint64_t i = 0; i < n_items; i++)
       if (stv[i] == BV_ACCEPT) res->accept_bits[i / 64] |= 1ull << (i % 64);
   }
   bv_timing &t = ctx->timing;
-  t.ms_total = t.ms_verify = elapsed(ev[E_START], ev[E_END]);
+  // (the device span is read from the events once the kernel has ended: at
+  // the next call's wait, or here when it already has)
+  ctx->small_span = ctx->cur + 1;  // read lazily (bv_get_timing / bv_read_small_span)
+  if (hipEventQuery(ctx->ev_done) == hipSuccess) bv_read_small_span(ctx);
   t.key_path = kc && hits ? BV_KCW : 0;
   t.kc_hits = hits;
   t.kc_keys = (uint32_t)ctx->kc_index.size();

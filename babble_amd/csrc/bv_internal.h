@@ -291,6 +291,7 @@ struct bv_ctx {
   uint64_t table_min_items_many = 192;  // the same above kManyKeys keys
   uint64_t k12_min_items = 2048;  // per-batch K12 (not K8) tables from this many items per key
   bool small_stamps = false;      // BV_SMALL_STAMPS=1: print k_small's phase clocks to stderr
+  uint32_t small_span = 0;        // 1 + the slot of a small batch whose device span is not read yet
   uint64_t small_warm_max = 512;  // k_small for batches whose keys are all cached (BV_SMALL_WARM_MAX)
   uint32_t lat_table_keys = 256;  // latency rule: K8 tables for batches of <= 4096 items from up to this many keys (BV_LAT_TABLE_KEYS)
 };
@@ -304,7 +305,8 @@ struct bv_host_call {
   bool direct_in = false;                          // message bytes DMA'd from the caller's pinned buffer
   bool direct_hash = false, direct_status = false;  // results DMA'd into the caller's pinned buffers
 };
-bool bv_is_pinned(const void *p, size_t n);  // [p, p+n) inside one bv_host_alloc block
+bool bv_is_pinned(const void *p, size_t n);
+void bv_read_small_span(bv_ctx *ctx);  // a small batch's device span into ctx->timing (bv_api.cpp)  // [p, p+n) inside one bv_host_alloc block
 
 int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess);
 hipStream_t bv_copy_stream(bv_ctx *ctx);   // the device's copy stream (created on first use; nullptr on failure)

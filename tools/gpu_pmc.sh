@@ -17,5 +17,5 @@ run_pass fetch FETCH_SIZE
 run_pass write WRITE_SIZE
 run_pass valu SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
 run_pass busy SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE
-python3 tools/pmc_summary.py gpurun_out $EV gpurun_out/r04_kverify_pmc.json > gpurun_out/pmc_summary.json
+python3 tools/pmc_summary.py gpurun_out $EV gpurun_out/${ROUND:-r05}_kverify_pmc.json > gpurun_out/pmc_summary.json
 cat gpurun_out/pmc_summary.json

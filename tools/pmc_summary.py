@@ -4,9 +4,12 @@
 
 Reads every gpurun_out/pmc_*/**/*counter_collection.csv, averages each
 counter per dispatch of each kernel, and derives:
-  * hbm_read_bytes  = FETCH_SIZE (KiB) x 1024 x 2   (gfx950 correction: the
-    memory-side counter tallies 128-B requests at 64 B for wide 16-B/lane
-    reads — MI355X_MICROARCH.md §HBM; our table gathers are dwordx4)
+  * hbm_read_bytes  = FETCH_SIZE (KiB) x 1024 x f, f per kernel from the
+    calibration of the kernel's access pattern (profiles/r05_gather_calib.json,
+    tools/ubench_gather.hip): 1.00 for the verify kernels, whose reads are
+    random 64-B table entries (64 B per TCC_EA0_RDREQ: counted exactly), 2.00
+    for the streaming kernels (16 B per lane, 128-B requests tallied at 64 B —
+    MI355X_MICROARCH.md §HBM)
   * hbm_write_bytes = WRITE_SIZE (KiB) x 1024       (exact for wide stores)
   * valu_issue_util = (SQ_INSTS_VALU_INT64 x 5.39 + other SQ_INSTS_VALU x 3.03)
     / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the fraction of SIMD cycles spent
@@ -65,6 +68,15 @@ def load(root: str):
     return vals, dur
 
 
+# FETCH_SIZE correction per kernel access pattern (profiles/r05_gather_calib.json):
+# random 64-B gathers are counted exactly, 16-B/lane streams at half
+GATHER_KERNELS = ("k_verify_g", "k_verify_q", "k_verify_gq", "k_verify_generic", "k_small")
+
+
+def fetch_factor(kernel: str) -> float:
+    return 1.0 if kernel.startswith(GATHER_KERNELS) else 2.0
+
+
 def summarise(root: str) -> dict:
     vals, dur = load(root)
     out = {}
@@ -75,7 +87,8 @@ def summarise(root: str) -> dict:
         t = sum(durs) / len(durs) if durs else None
         e = {"dispatches_per_pass": n_disp, "counters": avg, "avg_duration_s_profiled": t}
         if "FETCH_SIZE" in avg:
-            e["hbm_read_bytes"] = avg["FETCH_SIZE"] * 1024 * 2
+            e["fetch_factor"] = fetch_factor(k)
+            e["hbm_read_bytes"] = avg["FETCH_SIZE"] * 1024 * fetch_factor(k)
         if "WRITE_SIZE" in avg:
             e["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024
         if "hbm_read_bytes" in e and "hbm_write_bytes" in e:
@@ -99,9 +112,17 @@ def kverify(summary: dict, items: int, source: str) -> dict:
     ks = [k for k in summary if k.startswith("k_verify_g") or k.startswith("k_verify_q<12")]
     tot = lambda f: sum(summary[k].get(f, 0.0) for k in ks)  # noqa: E731
     cnt = lambda c: sum(summary[k]["counters"].get(c, 0.0) for k in ks)  # noqa: E731
+    # algorithmic bytes per item: 32 table entries of 64 B (10 G windows +
+    # 22 K12 windows) plus the SoA streams the two kernels read and write
+    # (r, w, digest, pre, item_key, item_msg, key status ~110 B; R_G 132 B +
+    # u12 48 B written by k_verify_g and read back by k_verify_q; status 1 B)
+    table, stream = 32 * 64, 110 + 2 * (132 + 48) + 1
     return {"source": source, "kernels": ks, "items_per_launch": items,
             "hbm_bytes_per_launch": tot("hbm_bytes"), "hbm_read_bytes_uncorrected": cnt("FETCH_SIZE") * 1024,
-            "algorithmic_table_bytes": items * (10 + 22) * 64,  # 10 G (26-bit) + 22 K12 table entries per item
+            "fetch_factor": "1.00 (64-B gathers, profiles/r05_gather_calib.json)",
+            "algorithmic_table_bytes": items * table,
+            "algorithmic_bytes": items * (table + stream),
+            "traffic_over_algorithmic": tot("hbm_bytes") / (items * (table + stream)),
             "valu_wave_insts": cnt("SQ_INSTS_VALU"), "valu_int64_wave_insts": cnt("SQ_INSTS_VALU_INT64"),
             "valu_issue_util": {k: summary[k].get("valu_issue_util") for k in ks}}
 

@@ -47,9 +47,67 @@ __device__ __forceinline__ int32_t divsteps_30_sel(int32_t eta, uint32_t f0, uin
   return eta;
 }
 
-// the inversion with the divsteps variant D (0: modinv.h, 1: selects)
+// Jump divsteps: a table of every 5-divstep transition, indexed by eta
+// (clamped to [-5, 5]: beyond it the next 5 steps take the same decisions),
+// f mod 32 (odd) and g mod 32; entry = int8 (u, v, q, r) with
+// (f5, g5) 2^5 = (u f + v g, q f + r g), and eta5 = s eta + c (s = +-1).
+// 11 x 16 x 32 entries of 8 bytes = 45 KB of LDS, built by the workgroup.
+constexpr int kJumpK = 5;
+constexpr int kJumpEntries = (2 * kJumpK + 1) * 16 * 32;
+__device__ __forceinline__ uint2 jump_entry(int idx) {
+  int eta = idx / 512 - kJumpK;
+  uint32_t f = (((idx >> 5) & 15u) << 1) | 1u, g = idx & 31u;
+  int u = 1, v = 0, q = 0, r = 1, sgn = 1, c = 0;
+  int32_t fi = (int32_t)f, gi = (int32_t)g;
+  for (int i = 0; i < kJumpK; i++) {
+    if (gi & 1) {
+      if (eta < 0) {
+        int t;
+        eta = -eta, sgn = -sgn, c = -c;
+        t = fi, fi = gi, gi = -t;
+        t = u, u = q, q = -t;
+        t = v, v = r, r = -t;
+      }
+      gi += fi, q += u, r += v;
+    }
+    gi >>= 1, u *= 2, v *= 2, eta -= 1, c -= 1;
+  }
+  const uint32_t lo = (uint32_t)(uint8_t)u | ((uint32_t)(uint8_t)v << 8) | ((uint32_t)(uint8_t)q << 16) |
+                      ((uint32_t)(uint8_t)r << 24);
+  const uint32_t hi = (uint32_t)(uint8_t)c | ((sgn < 0 ? 1u : 0u) << 8);
+  return make_uint2(lo, hi);
+}
+
+__device__ __forceinline__ int32_t divsteps_30_jump(int32_t eta, uint32_t f0, uint32_t g0, int32_t t[4],
+                                                    const uint2 *tab) {
+  int32_t U = 1, V = 0, Q = 0, R = 1;
+  int32_t f = (int32_t)f0, g = (int32_t)g0;
+#pragma unroll
+  for (int j = 0; j < 30 / kJumpK; j++) {
+    const int ec = eta < -kJumpK ? -kJumpK : (eta > kJumpK ? kJumpK : eta);
+    const int idx = ((ec + kJumpK) << 9) | ((((uint32_t)f >> 1) & 15u) << 5) | ((uint32_t)g & 31u);
+    const uint2 e = tab[idx];
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(e.x), hi = __builtin_amdgcn_readfirstlane(e.y);
+    const int32_t u = (int8_t)lo, v = (int8_t)(lo >> 8), q = (int8_t)(lo >> 16), r = (int8_t)(lo >> 24);
+    const int32_t c = (int8_t)hi;
+    eta = ((hi >> 8) & 1u ? -eta : eta) + c;
+    const int32_t nf = (int32_t)((uint32_t)u * (uint32_t)f + (uint32_t)v * (uint32_t)g) >> kJumpK;
+    const int32_t ng = (int32_t)((uint32_t)q * (uint32_t)f + (uint32_t)r * (uint32_t)g) >> kJumpK;
+    f = nf, g = ng;
+    const int32_t nU = u * U + v * Q, nV = u * V + v * R, nQ = q * U + r * Q, nR = q * V + r * R;
+    U = nU, V = nV, Q = nQ, R = nR;
+  }
+  t[0] = U;
+  t[1] = V;
+  t[2] = Q;
+  t[3] = R;
+  return eta;
+}
+
+// the inversion with the divsteps variant D (0: modinv.h, 1: selects, 2: jump table)
 template <int D>
-__device__ __forceinline__ void modinv_variant(uint32_t r[8], const uint32_t x[8], const modinfo30 &mi) {
+__device__ __forceinline__ void modinv_variant(uint32_t r[8], const uint32_t x[8], const modinfo30 &mi,
+                                               const uint2 *tab) {
   s30 d, e, f, g;
 #pragma unroll
   for (int i = 0; i < 9; i++) {
@@ -62,8 +120,9 @@ __device__ __forceinline__ void modinv_variant(uint32_t r[8], const uint32_t x[8
   int32_t eta = -1;
   for (;;) {
     int32_t t[4];
-    eta = D ? divsteps_30_sel(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t)
-            : divsteps_30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    eta = D == 2   ? divsteps_30_jump(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t, tab)
+          : D == 1 ? divsteps_30_sel(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t)
+                   : divsteps_30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
     update_de_30(d, e, t, mi);
     update_fg_30(f, g, t);
     int32_t z = 0;
@@ -76,8 +135,15 @@ __device__ __forceinline__ void modinv_variant(uint32_t r[8], const uint32_t x[8
 }
 
 template <int D>
-__global__ void __launch_bounds__(64) k_variant(const uint32_t *__restrict__ xs, int reps, uint32_t *__restrict__ out,
-                                                uint64_t *__restrict__ clk) {
+__global__ void __launch_bounds__(256) k_variant(const uint32_t *__restrict__ xs, int reps, uint32_t *__restrict__ out,
+                                                 uint64_t *__restrict__ clk) {
+  __shared__ uint2 tab[kJumpEntries];
+  const uint64_t b0 = __builtin_amdgcn_s_memtime();
+  if (D == 2) {
+    for (int i = threadIdx.x; i < kJumpEntries; i += blockDim.x) tab[i] = jump_entry(i);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) clk[4] = __builtin_amdgcn_s_memtime() - b0;
   if (threadIdx.x != 0) return;
   modinfo30 mi;
   modinfo_n(mi);
@@ -87,7 +153,7 @@ __global__ void __launch_bounds__(64) k_variant(const uint32_t *__restrict__ xs,
 #pragma unroll
     for (int i = 0; i < 8; i++) x[i] = __builtin_amdgcn_readfirstlane(xs[8 * k + i]);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    modinv_variant<D>(r, x, mi);
+    modinv_variant<D>(r, x, mi, tab);
     c_all += __builtin_amdgcn_s_memtime() - t0;
 #pragma unroll
     for (int i = 0; i < 8; i++) out[8 * k + i] = r[i];
@@ -203,16 +269,20 @@ int main() {
   uint64_t c2[8];
   uint32_t r0[8 * reps], r1[8 * reps];
   for (int rep = 0; rep < 2; rep++) {
-    hipLaunchKernelGGL(k_variant<0>, dim3(1), dim3(64), 0, 0, dx, reps, dout2, dclk2);
+    hipLaunchKernelGGL(k_variant<0>, dim3(1), dim3(256), 0, 0, dx, reps, dout2, dclk2);
     hipMemcpy(r0, dout2, sizeof r0, hipMemcpyDeviceToHost);
-    hipLaunchKernelGGL(k_variant<1>, dim3(1), dim3(64), 0, 0, dx, reps, dout2, dclk2);
+    hipLaunchKernelGGL(k_variant<1>, dim3(1), dim3(256), 0, 0, dx, reps, dout2, dclk2);
     hipMemcpy(r1, dout2, sizeof r1, hipMemcpyDeviceToHost);
+    hipLaunchKernelGGL(k_variant<2>, dim3(1), dim3(256), 0, 0, dx, reps, dout2, dclk2);
   }
+  uint32_t r2[8 * reps];
+  hipMemcpy(r2, dout2, sizeof r2, hipMemcpyDeviceToHost);
   hipMemcpy(c2, dclk2, 64, hipMemcpyDeviceToHost);
-  int diff = 0;
-  for (int i = 0; i < 8 * reps; i++) diff += r0[i] != r1[i];
+  int diff = 0, diff2 = 0;
+  for (int i = 0; i < 8 * reps; i++) diff += r0[i] != r1[i], diff2 += r0[i] != r2[i];
   printf("modinv_var per inversion: divsteps_30_var %.0f clocks, divsteps with select swap %.0f clocks "
-         "(%d differing words)\n", (double)c2[0] / reps, (double)c2[1] / reps, diff);
+         "(%d differing words), jump table %.0f clocks (%d differing words; table build %.0f clocks)\n",
+         (double)c2[0] / reps, (double)c2[1] / reps, diff, (double)c2[2] / reps, diff2, (double)c2[4]);
   printf("modinv_var per inversion (shader clocks): total %.0f  divsteps %.0f  update_de %.0f  update_fg %.0f  "
          "normalize+convert %.0f  outer iterations %.2f\n",
          (double)c[0] / reps, (double)c[1] / reps, (double)c[2] / reps, (double)c[3] / reps, (double)c[4] / reps,
