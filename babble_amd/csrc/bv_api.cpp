@@ -1304,6 +1304,7 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   t.kc_keys = (uint32_t)ctx->kc_index.size();
   t.ms_host = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (stamps) {  // diagnostics: workgroup 0's phase clocks, relative to its start
+    bv_read_small_span(ctx);
     uint64_t h[16];
     HIPCHK(hipMemcpy(h, stamps, sizeof h, hipMemcpyDeviceToHost), BV_E_LAUNCH, "d2h stamps");
     auto us = [&](std::chrono::steady_clock::time_point a) {

@@ -582,6 +582,74 @@ DEV void small_leaf_pairs(const fe &x, const fe &y, bool zero, SmallNode *to, Sm
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __builtin_amdgcn_wave_barrier();
 }
+// s^-1 of one item split over two waves (both run it on the scalar unit).
+// The Bernstein-Yang batches' critical chain is divsteps + the (f, g)
+// update: each batch's 2x2 matrix depends on the new f, g low words only.
+// The (d, e) update of each batch (whose result is needed only at the end)
+// runs on another wave, fed the matrices through an LDS ring.
+constexpr int kSinvRing = 16;
+struct SinvMail {
+  int32_t t[kSinvRing][4];
+  uint32_t produced, consumed, done;  // matrices published / applied; total + 1 once g = 0 (0: running)
+  int32_t f_sign;
+};
+DEV uint32_t lds_acquire(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+DEV void lds_release(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// producer (the s^-1 chain): divsteps and the (f, g) updates
+DEV void sinv_split_fg(SinvMail &mb, const sc &s) {
+  modinfo30 mi;
+  modinfo_n(mi);
+  s30 f, g;
+#pragma unroll
+  for (int i = 0; i < 9; i++) f.v[i] = mi.m[i];
+  s30_from_u256(g, s.v);
+  int32_t eta = -1;
+  uint32_t k = 0;
+  for (;;) {
+    int32_t t[4];
+    eta = divsteps_30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    while (k - lds_acquire(&mb.consumed) >= (uint32_t)kSinvRing) __builtin_amdgcn_s_sleep(1);  // ring full
+#pragma unroll
+    for (int i = 0; i < 4; i++) mb.t[k % kSinvRing][i] = t[i];
+    lds_release(&mb.produced, ++k);
+    update_fg_30(f, g, t);
+    int32_t z = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) z |= g.v[i];
+    if (z == 0) break;
+  }
+  mb.f_sign = f.v[8] >> 31;
+  lds_release(&mb.done, k + 1);
+}
+// consumer: the (d, e) updates, then w = s^-1 R mod N (as sinv_one)
+DEV void sinv_split_de(SinvMail &mb, sc &w) {
+  modinfo30 mi;
+  modinfo_n(mi);
+  s30 d, e;
+#pragma unroll
+  for (int i = 0; i < 9; i++) d.v[i] = 0, e.v[i] = 0;
+  e.v[0] = 1;
+  for (uint32_t k = 0;; k++) {
+    uint32_t done;
+    while (k >= lds_acquire(&mb.produced) && !(done = lds_acquire(&mb.done))) __builtin_amdgcn_s_sleep(1);
+    if (k >= lds_acquire(&mb.produced)) break;  // (done: every matrix applied)
+    int32_t t[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) t[i] = __builtin_amdgcn_readfirstlane(mb.t[k % kSinvRing][i]);
+    update_de_30(d, e, t, mi);
+    lds_release(&mb.consumed, k + 1);
+  }
+  normalize_30(d, __builtin_amdgcn_readfirstlane(mb.f_sign), mi);
+  sc inv, r3, r, one;
+  s30_to_u256(inv.v, d);
+  sc_load_const(r3, SC_R3);
+  sc_mont(r, inv, r3);  // s^-1 R^2 ...
+#pragma unroll
+  for (int k = 0; k < 8; k++) one.v[k] = k == 0 ? 1u : 0u;
+  sc_mont(w, r, one);  // ... s^-1 R
+}
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t *__restrict__ digest_words,
@@ -602,8 +670,12 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
   __shared__ uint32_t sh_w[8], sh_q[16], sh_u1[8], sh_k[8], sh_r[8], sh_s[8], sh_e[8];
   __shared__ uint32_t sh_ks, sh_go, sh_signs, sh_pre;
   __shared__ uint64_t sh_tab;
+  __shared__ SinvMail sh_mail;
+  __shared__ uint32_t sh_sok;
   __shared__ SmallNode sh_a[kSmallLeaves], sh_b[kSmallLeaves / 2 + 1], sh_c[kSmallLeaves / 4 + 2], sh_d[3];
   if (b >= n_items) return;  // (the grid is n_items)
+  if (t == 0) sh_mail.produced = sh_mail.consumed = sh_mail.done = 0;
+  __syncthreads();
   // ---- phase 1 (the inputs live in host memory, read in place: wave 0
   // fetches what phases 2-4 need while s^-1 runs)
   if (lane == 0 && wave == 0) {
@@ -614,14 +686,19 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
     for (int k = 0; k < 8; k++) sh_e[k] = digest_words[8 * (uint64_t)m + k];
     sh_pre = pre ? pre[b] : 0u;
     sh_tab = kc_tabs ? kc_tabs[item_key[b]] : 0;
-  } else if (lane == 0 && wave == 1) {
-    sc s, w;
+  } else if (lane == 0 && wave == 1) {  // s^-1: divsteps and (f, g) (wave 3 applies (d, e))
+    sc s;
     sc_load_be_words(s, s_be + 8 * (uint64_t)b);
 #pragma unroll
     for (int k = 0; k < 8; k++) sh_s[k] = s_be[8 * (uint64_t)b + k];
-    if (s_usable(pre, b, s)) {
-      sinv_one(w, s);
-    } else {
+    const bool ok = s_usable(pre, b, s);
+    sh_sok = ok;
+    if (ok) sinv_split_fg(sh_mail, s);
+    else lds_release(&sh_mail.done, 1);
+  } else if (lane == 0 && wave == 3) {
+    sc w;
+    sinv_split_de(sh_mail, w);
+    if (!__builtin_amdgcn_readfirstlane(sh_sok)) {  // (published before done)
 #pragma unroll
       for (int k = 0; k < 8; k++) w.v[k] = 0;
     }
