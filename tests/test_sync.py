@@ -169,9 +169,12 @@ def test_missing_self_parent_not_found_text():
 @pytest.mark.gpu
 @pytest.mark.parametrize("bad", [None, 33])
 def test_sync_verify_device_equals_host_path(bad):
-    """sync_verify_device (bodies serialized and DAG-hashed ON the device,
-    bv_verify_events) == sync_verify (host bodies, per-level hashing): same
-    bodies, digests, outcomes and first read error."""
+    """sync_verify_device (one bv_verify_events call: the library builds the
+    bodies from wire fields and, for this in-batch DAG, hashes them on the
+    host in topological order with SHA-NI while the device decodes keys and
+    inverts s; the device then verifies) == sync_verify (the mirror's host
+    bodies, per-level hashing): same bodies, digests, outcomes and first read
+    error."""
     import time
 
     from babble_amd.verifier import Verifier
