@@ -77,8 +77,20 @@ def fetch_factor(kernel: str) -> float:
     return 1.0 if kernel.startswith(GATHER_KERNELS) else 2.0
 
 
+def isa_scales() -> dict:
+    """Per-kernel issue-cost scale of the static opcode mix over the
+    two-class model (tools/isa_mix.py -> profiles/r05_isa_mix.json)."""
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r05_isa_mix.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+    return {k: v["issue_scale"] for k, v in d.items() if isinstance(v, dict)}
+
+
 def summarise(root: str) -> dict:
     vals, dur = load(root)
+    scales = isa_scales()
     out = {}
     for k, counters in vals.items():
         avg = {c: sum(d.values()) / len(d) for c, d in counters.items() if d}
@@ -97,6 +109,9 @@ def summarise(root: str) -> dict:
             i64 = avg["SQ_INSTS_VALU_INT64"]
             cyc = i64 * CYC_MAD64 + (avg["SQ_INSTS_VALU"] - i64) * CYC_VALU32
             e["valu_issue_util"] = cyc / (N_CU * 4) / (avg["GRBM_GUI_ACTIVE"] / N_XCD)
+            sc = next((v for name, v in scales.items() if k.startswith(name)), None)
+            if sc is not None:  # with the kernel's measured opcode mix
+                e["valu_issue_util_mix"] = e["valu_issue_util"] * sc
         if "SQ_INSTS_VALU" in avg and t:
             e["valu_wave_insts"] = avg["SQ_INSTS_VALU"]
             e["valu_lane_ops_per_s"] = avg["SQ_INSTS_VALU"] * 64 / t
