@@ -453,6 +453,9 @@ def run(args, world: int, rank: int, local: int, worker) -> None:
             # peak, and VALU issue occupancy with the measured per-class costs
             i64, ivalu = pmc["valu_int64_wave_insts"], pmc["valu_wave_insts"]
             roof["traffic"] = pmc["hbm_bytes_per_launch"]
+            if "traffic_over_algorithmic" in pmc:  # FETCH_SIZE calibrated for the 64-B gathers
+                roof["traffic_over_algorithmic"] = pmc["traffic_over_algorithmic"]
+                roof["traffic_calibration"] = pmc.get("fetch_factor")
             roof["executed_frac"] = i64 * 64 / kv_s / PEAK_IMUL32_PER_S
             roof["valu_issue_frac"] = (i64 * CYC_MAD64 + (ivalu - i64) * CYC_VALU32) / (N_SIMD * 2.4e9 * kv_s)
             roof["pmc_source"] = pmc["source"]
