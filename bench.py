@@ -30,7 +30,12 @@ Rank 0 prints one JSON line.  `value` is the headline above.  Beside it:
   * `cpu_baseline` — the faster of two CPU legs on this host's cores, each on
     a bounded sample of the same batch: the C oracle (oracle/oracle.c, a
     restatement of the Go path) and the OpenSSL libcrypto proxy of SURVEY
-    §8d (oracle/openssl_ref.c); both are reported.
+    §8d (oracle/openssl_ref.c); both are reported;
+  * at N > 1 (bench_multi.py): `concurrent` — every rank's pinned host
+    entries at once (the node's shared host feed), and `group` — the
+    library's own multi-GPU entry, bv_group_verify_batch over all N devices
+    from one process on C3 chunks (one ncclAllGather), run by rank 0's
+    worker process while the other ranks wait at a store barrier.
 """
 from __future__ import annotations
 
