@@ -11,6 +11,15 @@ v_add3, v_perm: ~4.6-4.7 cycles) is busier than the two-class model says.
 
 The mix is static (each unrolled body counted once); for a kernel that is
 one unrolled loop body (k_sha256's compression) it is the dynamic mix.
+Inline-asm lines (the generated field arithmetic) carry no indent in the
+listing and are counted too.
+
+What it showed (round 5): the single-opcode costs do NOT add up in a mixed
+stream.  Weighted by them, k_verify_g / k_verify_q would issue at 1.12-1.13
+(impossible: the mads and carry ops overlap), k_sha256 at 0.89.  So the mix
+model is a diagnostic, not a utilisation; the floor of k_sha256 was settled
+by timing instead: the kernel runs within 2 % of the same compressions with
+the words in registers (profiles/r05_ubench_sha_tp.txt).
 """
 import json
 import os
@@ -64,7 +73,7 @@ def main():
         if body is None:
             out[name] = None
             continue
-        mix = Counter(m.group(1) for x in body if (m := re.match(r"^\s+(v_[a-z0-9_]+)", x)))
+        mix = Counter(m.group(1) for x in body if (m := re.match(r"^\s*(v_[a-z0-9_]+)", x)))  # (inline asm lines carry no indent)
         tot = sum(mix.values())
         weighted, unknown = 0.0, 0
         for op, c in mix.items():

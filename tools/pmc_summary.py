@@ -18,6 +18,9 @@ counter per dispatch of each kernel, and derives:
     instruction, 32-bit VALU 3.03).  On ROCm 7.2 / gfx950 SQ_ACTIVE_INST_VALU
     equals SQ_INSTS_VALU (an instruction count, not quad-cycles), so the
     gfx94x VALUBusy formula over-counts; this one is <= 1 up to noise.
+  * valu_issue_util_mix = valu_issue_util x the kernel's static opcode-mix
+    scale (tools/isa_mix.py): a diagnostic only — single-opcode costs do not
+    add in mixed streams (the verify kernels read 1.12-1.13 on it)
   * valu_insts_per_s (wave instructions x 64 lanes / kernel time)
 Writes nothing itself; bench.py reads profiles/kverify_traffic.json, which is
 this script's output for k_verify_q copied into profiles/.
