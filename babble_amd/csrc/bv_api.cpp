@@ -438,6 +438,7 @@ static int create_impl(bv_ctx *ctx) {
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS_MANY")) ctx->table_min_items_many = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_K12_MIN_ITEMS")) ctx->k12_min_items = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_SMALL_WARM_MAX")) ctx->small_warm_max = (uint64_t)std::max(0, atoi(s));
+  if (const char *s = getenv("BV_SMALL_MAX")) ctx->small_max = (uint64_t)std::max(0, atoi(s));
   if (const char *s = getenv("BV_LAT_TABLE_KEYS")) ctx->lat_table_keys = (uint32_t)atoi(s);
   return BV_OK;
 }
@@ -1165,20 +1166,20 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
 // tables; with the key cache 0.18 ms against 0.47 ms,
 // profiles/r04_small_lat.log).
 // ---------------------------------------------------------------------------
-constexpr uint64_t kSmallItems = 256;       // items (and messages) per small batch
 constexpr uint64_t kSmallMsgLen = 16 << 10;  // longest message (hashed on the host, inside the call)
 constexpr uint8_t kSmallPending = 0xFF;      // status sentinel (statuses are 0..3)
 
-// Small batches: <= 256 items, or up to ctx->small_warm_max (512) items when
-// every well-formed key already has a key-cache table (no item needs the
-// cooperative NAF chain).  k_small costs ~0.18 ms + ~0.6 us per item, the
-// bulk pipeline ~0.5 ms from 512 to 4096 warm items: 512 items 0.34 against
-// 0.48-0.63 ms, 1000 items equal, 2000 items 0.92 against 0.67
-// (profiles/r04_ab_small_warm.log).
+// Small batches: <= ctx->small_max (768) items, or up to ctx->small_warm_max
+// (1024) items when every well-formed key already has a key-cache table (no
+// item needs the doubling chain).  Same-box medians, 4 creators
+// (profiles/r05_ab_small_max.log): cold k_small 0.32 / 0.40 / 0.74 ms at
+// 256 / 512 / 1000 items against 0.72-0.73 ms for the bulk pipeline's K8
+// tables (more creators only lengthen the bulk build); warm 0.14 / 0.18 /
+// 0.29 / 0.52 ms at 256 / 512 / 1000 / 2000 against 0.45-0.70 / 0.52.
 static bool small_batch(bv_ctx *ctx, const bv_batch *b) {
   if (b->n_items == 0) return false;
   const uint64_t n = std::max<uint64_t>(b->n_items, b->n_msgs);
-  if (n > kSmallItems) {
+  if (n > ctx->small_max) {
     if (n > ctx->small_warm_max || !(ctx->flags & BV_F_KEY_CACHE) || b->n_keys == 0 || b->n_keys > kKcMaxBatchKeys)
       return false;
     // the key bytes are read below: only a well-formed batch (the bulk path

@@ -305,26 +305,27 @@ def test_small_batch_kernel_equals_oracle(monkeypatch):
         verifier.close()
 
 
-def test_small_batch_kernel_warm_up_to_512(monkeypatch):
-    """A 500-event batch whose keys all have key-cache tables takes k_small
-    (no per-item NAF chain: BV_SMALL_WARM_MAX, 512); the same batch through
-    the bulk pipeline (limit 256).  Both equal to the oracle, corrupted
-    signatures included."""
+def test_small_batch_kernel_warm_up_to_1024(monkeypatch):
+    """A 1000-event batch whose keys all have key-cache tables takes k_small
+    (no doubling chain: BV_SMALL_WARM_MAX, 1024, above the cold limit
+    BV_SMALL_MAX); the same batch through the bulk pipeline (limits 256).
+    Both equal to the oracle, corrupted signatures included."""
     from babble_amd.verifier import Verifier
 
-    b = synth.events(500, n_creators=6, seed=911)
+    b = synth.events(1000, n_creators=6, seed=911)
     b.r_be[7, 31] ^= 1
     b.s_be[300, 0] ^= 0x40
     keys = [b.key(k) for k in range(b.n_keys)]
-    for limit, small in (("512", True), ("256", False)):
+    for limit, small in (("1024", True), ("256", False)):
         monkeypatch.setenv("BV_SMALL_WARM_MAX", limit)  # read at bv_create
+        monkeypatch.setenv("BV_SMALL_MAX", "256")
         v = Verifier(device=0, flags=native.F_KEY_CACHE)
         try:
             v.register_keys(keys)
             res = check_against_oracle(v, b)
             t = v.timing()
             assert t["key_path"] == 22 and (t["ms_sha256"] == 0) == small  # k_small has no separate hashing span
-            assert int((res.status == 1).sum()) == 498
+            assert int((res.status == 1).sum()) == 998
         finally:
             v.close()
 
