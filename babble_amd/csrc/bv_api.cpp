@@ -39,28 +39,30 @@ constexpr uint64_t kKTableBytes = BV_KTABLE_U32 * 4;
 constexpr uint64_t kK12TableBytes = BV_K12TABLE_U32 * 4;
 constexpr uint64_t kK12SubBytes = BV_K12SUB_U32 * 4;
 constexpr uint64_t kK12PrefixBytes = (uint64_t)BV_K12NWIN * BV_K12ENT * 32;  // one fe per entry
-constexpr uint32_t kBasesPerKey = 22;       // max(K8 16, K12 22, KC 14) bases per key
-// Per-batch K12 (22 lookups per item) or K8 (32) tables: K12 for every
-// table-mode batch above the latency rule's size (kLatTableItems) with at
-// most kMaxK12Keys keys, and for smaller ones from ctx->k12_min_items (2048,
-// BV_K12_MIN_ITEMS) items per key; K8 otherwise (the latency rule's small
-// batches: K8's chain is one launch shorter, 1000-4000 cold events
-// 0.03-0.05 ms).  The cheaper lookups win over K12's larger build at every
-// measured key count, two batches in flight (profiles/r04_ab_k12min*.log):
-// 64 keys, 16k / 125k events 25.2 -> 30.5, 178.5 -> 205.0 M/s; 200 keys,
-// 50k / 200k 39.4 -> 51.0, 136.7 -> 208.0; 1000 keys, 64k / 1M 13.1 -> 19.1
-// (32 items per key), 143.1 -> 217.2.
+constexpr uint64_t kKSubBytes = BV_KSUB_U32 * 4;
+constexpr uint64_t kKPrefixBytes = (uint64_t)BV_KNWIN * (1u << BV_KW) * 32;  // one fe per entry
+constexpr uint32_t kBasesPerKey = 32;       // max(K8 32, K12 22, KC 12) bases per key
+// Per-batch K12 (22 lookups per item) or K8 (32) tables.  K8 entries are
+// chord sums of 4-bit sub-table points (k_table_pair_u, one field inversion
+// per key), so a K8 key costs ~12x less to build than a K12 key; K12's
+// cheaper lookups pay only from ctx->k12_min_items (8192, BV_K12_MIN_ITEMS)
+// items per key, with at most kMaxK12Keys keys.  Same-box A/Bs, two batches
+// in flight (profiles/r05_ab_k8_rule.log): 64 keys 16k / 125k / 1M events
+// K8 34.4 / 236.6 / 438.0 against K12 31.1 / 213.8 / 489.4 M/s; 200 keys
+// 50k / 200k / 1M 98.3 / 302.1 / 426.6 against 53.5 / 213.5 / 416.1;
+// 1000 keys 1M 348.0 against 222.7.
 constexpr uint32_t kMaxTableKeys = 8192;       // K8: 4 GiB of key tables
 constexpr uint32_t kMaxK12Keys = 1024;         // K12: 2.8 GiB
-// Table or generic: the per-batch build costs ~3.3 us per key (K12 and K8,
-// two batches in flight) but serves each item ~8x cheaper than the generic
-// path (~16.5 ns per item, floor ~1.2 ms per batch).  Up to kManyKeys keys
-// the build is inside that floor and tables win from 16 items per key
-// (ctx->table_min_items); above it from 192 (ctx->table_min_items_many):
-// 1000 keys, 64k / 128k events generic 45.9 / 59.1 M/s against K12 19.0 /
-// 37.7; 3000 keys at 192 per key K8 64.5 against 62.6
-// (profiles/r04_ab_generic_vs_tables.log, r04_ab_generic_lat.log).
-constexpr uint32_t kManyKeys = 256;
+// Table or generic: the generic path costs ~16.5 ns per item with a floor
+// of ~1.2 ms per batch; the K8 build grows with the key count.  Up to
+// kManyKeys keys tables win from 8 items per key (ctx->table_min_items;
+// 1000 keys, 8k / 16k / 32k / 128k events: K8 8.7 / 17.0 / 34.0 / 127.0
+// against generic 6.5 / 12.9 / 25.8 / 59.2 M/s), above it from 48
+// (ctx->table_min_items_many; 2000 keys 32 / 64 per key: generic 46.0
+// against 42.8, K8 82.2 against 59.2; 3000 keys 32 / 48 / 64 per key:
+// generic 55.8 / 60.3 / 62.0 against K8 46.6 / 68.3 / 88.4;
+// profiles/r05_ab_k8_rule.log, r05_ab_k8_rule2.log, r05_ab_k8_chord_1000.log).
+constexpr uint32_t kManyKeys = 1024;
 // Latency rule: a small batch is bound by its longest serial chain, not by
 // total work.  The per-lane generic path runs 128 doublings AND ~128
 // additions in one lane per item (~2.6 ms); the K8 tables cost one wave's
@@ -439,6 +441,8 @@ static int create_impl(bv_ctx *ctx) {
   if (const char *s = getenv("BV_K12_MIN_ITEMS")) ctx->k12_min_items = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_SMALL_WARM_MAX")) ctx->small_warm_max = (uint64_t)std::max(0, atoi(s));
   if (const char *s = getenv("BV_SMALL_MAX")) ctx->small_max = (uint64_t)std::max(0, atoi(s));
+  if (const char *s = getenv("BV_FORCE_K8"))  // (A/B knob: as the BV_F_K8 flag)
+    if (atoi(s) != 0) ctx->flags |= BV_F_K8;
   if (const char *s = getenv("BV_LAT_TABLE_KEYS")) ctx->lat_table_keys = (uint32_t)atoi(s);
   return BV_OK;
 }
@@ -569,8 +573,7 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
                           (n_keys <= ctx->lat_table_keys && n_items <= kLatTableItems && n_items > 0);
   const int key_w = kc ? BV_KCW
                     : !table_mode ? 0
-                    : (n_keys <= kMaxK12Keys && (n_items >= ctx->k12_min_items * n_keys || n_items > kLatTableItems) &&
-                       !(ctx->flags & BV_F_K8))
+                    : (n_keys <= kMaxK12Keys && n_items >= ctx->k12_min_items * n_keys && !(ctx->flags & BV_F_K8))
                         ? 12
                         : 8;
   ctx->table_mode = table_mode;
@@ -580,10 +583,10 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
     if (!kc) {
       const uint64_t nk = std::max<uint32_t>(n_keys, 1);
       HIPCHK(ctx->S().bases_jac.ensure(nk * kBasesPerKey * 96ull), BV_E_OOM, "alloc bases");
-      if (key_w == 12) {
-        HIPCHK(ctx->S().key_sub.ensure(nk * kK12SubBytes), BV_E_OOM, "alloc key sub-tables");
-        HIPCHK(ctx->S().key_pscr.ensure(nk * kK12PrefixBytes), BV_E_OOM, "alloc key prefix scratch");
-      }
+      HIPCHK(ctx->S().key_sub.ensure(nk * (key_w == 12 ? kK12SubBytes : kKSubBytes)), BV_E_OOM,
+             "alloc key sub-tables");
+      HIPCHK(ctx->S().key_pscr.ensure(nk * (key_w == 12 ? kK12PrefixBytes : kKPrefixBytes)), BV_E_OOM,
+             "alloc key prefix scratch");
       HIPCHK(ctx->S().key_table.ensure(nk * (key_w == 12 ? kK12TableBytes : kKTableBytes)), BV_E_OOM,
              "alloc key tables");
     }

@@ -287,9 +287,9 @@ struct bv_ctx {
   // small host batches through k_small (BV_SMALL=0: the bulk pipeline)
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
   bool ev_split_verify = true, small_path = true;
-  uint64_t table_min_items = 16;   // per-batch tables (not the generic path) from this many items per key
-  uint64_t table_min_items_many = 192;  // the same above kManyKeys keys
-  uint64_t k12_min_items = 2048;  // per-batch K12 (not K8) tables from this many items per key
+  uint64_t table_min_items = 8;    // per-batch tables (not the generic path) from this many items per key
+  uint64_t table_min_items_many = 48;  // the same above kManyKeys keys
+  uint64_t k12_min_items = 8192;  // per-batch K12 (not K8) tables from this many items per key
   bool small_stamps = false;      // BV_SMALL_STAMPS=1: print k_small's phase clocks to stderr
   uint32_t small_span = 0;        // 1 + the slot of a small batch whose device span is not read yet
   uint64_t small_max = 768;       // k_small for batches of at most this many items and messages (BV_SMALL_MAX)

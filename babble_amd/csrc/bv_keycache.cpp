@@ -41,7 +41,7 @@
 namespace {
 constexpr uint64_t kKcTableBytes = BV_KCTABLE_U32 * 4;  // 805 MB per cached key
 constexpr uint64_t kKcSubBytes = BV_KCSUB_U32 * 4;
-constexpr uint32_t kKcBases = 22;       // bases_jac stride (bv_api.cpp kBasesPerKey)
+constexpr uint32_t kKcBases = 22;       // bases_jac allocation per key (>= BV_KCNSUB)
 constexpr uint32_t kKcBuildGroup = 8;   // keys per KC build launch (pscr: 403 MB per key)
 constexpr size_t kKcMemoMax = 4096;     // entries of kc_seen / kc_bad
 

@@ -43,6 +43,9 @@
 #define BV_KNWIN 16      //   x 16 windows (128 bits) x 256 entries
 #define BV_KHALF_U32 ((uint64_t)BV_KNWIN * (1ull << BV_KW) * BV_ENTRY_U32)
 #define BV_KTABLE_U32 (2 * BV_KHALF_U32)
+#define BV_KL 4          // K8 sub-table bits: S_k[x] = x 2^(4k) Q, x < 16
+#define BV_KNSUB 32      //   k < 32; entry (j, d) = S_2j[d mod 16] + S_2j+1[d / 16]
+#define BV_KSUB_U32 ((uint64_t)BV_KNSUB * (1ull << BV_KL) * BV_ENTRY_U32)
 #define BV_K12W 12       // K12 window bits
 #define BV_K12NWIN 11    //   x 11 windows (132 bits; the top one holds 8)
 #define BV_K12L 6        // K12 sub-table bits: S_k[x] = x 2^(6k) Q, x < 64

@@ -135,24 +135,68 @@ __global__ void __launch_bounds__(64) k_table_bases_coop(uint32_t n_bases, const
   coop_bases_one(b, bxy, bases_jac, w, nwin);
 }
 
-// blockDim = BLOCK (<= 2^W), grid (NWIN * 2^W/BLOCK, n_bases).  Block (j, c)
-// computes entries d = BLOCK c + t of window j and normalises them to
-// affine with one field inversion (prefix/suffix products in LDS).  PHI:
-// also write the phi(T) half of a GLV key table.
+// Montgomery batch inversion over a block of N threads, one non-zero value
+// each: an in-place binary product tree in LDS (heap order; T holds 2N - 1
+// elements, the leaves at N - 1 + t).  N - 1 products up, ONE field
+// inversion at the root (thread 0), 2N - 2 products down (a child's inverse
+// is its parent's inverse times its sibling): ~3 products per thread where a
+// prefix / suffix scan of the block spends 16, in 2 log2(N) levels.
+// v <- v^-1.
+template <int N>
+__device__ __forceinline__ void block_inverse(fe *T, fe &v, uint32_t t) {
+  static_assert((N & (N - 1)) == 0, "power of two");
+  T[N - 1 + t] = v;
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t n = N / 2; n >= 1; n >>= 1) {  // nodes n-1 .. 2n-2 from their children
+    if (t < n) {
+      const uint32_t p = n - 1 + t;
+      fe a = T[2 * p + 1], b = T[2 * p + 2], r;
+      fe_mul(r, a, b);
+      T[p] = r;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    fe x, root = T[0];
+    fe_inv_var(x, root);
+    T[0] = x;
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t n = 1; n < N; n <<= 1) {  // the 2n nodes 2n-1 .. 4n-2
+    const uint32_t c = 2 * n - 1 + t;
+    fe r;
+    if (t < 2 * n) {
+      fe a = T[(c - 1) / 2], b = T[(c & 1u) ? c + 1 : c - 1];
+      fe_mul(r, a, b);
+    }
+    __syncthreads();
+    if (t < 2 * n) T[c] = r;
+    __syncthreads();
+  }
+  v = T[N - 1 + t];
+}
+
+// blockDim = BLOCK, grid (NWIN * 2^W / BLOCK, n_bases).  Thread t of block c
+// computes the entry f = BLOCK c + t of the key's flat (window, digit) list
+// — window j = f / 2^W, digit d = f mod 2^W; a block spans part of one
+// window or (BLOCK > 2^W: the K8 sub-tables) several — and the block
+// normalises its entries to affine with one field inversion (prefix/suffix
+// products in LDS).  PHI: also write the phi(T) half of a GLV key table.
 template <int W, int NWIN, bool PHI, int BLOCK = 256, bool LAT = true>
 __global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict__ bases_jac,
                                                       const uint8_t *__restrict__ bstatus,
                                                       uint32_t *__restrict__ table) {
-  constexpr uint32_t chunks = (1u << W) / BLOCK;
+  static_assert(((NWIN << W) % BLOCK) == 0, "blocks cover whole keys");
   constexpr uint64_t half_u32 = (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
   const uint32_t b = blockIdx.y;
-  const uint32_t j = blockIdx.x / chunks;
-  const uint32_t d = (blockIdx.x % chunks) * BLOCK + threadIdx.x;
+  const uint32_t f = blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t j = f >> W;
+  const uint32_t d = f & ((1u << W) - 1u);
   const uint32_t t = threadIdx.x;
   if (bstatus && bstatus[b] != KS_OK) return;  // uniform per block
-  __shared__ fe sPre[BLOCK];
-  __shared__ fe sSuf[BLOCK];
-  __shared__ fe sInvTotal;
+  __shared__ fe sT[2 * BLOCK - 1];
   // The base B = (X, Y, Z) stays Jacobian: (X, Y) is an affine point of the
   // isomorphic curve y^2 = x^3 + 7 Z^6, and the a = 0 doubling / mixed-add
   // formulas never use b, so d (X, Y) computed there as (X', Y', Z') is
@@ -167,27 +211,8 @@ __global__ void __launch_bounds__(BLOCK) k_table_fill(const uint32_t *__restrict
   fe Z;
   table_point<LAT>(R, inf, Z, bx, by, d, W);
   if (!inf) fe_mul(Z, Z, bz);
-  sPre[t] = Z;
-  sSuf[t] = Z;
-  __syncthreads();
-  for (uint32_t s = 1; s < BLOCK; s <<= 1) {
-    fe p = sPre[t], q = sSuf[t];
-    if (t >= s) fe_mul(p, p, sPre[t - s]);
-    if (t + s < BLOCK) fe_mul(q, q, sSuf[t + s]);
-    __syncthreads();
-    sPre[t] = p;
-    sSuf[t] = q;
-    __syncthreads();
-  }
-  if (t == 0) {
-    fe x;
-    fe_inv_var(x, sPre[BLOCK - 1]);
-    sInvTotal = x;
-  }
-  __syncthreads();
-  fe zi = sInvTotal;  // Z_t^-1 = prefix(t-1) * suffix(t+1) * (prod Z)^-1
-  if (t > 0) fe_mul(zi, zi, sPre[t - 1]);
-  if (t < BLOCK - 1) fe_mul(zi, zi, sSuf[t + 1]);
+  fe zi = Z;
+  block_inverse<BLOCK>(sT, zi, t);  // Z_t^-1
   uint32_t *entry = table + (uint64_t)b * (PHI ? 2 : 1) * half_u32 + (((uint64_t)j << W) + d) * BV_ENTRY_U32;
   table_store(entry, PHI ? entry + half_u32 : nullptr, d, R, inf, zi);
 }
@@ -215,7 +240,7 @@ __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__
   const int live_bits = 128 - W * (int)j;
   const uint32_t e_live = live_bits >= W - 1 ? E : ((1u << live_bits) + 1u + 255u) / 256u;
   __shared__ uint32_t sLo[NS * BV_ENTRY_U32], sHi[NS * BV_ENTRY_U32];
-  __shared__ fe sPre[256], sSuf[256], sInv;
+  __shared__ fe sT[511];
   const uint32_t *sk = sub + ((uint64_t)b * 2 * NWIN + 2 * j) * NS * BV_ENTRY_U32;
   for (uint32_t x = t; x < NS * BV_ENTRY_U32; x += 256) {
     sLo[x] = sk[x];
@@ -235,27 +260,8 @@ __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__
     ps[(2 * e + 1) * 256] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
     fe_mul(acc, acc, H);
   }
-  sPre[t] = acc;
-  sSuf[t] = acc;
-  __syncthreads();
-  for (uint32_t s = 1; s < 256; s <<= 1) {
-    fe p = sPre[t], q = sSuf[t];
-    if (t >= s) fe_mul(p, p, sPre[t - s]);
-    if (t + s < 256) fe_mul(q, q, sSuf[t + s]);
-    __syncthreads();
-    sPre[t] = p;
-    sSuf[t] = q;
-    __syncthreads();
-  }
-  if (t == 0) {
-    fe x;
-    fe_inv_var(x, sPre[255]);
-    sInv = x;
-  }
-  __syncthreads();
-  fe q = sInv;  // (this thread's product)^-1 = prefix(t-1) * suffix(t+1) * total^-1
-  if (t > 0) fe_mul(q, q, sPre[t - 1]);
-  if (t < 255) fe_mul(q, q, sSuf[t + 1]);
+  fe q = acc;
+  block_inverse<256>(sT, q, t);  // (this thread's product)^-1
   uint32_t *base = table + (uint64_t)b * 2 * half_u32 + (uint64_t)j * ENT * BV_ENTRY_U32;
 #pragma unroll 1
   for (int e = (int)e_live - 1; e >= 0; e--) {
@@ -274,6 +280,70 @@ __global__ void __launch_bounds__(256) k_table_pair(const uint32_t *__restrict__
   }
 }
 
+// K8 key tables from the 4-bit sub-tables: one block of 256
+// threads per WPB windows of a key; thread t builds digit d = t = lo + 16 hi
+// of each of its windows j as the affine chord S_2j[lo] + S_2j+1[hi] (the
+// two are never equal or opposite: lo < 16 <= 16 hi), and the block's chord
+// denominators are inverted with ONE field inversion: per-thread running
+// products (their prefixes in `pscr`, coalesced), then block_inverse.
+// Replaces the per-entry double-and-add of k_table_fill<8, 16, true> (~12
+// point operations and a 256-entry inversion share per entry) with one
+// affine addition; digit 0 stays the (0, 0) identity.  WPB = 16 (one
+// inversion per key) when many keys fill the chip, 1 when a few keys' latency
+// is the point.  The block's sub-tables are staged in LDS.
+template <int W, int L, int NWIN, int WPB>
+__global__ void __launch_bounds__(256) k_table_pair_u(const uint32_t *__restrict__ sub,
+                                                      const uint8_t *__restrict__ bstatus,
+                                                      uint32_t *__restrict__ table, uint4 *__restrict__ pscr) {
+  constexpr uint32_t NS = 1u << L, SUB_U32 = 2 * WPB * NS * BV_ENTRY_U32;
+  constexpr uint64_t half_u32 = (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
+  static_assert((1u << W) == 256 && W == 2 * L && half_u32 == BV_KHALF_U32 && NWIN % WPB == 0, "K8 geometry");
+  const uint32_t b = blockIdx.y, j0 = blockIdx.x * WPB, t = threadIdx.x;
+  if (bstatus && bstatus[b] != KS_OK) return;
+  __shared__ uint32_t sS[SUB_U32];
+  __shared__ fe sT[511];
+  const uint32_t *sk = sub + ((uint64_t)b * 2 * NWIN + 2 * j0) * NS * BV_ENTRY_U32;
+  for (uint32_t x = t; x < SUB_U32; x += 256) sS[x] = sk[x];
+  __syncthreads();
+  const uint32_t lo = t & (NS - 1), hi = t >> L;
+  const int kind = pair_kind(lo, hi);
+  uint4 *ps = pscr + ((uint64_t)b * NWIN + j0) * 2 * 256 + t;
+  fe acc;
+  fe_set(acc, 1);
+#pragma unroll 1
+  for (uint32_t e = 0; e < WPB; e++) {
+    fe x1, y1, x2, y2, H;
+    pair_load(sS + 2 * e * NS * BV_ENTRY_U32, sS + (2 * e + 1) * NS * BV_ENTRY_U32, lo, hi, x1, y1, x2, y2);
+    pair_denominator(H, kind, x1, x2);
+    if (WPB > 1) {
+      ps[(2 * e) * 256] = make_uint4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
+      ps[(2 * e + 1) * 256] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
+    }
+    fe_mul(acc, acc, H);
+  }
+  fe q = acc;
+  block_inverse<256>(sT, q, t);  // (this thread's product)^-1
+  uint32_t *base = table + (uint64_t)b * 2 * half_u32 + (((uint64_t)j0 << W) + t) * BV_ENTRY_U32;
+#pragma unroll 1
+  for (int e = WPB - 1; e >= 0; e--) {
+    fe x1, y1, x2, y2, H, Hinv;
+    pair_load(sS + 2 * e * NS * BV_ENTRY_U32, sS + (2 * e + 1) * NS * BV_ENTRY_U32, lo, hi, x1, y1, x2, y2);
+    if (WPB > 1) {
+      fe pre;
+      pair_denominator(H, kind, x1, x2);
+      const uint4 p0 = ps[(2 * e) * 256], p1 = ps[(2 * e + 1) * 256];
+      pre.v[0] = p0.x; pre.v[1] = p0.y; pre.v[2] = p0.z; pre.v[3] = p0.w;
+      pre.v[4] = p1.x; pre.v[5] = p1.y; pre.v[6] = p1.z; pre.v[7] = p1.w;
+      fe_mul(Hinv, q, pre);
+      fe_mul(q, q, H);
+    } else {
+      Hinv = q;
+    }
+    uint32_t *entry = base + ((uint64_t)e << W) * BV_ENTRY_U32;
+    pair_store(entry, entry + half_u32, kind, x1, y1, x2, y2, Hinv);
+  }
+}
+
 // Generator table window j from the G sub-tables (geometry.h, signed
 // digits): block c holds slots s = 4096 c + 256 e + t (e < 16) of window j,
 // digit k12_digit(s) (slot 0 builds digit 2^(W-1), which lands in window
@@ -288,7 +358,7 @@ __global__ void __launch_bounds__(256) k_table_pair_g(const uint32_t *__restrict
   const uint32_t c = c0 + blockIdx.x, t = threadIdx.x;
   const uint32_t *s_lo = sub + (uint64_t)(2 * j) * NS * BV_ENTRY_U32;
   const uint32_t *s_hi = s_lo + (uint64_t)NS * BV_ENTRY_U32;
-  __shared__ fe sPre[256], sSuf[256], sInv;
+  __shared__ fe sT[511];
   uint4 *ps = pscr + (uint64_t)blockIdx.x * E * 2 * 256 + t;
   fe acc;
   fe_set(acc, 1);
@@ -302,27 +372,8 @@ __global__ void __launch_bounds__(256) k_table_pair_g(const uint32_t *__restrict
     ps[(2 * e + 1) * 256] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
     fe_mul(acc, acc, H);
   }
-  sPre[t] = acc;
-  sSuf[t] = acc;
-  __syncthreads();
-  for (uint32_t s = 1; s < 256; s <<= 1) {
-    fe p = sPre[t], q = sSuf[t];
-    if (t >= s) fe_mul(p, p, sPre[t - s]);
-    if (t + s < 256) fe_mul(q, q, sSuf[t + s]);
-    __syncthreads();
-    sPre[t] = p;
-    sSuf[t] = q;
-    __syncthreads();
-  }
-  if (t == 0) {
-    fe x;
-    fe_inv_var(x, sPre[255]);
-    sInv = x;
-  }
-  __syncthreads();
-  fe q = sInv;
-  if (t > 0) fe_mul(q, q, sPre[t - 1]);
-  if (t < 255) fe_mul(q, q, sSuf[t + 1]);
+  fe q = acc;
+  block_inverse<256>(sT, q, t);  // (this thread's product)^-1
   uint32_t *base = table + (uint64_t)j * ENT * BV_ENTRY_U32;
 #pragma unroll 1
   for (int e = (int)E - 1; e >= 0; e--) {
@@ -438,7 +489,7 @@ __global__ void __launch_bounds__(256) k_table_pair_kc(const uint32_t *__restric
   if (live_bits < W - 1 && (uint64_t)BV_KCPAIR_ENT * c > (1ull << live_bits) + 1) return;  // uniform per block
   const uint32_t *s_lo = sub + ((uint64_t)b * 2 * NWIN + 2 * j) * NS * BV_ENTRY_U32;
   const uint32_t *s_hi = s_lo + (uint64_t)NS * BV_ENTRY_U32;
-  __shared__ fe sPre[256], sSuf[256], sInv;
+  __shared__ fe sT[511];
   uint4 *ps = pscr + ((uint64_t)b * gridDim.x + blockIdx.x) * E * 2 * 256 + t;
   fe acc;
   fe_set(acc, 1);
@@ -452,27 +503,8 @@ __global__ void __launch_bounds__(256) k_table_pair_kc(const uint32_t *__restric
     ps[(2 * e + 1) * 256] = make_uint4(acc.v[4], acc.v[5], acc.v[6], acc.v[7]);
     fe_mul(acc, acc, H);
   }
-  sPre[t] = acc;
-  sSuf[t] = acc;
-  __syncthreads();
-  for (uint32_t s = 1; s < 256; s <<= 1) {
-    fe p = sPre[t], q = sSuf[t];
-    if (t >= s) fe_mul(p, p, sPre[t - s]);
-    if (t + s < 256) fe_mul(q, q, sSuf[t + s]);
-    __syncthreads();
-    sPre[t] = p;
-    sSuf[t] = q;
-    __syncthreads();
-  }
-  if (t == 0) {
-    fe x;
-    fe_inv_var(x, sPre[255]);
-    sInv = x;
-  }
-  __syncthreads();
-  fe q = sInv;
-  if (t > 0) fe_mul(q, q, sPre[t - 1]);
-  if (t < 255) fe_mul(q, q, sSuf[t + 1]);
+  fe q = acc;
+  block_inverse<256>(sT, q, t);  // (this thread's product)^-1
   uint32_t *base = (uint32_t *)tabs[b] + (uint64_t)j * ENT * BV_ENTRY_U32;
 #pragma unroll 1
   for (int e = (int)E - 1; e >= 0; e--) {
@@ -1094,11 +1126,25 @@ static const bool g_coop_bases = [] {
   return s == nullptr || atoi(s) != 0;
 }();
 
+// K8 for at most this many keys: each entry by its own double-and-add from
+// the 8-bit bases (k_table_fill<8, 16, true>: one launch after the chain,
+// the shortest chain for a few keys); above it the 4-bit sub-tables and
+// chord sums (k_table_pair_u: ~12x less work per key).  Cold latency,
+// 1000 / 4000 events: 4 keys 0.741 / 0.763 ms direct against 0.768 / 0.816
+// chord, 16 keys 0.744 / 0.775 against 0.768 / 0.796, 32 keys equal
+// (profiles/r05_ab_k8_direct.log); 64 keys chord 0.80 against 0.955
+// (r05_ab_k8_lat.log).  BV_K8_DIRECT_KEYS.
+static const uint32_t g_k8_direct_keys = [] {
+  const char *s = getenv("BV_K8_DIRECT_KEYS");
+  return s ? (uint32_t)atoi(s) : 24u;
+}();
+
 hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus,
                         uint32_t *bases_jac, uint32_t *sub, uint32_t *pscr, uint32_t *table, uint64_t n_items) {
+  const bool k8_direct = kw == 8 && n_bases <= g_k8_direct_keys;
   if (n_bases == 0) return hipSuccess;
-  const int w = kw == 0 ? BV_GL : kw == 8 ? BV_KW : BV_K12L;
-  const int nwin = kw == 0 ? BV_GNSUB : kw == 8 ? BV_KNWIN : BV_K12NSUB;
+  const int w = kw == 0 ? BV_GL : kw == 8 ? (k8_direct ? BV_KW : BV_KL) : BV_K12L;
+  const int nwin = kw == 0 ? BV_GNSUB : kw == 8 ? (k8_direct ? BV_KNWIN : BV_KNSUB) : BV_K12NSUB;
   // K12 (large batches) builds beside the bulk kernels on a busy chip, where
   // a kernel's VGPR footprint decides when its waves get a SIMD: there the
   // throughput point ops (fewer VGPRs) win; elsewhere the zipped ones.
@@ -1132,15 +1178,32 @@ hipError_t build_tables(hipStream_t st, int kw, uint32_t n_bases, const uint32_t
         if (e != hipSuccess) return e;
       }
     }
+  } else if (k8_direct) {
+    hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
+                       dim3(256), 0, st, bases_jac, bstatus, table);
   } else if (kw == 8) {
-    // (as K12: the throughput point ops above the latency range; 3000 keys,
-    // 144k-576k events 10.3 -> 17.9, 38.4 -> 64.5 M/s, r04_ab_k8_fill.log)
-    if (lat_variant(n_items))
-      hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true>), dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases),
-                         dim3(256), 0, st, bases_jac, bstatus, table);
+    // 4-bit sub-tables (16 per block of 256: one inversion per block), then
+    // the chord sums.  The zipped point ops only for few keys and a small
+    // batch: their VGPRs allow 2 blocks per CU, and 1000 keys' 2000 blocks
+    // then take 4 rounds (0.55 ms per fill)
+    constexpr uint32_t fill_blocks = (BV_KNSUB << BV_KL) / 256u;
+    if (lat_variant(n_items) && n_bases <= 256)
+      hipLaunchKernelGGL((k_table_fill<BV_KL, BV_KNSUB, false, 256, true>), dim3(fill_blocks, n_bases), dim3(256), 0,
+                         st, bases_jac, bstatus, sub);
     else
-      hipLaunchKernelGGL((k_table_fill<BV_KW, BV_KNWIN, true, 256, false>),
-                         dim3(BV_KNWIN * ((1u << BV_KW) / 256u), n_bases), dim3(256), 0, st, bases_jac, bstatus, table);
+      hipLaunchKernelGGL((k_table_fill<BV_KL, BV_KNSUB, false, 256, false>), dim3(fill_blocks, n_bases), dim3(256), 0,
+                         st, bases_jac, bstatus, sub);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (n_bases <= 64)  // latency: 16 blocks (one inversion each) per key
+      hipLaunchKernelGGL((k_table_pair_u<BV_KW, BV_KL, BV_KNWIN, 1>), dim3(BV_KNWIN, n_bases), dim3(256), 0, st, sub,
+                         bstatus, table, (uint4 *)pscr);
+    else if (n_bases <= 256)
+      hipLaunchKernelGGL((k_table_pair_u<BV_KW, BV_KL, BV_KNWIN, 4>), dim3(BV_KNWIN / 4, n_bases), dim3(256), 0, st, sub,
+                         bstatus, table, (uint4 *)pscr);
+    else  // throughput: one inversion per key
+      hipLaunchKernelGGL((k_table_pair_u<BV_KW, BV_KL, BV_KNWIN, BV_KNWIN>), dim3(1, n_bases), dim3(256), 0, st, sub,
+                         bstatus, table, (uint4 *)pscr);
   } else {
     if (lat & 2)
       hipLaunchKernelGGL((k_table_fill<BV_K12L, BV_K12NSUB, false, 1 << BV_K12L, true>), dim3(BV_K12NSUB, n_bases),

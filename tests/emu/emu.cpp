@@ -120,9 +120,18 @@ void emu_pair_chunk(const uint32_t *s_lo, const uint32_t *s_hi, uint32_t L, uint
 void emu_build_tables(int kw, uint32_t n_bases, const uint32_t *bxy, const uint8_t *bstatus, uint32_t *table,
                       int nt) {
   std::vector<uint32_t> bases;
-  if (kw == 8) {
-    emu_bases(n_bases, bxy, bstatus, bases, BV_KW, BV_KNWIN, nt);
-    emu_fill(n_bases, bstatus, bases.data(), BV_KW, BV_KNWIN, true, 256, table, nt);
+  if (kw == 8) {  // 4-bit sub-tables, then k_table_pair_u's chord sums (one block per window and key)
+    emu_bases(n_bases, bxy, bstatus, bases, BV_KL, BV_KNSUB, nt);
+    std::vector<uint32_t> sub((size_t)n_bases * BV_KSUB_U32 + 16);
+    emu_fill(n_bases, bstatus, bases.data(), BV_KL, BV_KNSUB, false, 1u << BV_KL, sub.data(), nt);
+    constexpr uint32_t NS = 1u << BV_KL;
+    parallel_for((uint64_t)n_bases * BV_KNWIN, nt, [&](uint64_t task) {
+      const uint32_t b = (uint32_t)(task / BV_KNWIN), j = (uint32_t)(task % BV_KNWIN);
+      if (bstatus && bstatus[b] != KS_OK) return;
+      const uint32_t *s_lo = sub.data() + ((uint64_t)b * BV_KNSUB + 2 * j) * NS * BV_ENTRY_U32;
+      uint32_t *base = table + (uint64_t)b * BV_KTABLE_U32 + ((uint64_t)j << BV_KW) * BV_ENTRY_U32;
+      emu_pair_chunk(s_lo, s_lo + NS * BV_ENTRY_U32, BV_KL, 0, 1u << BV_KW, base, BV_KHALF_U32);
+    });
     return;
   }
   if (kw == 0) {

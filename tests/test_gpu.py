@@ -100,10 +100,10 @@ def test_c4_adversarial_mix(verifier, device_api):
 
 def test_c4_adversarial_full_rate(verifier):
     """C4 at 10^5 items with the exact per-million corruption mix (~70 keys,
-    ~1.4k items per key: the K12 tables)."""
+    ~1.4k items per key: the K8 chord-sum tables)."""
     b = synth.adversarial(100_000, seed=44)
     check_against_oracle(verifier, b)
-    assert verifier.timing()["key_path"] == 12
+    assert verifier.timing()["key_path"] == 8
 
 
 def test_k8_tables_many_keys(monkeypatch):
@@ -123,21 +123,22 @@ def test_k8_tables_many_keys(monkeypatch):
 
 
 def test_generic_path_many_keys_few_items(verifier):
-    """More than 256 keys with fewer than 192 items each: the generic
+    """More than 1024 keys with fewer than 48 items each: the generic
     per-lane path, at 40k items (throughput variant) and 20k (latency)."""
     for n in (40_000, 20_000):
         b = synth.adversarial(n, seed=47, n_creators=1100, scale_per_million=MIX)
-        assert b.n_keys > 256 and b.n_items < 192 * b.n_keys
+        assert b.n_keys > 1024 and b.n_items < 48 * b.n_keys
         check_against_oracle(verifier, b)
         assert verifier.timing()["key_path"] == 0
 
 
-def test_k12_tables_many_keys_few_items(verifier):
-    """200 keys with ~300 items each (above the latency rule's size): K12."""
+def test_k8_tables_many_keys_few_items(verifier):
+    """200 keys with ~300 items each (above the latency rule's size, below
+    K12's 8192 items per key): the K8 chord-sum tables."""
     b = synth.adversarial(60_000, seed=46, n_creators=200, scale_per_million=MIX)
-    assert b.n_items > 4096 and b.n_items < 2048 * b.n_keys
+    assert b.n_items > 4096 and b.n_items < 8192 * b.n_keys
     check_against_oracle(verifier, b)
-    assert verifier.timing()["key_path"] == 12
+    assert verifier.timing()["key_path"] == 8
 
 
 def test_c4_adversarial_1m(verifier):
@@ -153,8 +154,9 @@ def test_c4_adversarial_1m(verifier):
 
 
 def test_k12_tables_adversarial(verifier):
-    """>= 2048 items per key: 12-bit key tables (sub-table chord sums)."""
-    b = synth.adversarial(120_000, seed=12, n_creators=16, scale_per_million=MIX)
+    """>= 8192 items per key: 12-bit key tables (sub-table chord sums)."""
+    b = synth.adversarial(120_000, seed=12, n_creators=8, scale_per_million=MIX)
+    assert b.n_items >= 8192 * b.n_keys
     check_against_oracle(verifier, b)
     assert verifier.timing()["key_path"] == 12
 
@@ -171,7 +173,7 @@ def test_host_entry_item_order(monkeypatch):
 
     monkeypatch.setenv("BV_HOST_CHUNK_MB", "8")  # read at bv_create
     verifier = Verifier(device=0)
-    b = synth.adversarial(120_000, seed=13, n_creators=16, scale_per_million=MIX)
+    b = synth.adversarial(120_000, seed=13, n_creators=8, scale_per_million=MIX)
     assert np.all(np.diff(b.item_msg.astype(np.int64)) >= 0)
     check_against_oracle(verifier, b)
     rng = np.random.default_rng(13)
@@ -209,7 +211,7 @@ def test_throughput_variants_above_latency_threshold(verifier):
     """Batches of <= 128k items take the verify kernels' latency variants
     (zipped point ops), larger ones the throughput variants: just above the
     threshold (a ragged last word), the C4 mix, K12 tables, bit-exact."""
-    b = synth.adversarial(131_072 + 64 + 5, seed=14, n_creators=16, scale_per_million=MIX)
+    b = synth.adversarial(131_072 + 64 + 5, seed=14, n_creators=8, scale_per_million=MIX)
     check_against_oracle(verifier, b)
     assert verifier.timing()["key_path"] == 12
 
@@ -228,10 +230,10 @@ def test_k8_tables_forced_by_flag():
 
 
 def test_generic_path_few_items_per_key(verifier):
-    """Keys with fewer than 16 items each take the per-lane path once the
+    """Keys with fewer than 8 items each take the per-lane path once the
     batch is past the latency rule (> 4096 items or > 256 keys)."""
-    b = synth.adversarial(6000, seed=9, n_creators=512, scale_per_million=MIX)
-    assert 4096 < b.n_items < 16 * b.n_keys
+    b = synth.adversarial(6000, seed=9, n_creators=1000, scale_per_million=MIX)
+    assert 4096 < b.n_items < 8 * b.n_keys and b.n_keys <= 1024
     check_against_oracle(verifier, b)
     assert verifier.timing()["key_path"] == 0
 
