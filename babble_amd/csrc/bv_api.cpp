@@ -435,6 +435,9 @@ static int create_impl(bv_ctx *ctx) {
   }
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
   if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
+  if (const char *s = getenv("BV_QFIRST")) ctx->qfirst = atoi(s) != 0;
+  if (const char *s = getenv("BV_EV_D2H")) ctx->ev_d2h = atoi(s);
+  if (const char *s = getenv("BV_EV_TAIL")) ctx->ev_tail = atoi(s) != 0;
   if (const char *s = getenv("BV_SMALL_STAMPS")) ctx->small_stamps = atoi(s) != 0;
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS")) ctx->table_min_items = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS_MANY")) ctx->table_min_items_many = (uint64_t)std::max(1, atoi(s));
@@ -685,8 +688,41 @@ int bv_launch_items(bv_ctx *ctx, const bv_batch *b, const bv_out &o, hipStream_t
   return BV_OK;
 }
 
+int bv_item_pipe::key_part(hipStream_t ks, hipEvent_t ready) {
+  if (!ctx->table_mode || !ctx->qfirst || b->n_items == 0) return BV_OK;
+  hipEvent_t *ev = ctx->S().ev;
+  HIPCHK(hipStreamWaitEvent(ks, ev[E_SINV], 0), BV_E_LAUNCH, "join");
+  HIPCHK(hipStreamWaitEvent(ks, ready, 0), BV_E_LAUNCH, "join");
+  HIPCHK(hipStreamWaitEvent(ks, ev[E_KEYS], 0), BV_E_LAUNCH, "join");
+  if (kc && ks != ctx->stream) {  // kc_tabs (and any KC build) enqueued on ctx->stream by bv_kc_prepare
+    HIPCHK(hipEventRecord(ev[E_KCTAB], ctx->stream), BV_E_LAUNCH, "event");
+    HIPCHK(hipStreamWaitEvent(ks, ev[E_KCTAB], 0), BV_E_LAUNCH, "join");
+  }
+  HIPCHK(hipEventRecord(ev[E_SCALAR], ks), BV_E_LAUNCH, "event");  // ms_verify_g: the key part
+  HIPCHK(hipEventRecord(ev[E_JOINED], ks), BV_E_LAUNCH, "event");  // ms_verify: key part to the last decision
+  const uint64_t n = b->n_items;
+  HIPCHK(bvk::verify_qf(ks, ctx->key_w, n, 0, n, b->item_key, (const uint32_t *)b->r_be, (const uint32_t *)b->s_be,
+                        b->pre, ctx->S().kstatus.as<uint8_t>(), ctx->S().scratch.as<uint32_t>(),
+                        ctx->S().key_table.as<uint32_t>(), kc ? ctx->S().kc_tabs.as<uint64_t>() : nullptr,
+                        ctx->S().rg.as<uint32_t>()),
+         BV_E_LAUNCH, "k_verify_qf");
+  HIPCHK(hipEventRecord(ev[E_G], ks), BV_E_LAUNCH, "event");
+  qf = true;
+  return BV_OK;
+}
+
 int bv_item_pipe::upto(uint64_t end) {
   if (end <= done) return BV_OK;
+  if (qf) {  // the key part is in rg: u1 G and the decision
+    const uint64_t n = b->n_items;
+    if (done == 0) HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_G], 0), BV_E_LAUNCH, "join key part");
+    HIPCHK(bvk::verify_gf(st, n, done, end, b->item_key, (const uint32_t *)b->r_be, (const uint32_t *)b->s_be, b->pre,
+                          ctx->S().kstatus.as<uint8_t>(), b->item_msg, o.dig, ctx->S().scratch.as<uint32_t>(),
+                          ctx->g_table, ctx->S().rg.as<uint32_t>(), o.status, o.bits),
+           BV_E_LAUNCH, "k_verify_gf");
+    done = end;
+    return BV_OK;
+  }
   if (done == 0) {
     HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SINV], 0), BV_E_LAUNCH, "join");
     HIPCHK(hipEventRecord(ctx->S().ev[E_SCALAR], st), BV_E_LAUNCH, "event");
@@ -1034,6 +1070,10 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
                         });
   bv_item_pipe pipe{ctx, &d, {}, st, kc};
   rc = bv_out_bufs(ctx, &d, nullptr, nullptr, nullptr, true, &pipe.o);
+  if (rc != BV_OK) return rc;
+  // the key part of every item (R_Q) on the s^-1 stream once r and the item
+  // keys are in: it needs no digest, so it runs under the message transfer
+  rc = pipe.key_part(ctx->sstream, ctx->S().ev[E_SMALL]);
   if (rc != BV_OK) return rc;
 
   // message bytes: chunks on message boundaries, each hashed once it lands

@@ -32,6 +32,7 @@ namespace {
 // chunk = 8.6-9.0 / 7.8-8.3 / 7.25-7.5 / 7.7 / 7.7-8.2 ms per call from
 // pinned arrays, tools/events_prof.py)
 constexpr size_t kChunk = 64ull << 20;
+constexpr uint64_t kEvTailMin = 65536;  // events: the smallest chunk the halving tail splits off
 
 int validate(bv_ctx *ctx, const bv_event_batch *b) {
   const uint64_t n = b->n_events;
@@ -283,10 +284,17 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   const size_t o_s = add(eb->s_be, n * 32, ALL);
   const size_t o_pre = add(eb->pre, eb->pre ? n : 0, ALL);
   const size_t s_end = total;
+  // key part first (ctx->qfirst): r and the creators cross before the
+  // chunks, so every item's k1 Q + k2 phi(Q) is summed under the transfer
+  // of the bodies and only u1 G waits for each chunk's digests
+  const bool qf = ctx->qfirst;
+  const size_t o_r = qf ? add(eb->r_be, n * 32, ALL) : 0;
+  const size_t o_cr = qf ? add(eb->creator, n * 4, ALL) : 0;
+  const size_t r_end = total;
   const size_t o_ph = add(eb->parent_hashes, eb->parent_hashes ? eb->n_parent_hashes * 32 : 0, ALL);
   const size_t small_end = total;
-  const size_t o_r = add(eb->r_be, n * 32, EV, 32);
-  const size_t o_cr = add(eb->creator, n * 4, EV, 4);
+  const size_t o_r_ev = qf ? o_r : add(eb->r_be, n * 32, EV, 32);
+  const size_t o_cr_ev = qf ? o_cr : add(eb->creator, n * 4, EV, 4);
   const size_t o_ix = add(eb->index, n * 8, EV, 8);
   const size_t o_ts = add(eb->timestamp, n * 8, EV, 8);
   const size_t o_pk = add(eb->parent_kind, n * 2, EV, 2);
@@ -318,12 +326,24 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
 
   // event chunks of ~kChunk staged bytes (whole 256-event groups, so each
   // chunk's items fill whole words of the accept bitmask)
+  // chunks: at most ~ev_chunk bytes; with ev_tail (BV_EV_TAIL=1), each
+  // takes at most half of what is left (down to kEvTailMin events), so the
+  // last chunk to land, whose hashing and verify are the call's tail, is
+  // small.  Not the default: each chunk costs one DMA command per wire
+  // field, and equal chunks measured 5.18-5.26 ms per 1M pinned events
+  // against 5.37-5.39 (profiles/r05_ab_ev_qfirst.log)
   std::vector<uint64_t> cb{0};
   const uint64_t chunk_bytes = ctx->ev_chunk;  // 0 = one chunk (A/B knob, bv_create)
   if (chunk_bytes > 0) {
     const uint64_t per_ev = std::max<uint64_t>(1, (total - small_end) / n);
     const uint64_t per = std::max<uint64_t>(256, chunk_bytes / per_ev / 256 * 256);
-    for (uint64_t e = per; e < n; e += per) cb.push_back(e);
+    for (uint64_t e = 0; e < n;) {
+      uint64_t c = per;
+      if (ctx->ev_tail) c = std::min(per, ((n - e) / 2 + 255) / 256 * 256);
+      if (n - e <= c || (ctx->ev_tail && n - e - c < kEvTailMin)) break;
+      e += c;
+      cb.push_back(e);
+    }
   }
   cb.push_back(n);
 
@@ -337,7 +357,7 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   bv_event_batch d = *eb;
   d.key_off = (const uint64_t *)(dev + o_koff);
   d.key_bytes = dev + o_kb;
-  d.creator = (const uint32_t *)(dev + o_cr);
+  d.creator = (const uint32_t *)(dev + o_cr_ev);
   d.index = (const int64_t *)(dev + o_ix);
   d.timestamp = (const int64_t *)(dev + o_ts);
   d.parent_kind = dev + o_pk;
@@ -352,7 +372,7 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   d.itx_json = dev + o_ij;
   d.bsig_off = eb->bsig_off ? (const uint64_t *)(dev + o_bo) : nullptr;
   d.bsig_json = dev + o_bj;
-  d.r_be = dev + o_r;
+  d.r_be = dev + o_r_ev;
   d.s_be = dev + o_s;
   d.pre = eb->pre ? dev + o_pre : nullptr;
 
@@ -435,15 +455,36 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   pipe.kc = kc;
   rc = bv_run_keys(ctx, &vb, ctx->S().ev[E_KREADY], ctx->S().ev[E_SREADY], kc);
   if (rc != BV_OK) return rc;
-  rc = stage(s_end, small_end);  // the parent hashes
+  if (qf) {
+    rc = stage(s_end, r_end);  // r, the creators: the key part
+    if (rc != BV_OK) return rc;
+    HIPCHK(hipEventRecord(ctx->S().ev[E_RREADY], cs), BV_E_LAUNCH, "event");
+    rc = pipe.key_part(vst, ctx->S().ev[E_RREADY]);
+    if (rc != BV_OK) return rc;
+  }
+  rc = stage(r_end, small_end);  // the parent hashes
   if (rc != BV_OK) return rc;
   HIPCHK(hipEventRecord(ctx->S().ev[E_SMALL], cs), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SMALL], 0), BV_E_LAUNCH, "join");
   HIPCHK(bvk::iota(st, n, ctx->ev_iota.as<uint32_t>()), BV_E_LAUNCH, "k_iota");
   HIPCHK(hipEventRecord(ctx->S().ev[E_FORK], st), BV_E_LAUNCH, "event");
 
+  // results: digests chunk by chunk (below), statuses and bits at the end
+  const size_t o_st = align256(n * 32), o_bits = o_st + align256(n);
+  HIPCHK(ctx->pin_out.ensure(o_bits + align256((n + 63) / 64 * 8) + 256), BV_E_OOM, "alloc pinned results");
+  uint8_t *pout = (uint8_t *)ctx->pin_out.p;
+  call.pout = pout;
+  call.o_st = o_st;
+  call.o_bits = o_bits;
+  call.direct_hash = res && bv_is_pinned(res->msg_hash, n * 32);  // results straight into pinned caller buffers
+  call.direct_status = res && bv_is_pinned(res->status, n);
+  uint8_t *hout = call.direct_hash ? res->msg_hash : pout;
+  const int d2h = ctx->ev_d2h;
+
   // per chunk: its fields cross PCIe on the copy stream; on the main stream
-  // the chunk's bodies are hashed (k_ev_body_hash) and its items verified
+  // the chunk's bodies are hashed (k_ev_body_hash) and its digests go back
+  // (the D2H direction is idle while the next chunk crosses); its items are
+  // verified on `vst`
   for (size_t c = 0; c + 1 < cb.size(); c++) {
     const uint64_t e0 = cb[c], e1 = cb[c + 1];
     std::vector<CopyPool::Piece> pieces;
@@ -476,25 +517,19 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
     }
     rc = pipe.upto(e1);
     if (rc != BV_OK) return rc;
+    if (d2h == 1)
+      HIPCHK(hipMemcpyAsync(hout + e0 * 32, dig + e0 * 8, (e1 - e0) * 32, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
+             "d2h digests");
+  }
+  if (d2h == 0) {  // one copy once the last chunk is hashed, on the copy stream
+    HIPCHK(hipStreamWaitEvent(cs, ctx->S().ev[E_HASHED], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipMemcpyAsync(hout, dig, n * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH, "d2h digests");
   }
   HIPCHK(hipEventRecord(ctx->S().ev[E_STAGED], cs), BV_E_LAUNCH, "event");
   call.ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call.t0).count();
 
   HIPCHK(hipEventRecord(ctx->S().ev[E_SHA], st), BV_E_LAUNCH, "event");
-
-  // the digests go back on the copy stream while the last verify kernels run
-  const size_t o_st = align256(n * 32), o_bits = o_st + align256(n);
-  HIPCHK(ctx->pin_out.ensure(o_bits + align256((n + 63) / 64 * 8) + 256), BV_E_OOM, "alloc pinned results");
-  uint8_t *pout = (uint8_t *)ctx->pin_out.p;
-  call.pout = pout;
-  call.o_st = o_st;
-  call.o_bits = o_bits;
-  HIPCHK(hipStreamWaitEvent(cs, ctx->S().ev[E_HASHED], 0), BV_E_LAUNCH, "join");
-  call.direct_hash = res && bv_is_pinned(res->msg_hash, n * 32);  // results straight into pinned caller buffers
-  call.direct_status = res && bv_is_pinned(res->status, n);
-  HIPCHK(hipMemcpyAsync(call.direct_hash ? res->msg_hash : pout, dig, n * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH,
-         "d2h digests");
-  HIPCHK(hipEventRecord(ctx->S().ev[E_CSDONE], cs), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_CSDONE], d2h == 0 ? cs : st), BV_E_LAUNCH, "event");
 
   rc = pipe.finish();  // the last chunk's items
   if (rc != BV_OK) return rc;

@@ -44,6 +44,12 @@ hipError_t sinv(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint8_t
 hipError_t verify_gq(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
                      const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
                      const uint32_t *, const uint64_t *, uint8_t *, uint64_t *);
+hipError_t verify_qf(hipStream_t, int, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
+                     const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
+                     const uint64_t *, uint32_t *);
+hipError_t verify_gf(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
+                     const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
+                     const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
 hipError_t verify_g(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
                     const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
                     const uint32_t *, uint32_t *);
@@ -195,7 +201,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // timing / ordering events (see bv_read_timing)
 enum {
   E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_SINV,
-  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_KDEC, E_KCDEC, E_COUNT
+  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_RREADY, E_KCTAB, E_KDEC, E_KCDEC, E_COUNT
 };
 
 constexpr uint32_t kKcMaxBatchKeys = 4096;  // key cache: batches with more keys use per-batch tables
@@ -284,9 +290,16 @@ struct bv_ctx {
   // chunk (BV_HOST_CHUNK_MB, >= 1 MB), event staging chunk (BV_EV_CHUNK_MB,
   // 0 = one chunk; chunks hold >= 256 events), bulk events' verify beside the next chunk
   // (BV_EV_VERIFY_STREAM=0: on the main stream)
-  // small host batches through k_small (BV_SMALL=0: the bulk pipeline)
+  // small host batches through k_small (BV_SMALL=0: the bulk pipeline);
+  // host entries sum the key part of every item before the messages land
+  // (BV_QFIRST=0: G part first, as device-resident batches)
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
-  bool ev_split_verify = true, small_path = true;
+  bool ev_split_verify = true, small_path = true, qfirst = true;
+  // bulk events' digests to the host (BV_EV_D2H): 1 = one copy per hashed
+  // chunk, 0 = one copy after the last chunk (stores by the hashing kernel
+  // through the pinned buffer's device alias measured no better)
+  int ev_d2h = 1;
+  bool ev_tail = false;  // bulk events: chunks halve after the first (BV_EV_TAIL=0: equal chunks)
   uint64_t table_min_items = 8;    // per-batch tables (not the generic path) from this many items per key
   uint64_t table_min_items_many = 48;  // the same above kManyKeys keys
   uint64_t k12_min_items = 8192;  // per-batch K12 (not K8) tables from this many items per key
@@ -346,7 +359,13 @@ struct bv_item_pipe {
   bv_out o;
   hipStream_t st;
   bool kc;
+  bool qf = false;  // key part launched for every item (key_part): upto runs k_verify_gf
   uint64_t done = 0;
+  // table mode, BV_QFIRST: R_Q of every item on `ks` after s^-1, the key
+  // tables and `ready` (r and the item keys in HBM); the first upto orders
+  // `st` after it.  Key cache: also after the call's kc_prepare work on
+  // ctx->stream (kc_tabs), so call it right after bv_run_keys.
+  int key_part(hipStream_t ks, hipEvent_t ready);
   int upto(uint64_t end);
   int finish();  // the rest, and the timing events even when there are no items
 };

@@ -449,6 +449,41 @@ __global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_QWAVES) k_verify_q(u
   write_status(i, hi, st, status, bits);
 }
 
+// Key part first (verify_core.h: verify_item_qfirst / verify_item_gfinish):
+// host entries run k_verify_qf over the whole batch while its messages
+// cross PCIe, then k_verify_gf per hashed chunk.
+template <int W, int NWIN, bool LAT>
+__global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_QWAVES) k_verify_qf(uint64_t n_items, uint64_t lo, uint64_t hi,
+                                                   const uint32_t *__restrict__ item_key,
+                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
+                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
+                                                   const uint32_t *__restrict__ w_in,
+                                                   const uint32_t *__restrict__ key_table,
+                                                   const uint64_t *__restrict__ key_tabs, uint32_t *__restrict__ rq) {
+  const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < hi)
+    verify_item_qfirst<W, NWIN, LAT>(i, n_items, item_key, r_be, s_be, pre, kstatus, w_in, key_table, key_tabs, rq);
+}
+
+template <bool LAT>
+__global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_QWAVES) k_verify_gf(uint64_t n_items, uint64_t lo, uint64_t hi,
+                                                   const uint32_t *__restrict__ item_key,
+                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
+                                                   const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
+                                                   const uint32_t *__restrict__ item_msg,
+                                                   const uint32_t *__restrict__ digest_words,
+                                                   const uint32_t *__restrict__ w_in,
+                                                   const uint32_t *__restrict__ g_table,
+                                                   const uint32_t *__restrict__ rq, uint8_t *__restrict__ status,
+                                                   uint64_t *__restrict__ bits) {
+  const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint8_t st = BV_REJECT;
+  if (i < hi)
+    st = verify_item_gfinish<LAT>(i, n_items, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, g_table,
+                                  rq);
+  write_status(i, hi, st, status, bits);
+}
+
 // Key-cache path, G and Q parts fused (verify_core.h: verify_item_gq_kc).
 template <bool LAT>
 __global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_QWAVES) k_verify_gq(uint64_t n_items, uint64_t lo, uint64_t hi,
@@ -1264,6 +1299,46 @@ hipError_t verify_q(hipStream_t st, int kw, uint64_t n, uint64_t lo, uint64_t hi
     BV_LAUNCH_Q(BV_KCW, BV_KCNWIN, nullptr, key_tabs)
   }
 #undef BV_LAUNCH_Q
+  return hipGetLastError();
+}
+
+// Key part first: R_Q of items [lo, hi) into rq (SoA, stride n); kw as
+// verify_q.
+hipError_t verify_qf(hipStream_t st, int kw, uint64_t n, uint64_t lo, uint64_t hi, const uint32_t *item_key,
+                     const uint32_t *r_be, const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst,
+                     const uint32_t *w, const uint32_t *key_table, const uint64_t *key_tabs, uint32_t *rq) {
+  if (hi <= lo) return hipSuccess;
+  const bool lat = lat_variant(n);
+#define BV_LAUNCH_QF(W, NWIN, KT, KTABS)                                                                            \
+  if (lat)                                                                                                       \
+    hipLaunchKernelGGL((k_verify_qf<W, NWIN, true>), grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, \
+                       r_be, s_be, pre, kst, w, KT, KTABS, rq);                                                  \
+  else                                                                                                           \
+    hipLaunchKernelGGL((k_verify_qf<W, NWIN, false>), grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, \
+                       r_be, s_be, pre, kst, w, KT, KTABS, rq);
+  if (kw == 8) {
+    BV_LAUNCH_QF(BV_KW, BV_KNWIN, key_table, nullptr)
+  } else if (kw == 12) {
+    BV_LAUNCH_QF(BV_K12W, BV_K12NWIN, key_table, nullptr)
+  } else {
+    BV_LAUNCH_QF(BV_KCW, BV_KCNWIN, nullptr, key_tabs)
+  }
+#undef BV_LAUNCH_QF
+  return hipGetLastError();
+}
+
+// ... then u1 G and the decision for items [lo, hi) once their digests are in.
+hipError_t verify_gf(hipStream_t st, uint64_t n, uint64_t lo, uint64_t hi, const uint32_t *item_key,
+                     const uint32_t *r_be, const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst,
+                     const uint32_t *item_msg, const uint32_t *dig, const uint32_t *w, const uint32_t *g_table,
+                     const uint32_t *rq, uint8_t *status, uint64_t *bits) {
+  if (hi <= lo) return hipSuccess;
+  if (lat_variant(n))
+    hipLaunchKernelGGL(k_verify_gf<true>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be, pre,
+                       kst, item_msg, dig, w, g_table, rq, status, bits);
+  else
+    hipLaunchKernelGGL(k_verify_gf<false>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be, pre,
+                       kst, item_msg, dig, w, g_table, rq, status, bits);
   return hipGetLastError();
 }
 

@@ -658,6 +658,79 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
   return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
 }
 
+// Key part first, for host entries whose messages are still crossing PCIe:
+// u2 = r s^-1 needs no digest, so R_Q = k1 Q + k2 phi(Q) is summed as soon
+// as r, s, the keys and their tables are in HBM (k_verify_qf), and only
+// u1 G and the decision wait for each chunk's digests (k_verify_gf).  The
+// same additions as verify_item_g + verify_item_q in the other order; R_Q
+// goes through the R_G buffer (rg_store), and no u12 round trip.
+template <int W, int NWIN, bool LAT = false>
+DEV void verify_item_qfirst(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
+                            const uint32_t *s_be, const uint8_t *pre, const uint8_t *kstatus, const uint32_t *w_in,
+                            const uint32_t *key_table, const uint64_t *key_tabs, uint32_t *rq) {
+  constexpr bool SIGNED = W != BV_KW;
+  constexpr bool KC = W == BV_KCW;
+  constexpr uint64_t half =
+      SIGNED ? ((uint64_t)NWIN * (1ull << (W - 1)) + 1) * BV_ENTRY_U32 : (uint64_t)NWIN * (1ull << W) * BV_ENTRY_U32;
+  fe r;
+  if (classify_item(i, item_key, r_be, s_be, pre, kstatus, r) != 0xFF) return;
+  uint32_t k1[4], k2[4], signs;
+  {
+    sc w, rs, b;
+    const uint4 *q = (const uint4 *)(w_in + 8 * i);
+    const uint4 x = q[0], y = q[1];
+    w.v[0] = x.x; w.v[1] = x.y; w.v[2] = x.z; w.v[3] = x.w;
+    w.v[4] = y.x; w.v[5] = y.y; w.v[6] = y.z; w.v[7] = y.w;
+    sc_load_be_words(rs, r_be + 8 * i);
+    sc_mont(b, rs, w);  // r * s^-1 mod N
+    glv_split(k1, k2, signs, b);
+  }
+  gexz R;
+  bool inf = true;
+  fe_set(R.X, 0);
+  fe_set(R.Y, 0);
+  fe_set(R.ZZ, 0);
+  fe_set(R.ZZZ, 0);
+  const uint32_t *tab = key_tabs ? (const uint32_t *)key_tabs[item_key[i]]
+                                 : key_table + (uint64_t)item_key[i] * (KC ? 1 : 2) * half;
+#pragma unroll 1
+  for (int h = 0; h < 2; h++) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) kk[c] = h ? k2[c] : k1[c];
+    key_table_add<W, NWIN, SIGNED, LAT>(R, inf, tab + (h && !KC ? half : 0), kk, (signs >> h) & 1u, KC && h);
+  }
+  rg_store(rq, n, i, R, inf);
+}
+
+template <bool LAT = false>
+DEV uint8_t verify_item_gfinish(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be,
+                                const uint32_t *s_be, const uint8_t *pre, const uint8_t *kstatus,
+                                const uint32_t *item_msg, const uint32_t *digest_words, const uint32_t *w_in,
+                                const uint32_t *g_table, const uint32_t *rq) {
+  fe r;
+  const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
+  if (st != 0xFF) return st;
+  uint32_t u[8];
+  {
+    sc w, e, a;
+    const uint4 *q = (const uint4 *)(w_in + 8 * i);
+    const uint4 x = q[0], y = q[1];
+    w.v[0] = x.x; w.v[1] = x.y; w.v[2] = x.z; w.v[3] = x.w;
+    w.v[4] = y.x; w.v[5] = y.y; w.v[6] = y.z; w.v[7] = y.w;
+    sc_load_be_words(e, digest_words + 8 * (uint64_t)item_msg[i]);
+    sc_mont(a, e, w);  // e * s^-1 mod N  (e < 2^256 = R, w < N)
+#pragma unroll
+    for (int k = 0; k < 8; k++) u[k] = a.v[k];
+  }
+  gexz R;
+  bool inf;
+  rg_load(rq, n, i, R, inf);
+  g_table_add<BV_GW, BV_GNWIN, LAT>(R, inf, g_table, u);
+  fe_load_be_words(r, r_be + 8 * i);
+  return final_check(R, inf, r) ? BV_ACCEPT : BV_REJECT;
+}
+
 // Key-cache path in ONE pass (k_verify_gq): R = u1 G + k1 T + k2 phi(T) with
 // the G table and the key's cached table, R_G kept in registers (no HBM
 // round trip of R_G / u12 between two kernels, no kernel boundary).  Same

@@ -331,7 +331,10 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
   uint32_t *u12 = aligned<uint32_t>(s_u12, n_items * BV_U_STRIDE * 4 + 64);
   parallel_for(n_msgs, n_threads, [&](uint64_t m) { sha256_one(m, msg, b->msg_off, dig); });
   for (uint32_t k = 0; k < n_keys; k++) key_decode_one(k, b->key_bytes, b->key_off, kst, kxy);
-  int mode = force_mode;
+  // force_mode 5 / 6: K8 / K12 with the key part first (verify_item_qfirst,
+  // then verify_item_gfinish), as the host entries run them; returns 1 / 2
+  const bool qfirst = force_mode == 5 || force_mode == 6;
+  int mode = qfirst ? force_mode - 4 : force_mode;
   if (mode < 0) {
     mode = (n_keys <= 8192 && n_items >= 16ull * n_keys) ? 1 : 0;
     if (mode == 1 && n_keys <= 1024 && n_items >= 2048ull * n_keys) mode = 2;
@@ -352,6 +355,16 @@ int emu_verify_batch(const bv_batch *b, uint8_t *msg_hash, uint8_t *status, uint
   std::vector<uint8_t> st(n_items + 1);
   if (mode == 3) {
     parallel_for(n_items, n_threads, [&](uint64_t i) { st[i] = small_item(i, b, msg, r, s, gt); });
+  } else if (table_mode && qfirst) {
+    parallel_for(n_items, n_threads, [&](uint64_t i) {
+      if (mode == 2)
+        verify_item_qfirst<BV_K12W, BV_K12NWIN>(i, n_items, b->item_key, r, s, b->pre, kst, scratch, kt, nullptr, rg);
+      else
+        verify_item_qfirst<BV_KW, BV_KNWIN>(i, n_items, b->item_key, r, s, b->pre, kst, scratch, kt, nullptr, rg);
+    });
+    parallel_for(n_items, n_threads, [&](uint64_t i) {
+      st[i] = verify_item_gfinish(i, n_items, b->item_key, r, s, b->pre, kst, b->item_msg, dig, scratch, gt, rg);
+    });
   } else if (table_mode) {
     parallel_for(n_items, n_threads,
                  [&](uint64_t i) {

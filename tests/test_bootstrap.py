@@ -102,10 +102,32 @@ def test_bootstrap_all_valid_and_insert_error():
     assert log[-1] == ("insert", 150)
 
 
+class CheckedVerifier:
+    """The default device Verifier, each batch also checked against the C
+    oracle (a wrong status is reported as such, not as a replay error)."""
+
+    def __init__(self):
+        self.mismatches = []
+
+    def verify(self, packed):
+        res = H.default_verifier().verify(packed)
+        h, st, _ = coracle.verify_batch(packed.as_dict())
+        bad = np.flatnonzero(res.status != st)
+        if bad.size or not np.array_equal(res.msg_hash, h):
+            self.mismatches.append((packed.n_items, bad[:8].tolist(), res.status[bad[:8]].tolist(),
+                                    st[bad[:8]].tolist(), H.default_verifier().timing()))
+        return res
+
+    def sha256(self, msgs):
+        return H.default_verifier().sha256(msgs)
+
+
 @pytest.mark.gpu
 def test_bootstrap_on_device():
     evs = make_db(1200, bad={1111})
-    err, log = run(evs, 500, None)
+    cv = CheckedVerifier()
+    err, log = run(evs, 500, cv)
+    assert not cv.mismatches, f"device statuses differ from the oracle: {cv.mismatches}"
     assert err == "Invalid Event signature %s" % evs[1111].Hex()
     assert sum(1 for x in log if x[0] == "insert") == 1111
     assert all(e._hash is not None for e in evs[:1112])

@@ -89,15 +89,17 @@ def test_glv_constants_and_split():
         assert (k1 + k2 * LAMBDA - k) % N == 0, hex(k)
 
 
-@pytest.mark.parametrize("mode", [2, 1, 0, 3])
+# 5 / 6: K8 / K12 with the key part first (k_verify_qf, then k_verify_gf:
+# the host entries' order), reported as modes 1 / 2
+@pytest.mark.parametrize("mode", [2, 1, 0, 3, 5, 6])
 def test_golden_items(mode):
     batch, expected, _ = golden_items_batch()
     h, st, bits, m = emu.verify_batch(batch.as_dict(), force_mode=mode)
-    assert m == mode
+    assert m == (mode - 4 if mode >= 5 else mode)
     assert np.array_equal(st, expected)
 
 
-@pytest.mark.parametrize("mode", [2, 1, 0, 3])
+@pytest.mark.parametrize("mode", [2, 1, 0, 3, 5, 6])
 def test_adversarial_mix(mode):
     b = synth.adversarial(2500, seed=21, n_creators=4, scale_per_million=dict(
         rflip=20000, sflip=20000, body=10000, highs=10000, range=8000, fmt=8000, key=12000))

@@ -188,6 +188,26 @@ def test_host_entry_item_order(monkeypatch):
     verifier.close()
 
 
+@pytest.mark.parametrize("qfirst", ["1", "0"])
+def test_host_entry_key_part_order(monkeypatch, qfirst):
+    """Host entries sum every item's k1 Q + k2 phi(Q) before its message is
+    hashed (k_verify_qf over the batch, then k_verify_gf per hashed chunk;
+    BV_QFIRST=0 keeps the device batches' order, u1 G first): both orders on
+    K12 (8 keys, 8 MB message chunks) and K8 (200 keys) batches of the C4
+    mix, ragged last word, bit-exact against the oracle."""
+    from babble_amd.verifier import Verifier
+
+    monkeypatch.setenv("BV_QFIRST", qfirst)  # read at bv_create
+    monkeypatch.setenv("BV_HOST_CHUNK_MB", "8")
+    verifier = Verifier(device=0)
+    for n, keys, w in ((120_000 + 37, 8, 12), (60_000 + 5, 200, 8)):
+        b = synth.adversarial(n, seed=15 + keys, n_creators=keys, scale_per_million=MIX)
+        res = check_against_oracle(verifier, b)
+        assert verifier.timing()["key_path"] == w
+        assert set(np.unique(res.status)) == {0, 1, 2, 3}
+    verifier.close()
+
+
 def test_host_entry_single_copy_staging(verifier):
     """Host batches whose staging layout is <= 1 MB cross PCIe as one copy
     (bv_api.cpp kSmallStage): a ~0.8 MB adversarial batch in message order

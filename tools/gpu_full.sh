@@ -4,6 +4,7 @@
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
+echo "box $(hostname)"
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST FAILED; tail -60 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
