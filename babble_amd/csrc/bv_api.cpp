@@ -437,7 +437,7 @@ static int create_impl(bv_ctx *ctx) {
   if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
   if (const char *s = getenv("BV_QFIRST")) ctx->qfirst = atoi(s) != 0;
   if (const char *s = getenv("BV_EV_D2H")) ctx->ev_d2h = atoi(s);
-  if (const char *s = getenv("BV_EV_TAIL")) ctx->ev_tail = atoi(s) != 0;
+  if (const char *s = getenv("BV_EV_TAIL")) ctx->ev_tail = atoi(s);
   if (const char *s = getenv("BV_SMALL_STAMPS")) ctx->small_stamps = atoi(s) != 0;
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS")) ctx->table_min_items = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS_MANY")) ctx->table_min_items_many = (uint64_t)std::max(1, atoi(s));
@@ -1076,6 +1076,21 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   rc = pipe.key_part(ctx->sstream, ctx->S().ev[E_SMALL]);
   if (rc != BV_OK) return rc;
 
+  // results into pinned memory (straight into the caller's bv_host_alloc
+  // buffers when they are): digests chunk by chunk on `st` as each chunk is
+  // hashed (ctx->ev_d2h; after the last chunk, on the copy stream, when long
+  // messages' digests are put in afterwards), statuses and bits at the end
+  const size_t o_st = align256(n_msgs * 32), o_bits = o_st + align256(n_items);
+  HIPCHK(ctx->pin_out.ensure(o_bits + align256((n_items + 63) / 64 * 8) + 256), BV_E_OOM, "alloc pinned results");
+  uint8_t *pout = (uint8_t *)ctx->pin_out.p;
+  call->pout = pout;
+  call->o_st = o_st;
+  call->o_bits = o_bits;
+  call->direct_hash = res && bv_is_pinned(res->msg_hash, n_msgs * 32);
+  call->direct_status = res && bv_is_pinned(res->status, n_items);
+  uint8_t *hout = call->direct_hash ? res->msg_hash : pout;
+  const bool d2h_chunks = ctx->ev_d2h == 1 && longm.empty();
+
   // message bytes: chunks on message boundaries, each hashed once it lands
   if (ctx->has_done) HIPCHK(hipStreamWaitEvent(st, ctx->ev_done, 0), BV_E_LAUNCH, "order");
   HIPCHK(hipEventRecord(ctx->S().ev[E_HASH0], st), BV_E_LAUNCH, "event");
@@ -1113,6 +1128,9 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
       rc = pipe.upto(i_end);
       if (rc != BV_OK) return rc;
     }
+    if (d2h_chunks)
+      HIPCHK(hipMemcpyAsync(hout + 32 * m0, pipe.o.dig + 8 * m0, (m1 - m0) * 32, hipMemcpyDeviceToHost, st),
+             BV_E_LAUNCH, "d2h digests");
     m0 = m1;
   }
   if (!longm.empty()) {
@@ -1148,22 +1166,10 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   rc = pipe.finish();
   if (rc != BV_OK) return rc;
 
-  // results into pinned memory: digests as soon as hashing ended (overlaps
-  // the verify kernels, on the copy stream), statuses and bits at the end
-  const size_t o_st = align256(n_msgs * 32), o_bits = o_st + align256(n_items);
-  HIPCHK(ctx->pin_out.ensure(o_bits + align256((n_items + 63) / 64 * 8) + 256), BV_E_OOM, "alloc pinned results");
-  uint8_t *pout = (uint8_t *)ctx->pin_out.p;
-  call->pout = pout;
-  call->o_st = o_st;
-  call->o_bits = o_bits;
-  // results straight into the caller's bv_host_alloc buffers when they are
-  call->direct_hash = res && bv_is_pinned(res->msg_hash, n_msgs * 32);
-  call->direct_status = res && bv_is_pinned(res->status, n_items);
-  if (n_msgs) {
+  if (n_msgs && !d2h_chunks) {  // the digests as soon as hashing ended, beside the verify kernels
     HIPCHK(hipStreamWaitEvent(cs, ctx->S().ev[E_HASHED], 0), BV_E_LAUNCH, "join");
-    HIPCHK(hipMemcpyAsync(call->direct_hash ? res->msg_hash : pout, ctx->S().digests.p, n_msgs * 32,
-                          hipMemcpyDeviceToHost, cs),
-           BV_E_LAUNCH, "d2h digests");
+    HIPCHK(hipMemcpyAsync(hout, ctx->S().digests.p, n_msgs * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH,
+           "d2h digests");
   }
   if (n_items) {
     HIPCHK(hipMemcpyAsync(call->direct_status ? res->status : pout + o_st, ctx->S().status.p, n_items,

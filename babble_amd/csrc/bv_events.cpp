@@ -337,12 +337,19 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   if (chunk_bytes > 0) {
     const uint64_t per_ev = std::max<uint64_t>(1, (total - small_end) / n);
     const uint64_t per = std::max<uint64_t>(256, chunk_bytes / per_ev / 256 * 256);
-    for (uint64_t e = 0; e < n;) {
-      uint64_t c = per;
-      if (ctx->ev_tail) c = std::min(per, ((n - e) / 2 + 255) / 256 * 256);
-      if (n - e <= c || (ctx->ev_tail && n - e - c < kEvTailMin)) break;
-      e += c;
-      cb.push_back(e);
+    if (ctx->ev_tail == 2 && n > 2 * kEvTailMin) {  // equal chunks, then one of kEvTailMin events
+      const uint64_t body = (n - kEvTailMin) / 256 * 256, k = (body + per - 1) / per;
+      const uint64_t c = ((body + k - 1) / k + 255) / 256 * 256;
+      for (uint64_t e = c; e < body; e += c) cb.push_back(e);
+      cb.push_back(body);
+    } else {
+      for (uint64_t e = 0; e < n;) {
+        uint64_t c = per;
+        if (ctx->ev_tail == 1) c = std::min(per, ((n - e) / 2 + 255) / 256 * 256);
+        if (n - e <= c || (ctx->ev_tail == 1 && n - e - c < kEvTailMin)) break;
+        e += c;
+        cb.push_back(e);
+      }
     }
   }
   cb.push_back(n);

@@ -295,11 +295,11 @@ struct bv_ctx {
   // (BV_QFIRST=0: G part first, as device-resident batches)
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
   bool ev_split_verify = true, small_path = true, qfirst = true;
-  // bulk events' digests to the host (BV_EV_D2H): 1 = one copy per hashed
+  // host entries' digests to the host (BV_EV_D2H): 1 = one copy per hashed
   // chunk, 0 = one copy after the last chunk (stores by the hashing kernel
   // through the pinned buffer's device alias measured no better)
   int ev_d2h = 1;
-  bool ev_tail = false;  // bulk events: chunks halve after the first (BV_EV_TAIL=0: equal chunks)
+  int ev_tail = 0;  // bulk events' chunk plan (BV_EV_TAIL): 0 equal, 1 halving, 2 equal + one small last chunk
   uint64_t table_min_items = 8;    // per-batch tables (not the generic path) from this many items per key
   uint64_t table_min_items_many = 48;  // the same above kManyKeys keys
   uint64_t k12_min_items = 8192;  // per-batch K12 (not K8) tables from this many items per key
