@@ -1218,13 +1218,15 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
 constexpr uint64_t kSmallMsgLen = 16 << 10;  // longest message (hashed on the host, inside the call)
 constexpr uint8_t kSmallPending = 0xFF;      // status sentinel (statuses are 0..3)
 
-// Small batches: <= ctx->small_max (768) items, or up to ctx->small_warm_max
+// Small batches: <= ctx->small_max (256) items, or up to ctx->small_warm_max
 // (1024) items when every well-formed key already has a key-cache table (no
-// item needs the doubling chain).  Same-box medians, 4 creators
-// (profiles/r05_ab_small_max.log): cold k_small 0.32 / 0.40 / 0.74 ms at
-// 256 / 512 / 1000 items against 0.72-0.73 ms for the bulk pipeline's K8
-// tables (more creators only lengthen the bulk build); warm 0.14 / 0.18 /
-// 0.29 / 0.52 ms at 256 / 512 / 1000 / 2000 against 0.45-0.70 / 0.52.
+// item needs the cooperative NAF chains).  Warm, same box, 4 creators
+// (profiles/r05_ab_small_max.log): 0.14 / 0.18 / 0.29 / 0.52 ms at 256 / 512
+// / 1000 / 2000 items against 0.45-0.70 / 0.52 for the bulk pipeline.  The
+// cold limit is round 4's (profiles/r04_small_lat.log): the right-to-left
+// cold path that measured 0.32 / 0.40 ms at 256 / 512 items gave a false
+// REJECT on ~1 in 3000 items of a process's first batch and was withdrawn
+// (DESIGN.md section 4, round 5).
 static bool small_batch(bv_ctx *ctx, const bv_batch *b) {
   if (b->n_items == 0) return false;
   const uint64_t n = std::max<uint64_t>(b->n_items, b->n_msgs);

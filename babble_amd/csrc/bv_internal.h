@@ -305,7 +305,7 @@ struct bv_ctx {
   uint64_t k12_min_items = 8192;  // per-batch K12 (not K8) tables from this many items per key
   bool small_stamps = false;      // BV_SMALL_STAMPS=1: print k_small's phase clocks to stderr
   uint32_t small_span = 0;        // 1 + the slot of a small batch whose device span is not read yet
-  uint64_t small_max = 768;       // k_small for batches of at most this many items and messages (BV_SMALL_MAX)
+  uint64_t small_max = 256;       // k_small for batches of at most this many items and messages (BV_SMALL_MAX)
   uint64_t small_warm_max = 1024;  // k_small for batches whose keys are all cached (BV_SMALL_WARM_MAX)
   uint32_t lat_table_keys = 256;  // latency rule: K8 tables for batches of <= 4096 items from up to this many keys (BV_LAT_TABLE_KEYS)
 };

@@ -584,32 +584,20 @@ __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, uint64
 // different waves run different code at the same time; lanes of one wave
 // only when they run the same code).  The host has hashed the messages
 // (SHA-NI, hostsha.cpp) and sends the digests.
-//   phase 1  waves 1 + 3: s^-1 (one Bernstein-Yang inversion split over two
-//            waves; wave-uniform, so it runs on the scalar unit)
+//   phase 1  wave 1: s^-1 (one Bernstein-Yang inversion; wave-uniform, so
+//            the compiler runs it on the scalar unit)
 //            wave 2: elliptic.Unmarshal of the item's key (Q)
-//            wave 0: the item's r, digest, pre and key-cache table address
-// Key WITH a key-cache table (all four waves meet at workgroup barriers):
 //   phase 2  wave 0 lane 0: decision table, u1 = e w;  wave 1 lane 0:
 //            u2 = r w and its GLV split (k1, k2, signs)
-//   phase 3  22 leaves in lanes 0..21 of wave 0, every table entry loaded
-//            at once — G windows 0..9 of u1, KC windows 0..5 of k1 (T) and
-//            of k2 (phi(T)) — summed by a binary tree (affine pairs, then
-//            XYZZ sums: 5 levels of zipped point additions through LDS)
+//   phase 3  key with a key-cache table: 22 leaves in lanes 0..21 of wave
+//            0, every table entry loaded at once — G windows 0..9 of u1,
+//            KC windows 0..5 of k1 (T) and of k2 (phi(T)) — summed by a
+//            binary tree (affine pairs, then XYZZ sums: 5 levels of zipped
+//            point additions, nodes handed over through LDS);
+//            key without one: waves 2 / 3 run k1 Q / k2 phi(Q) as
+//            wave-cooperative NAF chains (coop.h) while wave 0 sums the 10
+//            G leaves, then wave 0 lane 0 adds the three partial sums
 //   phase 4  wave 0 lane 0: x(R) mod N == r
-// Key WITHOUT one (no workgroup barrier after phase 1; waves hand over
-// through LDS flags): right-to-left over the NAF digits of k1 and k2.
-//            wave 2 doubles Q as soon as it is decoded — 2^i Q for
-//            i = 0..129 in XYZZ, with beta X for phi — cooperatively
-//            (coop.h dbl_xyzz: three levels of row products per doubling),
-//            publishing each into LDS;
-//            wave 0: decision table, u1, the 10 G leaves and their tree;
-//            wave 3: u2, the GLV split, then adds +-phi(2^i Q) for every
-//            non-zero digit of k2 as the chain produces it (add_xyzz);
-//            wave 1: the same for k1 with 2^i Q, plus the G sum; then adds
-//            wave 3's sum and decides.
-//            The chain no longer waits for s^-1 and u2, and the additions
-//            run beside it: ~130 doublings are the critical path instead of
-//            ~128 doublings + ~43 additions after phase 2.
 // Statuses only; the host packs a small batch's accept bits.  `stamps`
 // (BV_SMALL_STAMPS diagnostics): workgroup 0's shader clocks per phase.
 // ---------------------------------------------------------------------------
@@ -672,8 +660,11 @@ struct SinvMail {
   uint32_t produced, consumed, done;  // matrices published / applied; total + 1 once g = 0 (0: running)
   int32_t f_sign;
 };
+// A flag read, made wave-uniform (every lane takes lane 0's value, so a
+// branch on it is a scalar branch and no lane can see a different value of
+// a flag another wave is writing).
 DEV uint32_t lds_acquire(const uint32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 DEV void lds_release(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
 // producer (the s^-1 chain): divsteps and the (f, g) updates
@@ -729,79 +720,6 @@ DEV void sinv_split_de(SinvMail &mb, sc &w) {
   for (int k = 0; k < 8; k++) one.v[k] = k == 0 ? 1u : 0u;
   sc_mont(w, r, one);  // ... s^-1 R
 }
-
-// The cold path's LDS: the doubling chain 2^i Q (XYZZ + beta X, i < 130:
-// the NAF digits of a 128-bit GLV half) and the flags the waves hand over
-// with (release / acquire at workgroup scope; every wait also watches
-// `abort`, set when the decision table settles the item, so every wave
-// reaches its end whatever the item).
-constexpr uint32_t kChainBits = 130, kChainDead = 0x80000000u;
-struct ChainPt {
-  uint32_t x[8], bx[8], y[8], zz[8], zzz[8];
-};
-struct SmallCold {
-  ChainPt pt[kChainBits];
-  SmallNode acc2, fin;
-  uint32_t chain_n;  // entries published (kChainDead: no chain, the key is not valid)
-  uint32_t nbits;    // entries the digits need (wave 3, once k1 and k2 are known)
-  uint32_t abort_, f_pre, f_q, f_w, f_k, f_g, f_a2;
-};
-__device__ __forceinline__ uint32_t row_limb(const uint32_t *p) { return coop::pos() < 8 ? p[coop::pos()] : 0u; }
-__device__ __forceinline__ void row_store(uint32_t *p, uint32_t v) {
-  if (__lane_id() < 8) p[__lane_id()] = v;
-}
-// wait for flag != 0; false if the item was settled meanwhile
-__device__ __forceinline__ bool cold_wait(SmallCold &cs, const uint32_t *flag) {
-  for (;;) {
-    if (lds_acquire(flag)) return true;
-    if (lds_acquire(&cs.abort_)) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-// R += node (a SmallNode in LDS, X Y ZZ ZZZ + identity flag), cooperatively
-__device__ __forceinline__ void cold_add_node(uint32_t &X, uint32_t &Y, uint32_t &ZZ, uint32_t &ZZZ, bool &inf,
-                                              const SmallNode &nd) {
-  if (!nd.w[32]) coop::add_xyzz(X, Y, ZZ, ZZZ, inf, row_limb(nd.w), row_limb(nd.w + 8), row_limb(nd.w + 16),
-                                row_limb(nd.w + 24));
-}
-// k P for one GLV half, right-to-left: the sum of +-2^i P (h = 1: of
-// phi(2^i P)) over the non-zero NAF digits of k, each added as soon as the
-// chain has published 2^i P.  `g` (wave 1) is added in too, when it is
-// ready.  False if the item was settled meanwhile (or the chain is dead).
-__device__ __forceinline__ bool cold_half(SmallCold &cs, uint32_t h, const uint32_t kk[4], bool neg_all,
-                                          const SmallNode *g, uint32_t &X, uint32_t &Y, uint32_t &ZZ, uint32_t &ZZZ,
-                                          bool &inf) {
-  uint32_t pm[5], nm[5];
-  naf_masks(kk, pm, nm);
-  inf = true;
-  X = Y = ZZ = ZZZ = 0;
-  bool g_todo = g != nullptr;
-  for (uint32_t bit = 0; bit < kChainBits; bit++) {
-    const uint32_t p = (pm[bit >> 5] >> (bit & 31)) & 1u, n = (nm[bit >> 5] >> (bit & 31)) & 1u;
-    if (!(p | n)) continue;
-    for (;;) {  // 2^bit P published?
-      const uint32_t c = lds_acquire(&cs.chain_n);
-      if (c & kChainDead) return false;
-      if (c > bit) break;
-      if (lds_acquire(&cs.abort_)) return false;
-      if (g_todo && lds_acquire(&cs.f_g)) {  // the G sum is ready meanwhile
-        cold_add_node(X, Y, ZZ, ZZZ, inf, *g);
-        g_todo = false;
-        continue;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    const ChainPt &e = cs.pt[bit];
-    uint32_t y = row_limb(e.y);
-    if ((n != 0) != neg_all) y = coop::norm(coop::negw(y));
-    coop::add_xyzz(X, Y, ZZ, ZZZ, inf, row_limb(h ? e.bx : e.x), y, row_limb(e.zz), row_limb(e.zzz));
-  }
-  if (g_todo) {
-    if (!cold_wait(cs, &cs.f_g)) return false;
-    cold_add_node(X, Y, ZZ, ZZZ, inf, *g);
-  }
-  return true;
-}
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t *__restrict__ digest_words,
@@ -824,15 +742,9 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
   __shared__ uint64_t sh_tab;
   __shared__ SinvMail sh_mail;
   __shared__ uint32_t sh_sok;
-  __shared__ SmallNode sh_a[kSmallLeaves], sh_b[kSmallLeaves / 2 + 1], sh_c[kSmallLeaves / 4 + 2];
-  __shared__ SmallCold cs;
+  __shared__ SmallNode sh_a[kSmallLeaves], sh_b[kSmallLeaves / 2 + 1], sh_c[kSmallLeaves / 4 + 2], sh_d[3];
   if (b >= n_items) return;  // (the grid is n_items)
-  if (t == 0) {
-    sh_mail.produced = sh_mail.consumed = sh_mail.done = 0;
-    cs.chain_n = 0;
-    cs.nbits = kChainBits;
-    cs.abort_ = cs.f_pre = cs.f_q = cs.f_w = cs.f_k = cs.f_g = cs.f_a2 = 0;
-  }
+  if (t == 0) sh_mail.produced = sh_mail.consumed = sh_mail.done = 0;
   __syncthreads();
   // ---- phase 1 (the inputs live in host memory, read in place: wave 0
   // fetches what phases 2-4 need while s^-1 runs)
@@ -844,7 +756,6 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
     for (int k = 0; k < 8; k++) sh_e[k] = digest_words[8 * (uint64_t)m + k];
     sh_pre = pre ? pre[b] : 0u;
     sh_tab = kc_tabs ? kc_tabs[item_key[b]] : 0;
-    lds_release(&cs.f_pre, 1);
   } else if (lane == 0 && wave == 1) {  // s^-1: divsteps and (f, g) (wave 3 applies (d, e))
     sc s;
     sc_load_be_words(s, s_be + 8 * (uint64_t)b);
@@ -863,7 +774,6 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
     }
 #pragma unroll
     for (int k = 0; k < 8; k++) sh_w[k] = w.v[k];
-    lds_release(&cs.f_w, 1);
     SMALL_STAMP(2);
   } else if (lane == 0 && wave == 2) {
     const uint32_t k = item_key[b];
@@ -873,131 +783,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
 #pragma unroll
     for (int c = 0; c < 8; c++) sh_q[c] = x.v[c], sh_q[8 + c] = y.v[c];
     sh_ks = st;
-    lds_release(&cs.f_q, 1);
     SMALL_STAMP(3);
-  }
-  while (!lds_acquire(&cs.f_pre)) __builtin_amdgcn_s_sleep(1);  // the table address: which path
-  if (sh_tab == 0) {
-    // ---- no key-cache table: the right-to-left pipeline, no workgroup
-    // barrier from here on (wave 2 may still be doubling while the others
-    // finish)
-    if (wave == 2) {  // the chain 2^i Q, i < nbits
-      if (sh_ks != KS_OK) {
-        lds_release(&cs.chain_n, kChainDead);  // (the decision table rejects the item)
-        return;
-      }
-      uint32_t X = row_limb(sh_q), Y = row_limb(sh_q + 8), ZZ = coop::pos() == 0 ? 1u : 0u, ZZZ = ZZ;
-      uint32_t BX = coop::mul(X, coop::beta_limb());
-      for (uint32_t i = 0;; i++) {
-        ChainPt &e = cs.pt[i];
-        row_store(e.x, X), row_store(e.bx, BX), row_store(e.y, Y), row_store(e.zz, ZZ), row_store(e.zzz, ZZZ);
-        lds_release(&cs.chain_n, i + 1);
-        if (i + 1 >= kChainBits || i + 1 >= lds_acquire(&cs.nbits) || lds_acquire(&cs.abort_)) break;
-        coop::dbl_xyzz(X, Y, ZZ, ZZZ, BX);
-      }
-      if (lane == 0) SMALL_STAMP(12);
-      return;
-    }
-    if (wave == 0) {  // the decision table, u1, the G sum
-      if (!cold_wait(cs, &cs.f_w) || !cold_wait(cs, &cs.f_q)) return;  // (never settled before this)
-      if (lane == 0) {
-        fe r, sv;
-        fe_load_be_words(r, sh_r);
-        fe_load_be_words(sv, sh_s);
-        const uint8_t cls = classify((uint8_t)sh_pre, (uint8_t)sh_ks, r, sv);
-        sh_go = cls == 0xFF;
-        if (cls != 0xFF) {
-          status[b] = cls;
-          lds_release(&cs.abort_, 1);
-        } else {
-          sc w, e, a;
-#pragma unroll
-          for (int k = 0; k < 8; k++) w.v[k] = sh_w[k];
-          sc_load_be_words(e, sh_e);
-          sc_mont(a, e, w);
-#pragma unroll
-          for (int k = 0; k < 8; k++) sh_u1[k] = a.v[k];
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      if (!sh_go) return;
-      fe x, y;
-      bool zero = true;
-      if (lane < BV_GNWIN) {
-        uint32_t u[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) u[k] = sh_u1[k];
-        table_leaf<BV_GW, 8>(x, y, zero, g_table, u, (int)lane, false, false);
-      }
-      small_leaf_pairs(x, y, zero, sh_b, sh_a, BV_GNWIN, lane);  // 10 -> 5 -> 3 -> 2 -> 1
-      small_tree_level(sh_b, sh_c, 5, lane);
-      small_tree_level(sh_c, sh_b, 3, lane);
-      small_tree_level(sh_b, sh_c, 2, lane);  // the G sum in sh_c[0]
-      lds_release(&cs.f_g, 1);
-      if (lane == 0) SMALL_STAMP(7);
-      return;
-    }
-    // waves 1 and 3: the two GLV halves
-    if (wave == 3) {  // u2, the GLV split, the chain length
-      if (lane == 0) {
-        sc w, r, u2;
-#pragma unroll
-        for (int k = 0; k < 8; k++) w.v[k] = sh_w[k];
-        sc_load_be_words(r, sh_r);
-        sc_mont(u2, r, w);
-        uint32_t k1[4], k2[4], signs, p1[5], n1[5], p2[5], n2[5];
-        glv_split(k1, k2, signs, u2);
-        naf_masks(k1, p1, n1);
-        naf_masks(k2, p2, n2);
-        uint32_t nb = 0;
-        for (int i = 4; i >= 0 && nb == 0; i--) {
-          const uint32_t m = p1[i] | n1[i] | p2[i] | n2[i];
-          if (m) nb = 32 * i + 32 - __builtin_clz(m);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) sh_k[k] = k1[k], sh_k[4 + k] = k2[k];
-        sh_signs = signs;
-        lds_release(&cs.nbits, nb);
-        lds_release(&cs.f_k, 1);
-      }
-    } else if (!cold_wait(cs, &cs.f_k)) {
-      return;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t h = wave == 3 ? 1u : 0u;
-    uint32_t kk[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) kk[k] = sh_k[4 * h + k];
-    uint32_t X, Y, ZZ, ZZZ;
-    bool inf;
-    if (!cold_half(cs, h, kk, (sh_signs >> h) & 1u, h ? nullptr : &sh_c[0], X, Y, ZZ, ZZZ, inf)) return;
-    if (h) {  // wave 3: its half's sum to wave 1
-      row_store(cs.acc2.w, X), row_store(cs.acc2.w + 8, Y), row_store(cs.acc2.w + 16, ZZ),
-          row_store(cs.acc2.w + 24, ZZZ);
-      if (lane == 0) cs.acc2.w[32] = inf ? 1u : 0u;
-      lds_release(&cs.f_a2, 1);
-      if (lane == 0) SMALL_STAMP(10);
-      return;
-    }
-    // wave 1: (u1 G + k1 Q) + k2 phi(Q), then the decision
-    if (!cold_wait(cs, &cs.f_a2)) return;
-    cold_add_node(X, Y, ZZ, ZZZ, inf, cs.acc2);
-    row_store(cs.fin.w, X), row_store(cs.fin.w + 8, Y), row_store(cs.fin.w + 16, ZZ), row_store(cs.fin.w + 24, ZZZ);
-    if (lane == 0) cs.fin.w[32] = inf ? 1u : 0u;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-      gexz A;
-      bool ia;
-      part_load(cs.fin.w, A, ia);
-      fe r;
-      fe_load_be_words(r, sh_r);
-      status[b] = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
-      SMALL_STAMP(13);
-    }
-    return;
   }
   __syncthreads();
   if (t == 0) SMALL_STAMP(5);
@@ -1036,31 +822,86 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
   if (!sh_go) return;  // decided by the table (uniform)
   const uint32_t signs = sh_signs;
   const uint64_t tab = sh_tab;  // wave-uniform
-  // ---- phase 3 (the key-cache table)
-  if (wave == 0) {
-    fe x, y;
-    bool zero = true;
-    if (lane < BV_GNWIN) {  // G window `lane` of u1
-      uint32_t u[8];
+  // ---- phase 3
+  if (tab) {
+    if (wave == 0) {
+      fe x, y;
+      bool zero = true;
+      if (lane < BV_GNWIN) {  // G window `lane` of u1
+        uint32_t u[8];
 #pragma unroll
-      for (int k = 0; k < 8; k++) u[k] = sh_u1[k];
-      table_leaf<BV_GW, 8>(x, y, zero, g_table, u, (int)lane, false, false);
-    } else if (lane < (uint32_t)kSmallLeaves) {  // KC window j of k1 (T) or of k2 (phi(T))
-      const uint32_t q = lane - BV_GNWIN, h = q / BV_KCNWIN;
+        for (int k = 0; k < 8; k++) u[k] = sh_u1[k];
+        table_leaf<BV_GW, 8>(x, y, zero, g_table, u, (int)lane, false, false);
+      } else if (lane < (uint32_t)kSmallLeaves) {  // KC window j of k1 (T) or of k2 (phi(T))
+        const uint32_t q = lane - BV_GNWIN, h = q / BV_KCNWIN;
+        uint32_t kk[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) kk[k] = sh_k[4 * h + k];
+        table_leaf<BV_KCW, 4>(x, y, zero, (const uint32_t *)tab, kk, (int)(q % BV_KCNWIN), (signs >> h) & 1u,
+                              h != 0);
+      }
+      if (lane == 0) SMALL_STAMP(7);
+      small_leaf_pairs(x, y, zero, sh_b, sh_a, kSmallLeaves, lane);  // 22 leaves -> 11 nodes
+      if (lane == 0) SMALL_STAMP(8);
+      small_tree_level(sh_b, sh_c, 11, lane);  // -> 6
+      small_tree_level(sh_c, sh_b, 6, lane);   // -> 3
+      small_tree_level(sh_b, sh_c, 3, lane);   // -> 2
+      small_tree_level(sh_c, sh_b, 2, lane);   // -> 1
+      if (lane == 0) SMALL_STAMP(11);
+    }
+  } else {
+    if (wave == 0) {  // the G leaves and their subtree: 10 -> 5 -> 3 -> 2 -> 1
+      fe x, y;
+      bool zero = true;
+      if (lane < BV_GNWIN) {
+        uint32_t u[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) u[k] = sh_u1[k];
+        table_leaf<BV_GW, 8>(x, y, zero, g_table, u, (int)lane, false, false);
+      }
+      small_leaf_pairs(x, y, zero, sh_b, sh_a, BV_GNWIN, lane);
+      small_tree_level(sh_b, sh_c, 5, lane);
+      small_tree_level(sh_c, sh_b, 3, lane);
+      small_tree_level(sh_b, sh_c, 2, lane);  // the G sum in sh_c[0]
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 33; k++) sh_d[0].w[k] = sh_c[0].w[k];
+        SMALL_STAMP(7);
+      }
+    } else if (wave >= 2) {  // no table: k1 Q (wave 2) / k2 phi(Q) (wave 3), the NAF chain, wave-cooperative
+      const uint32_t h = wave - 2;
       uint32_t kk[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) kk[k] = sh_k[4 * h + k];
-      table_leaf<BV_KCW, 4>(x, y, zero, (const uint32_t *)tab, kk, (int)(q % BV_KCNWIN), (signs >> h) & 1u,
-                            h != 0);
+      const bool neg = (signs >> h) & 1u;
+      const uint32_t c = coop::pos();
+      uint32_t px = c < 8 ? sh_q[c] : 0u, py = c < 8 ? sh_q[8 + c] : 0u;
+      if (h) px = coop::mul(px, c < 8 ? FE_BETA[c] : 0u);  // phi(Q) = (beta x, y)
+      if (neg) py = coop::norm(coop::negw(py));
+      uint32_t X, Y, Z;
+      bool inf;
+      coop::naf_mul(X, Y, Z, inf, px, py, kk);
+      uint32_t ZZ = 0, ZZZ = 0;
+      if (!inf) {
+        ZZ = coop::mul(Z, Z);
+        ZZZ = coop::mul(ZZ, Z);
+      }
+      if (lane < 8) {
+        sh_d[1 + h].w[lane] = X;
+        sh_d[1 + h].w[8 + lane] = Y;
+        sh_d[1 + h].w[16 + lane] = ZZ;
+        sh_d[1 + h].w[24 + lane] = ZZZ;
+      }
+      if (lane == 0) {
+        sh_d[1 + h].w[32] = inf ? 1u : 0u;
+        SMALL_STAMP(9 + h);
+      }
     }
-    if (lane == 0) SMALL_STAMP(7);
-    small_leaf_pairs(x, y, zero, sh_b, sh_a, kSmallLeaves, lane);  // 22 leaves -> 11 nodes
-    if (lane == 0) SMALL_STAMP(8);
-    small_tree_level(sh_b, sh_c, 11, lane);  // -> 6
-    small_tree_level(sh_c, sh_b, 6, lane);   // -> 3
-    small_tree_level(sh_b, sh_c, 3, lane);   // -> 2
-    small_tree_level(sh_c, sh_b, 2, lane);   // -> 1
-    if (lane == 0) SMALL_STAMP(11);
+    __syncthreads();
+    if (wave == 0) {  // (G + k1 Q) + k2 phi(Q)
+      small_tree_level(sh_d, sh_c, 3, lane);
+      small_tree_level(sh_c, sh_b, 2, lane);
+    }
   }
   // ---- phase 4: the root (sh_b[0]) -> the decision
   if (t == 0) {

@@ -329,9 +329,9 @@ def test_small_batch_kernel_equals_oracle(monkeypatch):
 
 def test_small_batch_kernel_warm_up_to_1024(monkeypatch):
     """A 1000-event batch whose keys all have key-cache tables takes k_small
-    (no doubling chain: BV_SMALL_WARM_MAX, 1024, above the cold limit
-    BV_SMALL_MAX); the same batch through the bulk pipeline (limits 256).
-    Both equal to the oracle, corrupted signatures included."""
+    (no per-item NAF chain: BV_SMALL_WARM_MAX, 1024, above the cold limit
+    BV_SMALL_MAX, 256); the same batch through the bulk pipeline (limits
+    256).  Both equal to the oracle, corrupted signatures included."""
     from babble_amd.verifier import Verifier
 
     b = synth.events(1000, n_creators=6, seed=911)
@@ -350,6 +350,25 @@ def test_small_batch_kernel_warm_up_to_1024(monkeypatch):
             assert int((res.status == 1).sum()) == 998
         finally:
             v.close()
+
+
+def test_small_batch_first_call_in_fresh_processes():
+    """The first k_small batch of a process (cold instruction and
+    translation caches), in fresh child processes: 500 valid single-creator
+    events, every status equal to the oracle.  Round 5's right-to-left cold
+    path gave a false REJECT here in ~1 process of 6 (tools/dbg_first_call.py);
+    the round-4 cold path, 0 of 48."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CHILD="1", MODE="cold")
+    for _ in range(6):
+        r = subprocess.run([sys.executable, os.path.join(root, "tools", "dbg_first_call.py")], env=env,
+                           capture_output=True, text=True, timeout=120)
+        line = [x for x in r.stdout.splitlines() if x.startswith("result")]
+        assert r.returncode == 0 and line, r.stderr[-2000:]
+        assert line[-1].endswith("mismatches 0"), line[-1]
 
 
 def test_small_batch_randomized_against_oracle():

@@ -1,11 +1,10 @@
 """k_small phase clocks (BV_SMALL_STAMPS=1: the library prints workgroup 0's
 s_memtime stamps per call to stderr) for 1 / 100 events, key cache warm and
 cold, beside each call's host wall clock.  Stamps (clocks from the kernel's
-first instruction; -1 = not reached): 2 s^-1, 3 key decode, then
-  warm: 5 phase-1 barrier, 6 scalars (u1, u2, GLV), 7 leaves loaded,
-        8 affine leaf pairs, 11 tree root, 13 the decision;
-  cold: 7 the G sum (wave 0), 10 the k2 phi(Q) half (wave 3), 12 the
-        doubling chain's end (wave 2), 13 the decision (wave 1).
+first instruction): 1 SHA-256 of the item's message, 2 s^-1, 3 key decode,
+4 digest of message b, 5 phase-1 barrier, 6 scalars (u1, u2, GLV), 7/8 the
+two G halves, 9/10 the two Q halves, 11 phase-3 barrier, 12 the two pair
+sums, 13 the decision.
 
     python tools/small_stamps.py > gpurun_out/small_stamps.log 2>&1
 """
