@@ -738,6 +738,18 @@ int bv_item_pipe::upto(uint64_t end) {
   return BV_OK;
 }
 
+int bv_run_deferred(bv_ctx *ctx, const bv_batch *b, const bv_out &o, hipStream_t st) {
+  if (!ctx->S().kc_partial || b->n_items == 0) return BV_OK;
+  const uint64_t n = b->n_items;
+  HIPCHK(ctx->S().defer.ensure((n + 1) * 4), BV_E_OOM, "alloc deferred list");
+  HIPCHK(bvk::verify_deferred(st, n, ctx->S().defer.as<uint32_t>(), b->item_key, (const uint32_t *)b->r_be,
+                              (const uint32_t *)b->s_be, b->pre, ctx->S().kstatus.as<uint8_t>(),
+                              ctx->S().kxy.as<uint32_t>(), b->item_msg, o.dig, ctx->S().scratch.as<uint32_t>(),
+                              ctx->g_table, o.status, o.bits),
+         BV_E_LAUNCH, "k_verify_deferred");
+  return BV_OK;
+}
+
 int bv_item_pipe::finish() {
   const uint64_t n = b->n_items;
   if (n == 0) {
@@ -745,8 +757,9 @@ int bv_item_pipe::finish() {
     HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_KEYS], 0), BV_E_LAUNCH, "join");
     for (int e : {E_SCALAR, E_G, E_JOINED}) HIPCHK(hipEventRecord(ctx->S().ev[e], st), BV_E_LAUNCH, "event");
   }
-  const int r = upto(n);
+  int r = upto(n);
   if (r != BV_OK) return r;
+  if (kc && (r = bv_run_deferred(ctx, b, o, st)) != BV_OK) return r;
   HIPCHK(hipEventRecord(ctx->S().ev[E_END], st), BV_E_LAUNCH, "event");
   return bv_mark_done(ctx, st);
 }
@@ -775,6 +788,7 @@ int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
   HIPCHK(hipEventRecord(ev[E_JOINED], st), BV_E_LAUNCH, "event");
   rc = bv_launch_items(ctx, b, o, st, kc, 0, n_items, 2);
   if (rc != BV_OK) return rc;
+  if (kc && (rc = bv_run_deferred(ctx, b, o, st)) != BV_OK) return rc;
   HIPCHK(hipEventRecord(ev[E_END], st), BV_E_LAUNCH, "event");
   if (d_msg_hash && (uint8_t *)o.dig != d_msg_hash)
     HIPCHK(hipMemcpyAsync(d_msg_hash, o.dig, n_msgs * 32, hipMemcpyDeviceToDevice, st), BV_E_LAUNCH, "copy digests");

@@ -44,6 +44,10 @@ hipError_t sinv(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint8_t
 hipError_t verify_gq(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
                      const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
                      const uint32_t *, const uint64_t *, uint8_t *, uint64_t *);
+// list: n + 1 words (the deferred items' indices, then their count)
+hipError_t verify_deferred(hipStream_t, uint64_t, uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *,
+                           const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
+                           const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
 hipError_t verify_qf(hipStream_t, int, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
                      const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
                      const uint64_t *, uint32_t *);
@@ -255,6 +259,10 @@ struct bv_ctx {
     DevBuf kc_tabs;          // key-cache table address per batch key
     PinnedBuf pin_small;     // its host staging
     bool kc_decoded = false; // bv_kc_prepare already ran k_key_decode into kstatus / kxy on the call stream
+    // key cache, partial batch: a few valid keys have no table; their items
+    // are left BV_DEFERRED by the KC kernels and finished by bv_run_deferred
+    bool kc_partial = false;
+    DevBuf defer;  // the deferred items' indices, then their count
     // caller result ranges [lo, hi) of this slot's device calls that the
     // other slots' calls have not yet been ordered after (deduplicated)
     std::vector<std::array<uintptr_t, 6>> uncovered;
@@ -371,6 +379,9 @@ struct bv_item_pipe {
 };
 int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc);
+// key cache, partial batch (kc_partial): the BV_DEFERRED items by the
+// generic per-lane path, on `st` after the call's last verify kernel
+int bv_run_deferred(bv_ctx *ctx, const bv_batch *b, const bv_out &o, hipStream_t st);
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
                   const uint64_t *dko, hipStream_t st, bool *use, bool force_build = false);
 uint32_t bv_kc_lookup(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, uint64_t *tabs);

@@ -44,6 +44,7 @@ constexpr uint64_t kKcSubBytes = BV_KCSUB_U32 * 4;
 constexpr uint32_t kKcBases = 22;       // bases_jac allocation per key (>= BV_KCNSUB)
 constexpr uint32_t kKcBuildGroup = 8;   // keys per KC build launch (pscr: 403 MB per key)
 constexpr size_t kKcMemoMax = 4096;     // entries of kc_seen / kc_bad
+constexpr uint64_t kKcPartialRatio = 16;  // partial batches: at most 1 valid key in 16 without a table
 
 bool key_form_ok(const uint8_t *p, uint64_t len) { return len == 65 && p[0] == 4; }
 
@@ -92,6 +93,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
                   const uint64_t *dko, hipStream_t st, bool *use, bool force_build) {
   *use = false;
   ctx->S().kc_decoded = false;
+  ctx->S().kc_partial = false;
   if (n_keys == 0 || n_keys > kKcMaxBatchKeys) return BV_OK;
   if (ctx->S().has_done)  // the slot's pin_small may still feed its previous (async) call
     HIPCHK(hipEventSynchronize(ctx->S().done), BV_E_LAUNCH, "sync slot");
@@ -101,6 +103,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
   std::unordered_map<std::string, uint32_t> first;
   std::vector<uint32_t> unknown, admit;
   bool blocked = false;
+  uint32_t n_blocked = 0;  // distinct valid keys without a table that may not get one yet
   uint32_t hits = 0;
   auto key_of = [&](uint32_t k) { return std::string((const char *)hkb + hko[k], (size_t)(hko[k + 1] - hko[k])); };
   auto admitted = [&](const std::string &key, uint32_t seen) {
@@ -126,7 +129,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
     auto s = ctx->kc_seen.find(key);
     if (s != ctx->kc_seen.end()) {
       if (admitted(key, ++s->second)) admit.push_back(k);
-      else blocked = true;
+      else blocked = true, n_blocked++;
       continue;
     }
     unknown.push_back(k);
@@ -152,13 +155,14 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
       if (ctx->kc_seen.size() >= kKcMemoMax) ctx->kc_seen.clear();
       ctx->kc_seen[key] = 1;
       if (admitted(key, 1)) admit.push_back(k);
-      else blocked = true;
+      else blocked = true, n_blocked++;
     }
   }
   // Every return below that leaves *use false after this call's k_key_decode
   // was launched on `st` waits for it first: the per-batch path then decodes
   // the batch again on the s^-1 stream into the same buffers.
   auto bail = [&]() -> int {
+    ctx->S().kc_partial = false;
     ctx->timing.kc_hits = hits;
     ctx->timing.kc_builds = 0;
     ctx->timing.kc_keys = (uint32_t)ctx->kc_index.size();
@@ -168,7 +172,17 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
     }
     return BV_OK;
   };
-  if (blocked && !force_build) return bail();  // a valid key without a table: per-batch path
+  // A valid key without a table: when such keys are few against the batch's
+  // cached / admitted keys (at most 1 in kKcPartialRatio), the batch keeps
+  // the cache and only their items take the generic path afterwards
+  // (bv_run_deferred; ADVICE r4: a fresh key in every batch used to send the
+  // whole batch, cached validators included, to the per-batch tables);
+  // otherwise the per-batch path.
+  if (blocked && !force_build) {
+    const uint64_t tabled = hits + admit.size();
+    if (tabled == 0 || (uint64_t)n_blocked * kKcPartialRatio > tabled + n_blocked) return bail();
+    ctx->S().kc_partial = true;
+  }
 
   // Registration builds as many registered keys as the budget holds (in the
   // caller's order); the rest stay uncached (timing.kc_keys tells).  A
@@ -306,7 +320,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
   ctx->timing.kc_hits = hits;
   ctx->timing.kc_builds = builds;
   ctx->timing.kc_keys = (uint32_t)ctx->kc_index.size();
-  if (blocked) return BV_OK;  // force_build: the tables are built, this batch still takes the per-batch path
+  if (blocked && !ctx->S().kc_partial) return BV_OK;  // force_build: the tables are built, this batch still takes the per-batch path
   // per-batch array: the table address of every batch key (null: no table;
   // only keys whose batch decode is not KS_OK have none, and theirs is never read)
   HIPCHK(ctx->S().pin_small.ensure((uint64_t)n_keys * 8 + 64), BV_E_OOM, "alloc pinned");

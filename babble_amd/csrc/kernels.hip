@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "evjson.h"
@@ -575,6 +576,38 @@ __global__ void __launch_bounds__(256) k_verify_generic(uint64_t n_items, uint64
   if (i < hi)
     st = verify_item_generic<LAT>(i, item_key, r_be, s_be, pre, kstatus, kxy, item_msg, digest_words, w_in, g_table);
   write_status(i, hi, st, status, bits);
+}
+
+// Key cache, partial batch (verify_core.h BV_DEFERRED): the deferred items'
+// indices, appended in any order (`list[n]` counts them), then the generic
+// per-lane path over that list, grid-stride (they are few: keys without a
+// table yet).  A deferred item's accept bit is OR-ed into its word, whose
+// other bits the KC kernel already wrote.
+__global__ void __launch_bounds__(256) k_defer_list(uint64_t n, const uint8_t *__restrict__ status,
+                                                    uint32_t *__restrict__ list) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && status[i] == BV_DEFERRED) list[atomicAdd(list + n, 1u)] = (uint32_t)i;
+}
+__global__ void __launch_bounds__(64) k_verify_deferred(uint64_t n, const uint32_t *__restrict__ list,
+                                                        const uint32_t *__restrict__ item_key,
+                                                        const uint32_t *__restrict__ r_be,
+                                                        const uint32_t *__restrict__ s_be,
+                                                        const uint8_t *__restrict__ pre,
+                                                        const uint8_t *__restrict__ kstatus,
+                                                        const uint32_t *__restrict__ kxy,
+                                                        const uint32_t *__restrict__ item_msg,
+                                                        const uint32_t *__restrict__ digest_words,
+                                                        const uint32_t *__restrict__ w_in,
+                                                        const uint32_t *__restrict__ g_table,
+                                                        uint8_t *__restrict__ status, uint64_t *__restrict__ bits) {
+  const uint32_t cnt = list[n];
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < cnt; t += gridDim.x * blockDim.x) {
+    const uint64_t i = list[t];
+    const uint8_t st =
+        verify_item_generic<true>(i, item_key, r_be, s_be, pre, kstatus, kxy, item_msg, digest_words, w_in, g_table);
+    status[i] = st;
+    if (st == BV_ACCEPT) atomicOr((unsigned long long *)bits + (i >> 6), 1ull << (i & 63));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1231,6 +1264,19 @@ hipError_t verify_small(hipStream_t st, uint32_t n_items, const uint8_t *dig, co
   hipLaunchKernelGGL(k_small, dim3(n_items), dim3(256), 0, st, n_items, (const uint32_t *)dig, key_bytes, key_off,
                      item_msg, item_key, (const uint32_t *)r_be, (const uint32_t *)s_be, pre, kc_tabs, g_table,
                      status, stamps);
+  return hipGetLastError();
+}
+
+hipError_t verify_deferred(hipStream_t st, uint64_t n, uint32_t *list, const uint32_t *item_key,
+                           const uint32_t *r_be, const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst,
+                           const uint32_t *kxy, const uint32_t *item_msg, const uint32_t *dig, const uint32_t *w,
+                           const uint32_t *g_table, uint8_t *status, uint64_t *bits) {
+  if (n == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(list + n, 0, 4, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_defer_list, grid1(n, 256), dim3(256), 0, st, n, status, list);
+  hipLaunchKernelGGL(k_verify_deferred, dim3((unsigned)std::min<uint64_t>(1024, (n + 63) / 64)), dim3(64), 0, st, n,
+                     list, item_key, r_be, s_be, pre, kst, kxy, item_msg, dig, w, g_table, status, bits);
   return hipGetLastError();
 }
 

@@ -427,6 +427,12 @@ DEV void item_scalars(uint64_t i, const uint32_t *r_be, const uint32_t *item_msg
   glv_split(k1, k2, signs, b);
 }
 
+// Key-cache batches with a few keys that have no table yet (bv_kc_prepare's
+// partial mode): their items reach the math without a table; the
+// KC kernels leave them as BV_DEFERRED (accept bit 0) and k_verify_deferred
+// finishes them by the generic path.  Never returned to a caller.
+#define BV_DEFERRED 0xFE
+
 // ---------------------------------------------------------------------------
 // Item decision table.  Returns 0xFF when the item must run
 // the math, else its final status.  The host pre-class is re-checked against
@@ -645,6 +651,7 @@ DEV uint8_t verify_item_q(uint64_t i, uint64_t n, const uint32_t *item_key, cons
   rg_load(rg, n, i, R, inf);
   const uint32_t *tab = key_tabs ? (const uint32_t *)key_tabs[item_key[i]]
                                  : key_table + (uint64_t)item_key[i] * (KC ? 1 : 2) * half;
+  if (!tab) return BV_DEFERRED;  // key cache, partial batch: no table for this key
   // One loop body for both GLV halves (one inlined copy of the point
   // addition: smaller code, fewer live registers than two calls).
 #pragma unroll 1
@@ -693,6 +700,10 @@ DEV void verify_item_qfirst(uint64_t i, uint64_t n, const uint32_t *item_key, co
   fe_set(R.ZZZ, 0);
   const uint32_t *tab = key_tabs ? (const uint32_t *)key_tabs[item_key[i]]
                                  : key_table + (uint64_t)item_key[i] * (KC ? 1 : 2) * half;
+  if (!tab) {  // key cache, partial batch: k_verify_gf leaves the item BV_DEFERRED
+    rq[(uint64_t)32 * n + i] = 2u;
+    return;
+  }
 #pragma unroll 1
   for (int h = 0; h < 2; h++) {
     uint32_t kk[4];
@@ -711,6 +722,7 @@ DEV uint8_t verify_item_gfinish(uint64_t i, uint64_t n, const uint32_t *item_key
   fe r;
   const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
   if (st != 0xFF) return st;
+  if (rq[(uint64_t)32 * n + i] == 2u) return BV_DEFERRED;  // no key table (k_verify_qf)
   uint32_t u[8];
   {
     sc w, e, a;
@@ -743,6 +755,8 @@ DEV uint8_t verify_item_gq_kc(uint64_t i, const uint32_t *item_key, const uint32
   fe r;
   const uint8_t st = classify_item(i, item_key, r_be, s_be, pre, kstatus, r);
   if (st != 0xFF) return st;
+  const uint32_t *tab = (const uint32_t *)key_tabs[item_key[i]];
+  if (!tab) return BV_DEFERRED;  // partial batch: no table for this key
   uint32_t u[8], k1[4], k2[4], signs;
   item_scalars(i, r_be, item_msg, digest_words, w_in, u, k1, k2, signs);
   gexz R;
@@ -752,7 +766,6 @@ DEV uint8_t verify_item_gq_kc(uint64_t i, const uint32_t *item_key, const uint32
   fe_set(R.ZZ, 0);
   fe_set(R.ZZZ, 0);
   g_table_add<BV_GW, BV_GNWIN, LAT>(R, inf, g_table, u);
-  const uint32_t *tab = (const uint32_t *)key_tabs[item_key[i]];
 #pragma unroll 1
   for (int h = 0; h < 2; h++) {
     uint32_t kk[4];

@@ -71,10 +71,13 @@ extern "C" {
                              (env BV_KC_ADMIT); tables are LRU-evicted past
                              the cache budget (env BV_KEY_CACHE_GB, default
                              96), registered keys only for other registered
-                             keys.  Malformed keys are never given a table;
-                             a batch with a valid key that has no table takes
-                             the per-batch table path.  Off by default: tables
-                             are then rebuilt for every batch.                 */
+                             keys.  Malformed keys are never given a table.
+                             A batch whose valid keys without a table are at
+                             most 1 in 16 of its valid keys keeps the cache
+                             (their items are finished by the generic path
+                             after the cached ones); with more, the batch
+                             takes the per-batch table path.  Off by default:
+                             tables are then rebuilt for every batch.          */
 #define BV_F_K8 2u        /* per-batch tables: never use the 12-bit tables
                              (2.75 MiB per key); 8-bit only (512 KiB per key) */
 #define BV_F_KNOWN (BV_F_KEY_CACHE | BV_F_K8)

@@ -475,3 +475,40 @@ def test_pinned_host_entry_zero_copy():
     finally:
         v.close()
         arena.close()
+
+
+@pytest.mark.parametrize("device_api", [False, True])
+def test_key_cache_partial_batch(monkeypatch, device_api):
+    """a batch whose keys are all cached but one fresh valid key
+    (not registered, not yet admitted) keeps the key cache for the cached
+    keys; the fresh key's items are left BV_DEFERRED by the KC kernels and
+    finished by the generic path (bv_run_deferred).  Corrupted signatures
+    on both kinds of key; every status, digest and bit equal to the oracle.
+    With 3 fresh keys of 20 (more than 1 in 16) the batch takes the
+    per-batch tables as before."""
+    from babble_amd.verifier import Verifier
+
+    monkeypatch.setenv("BV_KC_ADMIT", "1000")  # no fresh key gets a table during the test (read at bv_create)
+    b = synth.events(30_000, n_creators=20, seed=62)
+    rng = np.random.default_rng(62)
+    for i in rng.choice(b.n_items, 300, replace=False):
+        b.r_be[i, int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
+    keys = [b.key(k) for k in range(b.n_keys)]
+    for fresh, partial in ((1, True), (3, False)):
+        v = Verifier(device=0, flags=native.F_KEY_CACHE)
+        try:
+            v.register_keys(keys[fresh:])
+            if device_api:
+                d = v.to_device(b)
+                v.verify_device(d)
+                res = d.result()
+            else:
+                res = v.verify(b)
+            st = oracle_check(res, b)
+            assert int((st == native.ACCEPT).sum()) == b.n_items - 300
+            t = v.timing()
+            assert (t["key_path"] == 22) == partial, t
+            if partial:
+                assert t["kc_hits"] == 20 - fresh and t["kc_builds"] == 0
+        finally:
+            v.close()

@@ -39,8 +39,13 @@ if mode == "warm":
     v.register_keys([evs[0].Body.Creator])
 else:
     v = Verifier(0)
-if os.environ.get("PRECALL"):  # one unrelated device call first
+if os.environ.get("PRECALL") == "1":  # one unrelated device call first
     v.sha256([b"x" * 100])
+elif os.environ.get("PRECALL") == "2":  # a different 500-event cold batch first
+    bb2 = BatchBuilder()
+    for ev in make_db(500, seed=77):
+        bb2.add_item(bb2.add_msg(ev.Body.Marshal()), bb2.add_key(ev.Body.Creator or b""), ev.Signature)
+    v.verify(bb2.pack())
 res = v.verify(p)
 h, st, _ = coracle.verify_batch(p.as_dict())
 bad = np.flatnonzero(res.status != st)
