@@ -517,10 +517,14 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
     HIPCHK(hipStreamWaitEvent(st, landed, 0), BV_E_LAUNCH, "join chunk");
     HIPCHK(bvk::ev_body_hash(st, d, e0, e1, dig), BV_E_LAUNCH, "k_ev_body_hash");
     HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");  // the last chunk's record is used
-    if (split_verify) {
-      hipEvent_t hashed = ctx->chunk_ev[(c + 32) % ctx->chunk_ev.size()];  // waited on at once: reuse is safe
-      HIPCHK(hipEventRecord(hashed, st), BV_E_LAUNCH, "event");
-      HIPCHK(hipStreamWaitEvent(vst, hashed, 0), BV_E_LAUNCH, "join chunk digests");
+    hipEvent_t hashed = ctx->chunk_ev[(c + 32) % ctx->chunk_ev.size()];  // waited on before chunk c+2's record
+    HIPCHK(hipEventRecord(hashed, st), BV_E_LAUNCH, "event");
+    if (split_verify) HIPCHK(hipStreamWaitEvent(vst, hashed, 0), BV_E_LAUNCH, "join chunk digests");
+    if (d2h == 2 && c > 0) {  // the previous chunk's digests, on the copy stream behind this chunk's H2D
+      const uint64_t p0 = cb[c - 1];
+      HIPCHK(hipStreamWaitEvent(cs, ctx->chunk_ev[(c + 31) % ctx->chunk_ev.size()], 0), BV_E_LAUNCH, "join");
+      HIPCHK(hipMemcpyAsync(hout + p0 * 32, dig + p0 * 8, (e0 - p0) * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH,
+             "d2h digests");
     }
     rc = pipe.upto(e1);
     if (rc != BV_OK) return rc;
@@ -531,21 +535,30 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   if (d2h == 0) {  // one copy once the last chunk is hashed, on the copy stream
     HIPCHK(hipStreamWaitEvent(cs, ctx->S().ev[E_HASHED], 0), BV_E_LAUNCH, "join");
     HIPCHK(hipMemcpyAsync(hout, dig, n * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH, "d2h digests");
+  } else if (d2h == 2) {  // the last chunk's digests
+    const uint64_t p0 = cb[cb.size() - 2];
+    HIPCHK(hipStreamWaitEvent(cs, ctx->S().ev[E_HASHED], 0), BV_E_LAUNCH, "join");
+    HIPCHK(hipMemcpyAsync(hout + p0 * 32, dig + p0 * 8, (n - p0) * 32, hipMemcpyDeviceToHost, cs), BV_E_LAUNCH,
+           "d2h digests");
   }
   HIPCHK(hipEventRecord(ctx->S().ev[E_STAGED], cs), BV_E_LAUNCH, "event");
   call.ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - call.t0).count();
 
   HIPCHK(hipEventRecord(ctx->S().ev[E_SHA], st), BV_E_LAUNCH, "event");
-  HIPCHK(hipEventRecord(ctx->S().ev[E_CSDONE], d2h == 0 ? cs : st), BV_E_LAUNCH, "event");
+  if (d2h != 2) HIPCHK(hipEventRecord(ctx->S().ev[E_CSDONE], d2h == 0 ? cs : st), BV_E_LAUNCH, "event");
 
   rc = pipe.finish();  // the last chunk's items
   if (rc != BV_OK) return rc;
-  if (split_verify) HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_END], 0), BV_E_LAUNCH, "join verify");
-  HIPCHK(hipMemcpyAsync(call.direct_status ? res->status : pout + o_st, pipe.o.status, n, hipMemcpyDeviceToHost, st),
+  // statuses and bits: on the copy stream (SDMA) with the digests in mode 2,
+  // else on the main stream
+  hipStream_t os = d2h == 2 ? cs : st;
+  if (split_verify || d2h == 2) HIPCHK(hipStreamWaitEvent(os, ctx->S().ev[E_END], 0), BV_E_LAUNCH, "join verify");
+  HIPCHK(hipMemcpyAsync(call.direct_status ? res->status : pout + o_st, pipe.o.status, n, hipMemcpyDeviceToHost, os),
          BV_E_LAUNCH, "d2h status");
-  HIPCHK(hipMemcpyAsync(pout + o_bits, pipe.o.bits, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, st), BV_E_LAUNCH,
+  HIPCHK(hipMemcpyAsync(pout + o_bits, pipe.o.bits, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, os), BV_E_LAUNCH,
          "d2h bits");
-  HIPCHK(hipEventRecord(ctx->S().ev[E_OUT], st), BV_E_LAUNCH, "event");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_OUT], os), BV_E_LAUNCH, "event");
+  if (d2h == 2) HIPCHK(hipEventRecord(ctx->S().ev[E_CSDONE], cs), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_CSDONE], 0), BV_E_LAUNCH, "join");  // digests out before ev_done
   HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_STAGED], 0), BV_E_LAUNCH, "join");  // staging free after ev_done
   rc = bv_mark_done(ctx, st);

@@ -304,8 +304,10 @@ struct bv_ctx {
   uint64_t host_msg_chunk = 64ull << 20, ev_chunk = 64ull << 20;
   bool ev_split_verify = true, small_path = true, qfirst = true;
   // host entries' digests to the host (BV_EV_D2H): 1 = one copy per hashed
-  // chunk, 0 = one copy after the last chunk (stores by the hashing kernel
-  // through the pinned buffer's device alias measured no better)
+  // chunk, 0 = one copy after the last chunk, 2 = bulk events only: each
+  // chunk's copy by SDMA on the copy stream behind the next chunk's H2D
+  // (profiles/r05_ab_ev_qfirst.log: 5.42-5.49 against 5.16-5.28 ms; stores
+  // by the hashing kernel through the pinned buffer's alias: no better)
   int ev_d2h = 1;
   int ev_tail = 0;  // bulk events' chunk plan (BV_EV_TAIL): 0 equal, 1 halving, 2 equal + one small last chunk
   uint64_t table_min_items = 8;    // per-batch tables (not the generic path) from this many items per key
