@@ -354,10 +354,11 @@ def test_small_batch_kernel_warm_up_to_1024(monkeypatch):
 
 def test_small_batch_first_call_in_fresh_processes():
     """The first k_small batch of a process (cold instruction and
-    translation caches), in fresh child processes: 500 valid single-creator
-    events, every status equal to the oracle.  Round 5's right-to-left cold
-    path gave a false REJECT here in ~1 process of 6 (tools/dbg_first_call.py);
-    the round-4 cold path, 0 of 48."""
+    translation caches), in fresh child processes: 256 valid single-creator
+    events (the cold k_small limit), every status equal to the oracle and
+    the batch on k_small's cold path (key_path 0).  Round 5's right-to-left
+    cold path gave a false REJECT on such first batches in ~1 process of 6
+    (tools/dbg_first_call.py, profiles/r05_small_r2l_investigation.log)."""
     import subprocess
     import sys
 
@@ -368,7 +369,7 @@ def test_small_batch_first_call_in_fresh_processes():
                            capture_output=True, text=True, timeout=120)
         line = [x for x in r.stdout.splitlines() if x.startswith("result")]
         assert r.returncode == 0 and line, r.stderr[-2000:]
-        assert line[-1].endswith("mismatches 0"), line[-1]
+        assert line[-1].endswith("mismatches 0") and "key_path 0 " in line[-1], line[-1]
 
 
 def test_small_batch_randomized_against_oracle():

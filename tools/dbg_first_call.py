@@ -28,7 +28,7 @@ from babble_amd.verifier import Verifier  # noqa: E402
 from oracle import coracle  # noqa: E402
 from tests.test_bootstrap import make_db  # noqa: E402
 
-evs = make_db(500)
+evs = make_db(int(os.environ.get("N_EVENTS", "256")))  # <= 256: the cold k_small limit
 bb = BatchBuilder()
 for ev in evs:
     bb.add_item(bb.add_msg(ev.Body.Marshal()), bb.add_key(ev.Body.Creator or b""), ev.Signature)
