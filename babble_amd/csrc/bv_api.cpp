@@ -28,6 +28,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <new>
 #include <thread>
 
 namespace {
@@ -201,6 +202,41 @@ extern "C" void bv_host_free(void *p) {
     g_pinned.erase(it);
   }
   (void)hipHostFree(p);
+}
+
+// The pinned arena (babbleverify.h): blocks that outlive calls.
+struct bv_arena {
+  void *p[BV_ARENA_SLOTS] = {};
+  size_t cap[BV_ARENA_SLOTS] = {};
+};
+
+extern "C" int bv_arena_create(bv_arena **out) {
+  if (!out) return BV_E_ARGS;
+  *out = new (std::nothrow) bv_arena();
+  return *out ? BV_OK : BV_E_OOM;
+}
+
+extern "C" void bv_arena_destroy(bv_arena *a) {
+  if (!a) return;
+  for (void *p : a->p) bv_host_free(p);
+  delete a;
+}
+
+extern "C" int bv_arena_reserve(bv_arena *a, uint32_t slot, size_t bytes, size_t keep, void **out, size_t *cap) {
+  if (!a || !out || slot >= BV_ARENA_SLOTS || keep > a->cap[slot]) return BV_E_ARGS;
+  if (bytes > a->cap[slot]) {
+    const size_t nc = std::max(bytes, 2 * a->cap[slot]);
+    void *np = nullptr;
+    const int rc = bv_host_alloc(nc, &np);
+    if (rc != BV_OK) return rc;
+    if (keep) memcpy(np, a->p[slot], keep);
+    bv_host_free(a->p[slot]);
+    a->p[slot] = np;
+    a->cap[slot] = nc;
+  }
+  *out = a->p[slot];
+  if (cap) *cap = a->cap[slot];
+  return BV_OK;
 }
 
 bool bv_is_pinned(const void *p, size_t n) {
@@ -485,12 +521,12 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
     if (ctx->has_done) (void)hipEventSynchronize(ctx->ev_done);
   }
   if (ctx->g_table) gtable_release(ctx->device);
-  DevBuf *bufs[] = {&ctx->d_in, &ctx->kc_kxy, &ctx->kc_btabs, &ctx->ev_iota};
+  DevBuf *bufs[] = {&ctx->d_in, &ctx->kc_kxy, &ctx->kc_btabs, &ctx->ev_iota, &ctx->d_stamps};
   for (auto *b : bufs) b->release();
   for (auto &sl : ctx->slot) {
     DevBuf *sb[] = {&sl.digests,   &sl.kstatus, &sl.kxy, &sl.bases_jac, &sl.key_sub, &sl.key_pscr,
                     &sl.key_table, &sl.scratch, &sl.u12, &sl.rg,        &sl.status,  &sl.bits,
-                    &sl.kc_tabs};
+                    &sl.kc_tabs,   &sl.defer};
     for (auto *b : sb) b->release();
     sl.pin_small.release();
     if (sl.done) (void)hipEventDestroy(sl.done);
@@ -529,13 +565,15 @@ void bv_read_small_span(bv_ctx *ctx) {
 
 extern "C" int bv_get_timing(const bv_ctx *ctx, bv_timing *out) {
   if (!ctx || !out) return BV_E_ARGS;
-  if (ctx->small_span) {  // (the ctx's own call bookkeeping, not its inputs)
-    bv_ctx *c = const_cast<bv_ctx *>(ctx);
-    std::lock_guard<std::mutex> lk(c->mu);
+  // under the ctx's lock: a call on another thread writes small_span and
+  // the timing; the span is the ctx's own call bookkeeping
+  bv_ctx *c = const_cast<bv_ctx *>(ctx);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->small_span) {
     (void)hipSetDevice(c->device);
     bv_read_small_span(c);
   }
-  *out = ctx->timing;
+  *out = c->timing;
   return BV_OK;
 }
 
@@ -866,7 +904,10 @@ static int verify_device_impl(bv_ctx *ctx, const bv_batch *dbatch, bv_result *dr
              "d2h key bytes");
       HIPCHK(bv_host_wait(ctx, st), BV_E_LAUNCH, "sync");
     }
-    int rc = bv_kc_prepare(ctx, nk, hkb.data(), hko.data(), dbatch->key_bytes, dbatch->key_off, st, &kc);
+    bv_kc_items items;
+    items.n_items = dbatch->n_items;
+    items.d_item_key = dbatch->item_key;
+    int rc = bv_kc_prepare(ctx, nk, hkb.data(), hko.data(), dbatch->key_bytes, dbatch->key_off, st, &kc, false, &items);
     if (rc != BV_OK) return rc;
   }
   return bv_run_device(ctx, dbatch, dresult->msg_hash, dresult->status, dresult->accept_bits, st, false, kc);
@@ -1065,7 +1106,10 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   bool kc = false;
   if ((ctx->flags & BV_F_KEY_CACHE) && n_keys && n_keys <= kKcMaxBatchKeys) {
     HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_KREADY], 0), BV_E_LAUNCH, "join");
-    rc = bv_kc_prepare(ctx, n_keys, b->key_bytes, b->key_off, d.key_bytes, d.key_off, st, &kc);
+    bv_kc_items items;
+    items.n_items = b->n_items;
+    items.h_item_key = b->item_key;
+    rc = bv_kc_prepare(ctx, n_keys, b->key_bytes, b->key_off, d.key_bytes, d.key_off, st, &kc, false, &items);
     if (rc != BV_OK) return rc;
   }
   // the key tables need only the keys and s^-1 only s: they run while the
@@ -1361,8 +1405,9 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
       if (stv[i] == BV_ACCEPT) res->accept_bits[i / 64] |= 1ull << (i % 64);
   }
   bv_timing &t = ctx->timing;
-  // (the device span is read from the events once the kernel has ended: at
-  // the next call's wait, or here when it already has)
+  // (the device span is read from the events once the kernel has ended:
+  // here when it already has, else when bv_get_timing asks; the next call
+  // on this ctx starts a new timing and drops an unread span)
   ctx->small_span = ctx->cur + 1;  // read lazily (bv_get_timing / bv_read_small_span)
   if (hipEventQuery(ctx->ev_done) == hipSuccess) bv_read_small_span(ctx);
   t.key_path = kc && hits ? BV_KCW : 0;

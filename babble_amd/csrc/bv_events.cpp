@@ -146,7 +146,10 @@ static int verify_events_dag_host(bv_ctx *ctx, const bv_event_batch *eb, bv_resu
   bool kc = false;
   if (ctx->flags & BV_F_KEY_CACHE) {
     HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_KREADY], 0), BV_E_LAUNCH, "join");
-    rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, vb.key_bytes, vb.key_off, st, &kc);
+    bv_kc_items items;
+    items.n_items = eb->n_events;
+    items.h_item_key = eb->creator;
+    rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, vb.key_bytes, vb.key_off, st, &kc, false, &items);
     if (rc != BV_OK) return rc;
   }
   put(o_s, eb->s_be, n * 32);
@@ -453,7 +456,10 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   HIPCHK(hipEventRecord(ctx->S().ev[E_KREADY], cs), BV_E_LAUNCH, "event");
   if (ctx->flags & BV_F_KEY_CACHE) {
     HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_KREADY], 0), BV_E_LAUNCH, "join");
-    rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, d.key_bytes, d.key_off, st, &kc);
+    bv_kc_items items;
+    items.n_items = eb->n_events;
+    items.h_item_key = eb->creator;
+    rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, d.key_bytes, d.key_off, st, &kc, false, &items);
     if (rc != BV_OK) return rc;
   }
   rc = stage(keys_end, s_end);  // s, pre: s^-1

@@ -329,8 +329,8 @@ struct bv_host_call {
   bool direct_in = false;                          // message bytes DMA'd from the caller's pinned buffer
   bool direct_hash = false, direct_status = false;  // results DMA'd into the caller's pinned buffers
 };
-bool bv_is_pinned(const void *p, size_t n);
-void bv_read_small_span(bv_ctx *ctx);  // a small batch's device span into ctx->timing (bv_api.cpp)  // [p, p+n) inside one bv_host_alloc block
+bool bv_is_pinned(const void *p, size_t n);  // [p, p+n) inside one bv_host_alloc block
+void bv_read_small_span(bv_ctx *ctx);        // a small batch's device span into ctx->timing (bv_api.cpp)
 
 int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess);
 hipStream_t bv_copy_stream(bv_ctx *ctx);   // the device's copy stream (created on first use; nullptr on failure)
@@ -384,8 +384,16 @@ int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
 // key cache, partial batch (kc_partial): the BV_DEFERRED items by the
 // generic per-lane path, on `st` after the call's last verify kernel
 int bv_run_deferred(bv_ctx *ctx, const bv_batch *b, const bv_out &o, hipStream_t st);
+// the batch's item -> key map for the partial-mode item bound (host copy,
+// or the device one, copied back only when the batch has table-less keys)
+struct bv_kc_items {
+  uint64_t n_items = 0;
+  const uint32_t *h_item_key = nullptr;
+  const uint32_t *d_item_key = nullptr;
+};
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
-                  const uint64_t *dko, hipStream_t st, bool *use, bool force_build = false);
+                  const uint64_t *dko, hipStream_t st, bool *use, bool force_build = false,
+                  const bv_kc_items *items = nullptr);
 uint32_t bv_kc_lookup(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, uint64_t *tabs);
 bool bv_kc_all_cached(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko);
 void bv_kc_init(bv_ctx *ctx);     // budget, admission and fault-injection settings (bv_create)

@@ -90,7 +90,7 @@ static hipError_t kc_table_alloc(bv_ctx *ctx, void **p) {
 // (bv_kc_register) builds the admitted keys even when the batch itself could
 // not use the cache.  hkb/hko: host copies of the key bytes; dkb/dko: device.
 int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64_t *hko, const uint8_t *dkb,
-                  const uint64_t *dko, hipStream_t st, bool *use, bool force_build) {
+                  const uint64_t *dko, hipStream_t st, bool *use, bool force_build, const bv_kc_items *items) {
   *use = false;
   ctx->S().kc_decoded = false;
   ctx->S().kc_partial = false;
@@ -102,6 +102,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
   std::vector<uint32_t> alias(n_keys);  // a repeated key -> its first index in the batch
   std::unordered_map<std::string, uint32_t> first;
   std::vector<uint32_t> unknown, admit;
+  std::vector<uint8_t> is_blocked(n_keys, 0);  // per batch key (first occurrence): valid, no table, not admitted
   bool blocked = false;
   uint32_t n_blocked = 0;  // distinct valid keys without a table that may not get one yet
   uint32_t hits = 0;
@@ -129,7 +130,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
     auto s = ctx->kc_seen.find(key);
     if (s != ctx->kc_seen.end()) {
       if (admitted(key, ++s->second)) admit.push_back(k);
-      else blocked = true, n_blocked++;
+      else blocked = true, n_blocked++, is_blocked[k] = 1;
       continue;
     }
     unknown.push_back(k);
@@ -155,7 +156,7 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
       if (ctx->kc_seen.size() >= kKcMemoMax) ctx->kc_seen.clear();
       ctx->kc_seen[key] = 1;
       if (admitted(key, 1)) admit.push_back(k);
-      else blocked = true, n_blocked++;
+      else blocked = true, n_blocked++, is_blocked[k] = 1;
     }
   }
   // Every return below that leaves *use false after this call's k_key_decode
@@ -177,10 +178,31 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
   // the cache and only their items take the generic path afterwards
   // (bv_run_deferred; ADVICE r4: a fresh key in every batch used to send the
   // whole batch, cached validators included, to the per-batch tables);
-  // otherwise the per-batch path.
+  // otherwise the per-batch path.  The deferred items run the per-lane
+  // generic path after the batch's last verify kernel (a ~2.6 ms serial
+  // chain of 128 doublings per lane), so they are bounded by ITEM count too
+  // (ADVICE r5): when the table-less keys carry more than 1 item in
+  // kKcPartialRatio, the per-batch tables take the batch.
   if (blocked && !force_build) {
     const uint64_t tabled = hits + admit.size();
     if (tabled == 0 || (uint64_t)n_blocked * kKcPartialRatio > tabled + n_blocked) return bail();
+    if (items && items->n_items) {
+      std::vector<uint32_t> keys;  // the caller's item -> key map, on the host
+      const uint32_t *ik = items->h_item_key;
+      if (!ik) {  // (device entry) one copy, only on this rare path
+        keys.resize(items->n_items);
+        HIPCHK(hipMemcpyAsync(keys.data(), items->d_item_key, items->n_items * 4, hipMemcpyDeviceToHost, st),
+               BV_E_LAUNCH, "d2h item_key");
+        HIPCHK(bv_host_wait(ctx, st), BV_E_LAUNCH, "sync");
+        ik = keys.data();
+      }
+      uint64_t deferred = 0;
+      for (uint64_t i = 0; i < items->n_items; i++) {
+        const uint32_t k = ik[i];
+        deferred += k < n_keys && is_blocked[alias[k]];
+      }
+      if (deferred * kKcPartialRatio > items->n_items) return bail();
+    }
     ctx->S().kc_partial = true;
   }
 

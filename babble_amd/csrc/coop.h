@@ -213,28 +213,89 @@ __device__ __forceinline__ void madd(uint32_t &X, uint32_t &Y, uint32_t &Z, bool
   Z = Z3;
 }
 
+// beta's limb for this lane (phi(x, y) = (beta x, y))
+__device__ __forceinline__ uint32_t beta_limb() { return pos() < 8 ? FE_BETA[pos()] : 0u; }
+
+// XYZZ doubling dbl-2008-s-1 (a = 0; x = X / ZZ, y = Y / ZZZ, the same
+// formulas as point.h gexz_double), state replicated in every row; the nine
+// products form three levels {U^2, X^2} -> {U V, X V, V ZZ, M^2} ->
+// {M (S - X3), W Y, W ZZZ, beta X3} with U = 2Y, M = 3X^2; the fourth product
+// of the last level is beta X3 of the result (phi's x for free).  The input
+// is not the identity; Y == 0 cannot occur on secp256k1.
+__device__ __forceinline__ void dbl_xyzz(uint32_t &X, uint32_t &Y, uint32_t &ZZ, uint32_t &ZZZ, uint32_t &BX) {
+  const uint32_t r = row();
+  const uint32_t U = norm(2ull * Y);
+  uint32_t m = mul(r == 0 ? U : X, r == 0 ? U : X);  // row 0: V = U^2, row 1: X^2
+  const uint32_t V = from_row(m, 0), XX = from_row(m, 1);
+  const uint32_t M = norm(3ull * XX);
+  // row 0: W = U V, row 1: S = X V, row 2: ZZ3 = V ZZ, row 3: M^2
+  m = mul(r == 0 ? U : r == 1 ? X : r == 2 ? ZZ : M, r == 3 ? M : V);
+  const uint32_t W = from_row(m, 0), S = from_row(m, 1), ZZ3 = from_row(m, 2), MM = from_row(m, 3);
+  const uint32_t X3 = norm((uint64_t)MM + 2ull * negw(S));  // M^2 - 2 S
+  const uint32_t t = norm((uint64_t)S + negw(X3));          // S - X3
+  // row 0: M (S - X3), row 1: W Y, row 2: ZZZ3 = W ZZZ, row 3: beta X3
+  m = mul(r == 0 ? M : r == 3 ? X3 : W, r == 0 ? t : r == 1 ? Y : r == 2 ? ZZZ : beta_limb());
+  const uint32_t Mt = from_row(m, 0), WY = from_row(m, 1), ZZZ3 = from_row(m, 2), B3 = from_row(m, 3);
+  Y = norm((uint64_t)Mt + negw(WY));
+  X = X3;
+  ZZ = ZZ3;
+  ZZZ = ZZZ3;
+  BX = B3;
+}
+
+// (X1, Y1, ZZ1, ZZZ1) += (X2, Y2, ZZ2, ZZZ2), both XYZZ (add-2008-s, the
+// formulas of point.h gexz_add), the second operand finite; complete: the
+// identity (`inf`, wave-uniform), P + P (doubling) and P + (-P).  Fourteen
+// products in four levels {U1, U2, S1, S2} -> {P^2, R^2, ZZ1 ZZ2, ZZZ1 ZZZ2}
+// -> {P PP, U1 PP, ZZ12 PP} -> {R (Q - X3), S1 PPP, ZZZ12 PPP}.
+__device__ __forceinline__ void add_xyzz(uint32_t &X1, uint32_t &Y1, uint32_t &ZZ1, uint32_t &ZZZ1, bool &inf,
+                                         uint32_t X2, uint32_t Y2, uint32_t ZZ2, uint32_t ZZZ2) {
+  if (inf) {
+    X1 = X2;
+    Y1 = Y2;
+    ZZ1 = ZZ2;
+    ZZZ1 = ZZZ2;
+    inf = false;
+    return;
+  }
+  const uint32_t r = row();
+  // row 0: U1 = X1 ZZ2, row 1: U2 = X2 ZZ1, row 2: S1 = Y1 ZZZ2, row 3: S2 = Y2 ZZZ1
+  uint32_t m = mul(r == 0 ? X1 : r == 1 ? X2 : r == 2 ? Y1 : Y2, r == 0 ? ZZ2 : r == 1 ? ZZ1 : r == 2 ? ZZZ2 : ZZZ1);
+  const uint32_t U1 = from_row(m, 0), U2 = from_row(m, 1), S1 = from_row(m, 2), S2 = from_row(m, 3);
+  const uint32_t P = norm((uint64_t)U2 + negw(U1)), R = norm((uint64_t)S2 + negw(S1));
+  if (is_zero(P)) {  // wave-uniform: the same x
+    if (is_zero(R)) {
+      uint32_t bx;
+      dbl_xyzz(X1, Y1, ZZ1, ZZZ1, bx);
+    } else {
+      inf = true;
+    }
+    return;
+  }
+  // row 0: PP = P^2, row 1: R^2, row 2: ZZ1 ZZ2, row 3: ZZZ1 ZZZ2
+  m = mul(r == 0 ? P : r == 1 ? R : r == 2 ? ZZ1 : ZZZ1, r == 0 ? P : r == 1 ? R : r == 2 ? ZZ2 : ZZZ2);
+  const uint32_t PP = from_row(m, 0), RR = from_row(m, 1), Z12 = from_row(m, 2), ZZZ12 = from_row(m, 3);
+  // row 0: PPP = P PP, row 1: Q = U1 PP, rows 2-3: ZZ3 = ZZ1 ZZ2 PP
+  m = mul(r == 0 ? P : r == 1 ? U1 : Z12, PP);
+  const uint32_t PPP = from_row(m, 0), Q = from_row(m, 1), ZZ3 = from_row(m, 2);
+  const uint32_t X3 = norm((uint64_t)RR + negw(PPP) + 2ull * negw(Q));  // R^2 - PPP - 2 Q
+  const uint32_t t = norm((uint64_t)Q + negw(X3));                       // Q - X3
+  // row 0: R (Q - X3), row 1: S1 PPP, rows 2-3: ZZZ3 = ZZZ1 ZZZ2 PPP
+  m = mul(r == 0 ? R : r == 1 ? S1 : ZZZ12, r == 0 ? t : PPP);
+  const uint32_t Rt = from_row(m, 0), SP = from_row(m, 1), ZZZ3 = from_row(m, 2);
+  Y1 = norm((uint64_t)Rt + negw(SP));
+  X1 = X3;
+  ZZ1 = ZZ3;
+  ZZZ1 = ZZZ3;
+}
+
 // (X, Y, Z) = k P for an affine P (NORMAL, replicated) and a 128-bit k
 // (4 limbs, wave-uniform): MSB-first over the non-adjacent form of k (~k/3
 // additions; verify_core.h naf_mul, per lane), every step cooperative.
 __device__ __forceinline__ void naf_mul(uint32_t &X, uint32_t &Y, uint32_t &Z, bool &inf, uint32_t px, uint32_t py,
                                         const uint32_t k[4]) {
-  uint32_t h[5], kk[5], pos_[5], neg_[5], c = 0, prev = 0;
-  for (int i = 0; i < 4; i++) kk[i] = k[i];
-  kk[4] = 0;
-  for (int i = 0; i < 5; i++) {  // h = 3k
-    const uint32_t k2 = (kk[i] << 1) | (prev >> 31);
-    prev = kk[i];
-    h[i] = addc32(kk[i], k2, c);
-  }
-  for (int i = 0; i < 5; i++) {
-    const uint32_t x = h[i] ^ kk[i];
-    pos_[i] = x & h[i];
-    neg_[i] = x & kk[i];
-  }
-  for (int i = 0; i < 5; i++) {
-    pos_[i] = (pos_[i] >> 1) | (i < 4 ? pos_[i + 1] << 31 : 0u);
-    neg_[i] = (neg_[i] >> 1) | (i < 4 ? neg_[i + 1] << 31 : 0u);
-  }
+  uint32_t pos_[5], neg_[5];
+  ::naf_masks(k, pos_, neg_);
   const uint32_t ny = norm(negw(py));
   inf = true;
   X = Y = Z = 0;

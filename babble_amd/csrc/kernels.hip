@@ -617,20 +617,26 @@ __global__ void __launch_bounds__(64) k_verify_deferred(uint64_t n, const uint32
 // different waves run different code at the same time; lanes of one wave
 // only when they run the same code).  The host has hashed the messages
 // (SHA-NI, hostsha.cpp) and sends the digests.
-//   phase 1  wave 1: s^-1 (one Bernstein-Yang inversion; wave-uniform, so
-//            the compiler runs it on the scalar unit)
-//            wave 2: elliptic.Unmarshal of the item's key (Q)
+//   phase 1  waves 1 + 3: s^-1 (one Bernstein-Yang inversion split over two
+//            waves, lane 0 each: wave-uniform, so it runs on the scalar unit)
+//            wave 2: elliptic.Unmarshal of the item's key (Q); without a
+//            key-cache table it then doubles Q (kColdD0 doublings)
+//            wave 0: the item's r, digest, pre and table address
 //   phase 2  wave 0 lane 0: decision table, u1 = e w;  wave 1 lane 0:
-//            u2 = r w and its GLV split (k1, k2, signs)
+//            u2 = r w, its GLV split (k1, k2, signs) and, without a table,
+//            the chain length and the phase count; wave 2: kColdD1 doublings
 //   phase 3  key with a key-cache table: 22 leaves in lanes 0..21 of wave
 //            0, every table entry loaded at once — G windows 0..9 of u1,
 //            KC windows 0..5 of k1 (T) and of k2 (phi(T)) — summed by a
 //            binary tree (affine pairs, then XYZZ sums: 5 levels of zipped
 //            point additions, nodes handed over through LDS);
-//            key without one: waves 2 / 3 run k1 Q / k2 phi(Q) as
-//            wave-cooperative NAF chains (coop.h) while wave 0 sums the 10
-//            G leaves, then wave 0 lane 0 adds the three partial sums
-//   phase 4  wave 0 lane 0: x(R) mod N == r
+//            key without one: right to left in barrier-separated phases
+//            (see SmallCold above): wave 2 doubles kColdChunk more entries
+//            per phase, waves 1 / 3 add the entries of earlier phases for
+//            k1 Q / k2 phi(Q); wave 3 first adds the G sum (wave 0 sums
+//            the G leaves in phase 2); then wave 1 adds wave 3's sum
+//   phase 4  x(R) mod N == r (wave 0 lane 0 with a table, wave 1 lane 0
+//            without)
 // Statuses only; the host packs a small batch's accept bits.  `stamps`
 // (BV_SMALL_STAMPS diagnostics): workgroup 0's shader clocks per phase.
 // ---------------------------------------------------------------------------
@@ -753,6 +759,72 @@ DEV void sinv_split_de(SinvMail &mb, sc &w) {
   for (int k = 0; k < 8; k++) one.v[k] = k == 0 ? 1u : 0u;
   sc_mont(w, r, one);  // ... s^-1 R
 }
+
+// ---- the cold path (no key-cache table), right to left in lockstep phases.
+// Wave 2 doubles Q from the moment it is decoded (2^i Q in XYZZ with beta X,
+// coop.h dbl_xyzz) into LDS; waves 1 and 3 add +-2^i Q / +-phi(2^i Q) for
+// the non-zero NAF digits of k1 / k2 (coop.h add_xyzz); wave 0 sums the G
+// leaves.  Every hand-over between waves goes through a workgroup barrier:
+// the doubling chain runs in chunks of kColdChunk doublings, one barrier
+// after each, and an entry is read only in a phase after the one that wrote
+// it.  What each wave does in phase j is a function of (j, k1, k2) alone,
+// so the additions happen in the same order whatever the waves' timing, and
+// no wave leaves the kernel before the last one has finished (the round-5
+// flag-driven form of this pipeline, withdrawn, had neither property;
+// DESIGN.md section 4).
+constexpr uint32_t kChainBits = 130;  // NAF digits of a GLV half (|k| < 2^129)
+constexpr uint32_t kColdD0 = 16;      // doublings beside s^-1 (phase 1: ~70k clocks, ~4.4k per doubling)
+constexpr uint32_t kColdD1 = 20;      // doublings beside u1, u2, the GLV split and the G sum (phase 2: ~90k clocks)
+constexpr uint32_t kColdPre = 1 + kColdD0 + kColdD1;  // entries published before the chunk loop
+constexpr uint32_t kColdChunk = 6;    // doublings per loop phase
+constexpr uint32_t kColdBudget = 4;   // additions per half per phase (an addition ~1.33 doublings)
+constexpr uint32_t kColdGJoin = 0;    // the phase in which wave 3 adds the G sum (wave 0 sums it in phase 2)
+struct ChainPt {
+  uint32_t x[8], bx[8], y[8], zz[8], zzz[8];
+};
+struct SmallCold {
+  ChainPt pt[kChainBits];
+  SmallNode acc3;  // wave 3's sum: k2 phi(Q) + u1 G
+};
+__device__ __forceinline__ uint32_t row_limb(const uint32_t *p) { return coop::pos() < 8 ? p[coop::pos()] : 0u; }
+__device__ __forceinline__ void row_store(uint32_t *p, uint32_t v) {
+  if (__lane_id() < 8) p[__lane_id()] = v;
+}
+// entries 2^i Q visible in phase j of the chunk loop (all written before
+// the barrier that opened it)
+DEV uint32_t cold_pub(uint32_t j, uint32_t nb) { return min(nb, kColdPre + j * kColdChunk); }
+// the digits a half takes in one phase: from `pos` up to `end`, stopping
+// before its (budget + 1)-th non-zero digit.  The kernel's additions and
+// the phase count (cold_phases) both follow this rule.
+DEV uint32_t cold_take(const uint32_t m[5], uint32_t pos, uint32_t end, uint32_t budget) {
+  for (; pos < end; pos++)
+    if ((m[pos >> 5] >> (pos & 31)) & 1u) {
+      if (budget == 0) break;
+      budget--;
+    }
+  return pos;
+}
+// phases until both halves have taken every digit (and wave 3 the G sum)
+DEV uint32_t cold_phases(const uint32_t m1[5], const uint32_t m3[5], uint32_t nb) {
+  uint32_t p1 = 0, p3 = 0, j = 0;
+  for (; j < 64 && (p1 < nb || p3 < nb || j <= kColdGJoin); j++) {
+    p1 = cold_take(m1, p1, cold_pub(j, nb), kColdBudget);
+    p3 = cold_take(m3, p3, cold_pub(j, nb), kColdBudget - (j == kColdGJoin ? 1u : 0u));
+  }
+  return j;
+}
+// wave 2: 2^i Q -> entry i (lanes 0..7 of row 0 store)
+__device__ __forceinline__ void cold_store(SmallCold &cs, uint32_t i, uint32_t X, uint32_t Y, uint32_t ZZ, uint32_t ZZZ,
+                                           uint32_t BX) {
+  ChainPt &e = cs.pt[i];
+  row_store(e.x, X), row_store(e.bx, BX), row_store(e.y, Y), row_store(e.zz, ZZ), row_store(e.zzz, ZZZ);
+}
+// R += node (a SmallNode in LDS: X Y ZZ ZZZ + identity flag), cooperatively
+__device__ __forceinline__ void cold_add_node(uint32_t &X, uint32_t &Y, uint32_t &ZZ, uint32_t &ZZZ, bool &inf,
+                                              const SmallNode &nd) {
+  if (!__builtin_amdgcn_readfirstlane(nd.w[32]))
+    coop::add_xyzz(X, Y, ZZ, ZZZ, inf, row_limb(nd.w), row_limb(nd.w + 8), row_limb(nd.w + 16), row_limb(nd.w + 24));
+}
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t *__restrict__ digest_words,
@@ -771,14 +843,18 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
   } while (0)
   if (t == 0) SMALL_STAMP(0);
   __shared__ uint32_t sh_w[8], sh_q[16], sh_u1[8], sh_k[8], sh_r[8], sh_s[8], sh_e[8];
-  __shared__ uint32_t sh_ks, sh_go, sh_signs, sh_pre;
+  __shared__ uint32_t sh_ks, sh_go, sh_signs, sh_pre, sh_nb, sh_nphase;
   __shared__ uint64_t sh_tab;
   __shared__ SinvMail sh_mail;
   __shared__ uint32_t sh_sok;
-  __shared__ SmallNode sh_a[kSmallLeaves], sh_b[kSmallLeaves / 2 + 1], sh_c[kSmallLeaves / 4 + 2], sh_d[3];
+  __shared__ SmallNode sh_a[kSmallLeaves], sh_b[kSmallLeaves / 2 + 1], sh_c[kSmallLeaves / 4 + 2];
+  __shared__ SmallCold cs;
   if (b >= n_items) return;  // (the grid is n_items)
   if (t == 0) sh_mail.produced = sh_mail.consumed = sh_mail.done = 0;
   __syncthreads();
+  // wave 2's doubling state (the cold path; replicated in every DPP row)
+  uint32_t dX = 0, dY = 0, dZZ = 0, dZZZ = 0, dBX = 0;
+  bool chain = false;  // wave 2: this item doubles Q (no table, Q decoded)
   // ---- phase 1 (the inputs live in host memory, read in place: wave 0
   // fetches what phases 2-4 need while s^-1 runs)
   if (lane == 0 && wave == 0) {
@@ -816,7 +892,25 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
 #pragma unroll
     for (int c = 0; c < 8; c++) sh_q[c] = x.v[c], sh_q[8 + c] = y.v[c];
     sh_ks = st;
+    // (wave 2 reads the table address itself: wave 0's copy is not
+    // published before the barrier)
+    chain = st == KS_OK && !(kc_tabs && kc_tabs[k]);
     SMALL_STAMP(3);
+  }
+  if (wave == 2) {
+    chain = __builtin_amdgcn_readfirstlane(chain ? 1u : 0u) != 0;
+    if (chain) {  // entries 0..kColdD0: Q, 2Q, ..., 2^kColdD0 Q
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // lane 0's sh_q, for the whole wave
+      __builtin_amdgcn_wave_barrier();
+      dX = row_limb(sh_q), dY = row_limb(sh_q + 8), dZZ = coop::pos() == 0 ? 1u : 0u, dZZZ = dZZ;
+      dBX = coop::mul(dX, coop::beta_limb());
+      cold_store(cs, 0, dX, dY, dZZ, dZZZ, dBX);
+      for (uint32_t i = 1; i <= kColdD0; i++) {
+        coop::dbl_xyzz(dX, dY, dZZ, dZZZ, dBX);
+        cold_store(cs, i, dX, dY, dZZ, dZZZ, dBX);
+      }
+      if (lane == 0) SMALL_STAMP(4);
+    }
   }
   __syncthreads();
   if (t == 0) SMALL_STAMP(5);
@@ -849,6 +943,41 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
 #pragma unroll
     for (int k = 0; k < 4; k++) sh_k[k] = k1[k], sh_k[4 + k] = k2[k];
     sh_signs = signs;
+    if (!sh_tab) {  // the cold path's chain length and phase count
+      uint32_t p1[5], n1[5], p2[5], n2[5], m1[5], m3[5], nb = 0;
+      naf_masks(k1, p1, n1);
+      naf_masks(k2, p2, n2);
+      for (int i = 0; i < 5; i++) m1[i] = p1[i] | n1[i], m3[i] = p2[i] | n2[i];
+      for (int i = 4; i >= 0 && nb == 0; i--)
+        if (m1[i] | m3[i]) nb = 32 * i + 32 - __builtin_clz(m1[i] | m3[i]);
+      nb = min(nb, kChainBits);
+      sh_nb = nb;
+      sh_nphase = cold_phases(m1, m3, nb);
+    }
+  } else if (wave == 2 && chain) {  // entries kColdD0 + 1 .. kColdPre - 1
+    for (uint32_t i = kColdD0 + 1; i < kColdPre; i++) {
+      coop::dbl_xyzz(dX, dY, dZZ, dZZZ, dBX);
+      cold_store(cs, i, dX, dY, dZZ, dZZZ, dBX);
+    }
+  }
+  if (wave == 0 && !sh_tab) {  // no table: the G leaves of u1 and their sum, 10 -> 5 -> 3 -> 2 -> 1 (sh_c[0])
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // lane 0's sh_go and sh_u1, for the whole wave
+    __builtin_amdgcn_wave_barrier();
+    if (__builtin_amdgcn_readfirstlane(sh_go)) {
+      fe x, y;
+      bool zero = true;
+      if (lane < BV_GNWIN) {
+        uint32_t u[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) u[k] = sh_u1[k];
+        table_leaf<BV_GW, 8>(x, y, zero, g_table, u, (int)lane, false, false);
+      }
+      small_leaf_pairs(x, y, zero, sh_b, sh_a, BV_GNWIN, lane);
+      small_tree_level(sh_b, sh_c, 5, lane);
+      small_tree_level(sh_c, sh_b, 3, lane);
+      small_tree_level(sh_b, sh_c, 2, lane);
+      if (lane == 0) SMALL_STAMP(7);
+    }
   }
   __syncthreads();
   if (t == 0) SMALL_STAMP(6);
@@ -882,70 +1011,82 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
       small_tree_level(sh_c, sh_b, 2, lane);   // -> 1
       if (lane == 0) SMALL_STAMP(11);
     }
-  } else {
-    if (wave == 0) {  // the G leaves and their subtree: 10 -> 5 -> 3 -> 2 -> 1
-      fe x, y;
-      bool zero = true;
-      if (lane < BV_GNWIN) {
-        uint32_t u[8];
+    // ---- phase 4: the root (sh_b[0]) -> the decision
+    if (t == 0) {
+      gexz A;
+      bool ia;
+      part_load(sh_b[0].w, A, ia);
+      fe r;
+      fe_load_be_words(r, sh_r);
+      status[b] = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
+      SMALL_STAMP(13);
+    }
+    return;
+  }
+  // ---- phase 3 without a table: the chunk loop (every wave runs every
+  // phase and its barrier; the counts are uniform, read from LDS)
+  const uint32_t nb = __builtin_amdgcn_readfirstlane(sh_nb), nphase = __builtin_amdgcn_readfirstlane(sh_nphase);
+  const uint32_t h = wave == 3 ? 1u : 0u;  // (waves 1 and 3: the GLV half)
+  uint32_t pm[5] = {}, nm[5] = {}, m[5] = {}, pos = 0;
+  uint32_t X = 0, Y = 0, ZZ = 0, ZZZ = 0;
+  bool inf = true;
+  const bool neg_all = (signs >> h) & 1u;
+  if (wave == 1 || wave == 3) {
+    uint32_t kk[4];
 #pragma unroll
-        for (int k = 0; k < 8; k++) u[k] = sh_u1[k];
-        table_leaf<BV_GW, 8>(x, y, zero, g_table, u, (int)lane, false, false);
-      }
-      small_leaf_pairs(x, y, zero, sh_b, sh_a, BV_GNWIN, lane);
-      small_tree_level(sh_b, sh_c, 5, lane);
-      small_tree_level(sh_c, sh_b, 3, lane);
-      small_tree_level(sh_b, sh_c, 2, lane);  // the G sum in sh_c[0]
-      if (lane == 0) {
+    for (int k = 0; k < 4; k++) kk[k] = __builtin_amdgcn_readfirstlane(sh_k[4 * h + k]);
+    naf_masks(kk, pm, nm);
 #pragma unroll
-        for (int k = 0; k < 33; k++) sh_d[0].w[k] = sh_c[0].w[k];
-        SMALL_STAMP(7);
+    for (int i = 0; i < 5; i++) m[i] = pm[i] | nm[i];
+  }
+  for (uint32_t j = 0; j < nphase; j++) {
+    if (wave == 2) {  // the chain: entries cold_pub(j) .. cold_pub(j + 1) - 1
+      for (uint32_t i = cold_pub(j, nb); i < cold_pub(j + 1, nb); i++) {
+        coop::dbl_xyzz(dX, dY, dZZ, dZZZ, dBX);
+        cold_store(cs, i, dX, dY, dZZ, dZZZ, dBX);
       }
-    } else if (wave >= 2) {  // no table: k1 Q (wave 2) / k2 phi(Q) (wave 3), the NAF chain, wave-cooperative
-      const uint32_t h = wave - 2;
-      uint32_t kk[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) kk[k] = sh_k[4 * h + k];
-      const bool neg = (signs >> h) & 1u;
-      const uint32_t c = coop::pos();
-      uint32_t px = c < 8 ? sh_q[c] : 0u, py = c < 8 ? sh_q[8 + c] : 0u;
-      if (h) px = coop::mul(px, c < 8 ? FE_BETA[c] : 0u);  // phi(Q) = (beta x, y)
-      if (neg) py = coop::norm(coop::negw(py));
-      uint32_t X, Y, Z;
-      bool inf;
-      coop::naf_mul(X, Y, Z, inf, px, py, kk);
-      uint32_t ZZ = 0, ZZZ = 0;
-      if (!inf) {
-        ZZ = coop::mul(Z, Z);
-        ZZZ = coop::mul(ZZ, Z);
+    } else if (wave != 0) {  // waves 1 / 3: +-2^i Q (h = 1: +-phi(2^i Q)) for the non-zero digits the phase takes
+      uint32_t budget = kColdBudget;
+      if (h && j == kColdGJoin) {  // the G sum (wave 0, phase 2)
+        cold_add_node(X, Y, ZZ, ZZZ, inf, sh_c[0]);
+        budget--;
       }
-      if (lane < 8) {
-        sh_d[1 + h].w[lane] = X;
-        sh_d[1 + h].w[8 + lane] = Y;
-        sh_d[1 + h].w[16 + lane] = ZZ;
-        sh_d[1 + h].w[24 + lane] = ZZZ;
-      }
-      if (lane == 0) {
-        sh_d[1 + h].w[32] = inf ? 1u : 0u;
-        SMALL_STAMP(9 + h);
+      for (const uint32_t end = cold_pub(j, nb); pos < end; pos++) {
+        if (!((m[pos >> 5] >> (pos & 31)) & 1u)) continue;
+        if (budget == 0) break;
+        budget--;
+        const ChainPt &e = cs.pt[pos];
+        uint32_t y = row_limb(e.y);
+        if ((((nm[pos >> 5] >> (pos & 31)) & 1u) != 0) != neg_all) y = coop::norm(coop::negw(y));
+        coop::add_xyzz(X, Y, ZZ, ZZZ, inf, row_limb(h ? e.bx : e.x), y, row_limb(e.zz), row_limb(e.zzz));
       }
     }
     __syncthreads();
-    if (wave == 0) {  // (G + k1 Q) + k2 phi(Q)
-      small_tree_level(sh_d, sh_c, 3, lane);
-      small_tree_level(sh_c, sh_b, 2, lane);
+  }
+  if (wave == 3) {  // k2 phi(Q) + u1 G to wave 1
+    row_store(cs.acc3.w, X), row_store(cs.acc3.w + 8, Y), row_store(cs.acc3.w + 16, ZZ),
+        row_store(cs.acc3.w + 24, ZZZ);
+    if (lane == 0) cs.acc3.w[32] = inf ? 1u : 0u;
+    if (lane == 0) SMALL_STAMP(10);
+  }
+  __syncthreads();
+  if (wave == 1) {  // k1 Q + (k2 phi(Q) + u1 G), then the decision
+    cold_add_node(X, Y, ZZ, ZZZ, inf, cs.acc3);
+    row_store(sh_b[0].w, X), row_store(sh_b[0].w + 8, Y), row_store(sh_b[0].w + 16, ZZ), row_store(sh_b[0].w + 24, ZZZ);
+    if (lane == 0) sh_b[0].w[32] = inf ? 1u : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      gexz A;
+      bool ia;
+      part_load(sh_b[0].w, A, ia);
+      fe r;
+      fe_load_be_words(r, sh_r);
+      status[b] = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
+      SMALL_STAMP(13);
     }
   }
-  // ---- phase 4: the root (sh_b[0]) -> the decision
-  if (t == 0) {
-    gexz A;
-    bool ia;
-    part_load(sh_b[0].w, A, ia);
-    fe r;
-    fe_load_be_words(r, sh_r);
-    status[b] = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
-    SMALL_STAMP(13);
-  }
+  __syncthreads();  // no wave leaves before the last cooperative step of the workgroup
 #undef SMALL_STAMP
 }
 

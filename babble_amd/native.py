@@ -23,7 +23,8 @@ REJECT, ACCEPT, REJECT_ERR, REF_PANIC = 0, 1, 2, 3
 SC_OK, SC_NIL, SC_NONPOS, SC_GE_N = 0, 1, 2, 3
 PRE_PARTS_BAD = 0x80
 F_DEFAULT = 0
-ABI_VERSION = 5
+ABI_VERSION = 6
+ARENA_SLOTS = 32
 F_KEY_CACHE = 1
 F_K8 = 2
 
@@ -34,7 +35,7 @@ EXPORTS = (
     "bv_hex_decode", "bv_group_create", "bv_group_destroy", "bv_group_last_error", "bv_group_verify_batch",
     "bv_group_get_timing", "bv_plan_shards", "bv_sync", "bv_peer_set_hash", "bv_verify_events",
     "bv_last_stream", "bv_host_alloc", "bv_host_free", "bv_merge_shard_bits", "bv_plan_group",
-    "bv_kc_register",
+    "bv_kc_register", "bv_arena_create", "bv_arena_destroy", "bv_arena_reserve",
 )
 
 
@@ -157,6 +158,13 @@ def lib() -> ctypes.CDLL:
     L.bv_plan_group.restype = ctypes.c_int
     L.bv_kc_register.argtypes = [P, ctypes.c_uint32, P, P]
     L.bv_kc_register.restype = ctypes.c_int
+    L.bv_arena_create.argtypes = [ctypes.POINTER(P)]
+    L.bv_arena_create.restype = ctypes.c_int
+    L.bv_arena_destroy.argtypes = [P]
+    L.bv_arena_destroy.restype = None
+    L.bv_arena_reserve.argtypes = [P, ctypes.c_uint32, ctypes.c_size_t, ctypes.c_size_t, ctypes.POINTER(P),
+                                   ctypes.POINTER(ctypes.c_size_t)]
+    L.bv_arena_reserve.restype = ctypes.c_int
     if L.bv_abi_version() != ABI_VERSION:
         raise BvError(BV_E_ARGS, "ABI version mismatch")
     _lib = L

@@ -248,8 +248,13 @@ def _cbatch(b: PackedBatch, keep: list) -> "native.BvBatch":
     conversion: a batch verified again (latency loops, streaming callers)
     skips the pointer look-ups (~25 us of Python per call)."""
     arrays = tuple(getattr(b, f) for f, _ in _CB_FIELDS)
+    # identity alone is not enough: an in-place ndarray.resize keeps the
+    # object but moves its data (ADVICE r5), so the cache is keyed on each
+    # array's data pointer and shape too
+    sig = tuple((a.__array_interface__["data"][0], a.shape) if isinstance(a, np.ndarray) else id(a) for a in arrays)
     cached = getattr(b, "_cb_cache", None)
-    if cached is not None and len(cached[0]) == len(arrays) and all(x is y for x, y in zip(cached[0], arrays)):
+    if (cached is not None and len(cached[0]) == len(arrays) and all(x is y for x, y in zip(cached[0], arrays))
+            and cached[3] == sig):
         keep.append(cached[2])
         return cached[1]
     conv = []
@@ -277,7 +282,7 @@ def _cbatch(b: PackedBatch, keep: list) -> "native.BvBatch":
     # caller's own arrays, so later in-place edits of them are seen
     if all(x is y for x, y in zip(conv, (a for a in arrays if a is not None))):
         try:
-            b._cb_cache = (arrays, cb, conv)
+            b._cb_cache = (arrays, cb, conv, sig)
         except AttributeError:  # (a batch type without a __dict__: no cache)
             pass
     return cb

@@ -27,6 +27,11 @@ Rank 0 prints one JSON line.  `value` is the headline above.  Beside it:
     caller sees: pinned staging, PCIe, kernels and copy-out in the timing;
   * `latency_ms` — bv_verify_batch at 1 / 100 / 1000 (SyncLimit,
     config.go:44) / 10^4 / 10^5 events, cold (no cache) and warm (key cache);
+  * `shim_path` — the cgo shim's call sequence
+    replayed in C (tests/cabi/shim_harness.c): one event, a 1000-event
+    SyncResponse and a 1M-event replay with the batch built in pooled pinned
+    arenas and the results copied out inside the clock, beside the
+    library-only numbers;
   * `cpu_baseline` — the faster of two CPU legs on this host's cores, each on
     a bounded sample of the same batch: the C oracle (oracle/oracle.c, a
     restatement of the Go path) and the OpenSSL libcrypto proxy of SURVEY
@@ -516,6 +521,7 @@ def run(args, world: int, rank: int, local: int, worker) -> None:
         line["host_entry_pinned"] = host_entry_pinned_leg(args, v, batch)
         line["latency_ms"] = latency_leg(args)
         line["events_entry"] = events_entry_leg(args)
+        line["shim_path"] = guarded(shim_path_leg, args, line)
         line["tx_sweep"] = tx_sweep_leg(args, v, local)
         line["c5_fast_sync"] = guarded(c5_leg, args, local)
         line["c1_insert"] = guarded(c1_leg, args, local)
@@ -975,6 +981,71 @@ def cpu_sync_dag(packed) -> dict:
     out["ms_median"] = out["all_cores"]["ms_median"]
     out["cores"] = cores
     out["what"] = "hashlib SHA-256 of the serialized bodies in order + oracle.c port_verify_batch"
+    return out
+
+
+def shim_path_leg(args, line):
+    """The Go shim's path through the C harness
+    (tests/cabi/shim_harness.c): the key-cache context, the creators
+    registered as the PeerSet (bv_kc_register), batches built field by field
+    in pooled pinned arenas, signature text decoded per event, results
+    copied out — all inside the clock (the harness's own wall time).  Shapes:
+    one event through bv_verify_batch (addSelfEvent, core.go:291), the
+    SyncLimit SyncResponse of `events_entry.sync_dag_1000` (1000 events, 4
+    creators, in-batch parents) and the C2 replay (1M events, store-hash
+    parents) through bv_verify_events.  Each beside the library-only number
+    of the same shape measured in this line."""
+    import numpy as np
+
+    from babble_amd import synth
+    from tests.cabi import harness
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    out = {}
+    sh = harness.Shim(device=local)
+    try:
+        one_packed, one = synth.event_fields(1, n_creators=1, seed=900 + 1, parents="hash")
+        sh.set_peers([one_packed.key(0)])
+        text, off = harness.encode_signatures(one.r_be, one.s_be)
+        body, key, sig = one_packed.message(0), one_packed.key(0), harness.signature_text(text, off, 0)
+        sh.verify_event(body, key, sig)
+        ts = []
+        for _ in range(31):
+            _, st, ms = sh.verify_event(body, key, sig)
+            assert st == 1
+            ts.append(ms)
+        lib1 = (line.get("latency_ms") or {}).get("1", {}).get("warm_key_cache")
+        out["event_1"] = {"ms_median": float(np.median(ts)), "library_ms": lib1,
+                          "over_library": float(np.median(ts)) / lib1 if lib1 else None}
+        dag_packed, dag = synth.event_fields(1000, n_creators=4, seed=31, parents="event")
+        sh.set_peers([dag_packed.key(k) for k in range(dag_packed.n_keys)])
+        sw, keep = sh.wire(dag)
+        sh.sync(sw)
+        ts = []
+        for _ in range(15):
+            _, st, ms = sh.sync(sw)
+            assert np.all(st == 1)
+            ts.append(ms)
+        libd = ((line.get("events_entry") or {}).get("sync_dag_1000") or {}).get("ms_median")
+        out["sync_dag_1000"] = {"ms_median": float(np.median(ts)), "library_ms": libd,
+                                "over_library": float(np.median(ts)) / libd if libd else None}
+        del sw, keep
+        packed, wire = synth.event_fields(args.events, n_creators=args.creators, seed=2, parents="hash")
+        sh.set_peers([packed.key(k) for k in range(packed.n_keys)])
+        del packed
+        sw, keep = sh.wire(wire)
+        sh.sync(sw)
+        ts = []
+        for _ in range(max(2, min(5, args.steps))):
+            _, st, ms = sh.sync(sw)
+            assert np.all(st == 1)
+            ts.append(ms)
+        ms = float(np.median(ts))
+        libb = ((line.get("events_entry") or {}).get("bulk_pinned") or {}).get("value")
+        out["bulk_1m"] = {"events": args.events, "ms_median": ms, "value": args.events / (ms * 1e-3),
+                          "unit": "verifies/s", "library_pinned_value": libb}
+    finally:
+        sh.close()
     return out
 
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define BV_ABI_VERSION 5
+#define BV_ABI_VERSION 6
 
 /* Return codes (per-item outcomes are never errors; they go to status[]). */
 #define BV_OK 0
@@ -73,10 +73,11 @@ extern "C" {
                              96), registered keys only for other registered
                              keys.  Malformed keys are never given a table.
                              A batch whose valid keys without a table are at
-                             most 1 in 16 of its valid keys keeps the cache
-                             (their items are finished by the generic path
-                             after the cached ones); with more, the batch
-                             takes the per-batch table path.  Off by default:
+                             most 1 in 16 of its valid keys, carrying at most
+                             1 in 16 of its items, keeps the cache (their
+                             items are finished by the generic path after the
+                             cached ones); otherwise the batch takes the
+                             per-batch table path.  Off by default:
                              tables are then rebuilt for every batch.          */
 #define BV_F_K8 2u        /* per-batch tables: never use the 12-bit tables
                              (2.75 MiB per key); 8-bit only (512 KiB per key) */
@@ -163,6 +164,25 @@ int bv_verify_batch(bv_ctx *ctx, const bv_batch *batch, bv_result *result);
  * pointers it did not allocate.  No device context is needed. */
 int bv_host_alloc(size_t bytes, void **out);
 void bv_host_free(void *p);
+
+/* A pinned arena: BV_ARENA_SLOTS growable blocks of bv_host_alloc memory
+ * that persist until bv_arena_destroy.  A caller that keeps its arena across
+ * calls (the cgo shim's pooled batch builders)
+ * page-locks and frees nothing per call: hipHostMalloc / hipHostFree cost
+ * tens of microseconds each and hipHostFree synchronises the device.  Arena
+ * memory is bv_host_alloc memory, so batches built in it are DMA'd in place.
+ * An arena is not thread-safe: one per concurrent builder.  No device
+ * context is needed. */
+#define BV_ARENA_SLOTS 32
+typedef struct bv_arena bv_arena;
+int bv_arena_create(bv_arena **out);
+void bv_arena_destroy(bv_arena *arena);
+/* Block `slot` (< BV_ARENA_SLOTS) with capacity >= `bytes`.  When it must
+ * grow, the new block holds max(bytes, 2 x the old capacity) bytes and its
+ * first `keep` bytes (<= the old capacity) are copied from the old one, which
+ * is freed.  *out = the block's base, *cap (may be NULL) = its capacity.
+ * BV_E_ARGS, BV_E_OOM (the old block is then kept). */
+int bv_arena_reserve(bv_arena *arena, uint32_t slot, size_t bytes, size_t keep, void **out, size_t *cap);
 
 /* Same, with every bv_batch / bv_result pointer in device memory of the ctx's
  * device (inputs already resident in HBM).  `stream` is a hipStream_t (NULL =

@@ -253,25 +253,41 @@ uint8_t small_item(uint64_t i, const bv_batch *b, const uint8_t *msg, const uint
     nodes.push_back(R);
     ninf.push_back(inf);
   }
-  tree_sum(nodes, ninf);
-  for (int hh = 0; hh < 2; hh++) {
-    fe px = qx, py = qy;
-    if (hh) {
-      fe beta;
-      fe_load(beta, FE_BETA);
-      fe_mul(px, px, beta);
+  tree_sum(nodes, ninf);  // the G sum
+  // the cold path (no key-cache table) in k_small's order: the doubling
+  // chain 2^i Q in XYZZ; half 1 (wave 3) starts from the G sum and adds
+  // +-phi(2^i Q), half 0 (wave 1) +-2^i Q, each over its non-zero NAF digits
+  // in increasing i (the kernel's phases only decide WHEN, never the order);
+  // then half 0 + half 1
+  uint32_t pm[2][5], nm[2][5];
+  naf_masks(k1, pm[0], nm[0]);
+  naf_masks(k2, pm[1], nm[1]);
+  gexz acc[2];
+  bool ai[2] = {true, true};
+  acc[1] = nodes[0];
+  ai[1] = ninf[0];
+  fe beta;
+  fe_load(beta, FE_BETA);
+  gexz P;
+  P.X = qx, P.Y = qy;
+  for (int c = 0; c < 8; c++) P.ZZ.v[c] = P.ZZZ.v[c] = c == 0 ? 1u : 0u;
+  for (uint32_t bit = 0; bit < 130; bit++) {
+    if (bit) {
+      gexz D;
+      gexz_double(D, P);
+      P = D;
     }
-    if ((signs >> hh) & 1u) fe_neg(py, py);
-    gej J;
-    bool inf;
-    gexz Q;
-    naf_mul<false>(J, inf, px, py, hh ? k2 : k1);
-    if (!inf) gexz_from_gej(Q, J);
-    nodes.push_back(Q);
-    ninf.push_back(inf);
+    for (int hh = 0; hh < 2; hh++) {
+      const uint32_t p = (pm[hh][bit >> 5] >> (bit & 31)) & 1u, n = (nm[hh][bit >> 5] >> (bit & 31)) & 1u;
+      if (!(p | n)) continue;
+      gexz T = P;
+      if (hh) fe_mul(T.X, T.X, beta);
+      if ((n != 0) != (((signs >> hh) & 1u) != 0)) fe_neg(T.Y, T.Y);
+      gexz_add_lat(acc[hh], ai[hh], T, false);
+    }
   }
-  tree_sum(nodes, ninf);  // (G + k1 Q) + k2 phi(Q)
-  return final_check(nodes[0], ninf[0], rf) ? BV_ACCEPT : BV_REJECT;
+  gexz_add_lat(acc[0], ai[0], acc[1], ai[1]);  // k1 Q + (u1 G + k2 phi(Q))
+  return final_check(acc[0], ai[0], rf) ? BV_ACCEPT : BV_REJECT;
 }
 
 template <class T>

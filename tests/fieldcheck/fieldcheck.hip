@@ -131,6 +131,53 @@ extern "C" int fc_xyzz(int lat, uint32_t n, const uint32_t *acc, const uint32_t 
   return e == hipSuccess ? 0 : -(int)e;
 }
 
+// The wave-cooperative XYZZ point ops of k_small's cold path (coop.h), one
+// wave per case: out[74 i ..] = acc + pt (33 words: X, Y, ZZ, ZZZ, identity
+// flag; add_xyzz), 2 pt (33 words; dbl_xyzz) and the doubling's beta X (8
+// words).  acc and pt are XYZZ (33 words each), pt finite.
+__global__ void __launch_bounds__(64) k_coop_xyzz(uint32_t n, const uint32_t *acc, const uint32_t *pts, uint32_t *out) {
+  const uint32_t b = blockIdx.x;
+  if (b >= n) return;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t c = coop::pos(), lane = __lane_id();
+  const uint32_t *a = acc + 33 * (uint64_t)b, *q = pts + 33 * (uint64_t)b;
+  const auto ld = [&](const uint32_t *p, int o) { return c < 8 ? p[o + c] : 0u; };
+  uint32_t X1 = ld(a, 0), Y1 = ld(a, 8), ZZ1 = ld(a, 16), ZZZ1 = ld(a, 24);
+  bool inf = a[32] != 0;
+  const uint32_t X2 = ld(q, 0), Y2 = ld(q, 8), ZZ2 = ld(q, 16), ZZZ2 = ld(q, 24);
+  coop::add_xyzz(X1, Y1, ZZ1, ZZZ1, inf, X2, Y2, ZZ2, ZZZ2);
+  uint32_t DX = X2, DY = Y2, DZZ = ZZ2, DZZZ = ZZZ2, BX;
+  coop::dbl_xyzz(DX, DY, DZZ, DZZZ, BX);
+  uint32_t *o = out + 74 * (uint64_t)b;
+  if (lane < 8) {
+    o[lane] = X1, o[8 + lane] = Y1, o[16 + lane] = ZZ1, o[24 + lane] = ZZZ1;
+    o[33 + lane] = DX, o[41 + lane] = DY, o[49 + lane] = DZZ, o[57 + lane] = DZZZ;
+    o[66 + lane] = BX;
+  }
+  if (lane == 0) o[32] = inf ? 1u : 0u, o[65] = 0u;
+#endif
+}
+
+extern "C" int fc_coop_xyzz(uint32_t n, const uint32_t *acc, const uint32_t *pts, uint32_t *out) {
+  uint32_t *da = nullptr, *dp = nullptr, *dr = nullptr;
+  const size_t ab = (size_t)(n ? n : 1) * 33 * 4, ob = (size_t)(n ? n : 1) * 74 * 4;
+  hipError_t e = hipMalloc(&da, ab);
+  if (e == hipSuccess) e = hipMalloc(&dp, ab);
+  if (e == hipSuccess) e = hipMalloc(&dr, ob);
+  if (e == hipSuccess && n) e = hipMemcpy(da, acc, ab, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) e = hipMemcpy(dp, pts, ab, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) {
+    hipLaunchKernelGGL(k_coop_xyzz, dim3(n), dim3(64), 0, 0, n, da, dp, dr);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess && n) e = hipMemcpy(out, dr, ob, hipMemcpyDeviceToHost);
+  (void)hipFree(da);
+  (void)hipFree(dp);
+  (void)hipFree(dr);
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
 // Key-table base chains B_j = 2^(w j) Q (j < nwin) of n affine points
 // (16 words each: x, y limbs), per lane (verify_core.h table_bases_one, the
 // zipped doubling) or wave-cooperative (coop.h: one wave per point, the

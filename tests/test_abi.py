@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_code_object():
     L = native.lib()
-    assert L.bv_abi_version() == native.ABI_VERSION == 5
+    assert L.bv_abi_version() == native.ABI_VERSION == 6
     # the library carries gfx950 device code (offload bundle entry name)
     blob = open(native.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob

@@ -396,6 +396,31 @@ def test_small_batch_randomized_against_oracle():
         warm.close()
 
 
+def test_small_batch_cold_path_many_batches():
+    """The cold k_small path (no key-cache table: wave 2 doubles Q while
+    waves 1 and 3 add the NAF digits of k1 / k2 in barrier-separated phases,
+    kernels.hip SmallCold) over 48 batches of up to 256 valid events from 1-4
+    creators with one corrupted signature each, in one process: ~12k items,
+    every status and digest equal to the C oracle.  Each batch runs twice on
+    the same context (the same statuses both times)."""
+    from babble_amd.verifier import Verifier
+
+    rng = np.random.default_rng(66)
+    v = Verifier(device=0)
+    try:
+        for it in range(48):
+            n = int(rng.integers(200, 257))
+            b = synth.events(n, n_creators=int(rng.integers(1, 5)), seed=5000 + it)
+            b.s_be[int(rng.integers(0, n)), 31] ^= 1
+            res = check_against_oracle(v, b)
+            assert v.timing()["key_path"] == 0
+            assert int((res.status == 1).sum()) == n - 1
+            again = v.verify(b)
+            assert np.array_equal(again.status, res.status)
+    finally:
+        v.close()
+
+
 def test_small_batch_kernel_key_cache(monkeypatch):
     """k_small with registered keys: every valid key registered -> the KC
     tables (6 lookups per GLV half; malformed keys need none); some keys

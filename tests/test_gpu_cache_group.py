@@ -494,21 +494,71 @@ def test_key_cache_partial_batch(monkeypatch, device_api):
     for i in rng.choice(b.n_items, 300, replace=False):
         b.r_be[i, int(rng.integers(0, 32))] ^= 1 << int(rng.integers(0, 8))
     keys = [b.key(k) for k in range(b.n_keys)]
+    def run(v, batch):
+        if device_api:
+            d = v.to_device(batch)
+            v.verify_device(d)
+            return d.result()
+        return v.verify(batch)
+
     for fresh, partial in ((1, True), (3, False)):
         v = Verifier(device=0, flags=native.F_KEY_CACHE)
         try:
             v.register_keys(keys[fresh:])
-            if device_api:
-                d = v.to_device(b)
-                v.verify_device(d)
-                res = d.result()
-            else:
-                res = v.verify(b)
-            st = oracle_check(res, b)
-            assert int((st == native.ACCEPT).sum()) == b.n_items - 300
-            t = v.timing()
-            assert (t["key_path"] == 22) == partial, t
-            if partial:
-                assert t["kc_hits"] == 20 - fresh and t["kc_builds"] == 0
+            # twice on one ctx: the second call finds the fresh
+            # key remembered (no decode in bv_kc_prepare), so the deferred
+            # items read the points bv_run_keys decoded on the s^-1 stream
+            for rep in range(2):
+                res = run(v, b)
+                st = oracle_check(res, b)
+                assert int((st == native.ACCEPT).sum()) == b.n_items - 300
+                t = v.timing()
+                assert (t["key_path"] == 22) == partial, (rep, t)
+                if partial:
+                    assert t["kc_hits"] == 20 - fresh and t["kc_builds"] == 0
         finally:
             v.close()
+    # the deferred share is bounded by ITEMS too: one fresh key
+    # of 20 that carries a fifth of the batch sends it to the per-batch tables
+    skew = synth.events(30_000, n_creators=20, seed=63)
+    skew.item_key = np.asarray(skew.item_key).copy()
+    skew.item_key[::5] = 0
+    v = Verifier(device=0, flags=native.F_KEY_CACHE)
+    try:
+        v.register_keys([skew.key(k) for k in range(1, 20)])
+        oracle_check(run(v, skew), skew)
+        assert v.timing()["key_path"] != 22
+    finally:
+        v.close()
+
+
+def test_key_cache_partial_batch_events_entry(monkeypatch):
+    """the partial key-cache mode through bv_verify_events (the
+    bulk wire path: key part first, the deferred tail on the split verify
+    stream), one fresh creator of 20, twice on one context; digests,
+    statuses and bits equal to the C oracle's."""
+    from babble_amd.verifier import Verifier
+    from oracle import coracle
+
+    monkeypatch.setenv("BV_KC_ADMIT", "1000")
+    packed, wire = synth.event_fields(30_000, n_creators=20, seed=64, parents="hash")
+    rng = np.random.default_rng(64)
+    bad = rng.choice(packed.n_items, 200, replace=False)
+    wire.s_be = np.asarray(wire.s_be).copy()
+    wire.s_be[bad, 3] ^= 0x10
+    packed.s_be[bad, 3] ^= 0x10
+    h, st, bits = coracle.verify_batch(packed.as_dict())
+    ko = np.asarray(wire.key_off, np.int64)
+    keys = [wire.key_bytes[ko[k]:ko[k + 1]].tobytes() for k in range(len(ko) - 1)]
+    v = Verifier(device=0, flags=native.F_KEY_CACHE)
+    try:
+        v.register_keys(keys[1:])
+        for rep in range(2):
+            res = v.verify_events(wire)
+            assert np.array_equal(res.msg_hash, h), rep
+            assert np.array_equal(res.status, st), rep
+            assert np.array_equal(res.accept_bits, bits), rep
+            assert v.timing()["key_path"] == 22, rep
+        assert int((st != native.ACCEPT).sum()) == len(bad)
+    finally:
+        v.close()

@@ -256,6 +256,65 @@ def test_xyzz_mixed_add_exceptional_cases(lat):
         assert (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P) == w, (i, i % 4)
 
 
+def test_coop_xyzz_add_and_double():
+    """The wave-cooperative XYZZ addition and doubling of k_small's cold
+    path (coop.h add_xyzz / dbl_xyzz: one point per wave, the products of a
+    level spread over the four DPP rows), against Python integers.  Both
+    operands in random projective form; generic sums, P + P (the doubling
+    branch), P + (-P) (the identity), the identity plus a point, and points
+    with extreme coordinates.  The doubling's fourth product is beta X3
+    (phi's x of the result)."""
+    G = (0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798,
+         0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8)
+    beta = 0x7AE96A2B657C07106E64479EAC3434E99CF0497512F58995C1396C28719501EE
+    rng = random.Random(29)
+
+    def proj(pt, z):
+        zz, zzz = z * z % P, z * z * z % P
+        return [pt[0] * zz % P, pt[1] * zzz % P, zz, zzz, 0]
+
+    accs, pts, want = [], [], []
+    extreme = [_ec_mul(N - 1, G), _ec_mul(2, G), G]
+    for i in range(192):
+        a = extreme[i % 3] if i < 12 else _ec_mul(rng.randrange(1, N), G)
+        kind = i % 4
+        b = a if kind == 1 else ((a[0], P - a[1]) if kind == 2 else _ec_mul(rng.randrange(1, N), G))
+        za = 1 if i % 16 == 0 else rng.randrange(1, P)
+        zb = 1 if i % 8 == 0 else (P - 1 if i % 8 == 1 else rng.randrange(1, P))
+        accs.append([0, 0, 0, 0, 1] if kind == 3 else proj(a, za))
+        want.append(b if kind == 3 else _ec_add(a, b))
+        pts.append((b, proj(b, zb)))
+    A = np.zeros((len(accs), 33), np.uint32)
+    B = np.zeros((len(pts), 33), np.uint32)
+    for i, (acc, (_, pb)) in enumerate(zip(accs, pts)):
+        for j in range(4):
+            A[i, 8 * j:8 * j + 8] = _pack([acc[j]])[0]
+            B[i, 8 * j:8 * j + 8] = _pack([pb[j]])[0]
+        A[i, 32] = acc[4]
+    R = np.zeros((len(accs), 74), np.uint32)
+    L = _lib()
+    L.fc_coop_xyzz.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.fc_coop_xyzz.restype = ctypes.c_int
+    assert L.fc_coop_xyzz(len(accs), A.ctypes.data, B.ctypes.data, R.ctypes.data) == 0
+
+    def affine(o):
+        X, Y, ZZ, ZZZ = (_unpack(R[i:i + 1, o + 8 * j:o + 8 * j + 8])[0] % P for j in range(4))
+        assert ZZ and pow(ZZ, 3, P) == pow(ZZZ, 2, P), i
+        return X, ZZ, (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P)
+
+    for i, w in enumerate(want):
+        if w is None:
+            assert R[i, 32] == 1, (i, "expected the identity")
+        else:
+            assert R[i, 32] == 0, i
+            assert affine(0)[2] == w, (i, i % 4)
+        b = pts[i][0]
+        X, ZZ, d = affine(33)
+        assert d == _ec_add(b, b), i
+        BX = _unpack(R[i:i + 1, 66:74])[0] % P
+        assert BX == beta * X % P, i
+
+
 @pytest.mark.parametrize("w,nwin", [(6, 22), (8, 16), (11, 12)], ids=["K12", "K8", "KC"])
 def test_coop_base_chain_equals_per_lane(w, nwin):
     """The wave-cooperative base chain (coop.h: field elements in 16-lane DPP
