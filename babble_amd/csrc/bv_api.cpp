@@ -461,7 +461,9 @@ static int create_impl(bv_ctx *ctx) {
   ctx->g_table = gtable_acquire(ctx->device, ctx->stream);
   if (!ctx->g_table) return bv_fail(ctx, BV_E_OOM, "generator table (geometry.h, ~21.5 GB of HBM) build failed");
   const unsigned hw = std::thread::hardware_concurrency();
-  ctx->pool = new CopyPool((int)std::min<unsigned>(hw ? hw - 1 : 0, 7));
+  int copy_threads = (int)std::min<unsigned>(hw ? hw - 1 : 0, 7);
+  if (const char *s = getenv("BV_COPY_THREADS")) copy_threads = std::max(0, std::min(63, atoi(s)));  // (A/B knob)
+  ctx->pool = new CopyPool(copy_threads);
   if (ctx->flags & BV_F_KEY_CACHE) bv_kc_init(ctx);
   // A/B knobs (bv_internal.h), read once here
   if (const char *s = getenv("BV_HOST_CHUNK_MB")) ctx->host_msg_chunk = (uint64_t)(std::max(1.0, atof(s)) * (1 << 20));
@@ -1366,13 +1368,11 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
     HIPCHK(hipMemsetAsync(ctx->d_stamps.p, 0, 16 * 8, st), BV_E_LAUNCH, "memset stamps");
     stamps = ctx->d_stamps.as<uint64_t>();
   }
-  HIPCHK(hipEventRecord(ev[E_START], st), BV_E_LAUNCH, "event");
   HIPCHK(bvk::verify_small(st, (uint32_t)n_items, dev + o_dig, dev + o_key, (const uint64_t *)(dev + o_koff),
                            (const uint32_t *)(dev + o_im), (const uint32_t *)(dev + o_ik), dev + o_r, dev + o_s,
                            b->pre ? dev + o_pre : nullptr, kc ? (const uint64_t *)(dev + o_tab) : nullptr,
-                           ctx->g_table, dev + o_st, stamps),
+                           ctx->g_table, dev + o_st, stamps, ev[E_START], ev[E_END]),
          BV_E_LAUNCH, "k_small");
-  HIPCHK(hipEventRecord(ev[E_END], st), BV_E_LAUNCH, "event");
   int rc = bv_mark_done(ctx, st);
   if (rc != BV_OK) return rc;
   const auto t_enq = std::chrono::steady_clock::now();

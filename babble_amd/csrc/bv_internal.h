@@ -63,7 +63,8 @@ hipError_t verify_q(hipStream_t, int, uint64_t, uint64_t, uint64_t, const uint32
 hipError_t verify_small(hipStream_t, uint32_t n_items, const uint8_t *dig, const uint8_t *key_bytes,
                         const uint64_t *key_off, const uint32_t *item_msg, const uint32_t *item_key,
                         const uint8_t *r_be, const uint8_t *s_be, const uint8_t *pre, const uint64_t *kc_tabs,
-                        const uint32_t *g_table, uint8_t *status, uint64_t *stamps = nullptr);
+                        const uint32_t *g_table, uint8_t *status, uint64_t *stamps, hipEvent_t ev_start,
+                        hipEvent_t ev_end);
 hipError_t verify_generic(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);

@@ -21,6 +21,7 @@
 // workgroup per item, one launch).  bv_verify_events' bulk batches hash each
 // body as it is serialised from wire fields (k_ev_body_hash: no body stored).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -706,10 +707,27 @@ DEV uint32_t lds_acquire(const uint32_t *p) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 DEV void lds_release(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// BV_SINV_VALU: the split inversion's values live in VGPRs (lane 0 of each
+// of the two waves), so the divsteps, the matrix products (one
+// v_mad_i64_i32 each) and the loop tests run on the VECTOR unit; the
+// scalar unit's dependent-instruction latency and taken branches made the
+// divsteps ~135 clocks each (profiles/r05_ubench_sinv.txt, r06_ubench_sinv.txt)
+#ifndef BV_SINV_VALU
+#define BV_SINV_VALU 1
+#endif
+DEV uint32_t in_vgpr(uint32_t x) {
+#if BV_SINV_VALU
+  asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
+#endif
+  return x;
+}
 // producer (the s^-1 chain): divsteps and the (f, g) updates
-DEV void sinv_split_fg(SinvMail &mb, const sc &s) {
+DEV void sinv_split_fg(SinvMail &mb, const sc &s_in) {
   modinfo30 mi;
   modinfo_n(mi);
+  sc s;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s.v[i] = in_vgpr(s_in.v[i]);
   s30 f, g;
 #pragma unroll
   for (int i = 0; i < 9; i++) f.v[i] = mi.m[i];
@@ -732,8 +750,10 @@ DEV void sinv_split_fg(SinvMail &mb, const sc &s) {
   mb.f_sign = f.v[8] >> 31;
   lds_release(&mb.done, k + 1);
 }
-// consumer: the (d, e) updates, then w = s^-1 R mod N (as sinv_one)
-DEV void sinv_split_de(SinvMail &mb, sc &w) {
+// consumer: the (d, e) updates, then inv = s^-1 mod N (plain, < N): phase
+// 2 forms u1 = e s^-1 and u2 = r s^-1 as ONE Montgomery product each, of inv
+// and the e R, r R that wave 0 prepared beside the inversion
+DEV void sinv_split_de(SinvMail &mb, sc &inv) {
   modinfo30 mi;
   modinfo_n(mi);
   s30 d, e;
@@ -746,18 +766,14 @@ DEV void sinv_split_de(SinvMail &mb, sc &w) {
     if (k >= lds_acquire(&mb.produced)) break;  // (done: every matrix applied)
     int32_t t[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) t[i] = __builtin_amdgcn_readfirstlane(mb.t[k % kSinvRing][i]);
+    for (int i = 0; i < 4; i++)
+      t[i] = BV_SINV_VALU ? (int32_t)in_vgpr((uint32_t)mb.t[k % kSinvRing][i])
+                          : __builtin_amdgcn_readfirstlane(mb.t[k % kSinvRing][i]);
     update_de_30(d, e, t, mi);
     lds_release(&mb.consumed, k + 1);
   }
   normalize_30(d, __builtin_amdgcn_readfirstlane(mb.f_sign), mi);
-  sc inv, r3, r, one;
   s30_to_u256(inv.v, d);
-  sc_load_const(r3, SC_R3);
-  sc_mont(r, inv, r3);  // s^-1 R^2 ...
-#pragma unroll
-  for (int k = 0; k < 8; k++) one.v[k] = k == 0 ? 1u : 0u;
-  sc_mont(w, r, one);  // ... s^-1 R
 }
 
 // ---- the cold path (no key-cache table), right to left in lockstep phases.
@@ -825,6 +841,16 @@ __device__ __forceinline__ void cold_add_node(uint32_t &X, uint32_t &Y, uint32_t
   if (!__builtin_amdgcn_readfirstlane(nd.w[32]))
     coop::add_xyzz(X, Y, ZZ, ZZZ, inf, row_limb(nd.w), row_limb(nd.w + 8), row_limb(nd.w + 16), row_limb(nd.w + 24));
 }
+// `to` = the sum of nodes [lo, hi) of `from` (one wave, cooperatively)
+__device__ __forceinline__ void coop_sum_nodes(const SmallNode *from, uint32_t lo, uint32_t hi, SmallNode &to) {
+  uint32_t X = 0, Y = 0, ZZ = 0, ZZZ = 0;
+  bool inf = true;
+  for (uint32_t j = lo; j < hi; j++) cold_add_node(X, Y, ZZ, ZZZ, inf, from[j]);
+  row_store(to.w, X), row_store(to.w + 8, Y), row_store(to.w + 16, ZZ), row_store(to.w + 24, ZZZ);
+  if (__lane_id() == 0) to.w[32] = inf ? 1u : 0u;
+}
+// the warm tree's first level: wave w sums leaf-pair nodes [kWarmSplit[w], kWarmSplit[w + 1])
+constexpr uint32_t kWarmSplit[5] = {0, 3, 6, 9, (kSmallLeaves + 1) / 2};
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t *__restrict__ digest_words,
@@ -842,7 +868,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
     if (stamps && b == 0) stamps[k] = __builtin_amdgcn_s_memtime();        \
   } while (0)
   if (t == 0) SMALL_STAMP(0);
-  __shared__ uint32_t sh_w[8], sh_q[16], sh_u1[8], sh_k[8], sh_r[8], sh_s[8], sh_e[8];
+  __shared__ uint32_t sh_w[8], sh_q[16], sh_u1[8], sh_k[8], sh_r[8], sh_s[8], sh_eR[8], sh_rR[8];
   __shared__ uint32_t sh_ks, sh_go, sh_signs, sh_pre, sh_nb, sh_nphase;
   __shared__ uint64_t sh_tab;
   __shared__ SinvMail sh_mail;
@@ -861,10 +887,18 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
 #pragma unroll
     for (int k = 0; k < 8; k++) sh_r[k] = r_be[8 * (uint64_t)b + k];
     const uint32_t m = item_msg[b];
-#pragma unroll
-    for (int k = 0; k < 8; k++) sh_e[k] = digest_words[8 * (uint64_t)m + k];
     sh_pre = pre ? pre[b] : 0u;
     sh_tab = kc_tabs ? kc_tabs[item_key[b]] : 0;
+    // e R and r R mod N beside the inversion (Montgomery form), so u1 and
+    // u2 are one product of each with s^-1 after it
+    sc e, r, R2, eR, rR;
+    sc_load_be_words(e, digest_words + 8 * (uint64_t)m);
+    sc_load_be_words(r, r_be + 8 * (uint64_t)b);
+    sc_load_const(R2, SC_R2);
+    sc_mont(eR, e, R2);  // (e < 2^256 = R unreduced, R2 < N)
+    sc_mont(rR, r, R2);
+#pragma unroll
+    for (int k = 0; k < 8; k++) sh_eR[k] = eR.v[k], sh_rR[k] = rR.v[k];
   } else if (lane == 0 && wave == 1) {  // s^-1: divsteps and (f, g) (wave 3 applies (d, e))
     sc s;
     sc_load_be_words(s, s_be + 8 * (uint64_t)b);
@@ -875,14 +909,14 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
     if (ok) sinv_split_fg(sh_mail, s);
     else lds_release(&sh_mail.done, 1);
   } else if (lane == 0 && wave == 3) {
-    sc w;
-    sinv_split_de(sh_mail, w);
+    sc inv;
+    sinv_split_de(sh_mail, inv);
     if (!__builtin_amdgcn_readfirstlane(sh_sok)) {  // (published before done)
 #pragma unroll
-      for (int k = 0; k < 8; k++) w.v[k] = 0;
+      for (int k = 0; k < 8; k++) inv.v[k] = 0;
     }
 #pragma unroll
-    for (int k = 0; k < 8; k++) sh_w[k] = w.v[k];
+    for (int k = 0; k < 8; k++) sh_w[k] = inv.v[k];  // s^-1 mod N
     SMALL_STAMP(2);
   } else if (lane == 0 && wave == 2) {
     const uint32_t k = item_key[b];
@@ -924,20 +958,18 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
     if (cls != 0xFF) {
       status[b] = cls;
     } else {
-      sc w, e, a;
+      sc inv, eR, a;
 #pragma unroll
-      for (int k = 0; k < 8; k++) w.v[k] = sh_w[k];
-      sc_load_be_words(e, sh_e);
-      sc_mont(a, e, w);  // e s^-1 mod N (e unreduced, < 2^256 = R)
+      for (int k = 0; k < 8; k++) inv.v[k] = sh_w[k], eR.v[k] = sh_eR[k];
+      sc_mont(a, eR, inv);  // e R s^-1 R^-1 = e s^-1 mod N
 #pragma unroll
       for (int k = 0; k < 8; k++) sh_u1[k] = a.v[k];
     }
   } else if (lane == 0 && wave == 1) {
-    sc w, r, u2;
+    sc inv, rR, u2;
 #pragma unroll
-    for (int k = 0; k < 8; k++) w.v[k] = sh_w[k];
-    sc_load_be_words(r, sh_r);
-    sc_mont(u2, r, w);  // r s^-1 mod N (only used when the item reaches the math)
+    for (int k = 0; k < 8; k++) inv.v[k] = sh_w[k], rR.v[k] = sh_rR[k];
+    sc_mont(u2, rR, inv);  // r s^-1 mod N (only used when the item reaches the math)
     uint32_t k1[4], k2[4], signs;
     glv_split(k1, k2, signs, u2);
 #pragma unroll
@@ -1003,12 +1035,21 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
                               h != 0);
       }
       if (lane == 0) SMALL_STAMP(7);
-      small_leaf_pairs(x, y, zero, sh_b, sh_a, kSmallLeaves, lane);  // 22 leaves -> 11 nodes
+      small_leaf_pairs(x, y, zero, sh_b, sh_a, kSmallLeaves, lane);  // 22 leaves -> 11 nodes (per lane)
       if (lane == 0) SMALL_STAMP(8);
-      small_tree_level(sh_b, sh_c, 11, lane);  // -> 6
-      small_tree_level(sh_c, sh_b, 6, lane);   // -> 3
-      small_tree_level(sh_b, sh_c, 3, lane);   // -> 2
-      small_tree_level(sh_c, sh_b, 2, lane);   // -> 1
+    }
+    __syncthreads();
+    // the XYZZ tree on DPP rows (coop.h add_xyzz, ~6k clocks an addition
+    // against ~21k for one lane's): 11 -> 4 (wave w sums nodes
+    // kWarmSplit[w] .. kWarmSplit[w + 1] - 1), 4 -> 2 (waves 0, 1), 2 -> 1
+    coop_sum_nodes(sh_b, kWarmSplit[wave], kWarmSplit[wave + 1], sh_c[wave]);
+    __syncthreads();
+    if (wave < 2) coop_sum_nodes(sh_c, 2 * wave, 2 * wave + 2, sh_a[wave]);
+    __syncthreads();
+    if (wave == 0) {
+      coop_sum_nodes(sh_a, 0, 2, sh_b[0]);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      __builtin_amdgcn_wave_barrier();
       if (lane == 0) SMALL_STAMP(11);
     }
     // ---- phase 4: the root (sh_b[0]) -> the decision
@@ -1021,6 +1062,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
       status[b] = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
       SMALL_STAMP(13);
     }
+    __syncthreads();  // no wave leaves before the last cooperative step of the workgroup
     return;
   }
   // ---- phase 3 without a table: the chunk loop (every wave runs every
@@ -1397,14 +1439,17 @@ hipError_t build_kc(hipStream_t st, uint32_t n, const uint32_t *kxy, const uint8
   return hipGetLastError();
 }
 
+// (the span's events ride on the kernel's own dispatch: no separate marker
+// packets or host calls around a latency-bound launch)
 hipError_t verify_small(hipStream_t st, uint32_t n_items, const uint8_t *dig, const uint8_t *key_bytes,
                         const uint64_t *key_off, const uint32_t *item_msg, const uint32_t *item_key,
                         const uint8_t *r_be, const uint8_t *s_be, const uint8_t *pre, const uint64_t *kc_tabs,
-                        const uint32_t *g_table, uint8_t *status, uint64_t *stamps) {
+                        const uint32_t *g_table, uint8_t *status, uint64_t *stamps, hipEvent_t ev_start,
+                        hipEvent_t ev_end) {
   if (n_items == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_small, dim3(n_items), dim3(256), 0, st, n_items, (const uint32_t *)dig, key_bytes, key_off,
-                     item_msg, item_key, (const uint32_t *)r_be, (const uint32_t *)s_be, pre, kc_tabs, g_table,
-                     status, stamps);
+  hipExtLaunchKernelGGL(k_small, dim3(n_items), dim3(256), 0, st, ev_start, ev_end, 0, n_items,
+                        (const uint32_t *)dig, key_bytes, key_off, item_msg, item_key, (const uint32_t *)r_be,
+                        (const uint32_t *)s_be, pre, kc_tabs, g_table, status, stamps);
   return hipGetLastError();
 }
 

@@ -77,6 +77,14 @@ sys.path.insert(0, ROOT)
 # (4,050 modmuls per verify) is reported only as `speedup_vs_canonical`.
 MODMUL_PER_ITEM_EXEC = 317
 IMUL32_PER_MODMUL = 80
+# The same executed work per kernel (k_verify_g counted on
+# its own).  k_verify_g: 9 G additions x 10 = 90, plus u1 = e w and u2 = r w
+# (two 8-limb Montgomery products mod N, 128 IMUL32 each = 1.6 modmuls) and
+# the GLV split of u2 (two 256x128-bit products + two 128x128, 96 IMUL32 =
+# 1.2) -> 94.4.  k_verify_q: 22 key-table additions x 10 + the final X == r ZZ
+# check (1) -> 221.  (Rounded into the 317 above: 94.4 + 221 + ~1.6 for the
+# digit recoding and sign handling that the modmul count does not see.)
+MODMUL_G, MODMUL_Q = 94.4, 221
 CANONICAL_MODMUL_PER_VERIFY = 4050
 PEAK_IMUL32_PER_S = 31.76e12
 # Measured gfx950 issue costs (profiles/r01_ubench_ops.txt): a wave64
@@ -132,13 +140,31 @@ def check_rank_env(args) -> int:
     if world != args.gpus:
         print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to print a line", file=sys.stderr)
         raise SystemExit(3)
-    if not args.dry_run:
+    if args.dry_run:  # (tests: a box with fewer GPUs than ranks, BENCH_DRY_VISIBLE_GPUS)
+        visible = int(os.environ.get("BENCH_DRY_VISIBLE_GPUS", str(args.gpus)))
+    else:
         import torch
 
-        if torch.cuda.device_count() < args.gpus:
-            print(f"bench.py: --gpus {args.gpus} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
-            raise SystemExit(4)
+        visible = torch.cuda.device_count()
+    if visible < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {visible} GPU(s) visible", file=sys.stderr)
+        raise SystemExit(4)
     return world
+
+
+def dry_fault(where: str, rank: int) -> None:
+    """Dry-run fault injection (tests/test_dist.py):
+    BENCH_DRY_FAULT=rccl_init makes every rank's collective init fail (as
+    dist.init_process_group("nccl") raising), rank_crash makes rank 1 die
+    after the rendezvous (os._exit, no cleanup, as a segfaulting rank).
+    Either way the launcher exits non-zero, no rank prints a line and no
+    child process is left behind."""
+    fault = os.environ.get("BENCH_DRY_FAULT", "")
+    if where == "init" and fault == "rccl_init":
+        raise RuntimeError("injected: collective (RCCL) initialisation failed")
+    if where == "after_init" and fault == "rank_crash" and rank == 1:
+        sys.stdout.flush()
+        os._exit(7)
 
 
 def dry_run(args, world: int, rank: int, worker) -> None:
@@ -150,8 +176,10 @@ def dry_run(args, world: int, rank: int, worker) -> None:
     import torch
     import torch.distributed as dist
 
+    dry_fault("init", rank)
     if world > 1:
         dist.init_process_group("gloo")
+    dry_fault("after_init", rank)
     words = expected_words(rank, args.events)
     t0 = time.perf_counter()
     mine = torch.from_numpy(words.view(np.int64).copy())
@@ -273,6 +301,7 @@ def pmc_profile(n_items: int):
     path = found[-1]
     with open(path) as f:
         tj = json.load(f)
+    tj["tracked_file"] = os.path.relpath(path, ROOT)  # the committed copy (tj["source"]: where it was written)
     return tj if tj.get("items_per_launch") == n_items else None
 
 
@@ -455,6 +484,13 @@ def run(args, world: int, rank: int, local: int, worker) -> None:
             # the whole chip over the timed region (two batches in flight):
             # the verify kernels' executed IMUL32 at the headline rate
             "chip_frac": value / world * MODMUL_PER_ITEM_EXEC * IMUL32_PER_MODMUL / PEAK_IMUL32_PER_S,
+            # per kernel, the same spans: each kernel's executed IMUL32 over its own time
+            "per_kernel": {
+                "k_verify_g": {"ms": kg_ms, "modmul_per_item": MODMUL_G,
+                               "frac": args.events * MODMUL_G * IMUL32_PER_MODMUL / (kg_ms * 1e-3) / PEAK_IMUL32_PER_S},
+                "k_verify_q": {"ms": kq_ms, "modmul_per_item": MODMUL_Q,
+                               "frac": args.events * MODMUL_Q * IMUL32_PER_MODMUL / (kq_ms * 1e-3) / PEAK_IMUL32_PER_S},
+            },
         }
         pmc = pmc_profile(args.events)
         if pmc:
@@ -468,7 +504,7 @@ def run(args, world: int, rank: int, local: int, worker) -> None:
                 roof["traffic_calibration"] = pmc.get("fetch_factor")
             roof["executed_frac"] = i64 * 64 / kv_s / PEAK_IMUL32_PER_S
             roof["valu_issue_frac"] = (i64 * CYC_MAD64 + (ivalu - i64) * CYC_VALU32) / (N_SIMD * 2.4e9 * kv_s)
-            roof["pmc_source"] = pmc["source"]
+            roof["pmc_source"] = pmc["tracked_file"]
         line = {
             "metric": "ECDSA event verifies/sec",
             "value": value,
@@ -748,23 +784,60 @@ def host_breakdown(ts):
             "host_out": mean(ts, "ms_host_out")}
 
 
+def host_diag(batch) -> dict:
+    """The host's state behind the pageable host entry: the
+    CPUs this process may use (affinity, cgroup quota), and one thread's
+    memcpy rate from the batch's pageable message bytes into page-locked
+    memory in this process right now."""
+    import numpy as np
+
+    from babble_amd.verifier import PinnedArena
+
+    out = {"affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+    try:
+        out["cgroup_cpu_max"] = open("/sys/fs/cgroup/cpu.max").read().strip()
+    except OSError:
+        out["cgroup_cpu_max"] = None
+    arena = PinnedArena()
+    try:
+        src = batch.msg_bytes
+        dst = arena.array(src.nbytes, np.uint8)
+        np.copyto(dst, src)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            np.copyto(dst, src)
+        out["memcpy_1thread_gb_s"] = 3 * src.nbytes / (time.perf_counter() - t0) / 1e9
+    finally:
+        arena.close()
+    return out
+
+
 def host_entry_leg(args, v, batch):
     """bv_verify_batch from pageable host buffers (the cgo entry point)."""
+    import resource
+
     msgs = batch.msg_bytes.nbytes
     staged = msgs + batch.msg_off.nbytes + batch.r_be.nbytes + batch.s_be.nbytes + batch.item_msg.nbytes * 2
     v.verify(batch)
     ts = []
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     reps = max(2, min(5, args.steps))
     for _ in range(reps):
         v.verify(batch)
         ts.append(v.timing())
     elapsed = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
     h2d = mean(ts, "ms_h2d")
+    diag = host_diag(batch)
+    diag.update({"minor_faults_per_call": (ru1.ru_minflt - ru0.ru_minflt) / reps,
+                 "invol_ctx_switches_per_call": (ru1.ru_nivcsw - ru0.ru_nivcsw) / reps,
+                 "host_cpu_s_per_call": ((ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)) / reps,
+                 "staging_gb_s": staged / (mean(ts, "ms_host_prep") * 1e-3) / 1e9})
     return {"value": args.events * reps / elapsed, "unit": "verifies/s", "ms_per_call": elapsed / reps * 1e3,
             "ms_h2d": h2d, "ms_d2h_tail": mean(ts, "ms_d2h"), "host_breakdown_ms": host_breakdown(ts),
             "bytes_staged": staged,
-            "pcie_gb_s": staged / (h2d * 1e-3) / 1e9 if h2d > 0 else None,
+            "pcie_gb_s": staged / (h2d * 1e-3) / 1e9 if h2d > 0 else None, "host_diag": diag,
             "note": "inputs in pageable host memory; staged through pinned chunks, hashing overlaps the transfer; "
                     "PCIe-bound (~520 B per event crosses the link)"}
 

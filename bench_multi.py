@@ -274,6 +274,8 @@ def worker_main(argv) -> int:
     a = ap.parse_args(argv)
     if sys.stdin.readline().strip() != "go":
         return 0  # not needed: exit before touching a GPU
+    if a.dry_run and os.environ.get("BENCH_DRY_FAULT") == "worker_crash":  # (tests: a crashing group worker)
+        os._exit(9)
     devices = [int(x) for x in a.devices.split(",")]
     res = _group_dry(devices, a.events_per_device) if a.dry_run else _group_gpu(devices, a.events_per_device, a.reps)
     print(json.dumps(res), flush=True)

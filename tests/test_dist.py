@@ -235,3 +235,88 @@ def test_bench_rank_refuses_world_mismatch():
                                                                        "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+# ------------------------------------------------ N > 1 failure paths --
+# every way an N-GPU run can fail ends with a non-zero exit,
+# no JSON line and no process left behind (the launcher's child
+# torch.distributed.run, its ranks, rank 0's group worker).
+
+def _leftovers(token: str):
+    import psutil
+
+    me = os.getpid()
+    out = []
+    for p in psutil.process_iter(["pid", "cmdline"]):
+        try:
+            cmd = p.info["cmdline"] or []
+            line = " ".join(cmd)
+            ours = any(x in line for x in ("bench.py", "bench_multi.py", "torch.distributed.run"))
+            if p.info["pid"] != me and cmd and "python" in os.path.basename(cmd[0]) and ours and token in line:
+                out.append((p.info["pid"], cmd))
+        except psutil.Error:
+            pass
+    return out
+
+
+def _assert_failed_cleanly(p, events: int):
+    import time
+
+    assert p.returncode != 0, p.stdout[-1000:]
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")], p.stdout
+    deadline = time.time() + 30  # (a terminated rank may take a moment to be reaped)
+    while _leftovers(f"--events {events}") and time.time() < deadline:
+        time.sleep(0.5)
+    assert not _leftovers(f"--events {events}")
+
+
+def test_bench_fewer_gpus_than_ranks_fails_without_a_line():
+    """Ranks that see fewer GPUs than --gpus exit 4 before any work; the
+    launcher fails and prints nothing."""
+    p = _bench(["--gpus", "2", "--dry-run", "--events", "5011"], env={"BENCH_DRY_VISIBLE_GPUS": "1"})
+    _assert_failed_cleanly(p, 5011)
+    assert "GPU(s) visible" in p.stderr
+
+
+def test_bench_collective_init_failure_fails_without_a_line():
+    """The ranks' collective initialisation failing (RCCL at N > 1) ends the
+    run non-zero, no line, no child left."""
+    p = _bench(["--gpus", "2", "--dry-run", "--events", "5012"], env={"BENCH_DRY_FAULT": "rccl_init"})
+    _assert_failed_cleanly(p, 5012)
+    assert "RCCL" in p.stderr
+
+
+def test_bench_rank_crash_fails_without_a_line():
+    """Rank 1 dying after the rendezvous (no cleanup): torch.distributed.run
+    stops rank 0, rank 0's group worker sees EOF and exits, and the launcher
+    exits non-zero without a line."""
+    p = _bench(["--gpus", "2", "--dry-run", "--events", "5013"], env={"BENCH_DRY_FAULT": "rank_crash"})
+    _assert_failed_cleanly(p, 5013)
+
+
+def test_bench_group_worker_crash_is_recorded_and_reaped():
+    """The group worker (bv_group_verify_batch over all N devices from one
+    process) crashing is an extra leg's failure: the line records it as the
+    group leg's error, the headline plumbing stands, and the worker is
+    reaped."""
+    p = _bench(["--gpus", "2", "--dry-run", "--events", "5014"], env={"BENCH_DRY_FAULT": "worker_crash"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    assert "error" in json.loads(lines[0])["group"]
+    assert not _leftovers("--events-per-device 5014")
+
+
+def test_group_create_more_devices_than_exist():
+    """bv_group_create naming devices the process cannot see returns
+    BV_E_NODEVICE (no context, no RCCL init, no crash)."""
+    import ctypes
+
+    import torch
+
+    from babble_amd import native
+
+    n = torch.cuda.device_count()
+    g = ctypes.c_void_p()
+    devs = (ctypes.c_int * 2)(0, n + 3)
+    assert native.lib().bv_group_create(ctypes.byref(g), devs, 2, 0) == native.BV_E_NODEVICE and not g.value

@@ -104,10 +104,20 @@ __device__ __forceinline__ int32_t divsteps_30_jump(int32_t eta, uint32_t f0, ui
   return eta;
 }
 
-// the inversion with the divsteps variant D (0: modinv.h, 1: selects, 2: jump table)
+// the inversion with the divsteps variant D (0: modinv.h, 1: selects, 2: jump
+// table, 3: selects on the VECTOR unit: the input is moved to VGPRs first, so
+// every value derived from it (f, g, eta, the matrices, d, e) is VALU work —
+// 64-bit products are single v_mad_i64_i32 — and the loop exit is an EXEC
+// test instead of a scalar branch on SALU results)
 template <int D>
-__device__ __forceinline__ void modinv_variant(uint32_t r[8], const uint32_t x[8], const modinfo30 &mi,
+__device__ __forceinline__ void modinv_variant(uint32_t r[8], const uint32_t x_in[8], const modinfo30 &mi,
                                                const uint2 *tab) {
+  uint32_t x[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    x[i] = x_in[i];
+    if (D == 3) asm volatile("v_mov_b32 %0, %1" : "=v"(x[i]) : "v"(x_in[i]));
+  }
   s30 d, e, f, g;
 #pragma unroll
   for (int i = 0; i < 9; i++) {
@@ -121,7 +131,7 @@ __device__ __forceinline__ void modinv_variant(uint32_t r[8], const uint32_t x[8
   for (;;) {
     int32_t t[4];
     eta = D == 2   ? divsteps_30_jump(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t, tab)
-          : D == 1 ? divsteps_30_sel(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t)
+          : D >= 1 ? divsteps_30_sel(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t)
                    : divsteps_30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
     update_de_30(d, e, t, mi);
     update_fg_30(f, g, t);
@@ -277,9 +287,14 @@ int main() {
   }
   uint32_t r2[8 * reps];
   hipMemcpy(r2, dout2, sizeof r2, hipMemcpyDeviceToHost);
+  uint32_t r3[8 * reps];
+  for (int rep = 0; rep < 2; rep++) hipLaunchKernelGGL(k_variant<3>, dim3(1), dim3(256), 0, 0, dx, reps, dout2, dclk2);
+  hipMemcpy(r3, dout2, sizeof r3, hipMemcpyDeviceToHost);
   hipMemcpy(c2, dclk2, 64, hipMemcpyDeviceToHost);
-  int diff = 0, diff2 = 0;
-  for (int i = 0; i < 8 * reps; i++) diff += r0[i] != r1[i], diff2 += r0[i] != r2[i];
+  int diff = 0, diff2 = 0, diff3 = 0;
+  for (int i = 0; i < 8 * reps; i++) diff += r0[i] != r1[i], diff2 += r0[i] != r2[i], diff3 += r0[i] != r3[i];
+  printf("modinv_var per inversion, selects on the VECTOR unit: %.0f clocks (%d differing words)\n",
+         (double)c2[3] / reps, diff3);
   printf("modinv_var per inversion: divsteps_30_var %.0f clocks, divsteps with select swap %.0f clocks "
          "(%d differing words), jump table %.0f clocks (%d differing words; table build %.0f clocks)\n",
          (double)c2[0] / reps, (double)c2[1] / reps, diff, (double)c2[2] / reps, diff2, (double)c2[4]);
