@@ -477,6 +477,7 @@ static int create_impl(bv_ctx *ctx) {
   if (const char *s = getenv("BV_EV_D2H")) ctx->ev_d2h = atoi(s);
   if (const char *s = getenv("BV_EV_TAIL")) ctx->ev_tail = atoi(s);
   if (const char *s = getenv("BV_SMALL_STAMPS")) ctx->small_stamps = atoi(s) != 0;
+  if (const char *s = getenv("BV_HOST_STAMPS")) ctx->host_stamps = atoi(s) != 0;
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS")) ctx->table_min_items = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS_MANY")) ctx->table_min_items_many = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_K12_MIN_ITEMS")) ctx->k12_min_items = (uint64_t)std::max(1, atoi(s));
@@ -523,7 +524,7 @@ extern "C" void bv_destroy(bv_ctx *ctx) {
     if (ctx->has_done) (void)hipEventSynchronize(ctx->ev_done);
   }
   if (ctx->g_table) gtable_release(ctx->device);
-  DevBuf *bufs[] = {&ctx->d_in, &ctx->kc_kxy, &ctx->kc_btabs, &ctx->ev_iota, &ctx->d_stamps};
+  DevBuf *bufs[] = {&ctx->d_in, &ctx->kc_kxy, &ctx->kc_btabs, &ctx->ev_iota, &ctx->d_stamps, &ctx->d_sig};
   for (auto *b : bufs) b->release();
   for (auto &sl : ctx->slot) {
     DevBuf *sb[] = {&sl.digests,   &sl.kstatus, &sl.kxy, &sl.bases_jac, &sl.key_sub, &sl.key_pscr,
@@ -971,6 +972,9 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   call->t0 = t0;
   int rc = bv_validate_host_batch(ctx, b);
   if (rc != BV_OK) return rc;
+  // BV_HOST_STAMPS (diagnostics): the host phases of this call on stderr
+  auto stamp_ms = [t0]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+  double st_validated = ctx->host_stamps ? stamp_ms() : 0, st_items = 0, st_first = 0;
   hipStream_t st = ctx->stream, cs = bv_copy_stream(ctx);
   if (!cs) return bv_fail(ctx, BV_E_NODEVICE, "copy stream");
   ctx->last = st;
@@ -1104,6 +1108,7 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   d.s_be = dev + segs[6].off;
   d.pre = b->pre ? dev + segs[7].off : nullptr;
 
+  if (ctx->host_stamps) st_items = stamp_ms();
   // key cache resolution needs the keys on the device (decode of misses)
   bool kc = false;
   if ((ctx->flags & BV_F_KEY_CACHE) && n_keys && n_keys <= kKcMaxBatchKeys) {
@@ -1177,6 +1182,7 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
     hipEvent_t e = chunk_event();
     HIPCHK(hipEventRecord(e, cs), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, e, 0), BV_E_LAUNCH, "join chunk");
+    if (m0 == 0 && ctx->host_stamps) st_first = stamp_ms();
     if (m0 == 0) HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SMALL], 0), BV_E_LAUNCH, "join offsets");
     HIPCHK(bvk::sha256(st, m1 - m0, d.msg_bytes, d.msg_off + m0, pipe.o.dig + 8 * m0, kHostHashLen), BV_E_LAUNCH,
            "k_sha256");
@@ -1220,6 +1226,11 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   }
   HIPCHK(hipEventRecord(ctx->S().ev[E_STAGED], cs), BV_E_LAUNCH, "event");
   call->ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (ctx->host_stamps)
+    fprintf(stderr,
+            "bv_host_launch ms: validated %.3f items_staged %.3f first_msg_chunk %.3f staged %.3f (msgs %.1f MB, "
+            "%d copy threads)\n",
+            st_validated, st_items, st_first, (double)call->ms_prep, msg_len / 1e6, (int)ctx->pool->th.size());
   HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_STAGED], 0), BV_E_LAUNCH, "join staging");
   HIPCHK(hipEventRecord(ctx->S().ev[E_SHA], st), BV_E_LAUNCH, "event");
   if (n_msgs == 0) HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");

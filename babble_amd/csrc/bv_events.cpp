@@ -38,8 +38,17 @@ int validate(bv_ctx *ctx, const bv_event_batch *b) {
   const uint64_t n = b->n_events;
   if (!n) return BV_OK;
   if (!b->creator || !b->index || !b->timestamp || !b->parent_kind || !b->parent_ref || !b->tx_start ||
-      !b->r_be || !b->s_be || !b->key_off)
+      (!b->sig_text && (!b->r_be || !b->s_be)) || !b->key_off)
     return bv_fail(ctx, BV_E_ARGS, "null event array");
+  if (b->sig_text) {  // signature text: offsets from 0, monotone
+    if (!b->sig_off || b->sig_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "sig_off missing or sig_off[0] != 0");
+    if (!ctx->pool->parallel_for(n, 1 << 17, [b](uint64_t lo, uint64_t hi) {
+          for (uint64_t e = lo; e < hi; e++)
+            if (b->sig_off[e] > b->sig_off[e + 1]) return false;
+          return true;
+        }))
+      return bv_fail(ctx, BV_E_ARGS, "sig_off not monotone");
+  }
   if (b->key_off[0] != 0) return bv_fail(ctx, BV_E_ARGS, "key_off[0] != 0");
   for (uint32_t k = 0; k < b->n_keys; k++)
     if (b->key_off[k] > b->key_off[k + 1]) return bv_fail(ctx, BV_E_ARGS, "key_off not monotone");
@@ -85,6 +94,24 @@ int validate(bv_ctx *ctx, const bv_event_batch *b) {
   return BV_OK;
 }
 
+// Signature text (eb->sig_text): the device decodes r, s and pre into
+// ctx->d_sig on the s^-1 stream once the text has landed (`text_ready`),
+// ahead of s^-1; E_SDEC marks them written.  Returns the device arrays.
+struct SigOut {
+  uint8_t *r = nullptr, *s = nullptr, *pre = nullptr;
+};
+int sig_decode_on_device(bv_ctx *ctx, uint64_t n, const uint64_t *d_off, const uint8_t *d_text, hipEvent_t text_ready,
+                         SigOut *out) {
+  const size_t rs = align256(n * 32);
+  HIPCHK(ctx->d_sig.ensure(2 * rs + align256(n)), BV_E_OOM, "alloc decoded signatures");
+  uint8_t *base = ctx->d_sig.as<uint8_t>();
+  out->r = base, out->s = base + rs, out->pre = base + 2 * rs;
+  HIPCHK(hipStreamWaitEvent(ctx->sstream, text_ready, 0), BV_E_LAUNCH, "join signature text");
+  HIPCHK(bvk::sig_decode(ctx->sstream, n, d_off, d_text, out->r, out->s, out->pre), BV_E_LAUNCH, "k_sig_decode");
+  HIPCHK(hipEventRecord(ctx->S().ev[E_SDEC], ctx->sstream), BV_E_LAUNCH, "event");
+  return BV_OK;
+}
+
 }  // namespace
 
 static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *res);
@@ -108,8 +135,11 @@ static int verify_events_dag_host(bv_ctx *ctx, const bv_event_batch *eb, bv_resu
     return o;
   };
   const size_t o_koff = at((eb->n_keys + 1) * 8ull), o_kb = at(key_len, 64), keys_end = total;
-  const size_t o_s = at(n * 32), o_pre = at(eb->pre ? n : 0), s_end = total;
-  const size_t o_r = at(n * 32), o_cr = at(n * 4), small_end = total;
+  // s and pre, or the signature text (decoded on the device: r, s, pre)
+  const bool text = eb->sig_text != nullptr;
+  const uint64_t text_len = text ? eb->sig_off[n] : 0;
+  const size_t o_s = at(text ? (n + 1) * 8 : n * 32), o_pre = at(text ? text_len : (eb->pre ? n : 0)), s_end = total;
+  const size_t o_r = at(text ? 0 : n * 32), o_cr = at(n * 4), small_end = total;
   const size_t o_dig = at(n * 32);
   if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // previous calls' work buffers / staging
   HIPCHK(ctx->pin_in.ensure(total), BV_E_OOM, "alloc pinned staging");
@@ -152,17 +182,29 @@ static int verify_events_dag_host(bv_ctx *ctx, const bv_event_batch *eb, bv_resu
     rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, vb.key_bytes, vb.key_off, st, &kc, false, &items);
     if (rc != BV_OK) return rc;
   }
-  put(o_s, eb->s_be, n * 32);
-  if (eb->pre) put(o_pre, eb->pre, n);
+  if (text) {
+    put(o_s, eb->sig_off, (n + 1) * 8);
+    put(o_pre, eb->sig_text, text_len);
+  } else {
+    put(o_s, eb->s_be, n * 32);
+    if (eb->pre) put(o_pre, eb->pre, n);
+  }
   if ((rc = h2d(keys_end, s_end)) != BV_OK) return rc;
   HIPCHK(hipEventRecord(ctx->S().ev[E_SREADY], cs), BV_E_LAUNCH, "event");
+  if (text) {
+    SigOut so;
+    rc = sig_decode_on_device(ctx, n, (const uint64_t *)(dev + o_s), dev + o_pre, ctx->S().ev[E_SREADY], &so);
+    if (rc != BV_OK) return rc;
+    vb.r_be = so.r, vb.s_be = so.s, vb.pre = so.pre;
+  }
   rc = bv_run_keys(ctx, &vb, ctx->S().ev[E_KREADY], ctx->S().ev[E_SREADY], kc);
   if (rc != BV_OK) return rc;
-  put(o_r, eb->r_be, n * 32);
+  if (!text) put(o_r, eb->r_be, n * 32);
   put(o_cr, eb->creator, n * 4);
   if ((rc = h2d(s_end, small_end)) != BV_OK) return rc;
   HIPCHK(hipEventRecord(ctx->S().ev[E_SMALL], cs), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SMALL], 0), BV_E_LAUNCH, "join");
+  if (text) HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SDEC], 0), BV_E_LAUNCH, "join decoded signatures");
   HIPCHK(bvk::iota(st, n, ctx->ev_iota.as<uint32_t>()), BV_E_LAUNCH, "k_iota");
   HIPCHK(hipEventRecord(ctx->S().ev[E_FORK], st), BV_E_LAUNCH, "event");
 
@@ -284,19 +326,21 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   const size_t o_koff = add(eb->key_off, (eb->n_keys + 1) * 8ull, ALL);
   const size_t o_kb = add(eb->key_bytes, key_len, ALL, 1, 64);
   const size_t keys_end = total;
-  const size_t o_s = add(eb->s_be, n * 32, ALL);
-  const size_t o_pre = add(eb->pre, eb->pre ? n : 0, ALL);
+  // s and pre, or the signature text (decoded on the device into r, s, pre)
+  const bool text = eb->sig_text != nullptr;
+  const size_t o_s = text ? add(eb->sig_off, (n + 1) * 8, ALL) : add(eb->s_be, n * 32, ALL);
+  const size_t o_pre = text ? add(eb->sig_text, eb->sig_off[n], ALL) : add(eb->pre, eb->pre ? n : 0, ALL);
   const size_t s_end = total;
   // key part first (ctx->qfirst): r and the creators cross before the
   // chunks, so every item's k1 Q + k2 phi(Q) is summed under the transfer
   // of the bodies and only u1 G waits for each chunk's digests
   const bool qf = ctx->qfirst;
-  const size_t o_r = qf ? add(eb->r_be, n * 32, ALL) : 0;
+  const size_t o_r = qf && !text ? add(eb->r_be, n * 32, ALL) : 0;
   const size_t o_cr = qf ? add(eb->creator, n * 4, ALL) : 0;
   const size_t r_end = total;
   const size_t o_ph = add(eb->parent_hashes, eb->parent_hashes ? eb->n_parent_hashes * 32 : 0, ALL);
   const size_t small_end = total;
-  const size_t o_r_ev = qf ? o_r : add(eb->r_be, n * 32, EV, 32);
+  const size_t o_r_ev = qf || text ? o_r : add(eb->r_be, n * 32, EV, 32);
   const size_t o_cr_ev = qf ? o_cr : add(eb->creator, n * 4, EV, 4);
   const size_t o_ix = add(eb->index, n * 8, EV, 8);
   const size_t o_ts = add(eb->timestamp, n * 8, EV, 8);
@@ -462,9 +506,16 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
     rc = bv_kc_prepare(ctx, eb->n_keys, eb->key_bytes, eb->key_off, d.key_bytes, d.key_off, st, &kc, false, &items);
     if (rc != BV_OK) return rc;
   }
-  rc = stage(keys_end, s_end);  // s, pre: s^-1
+  rc = stage(keys_end, s_end);  // s, pre (or the signature text): s^-1
   if (rc != BV_OK) return rc;
   HIPCHK(hipEventRecord(ctx->S().ev[E_SREADY], cs), BV_E_LAUNCH, "event");
+  if (text) {  // r, s, pre from the text, ahead of s^-1; the verify stream reads them
+    SigOut so;
+    rc = sig_decode_on_device(ctx, n, (const uint64_t *)(dev + o_s), dev + o_pre, ctx->S().ev[E_SREADY], &so);
+    if (rc != BV_OK) return rc;
+    vb.r_be = d.r_be = so.r, vb.s_be = d.s_be = so.s, vb.pre = d.pre = so.pre;
+    HIPCHK(hipStreamWaitEvent(vst, ctx->S().ev[E_SDEC], 0), BV_E_LAUNCH, "join decoded signatures");
+  }
   pipe.kc = kc;
   rc = bv_run_keys(ctx, &vb, ctx->S().ev[E_KREADY], ctx->S().ev[E_SREADY], kc);
   if (rc != BV_OK) return rc;

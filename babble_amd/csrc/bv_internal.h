@@ -34,6 +34,8 @@ hipError_t key_decode(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, 
 hipError_t sha256_chain(hipStream_t, uint32_t, const uint8_t *, const uint64_t *, uint8_t *, uint32_t *);
 hipError_t ev_body_hash(hipStream_t st, const bv_event_batch &b, uint64_t e0, uint64_t e1, uint32_t *dig);
 hipError_t iota(hipStream_t, uint64_t, uint32_t *);
+hipError_t sig_decode(hipStream_t, uint64_t n, const uint64_t *off, const uint8_t *text, uint8_t *r_be, uint8_t *s_be,
+                      uint8_t *pre);
 hipError_t build_tables(hipStream_t, int, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *,
                         uint32_t *, uint32_t *, uint64_t n_items);
 hipError_t build_kc(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *, uint32_t *, uint32_t *,
@@ -206,7 +208,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // timing / ordering events (see bv_read_timing)
 enum {
   E_START, E_FORK, E_SHA, E_SCALAR, E_G, E_JOINED, E_END, E_KEYS, E_SINV,
-  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_RREADY, E_KCTAB, E_KDEC, E_KCDEC, E_COUNT
+  E_CALL, E_SMALL, E_HASH0, E_STAGED, E_HASHED, E_OUT, E_CSDONE, E_READY, E_KREADY, E_SREADY, E_RREADY, E_KCTAB, E_KDEC, E_KCDEC, E_SDEC, E_COUNT
 };
 
 constexpr uint32_t kKcMaxBatchKeys = 4096;  // key cache: batches with more keys use per-batch tables
@@ -245,6 +247,7 @@ struct bv_ctx {
   PinnedBuf small_io;  // k_small's inputs and statuses, read / written by the kernel in place (mapped, coherent)
   DevBuf d_in;
   DevBuf d_stamps;  // BV_SMALL_STAMPS: k_small phase clocks (diagnostics)
+  DevBuf d_sig;     // bv_verify_events with signature text: the decoded r, s, pre
   // host entry: messages longer than kHostHashLen hashed on the host (their
   // index and digest), uploaded beside the device hashing
   PinnedBuf pin_long;
@@ -315,6 +318,7 @@ struct bv_ctx {
   uint64_t table_min_items_many = 48;  // the same above kManyKeys keys
   uint64_t k12_min_items = 8192;  // per-batch K12 (not K8) tables from this many items per key
   bool small_stamps = false;      // BV_SMALL_STAMPS=1: print k_small's phase clocks to stderr
+  bool host_stamps = false;       // BV_HOST_STAMPS=1: print the host entry's phases to stderr
   uint32_t small_span = 0;        // 1 + the slot of a small batch whose device span is not read yet
   uint64_t small_max = 256;       // k_small for batches of at most this many items and messages (BV_SMALL_MAX)
   uint64_t small_warm_max = 1024;  // k_small for batches whose keys are all cached (BV_SMALL_WARM_MAX)

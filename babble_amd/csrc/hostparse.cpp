@@ -23,7 +23,23 @@ namespace {
 const uint32_t kN[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
                         0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
 
+// digit value of a byte in base 36 (0-9, a-z, A-Z), 0xFF otherwise
+struct Digits36 {
+  uint8_t v[256];
+  constexpr Digits36() : v() {
+    for (int c = 0; c < 256; c++) v[c] = 0xFF;
+    for (int c = '0'; c <= '9'; c++) v[c] = (uint8_t)(c - '0');
+    for (int c = 'a'; c <= 'z'; c++) v[c] = (uint8_t)(c - 'a' + 10);
+    for (int c = 'A'; c <= 'Z'; c++) v[c] = (uint8_t)(c - 'A' + 10);
+  }
+};
+constexpr Digits36 kDigit36;
+
 // Parse one base-36 part.  Returns the class; for BV_SC_OK writes 32 BE bytes.
+// Up to 12 digits at a time are gathered into one word (36^12 < 2^63) and
+// folded into a 320-bit accumulator with one 64 x 64 -> 128-bit product per
+// limb (the Go shim decodes every event's signature on the host: ~10x fewer
+// operations than a 32-bit limb pass per digit).
 uint8_t parse36(const char *s, size_t len, uint8_t out[32]) {
   memset(out, 0, 32);
   if (len == 0) return BV_SC_NIL;  // scanSign hits EOF
@@ -35,49 +51,49 @@ uint8_t parse36(const char *s, size_t len, uint8_t out[32]) {
   } else if (s[0] == '+') {
     i = 1;
   }
-  uint32_t v[9] = {0};  // 288-bit accumulator
-  bool big = false;     // value >= 2^288 (certainly >= N)
-  size_t count = 0;
-  for (; i < len; i++) {
-    const unsigned char c = (unsigned char)s[i];
-    uint32_t d;
-    if (c >= '0' && c <= '9')
-      d = c - '0';
-    else if (c >= 'a' && c <= 'z')
-      d = c - 'a' + 10;
-    else if (c >= 'A' && c <= 'Z')
-      d = c - 'A' + 10;
-    else
-      break;
-    count++;
-    if (!big) {
-      uint64_t carry = d;
-      for (int k = 0; k < 9; k++) {
-        uint64_t t = (uint64_t)v[k] * 36u + carry;
-        v[k] = (uint32_t)t;
-        carry = t >> 32;
+  uint64_t v[5] = {0, 0, 0, 0, 0};  // 320-bit accumulator
+  bool big = false;                 // value >= 2^320 (certainly >= N)
+  const size_t first = i;
+  while (i < len) {
+    uint64_t chunk = 0, scale = 1;
+    size_t k = 0;
+    for (; k < 12 && i < len; k++, i++) {
+      const uint8_t d = kDigit36.v[(unsigned char)s[i]];
+      if (d == 0xFF) break;
+      chunk = chunk * 36u + d;
+      scale *= 36u;
+    }
+    if (k && !big) {  // v = v * 36^k + chunk
+      unsigned __int128 carry = chunk;
+      for (int j = 0; j < 5; j++) {
+        const unsigned __int128 t = (unsigned __int128)v[j] * scale + carry;
+        v[j] = (uint64_t)t;
+        carry = t >> 64;
       }
       if (carry) big = true;
     }
+    if (k < 12 && i < len) break;  // a byte that is not a digit
   }
-  if (count == 0) return BV_SC_NIL;  // errNoDigits
+  if (i == first) return BV_SC_NIL;  // errNoDigits
   if (i != len) return BV_SC_NIL;    // trailing garbage: not fully consumed
   bool zero = !big;
-  for (int k = 0; k < 9 && zero; k++) zero = v[k] == 0;
+  for (int k = 0; k < 5 && zero; k++) zero = v[k] == 0;
   if (zero) return BV_SC_NONPOS;     // "-0" and "0" are 0
   if (neg) return BV_SC_NONPOS;
-  if (big || v[8] != 0) return BV_SC_GE_N;
+  if (big || v[4] != 0) return BV_SC_GE_N;
+  uint32_t w32[8];
+  for (int k = 0; k < 4; k++) w32[2 * k] = (uint32_t)v[k], w32[2 * k + 1] = (uint32_t)(v[k] >> 32);
   // compare with N
   bool ge = true;
   for (int k = 7; k >= 0; k--) {
-    if (v[k] != kN[k]) {
-      ge = v[k] > kN[k];
+    if (w32[k] != kN[k]) {
+      ge = w32[k] > kN[k];
       break;
     }
   }
   if (ge) return BV_SC_GE_N;
   for (int k = 0; k < 8; k++) {
-    const uint32_t w = v[7 - k];
+    const uint32_t w = w32[7 - k];
     out[4 * k] = (uint8_t)(w >> 24);
     out[4 * k + 1] = (uint8_t)(w >> 16);
     out[4 * k + 2] = (uint8_t)(w >> 8);

@@ -104,6 +104,88 @@ __global__ void __launch_bounds__(EVH_NT) k_ev_body_hash(bv_event_batch b, uint6
   dst[1] = make_uint4(be[4], be[5], be[6], be[7]);
 }
 
+// keys.DecodeSignature + the range checks on the device, one lane per event
+// (bv_event_batch sig_text): the same rules as bv_decode_signature
+// (hostparse.cpp, Go 1.13 strings.Split + big.Int.SetString(., 36)): exactly
+// one '|'; each part an optional '+' / '-', then base-36 digits only, at
+// least one; classes NIL / NONPOS / GE_N / OK; r and s as 32 big-endian
+// bytes (zero unless OK) and the pre byte.  Six digits at a time (36^6 <
+// 2^32) are folded into a 288-bit value with one mad per limb.
+namespace {
+DEV uint32_t digit36(uint32_t c) {
+  if (c - '0' < 10u) return c - '0';
+  if (c - 'a' < 26u) return c - 'a' + 10;
+  if (c - 'A' < 26u) return c - 'A' + 10;
+  return 0xFFu;
+}
+DEV uint8_t sig_part36(const uint8_t *s, uint64_t len, uint8_t *out) {
+  uint32_t v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  bool big = false;
+  uint64_t i = 0;
+  bool neg = false;
+  if (len && (s[0] == '-' || s[0] == '+')) neg = s[0] == '-', i = 1;
+  const uint64_t first = i;
+  while (i < len) {
+    uint32_t chunk = 0, scale = 1, k = 0;
+    for (; k < 6 && i < len; k++, i++) {
+      const uint32_t d = digit36(s[i]);
+      if (d == 0xFFu) break;
+      chunk = chunk * 36u + d;
+      scale *= 36u;
+    }
+    if (k && !big) {
+      uint64_t carry = chunk;
+#pragma unroll
+      for (int j = 0; j < 9; j++) {
+        const uint64_t t = (uint64_t)v[j] * scale + carry;
+        v[j] = (uint32_t)t;
+        carry = t >> 32;
+      }
+      big = carry != 0;
+    }
+    if (k < 6 && i < len) break;  // not a digit
+  }
+  uint4 *o = (uint4 *)out;
+  o[0] = o[1] = make_uint4(0, 0, 0, 0);
+  if (len == 0 || i == first || i != len) return BV_SC_NIL;
+  bool zero = !big;
+#pragma unroll
+  for (int j = 0; j < 9; j++) zero = zero && v[j] == 0;
+  if (zero || neg) return BV_SC_NONPOS;
+  if (big || v[8]) return BV_SC_GE_N;
+  if (!u256_lt(v, SC_N)) return BV_SC_GE_N;
+  const uint32_t w[8] = {__builtin_bswap32(v[7]), __builtin_bswap32(v[6]), __builtin_bswap32(v[5]),
+                         __builtin_bswap32(v[4]), __builtin_bswap32(v[3]), __builtin_bswap32(v[2]),
+                         __builtin_bswap32(v[1]), __builtin_bswap32(v[0])};
+  o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  return BV_SC_OK;
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256) k_sig_decode(uint64_t n, const uint64_t *__restrict__ off,
+                                                     const uint8_t *__restrict__ text, uint8_t *__restrict__ r_be,
+                                                     uint8_t *__restrict__ s_be, uint8_t *__restrict__ pre) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint8_t *s = text + off[e];
+  const uint64_t len = off[e + 1] - off[e];
+  uint64_t bar = len, parts = 1;
+  for (uint64_t i = 0; i < len; i++)
+    if (s[i] == '|') {
+      if (parts == 1) bar = i;
+      parts++;
+    }
+  uint8_t *r = r_be + 32 * e, *sv = s_be + 32 * e;
+  if (parts != 2) {
+    ((uint4 *)r)[0] = ((uint4 *)r)[1] = ((uint4 *)sv)[0] = ((uint4 *)sv)[1] = make_uint4(0, 0, 0, 0);
+    pre[e] = BV_PRE_PARTS_BAD;
+    return;
+  }
+  const uint8_t rc = sig_part36(s, bar, r), sc = sig_part36(s + bar + 1, len - bar - 1, sv);
+  pre[e] = BV_PRE(rc, sc);
+}
+
 __global__ void __launch_bounds__(256) k_iota(uint64_t n, uint32_t *__restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = (uint32_t)i;
@@ -707,13 +789,15 @@ DEV uint32_t lds_acquire(const uint32_t *p) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 DEV void lds_release(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
-// BV_SINV_VALU: the split inversion's values live in VGPRs (lane 0 of each
-// of the two waves), so the divsteps, the matrix products (one
-// v_mad_i64_i32 each) and the loop tests run on the VECTOR unit; the
-// scalar unit's dependent-instruction latency and taken branches made the
-// divsteps ~135 clocks each (profiles/r05_ubench_sinv.txt, r06_ubench_sinv.txt)
+// BV_SINV_VALU (A/B, off): the split inversion's values in VGPRs (lane 0 of
+// each of the two waves), so the divsteps, the matrix products (one
+// v_mad_i64_i32 each) and the loop tests run on the VECTOR unit.  Alone it
+// is 13 % faster than the scalar unit (69k against 79k clocks per
+// inversion, profiles/r06_ubench_sinv.txt); inside k_small, beside the
+// other waves' vector work, the split inversion measured 75k-105k clocks
+// against 70k-75k on the scalar unit (profiles/r06_small_lat_b.log)
 #ifndef BV_SINV_VALU
-#define BV_SINV_VALU 1
+#define BV_SINV_VALU 0
 #endif
 DEV uint32_t in_vgpr(uint32_t x) {
 #if BV_SINV_VALU
@@ -1171,6 +1255,13 @@ hipError_t put_digests(hipStream_t st, uint64_t n, const uint64_t *idx, const ui
 hipError_t ev_body_hash(hipStream_t st, const bv_event_batch &b, uint64_t e0, uint64_t e1, uint32_t *dig) {
   if (e1 <= e0) return hipSuccess;
   hipLaunchKernelGGL(k_ev_body_hash, grid1(e1 - e0, EVH_NT), dim3(EVH_NT), 0, st, b, e0, e1, dig);
+  return hipGetLastError();
+}
+
+hipError_t sig_decode(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *text, uint8_t *r_be,
+                      uint8_t *s_be, uint8_t *pre) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sig_decode, grid1(n, 256), dim3(256), 0, st, n, off, text, r_be, s_be, pre);
   return hipGetLastError();
 }
 

@@ -36,7 +36,7 @@ class BvEventBatch(ctypes.Structure):
         ("creator", P), ("index", P), ("timestamp", P), ("parent_kind", P), ("parent_ref", P),
         ("n_parent_hashes", ctypes.c_uint64), ("parent_hashes", P), ("tx_start", P), ("tx_off", P),
         ("tx_bytes", P), ("tx_list_nil", P), ("tx_nil", P), ("itx_off", P), ("itx_json", P), ("bsig_off", P),
-        ("bsig_json", P), ("r_be", P), ("s_be", P), ("pre", P),
+        ("bsig_json", P), ("r_be", P), ("s_be", P), ("pre", P), ("sig_off", P), ("sig_text", P),
     ]
 
 
@@ -62,6 +62,10 @@ class EventWireBatch:
     r_be: np.ndarray            # u8 [n, 32]
     s_be: np.ndarray            # u8 [n, 32]
     pre: Optional[np.ndarray]   # u8 [n]
+    # or the Event.Signature text (decoded on the device; r_be / s_be / pre
+    # are then not sent): u64 [n + 1] offsets and the bytes
+    sig_off: Optional[np.ndarray] = None
+    sig_text: Optional[np.ndarray] = None
 
     @property
     def n_events(self) -> int:
@@ -88,8 +92,22 @@ class EventWireBatch:
         b.tx_list_nil, b.tx_nil = p(self.tx_list_nil), p(self.tx_nil)
         b.itx_off, b.itx_json = p(self.itx_off, np.uint64), p(self.itx_json)
         b.bsig_off, b.bsig_json = p(self.bsig_off, np.uint64), p(self.bsig_json)
-        b.r_be, b.s_be, b.pre = p(self.r_be), p(self.s_be), p(self.pre)
+        if self.sig_text is not None:  # the text only (the library decodes it on the device)
+            b.sig_off, b.sig_text = p(self.sig_off, np.uint64), p(self.sig_text)
+            if not b.sig_text:  # all signatures empty: a valid non-null pointer to zero bytes
+                keep.append(np.zeros(1, np.uint8))
+                b.sig_text = keep[-1].ctypes.data
+        else:
+            b.r_be, b.s_be, b.pre = p(self.r_be), p(self.s_be), p(self.pre)
         return b
+
+    def with_signature_text(self, text: np.ndarray, off: np.ndarray) -> "EventWireBatch":
+        """The same events carrying their Signature text instead of r / s /
+        pre (bv_event_batch sig_text)."""
+        import dataclasses
+
+        return dataclasses.replace(self, sig_off=np.asarray(off, np.uint64),
+                                   sig_text=np.asarray(text, np.uint8))
 
 
 Parent = Union[None, Tuple[str, Union[int, bytes]]]

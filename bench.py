@@ -807,6 +807,18 @@ def host_diag(batch) -> dict:
         for _ in range(3):
             np.copyto(dst, src)
         out["memcpy_1thread_gb_s"] = 3 * src.nbytes / (time.perf_counter() - t0) / 1e9
+        from concurrent.futures import ThreadPoolExecutor
+
+        for nt in (8, 16):  # numpy releases the GIL for the copies
+            step = (src.nbytes + nt - 1) // nt
+            with ThreadPoolExecutor(nt) as ex:
+                def part(k):
+                    np.copyto(dst[k * step:(k + 1) * step], src[k * step:(k + 1) * step])
+                list(ex.map(part, range(nt)))
+                t0 = time.perf_counter()
+                for _ in range(3):
+                    list(ex.map(part, range(nt)))
+                out[f"memcpy_{nt}threads_gb_s"] = 3 * src.nbytes / (time.perf_counter() - t0) / 1e9
     finally:
         arena.close()
     return out

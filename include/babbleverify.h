@@ -262,6 +262,14 @@ typedef struct {
   const uint8_t *r_be;           /* the event signature, as in bv_batch        */
   const uint8_t *s_be;
   const uint8_t *pre;
+  /* OR the Event.Signature text of every event (sig_off: n_events + 1 byte
+   * offsets into sig_text).  When sig_text is non-NULL, r_be / s_be / pre are
+   * ignored (may be NULL): the device decodes each signature as
+   * bv_decode_signature does (keys.DecodeSignature + the range checks) beside
+   * the key decode, so a caller holding Go strings copies bytes and makes no
+   * call per event. */
+  const uint64_t *sig_off;
+  const uint8_t *sig_text;
 } bv_event_batch;
 
 /* Host buffers in, results out (msg_hash: 32 * n_events; status, accept_bits

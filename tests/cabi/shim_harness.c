@@ -13,9 +13,10 @@
  *                     bv_host_alloc / bv_host_free)
  *   VerifySync        core.sync (core.go:210-245) after ReadWireBatch: the
  *                     resolved WireEvents appended field by field into the
- *                     arena (keys deduplicated by a map, each Signature text
- *                     decoded by bv_decode_signature), ONE bv_verify_events,
- *                     digests and statuses copied out (C.GoBytes)
+ *                     arena (keys deduplicated by a map, each Signature's
+ *                     text bytes copied: the library decodes them on the
+ *                     device), ONE bv_verify_events, digests and statuses
+ *                     copied out (C.GoBytes)
  *   VerifyEvents      Event.Verify (event.go:219-247) for one event through
  *                     bv_verify_batch (addSelfEvent, core.go:291)
  *
@@ -32,7 +33,8 @@
 
 enum {
   S_KEYS, S_KOFF, S_CREATOR, S_INDEX, S_TS, S_PKIND, S_PREF, S_PHASH, S_TXSTART, S_TXOFF, S_TXB, S_TXLNIL,
-  S_TXNIL, S_ITXOFF, S_ITX, S_BSOFF, S_BS, S_R, S_S, S_PRE, S_OUT, S_MSGS, S_MOFF, S_IMSG, S_IKEY, S_NSLOTS
+  S_TXNIL, S_ITXOFF, S_ITX, S_BSOFF, S_BS, S_R, S_S, S_PRE, S_OUT, S_MSGS, S_MOFF, S_IMSG, S_IKEY, S_SIGOFF,
+  S_SIGTXT, S_NSLOTS
 };
 
 /* a batch builder: arena blocks + fill levels (Go: the cbufs of `batch`)
@@ -186,7 +188,7 @@ int shim_sync(const shim_wire *w, uint8_t *digests, uint8_t *status, double *ms)
   const uint64_t n = w->n_events;
   uint64_t n_hashes = 0;
   if (put_u64(b, S_KOFF, 0) || put_u64(b, S_TXSTART, 0) || put_u64(b, S_TXOFF, 0) || put_u64(b, S_ITXOFF, 0) ||
-      put_u64(b, S_BSOFF, 0))
+      put_u64(b, S_BSOFF, 0) || put_u64(b, S_SIGOFF, 0))
     goto out;
   for (uint64_t e = 0; e < n; e++) {
     const uint32_t c = w->creator_id[e];
@@ -215,11 +217,11 @@ int shim_sync(const shim_wire *w, uint8_t *digests, uint8_t *status, double *ms)
     if (w->itx_off && put(b, S_ITX, w->itx_json + w->itx_off[e], w->itx_off[e + 1] - w->itx_off[e])) goto out;
     if (w->bsig_off && put(b, S_BS, w->bsig_json + w->bsig_off[e], w->bsig_off[e + 1] - w->bsig_off[e])) goto out;
     if (put_u64(b, S_ITXOFF, b->n[S_ITX]) || put_u64(b, S_BSOFF, b->n[S_BS])) goto out;
-    uint8_t r[32], s[32];
-    const uint8_t pre =
-        bv_decode_signature(w->sig_text + w->sig_off[e], w->sig_off[e + 1] - w->sig_off[e], r, s);
-    if (put(b, S_R, r, 32) || put(b, S_S, s, 32) || put_u8(b, S_PRE, pre)) goto out;
+    if (put(b, S_SIGTXT, w->sig_text + w->sig_off[e], w->sig_off[e + 1] - w->sig_off[e]) ||
+        put_u64(b, S_SIGOFF, b->n[S_SIGTXT]))
+      goto out;
   }
+  if (put(b, S_SIGTXT, "", 1)) goto out;  /* (a non-null text pointer even when every signature is empty) */
   {
     const size_t words = (n + 63) / 64, out_bytes = 32 * n + n + 8 * words + 8;
     void *op;
@@ -247,9 +249,8 @@ int shim_sync(const shim_wire *w, uint8_t *digests, uint8_t *status, double *ms)
     in.itx_json = b->p[S_ITX];
     in.bsig_off = w->bsig_off ? (const uint64_t *)b->p[S_BSOFF] : NULL;
     in.bsig_json = b->p[S_BS];
-    in.r_be = b->p[S_R];
-    in.s_be = b->p[S_S];
-    in.pre = b->p[S_PRE];
+    in.sig_off = (const uint64_t *)b->p[S_SIGOFF];
+    in.sig_text = b->p[S_SIGTXT];
     bv_result res;
     res.msg_hash = b->p[S_OUT];
     res.status = b->p[S_OUT] + 32 * n;

@@ -440,3 +440,50 @@ def test_verify_events_key_cache_matches_oracle(parents, n):
         v0.close()
         vc.close()
         vr.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parents,n", [("event", 1200), ("hash", 30_000)])
+def test_verify_events_signature_text_decoded_on_device(parents, n):
+    """bv_event_batch.sig_text: the Signature TEXT of every event, decoded on
+    the device (k_sig_decode) instead of r / s / pre from the host.  A fifth
+    of the events carry adversarial texts (the host fuzzer's corpus: wrong
+    part counts, signs, non-digits, values at and past N, 2^288+), the rest
+    their real signatures.  Statuses, digests and bits equal the same batch
+    with r / s / pre from bv_decode_signature (host) and the C oracle."""
+    import random as _random
+
+    from babble_amd import native
+    from babble_amd.verifier import Verifier
+    from oracle import coracle
+    from tests.cabi import harness
+    from tests.test_hostfuzz import _sig_cases
+
+    packed, wire = synth.event_fields(n, n_creators=6, seed=81, parents=parents)
+    text, off = harness.encode_signatures(wire.r_be, wire.s_be)
+    sigs = [harness.signature_text(text, off, i) for i in range(n)]
+    rng = _random.Random(n)
+    corpus = _sig_cases(_random.Random(7))
+    for i in rng.sample(range(n), n // 5):
+        sigs[i] = rng.choice(corpus)
+    dec = [native.decode_signature(s) for s in sigs]
+    pre = np.array([d[0] for d in dec], np.uint8)
+    r = np.frombuffer(b"".join(d[1] for d in dec), np.uint8).reshape(n, 32).copy()
+    s = np.frombuffer(b"".join(d[2] for d in dec), np.uint8).reshape(n, 32).copy()
+    wire.r_be, wire.s_be, wire.pre = r, s, pre
+    packed.r_be, packed.s_be, packed.pre = r.copy(), s.copy(), pre.copy()
+    h, st, bits = coracle.verify_batch(packed.as_dict())
+    toff = np.zeros(n + 1, np.uint64)
+    toff[1:] = np.cumsum([len(x) for x in sigs])
+    twire = wire.with_signature_text(np.frombuffer(b"".join(sigs), np.uint8).copy(), toff)
+    v = Verifier(0)
+    try:
+        ref = v.verify_events(wire)
+        got = v.verify_events(twire)
+        for res in (ref, got):
+            assert np.array_equal(res.msg_hash, h)
+            assert np.array_equal(res.status, st), np.flatnonzero(res.status != st)[:8]
+            assert np.array_equal(res.accept_bits, bits)
+        assert set(np.unique(st).tolist()) >= {0, 1, 2, 3}
+    finally:
+        v.close()
