@@ -17,6 +17,7 @@
 // chunk.  Digests are copied back as soon as hashing ends (overlapping the
 // verify kernels), statuses and bits after the last kernel.
 #include "bv_internal.h"
+#include "hostscalar.h"
 #include "hostsha.h"
 
 #include <algorithm>
@@ -478,6 +479,7 @@ static int create_impl(bv_ctx *ctx) {
   if (const char *s = getenv("BV_EV_TAIL")) ctx->ev_tail = atoi(s);
   if (const char *s = getenv("BV_SMALL_STAMPS")) ctx->small_stamps = atoi(s) != 0;
   if (const char *s = getenv("BV_HOST_STAMPS")) ctx->host_stamps = atoi(s) != 0;
+  if (const char *s = getenv("BV_HOST_SCALARS")) ctx->host_scalar_max = (uint32_t)atoi(s);
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS")) ctx->table_min_items = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_TABLE_MIN_ITEMS_MANY")) ctx->table_min_items_many = (uint64_t)std::max(1, atoi(s));
   if (const char *s = getenv("BV_K12_MIN_ITEMS")) ctx->k12_min_items = (uint64_t)std::max(1, atoi(s));
@@ -1336,6 +1338,9 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   const size_t o_dig = at(n_msgs * 32), o_key = at(key_len + 64), o_koff = at((n_keys + 1) * 8ull),
                o_im = at(n_items * 4), o_ik = at(n_items * 4), o_r = at(n_items * 32), o_s = at(n_items * 32),
                o_pre = at(n_items), o_tab = at(n_keys * 8ull), o_st = at(n_items);
+  // a latency batch: one host record per item (hostscalar.h) instead
+  const bool recs = n_items <= ctx->host_scalar_max;
+  const size_t o_rec = at(recs ? n_items * hrec::kWords * 4 : 0);
   if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // the previous call may still read the buffer
   const auto t_waited = std::chrono::steady_clock::now();
   ctx->small_io.flags = hipHostMallocMapped | hipHostMallocCoherent;
@@ -1371,6 +1376,15 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   const bool kc = (ctx->flags & BV_F_KEY_CACHE) && n_keys;
   uint32_t hits = 0;
   if (kc) hits = bv_kc_lookup(ctx, n_keys, b->key_bytes, b->key_off, (uint64_t *)(pin + o_tab));
+  if (recs) {
+    const uint64_t *tabs = (const uint64_t *)(pin + o_tab);
+    for (uint64_t i = 0; i < n_items; i++) {
+      const uint32_t k = b->item_key[i];
+      bv_host_item_record((uint32_t *)(pin + o_rec) + hrec::kWords * i, dig + 32ull * b->item_msg[i],
+                          b->r_be + 32 * i, b->s_be + 32 * i, b->pre ? b->pre[i] : 0, b->key_bytes + b->key_off[k],
+                          b->key_off[k + 1] - b->key_off[k], kc ? tabs[k] : 0);
+    }
+  }
   const auto t_staged = std::chrono::steady_clock::now();
   hipEvent_t *ev = ctx->S().ev;
   uint64_t *stamps = nullptr;
@@ -1382,7 +1396,8 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   HIPCHK(bvk::verify_small(st, (uint32_t)n_items, dev + o_dig, dev + o_key, (const uint64_t *)(dev + o_koff),
                            (const uint32_t *)(dev + o_im), (const uint32_t *)(dev + o_ik), dev + o_r, dev + o_s,
                            b->pre ? dev + o_pre : nullptr, kc ? (const uint64_t *)(dev + o_tab) : nullptr,
-                           ctx->g_table, dev + o_st, stamps, ev[E_START], ev[E_END]),
+                           ctx->g_table, dev + o_st, stamps, ev[E_START], ev[E_END],
+                           recs ? (const uint32_t *)(dev + o_rec) : nullptr),
          BV_E_LAUNCH, "k_small");
   int rc = bv_mark_done(ctx, st);
   if (rc != BV_OK) return rc;

@@ -66,7 +66,7 @@ hipError_t verify_small(hipStream_t, uint32_t n_items, const uint8_t *dig, const
                         const uint64_t *key_off, const uint32_t *item_msg, const uint32_t *item_key,
                         const uint8_t *r_be, const uint8_t *s_be, const uint8_t *pre, const uint64_t *kc_tabs,
                         const uint32_t *g_table, uint8_t *status, uint64_t *stamps, hipEvent_t ev_start,
-                        hipEvent_t ev_end);
+                        hipEvent_t ev_end, const uint32_t *rec);
 hipError_t verify_generic(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
@@ -319,6 +319,8 @@ struct bv_ctx {
   uint64_t k12_min_items = 8192;  // per-batch K12 (not K8) tables from this many items per key
   bool small_stamps = false;      // BV_SMALL_STAMPS=1: print k_small's phase clocks to stderr
   bool host_stamps = false;       // BV_HOST_STAMPS=1: print the host entry's phases to stderr
+  uint32_t host_scalar_max = 4;   // BV_HOST_SCALARS: k_small batches up to this many items get host
+                                  // item records (hostscalar.h; 0: the device inverts every item)
   uint32_t small_span = 0;        // 1 + the slot of a small batch whose device span is not read yet
   uint64_t small_max = 256;       // k_small for batches of at most this many items and messages (BV_SMALL_MAX)
   uint64_t small_warm_max = 1024;  // k_small for batches whose keys are all cached (BV_SMALL_WARM_MAX)

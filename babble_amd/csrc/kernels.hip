@@ -28,6 +28,7 @@
 #include <cstdlib>
 
 #include "evjson.h"
+#include "hostscalar.h"
 
 #include "verify_core.h"
 
@@ -705,6 +706,10 @@ __global__ void __launch_bounds__(64) k_verify_deferred(uint64_t n, const uint32
 //            wave 2: elliptic.Unmarshal of the item's key (Q); without a
 //            key-cache table it then doubles Q (kColdD0 doublings)
 //            wave 0: the item's r, digest, pre and table address
+//            (latency batches, <= BV_HOST_SCALARS items: `rec` holds one
+//            256-byte host record per item — key bytes, r, s, pre, table
+//            address and u1, k1, k2 computed on the host, hostscalar.h —
+//            read by ONE wave-wide load; no inversion, wave 2 decodes Q)
 //   phase 2  wave 0 lane 0: decision table, u1 = e w;  wave 1 lane 0:
 //            u2 = r w, its GLV split (k1, k2, signs) and, without a table,
 //            the chain length and the phase count; wave 2: kColdD1 doublings
@@ -945,7 +950,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
                                                const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                const uint8_t *__restrict__ pre, const uint64_t *__restrict__ kc_tabs,
                                                const uint32_t *__restrict__ g_table, uint8_t *__restrict__ status,
-                                               uint64_t *__restrict__ stamps) {
+                                               uint64_t *__restrict__ stamps, const uint32_t *__restrict__ rec) {
   const uint32_t b = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
 #define SMALL_STAMP(k)                                                     \
   do {                                                                     \
@@ -959,6 +964,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
   __shared__ uint32_t sh_sok;
   __shared__ SmallNode sh_a[kSmallLeaves], sh_b[kSmallLeaves / 2 + 1], sh_c[kSmallLeaves / 4 + 2];
   __shared__ SmallCold cs;
+  __shared__ uint32_t sh_rec[hrec::kWords];
   if (b >= n_items) return;  // (the grid is n_items)
   if (t == 0) sh_mail.produced = sh_mail.consumed = sh_mail.done = 0;
   __syncthreads();
@@ -966,8 +972,33 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
   uint32_t dX = 0, dY = 0, dZZ = 0, dZZZ = 0, dBX = 0;
   bool chain = false;  // wave 2: this item doubles Q (no table, Q decoded)
   // ---- phase 1 (the inputs live in host memory, read in place: wave 0
-  // fetches what phases 2-4 need while s^-1 runs)
-  if (lane == 0 && wave == 0) {
+  // fetches what phases 2-4 need while s^-1 runs).  With host records
+  // (hostscalar.h; `rec` is a kernel argument, so the branch is uniform):
+  // ONE 256-byte read, the scalars already there, wave 2 decodes Q.
+  if (rec) {
+    if (wave == 0) sh_rec[lane] = rec[hrec::kWords * (uint64_t)b + lane];
+    __syncthreads();
+    if (lane == 0 && wave == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        sh_r[k] = sh_rec[hrec::kR + k], sh_s[k] = sh_rec[hrec::kS + k], sh_u1[k] = sh_rec[hrec::kU1 + k];
+        sh_k[k] = sh_rec[hrec::kK + k];
+      }
+      sh_signs = sh_rec[hrec::kSigns];
+      sh_pre = sh_rec[hrec::kPre];
+      sh_tab = (uint64_t)sh_rec[hrec::kTab] | (uint64_t)sh_rec[hrec::kTab + 1] << 32;
+      SMALL_STAMP(2);
+    } else if (lane == 0 && wave == 2) {
+      uint8_t st;
+      fe x, y;
+      key_decode_point((const uint8_t *)(sh_rec + hrec::kKey), 0, sh_rec[hrec::kKeyLen], st, x, y);
+#pragma unroll
+      for (int c = 0; c < 8; c++) sh_q[c] = x.v[c], sh_q[8 + c] = y.v[c];
+      sh_ks = st;
+      chain = st == KS_OK && !(sh_rec[hrec::kTab] | sh_rec[hrec::kTab + 1]);
+      SMALL_STAMP(3);
+    }
+  } else if (lane == 0 && wave == 0) {
 #pragma unroll
     for (int k = 0; k < 8; k++) sh_r[k] = r_be[8 * (uint64_t)b + k];
     const uint32_t m = item_msg[b];
@@ -1041,7 +1072,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
     sh_go = cls == 0xFF;
     if (cls != 0xFF) {
       status[b] = cls;
-    } else {
+    } else if (!rec) {  // (a host record holds u1)
       sc inv, eR, a;
 #pragma unroll
       for (int k = 0; k < 8; k++) inv.v[k] = sh_w[k], eR.v[k] = sh_eR[k];
@@ -1050,15 +1081,21 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
       for (int k = 0; k < 8; k++) sh_u1[k] = a.v[k];
     }
   } else if (lane == 0 && wave == 1) {
-    sc inv, rR, u2;
+    uint32_t k1[4], k2[4];
+    if (!rec) {
+      sc inv, rR, u2;
 #pragma unroll
-    for (int k = 0; k < 8; k++) inv.v[k] = sh_w[k], rR.v[k] = sh_rR[k];
-    sc_mont(u2, rR, inv);  // r s^-1 mod N (only used when the item reaches the math)
-    uint32_t k1[4], k2[4], signs;
-    glv_split(k1, k2, signs, u2);
+      for (int k = 0; k < 8; k++) inv.v[k] = sh_w[k], rR.v[k] = sh_rR[k];
+      sc_mont(u2, rR, inv);  // r s^-1 mod N (only used when the item reaches the math)
+      uint32_t signs;
+      glv_split(k1, k2, signs, u2);
 #pragma unroll
-    for (int k = 0; k < 4; k++) sh_k[k] = k1[k], sh_k[4 + k] = k2[k];
-    sh_signs = signs;
+      for (int k = 0; k < 4; k++) sh_k[k] = k1[k], sh_k[4 + k] = k2[k];
+      sh_signs = signs;
+    } else {  // (the host record's split, in sh_k since phase 1)
+#pragma unroll
+      for (int k = 0; k < 4; k++) k1[k] = sh_k[k], k2[k] = sh_k[4 + k];
+    }
     if (!sh_tab) {  // the cold path's chain length and phase count
       uint32_t p1[5], n1[5], p2[5], n2[5], m1[5], m3[5], nb = 0;
       naf_masks(k1, p1, n1);
@@ -1536,11 +1573,11 @@ hipError_t verify_small(hipStream_t st, uint32_t n_items, const uint8_t *dig, co
                         const uint64_t *key_off, const uint32_t *item_msg, const uint32_t *item_key,
                         const uint8_t *r_be, const uint8_t *s_be, const uint8_t *pre, const uint64_t *kc_tabs,
                         const uint32_t *g_table, uint8_t *status, uint64_t *stamps, hipEvent_t ev_start,
-                        hipEvent_t ev_end) {
+                        hipEvent_t ev_end, const uint32_t *rec) {
   if (n_items == 0) return hipSuccess;
   hipExtLaunchKernelGGL(k_small, dim3(n_items), dim3(256), 0, st, ev_start, ev_end, 0, n_items,
                         (const uint32_t *)dig, key_bytes, key_off, item_msg, item_key, (const uint32_t *)r_be,
-                        (const uint32_t *)s_be, pre, kc_tabs, g_table, status, stamps);
+                        (const uint32_t *)s_be, pre, kc_tabs, g_table, status, stamps, rec);
   return hipGetLastError();
 }
 

@@ -933,8 +933,19 @@ def events_entry_leg(args):
         res = vc.verify_events(dag)
         ts.append((time.perf_counter() - t0) * 1e3)
     assert np.all(res.status == 1)
+    # the same response carrying Signature text (decoded on the device), as the shim passes it
+    from tests.cabi import harness
+    dag_t = dag.with_signature_text(*harness.encode_signatures(dag.r_be, dag.s_be))
+    vc.verify_events(dag_t)
+    tt = []
+    for _ in range(15):
+        t0 = time.perf_counter()
+        res = vc.verify_events(dag_t)
+        tt.append((time.perf_counter() - t0) * 1e3)
+    assert np.all(res.status == 1)
     vc.close()
-    out["sync_dag_1000"] = {"ms_median": float(np.median(ts)), "creators": 4, "dag_levels": dag_levels(dag),
+    out["sync_dag_1000"] = {"ms_median": float(np.median(ts)), "ms_median_sig_text": float(np.median(tt)),
+                            "creators": 4, "dag_levels": dag_levels(dag),
                             "cpu": None if args.no_cpu else cpu_sync_dag(dag_packed)}
     return out
 
@@ -1106,14 +1117,16 @@ def shim_path_leg(args, line):
         sh.set_peers([dag_packed.key(k) for k in range(dag_packed.n_keys)])
         sw, keep = sh.wire(dag)
         sh.sync(sw)
-        ts = []
+        ts, ph = [], []
         for _ in range(15):
             _, st, ms = sh.sync(sw)
             assert np.all(st == 1)
             ts.append(ms)
+            ph.append(sh.phases())
         libd = ((line.get("events_entry") or {}).get("sync_dag_1000") or {}).get("ms_median")
         out["sync_dag_1000"] = {"ms_median": float(np.median(ts)), "library_ms": libd,
-                                "over_library": float(np.median(ts)) / libd if libd else None}
+                                "over_library": float(np.median(ts)) / libd if libd else None,
+                                "phases_ms": {k: float(np.median([p[k] for p in ph])) for k in ph[0]}}
         del sw, keep
         packed, wire = synth.event_fields(args.events, n_creators=args.creators, seed=2, parents="hash")
         sh.set_peers([packed.key(k) for k in range(packed.n_keys)])
@@ -1121,14 +1134,17 @@ def shim_path_leg(args, line):
         sw, keep = sh.wire(wire)
         sh.sync(sw)
         ts = []
+        ph = []
         for _ in range(max(2, min(5, args.steps))):
             _, st, ms = sh.sync(sw)
             assert np.all(st == 1)
             ts.append(ms)
+            ph.append(sh.phases())
         ms = float(np.median(ts))
         libb = ((line.get("events_entry") or {}).get("bulk_pinned") or {}).get("value")
         out["bulk_1m"] = {"events": args.events, "ms_median": ms, "value": args.events / (ms * 1e-3),
-                          "unit": "verifies/s", "library_pinned_value": libb}
+                          "unit": "verifies/s", "library_pinned_value": libb,
+                          "phases_ms": {k: float(np.median([p[k] for p in ph])) for k in ph[0]}}
     finally:
         sh.close()
     return out

@@ -39,6 +39,8 @@ def lib():
         B = ctypes.c_char_p
         L.shim_verify_event.argtypes = [B, ctypes.c_size_t, B, ctypes.c_size_t, B, ctypes.c_size_t, P, P,
                                         ctypes.POINTER(ctypes.c_double)]
+        L.shim_last_phases.argtypes = [P]
+        L.shim_last_phases.restype = None
         L.shim_encode_signatures.argtypes = [ctypes.c_uint64, P, P, P, P]
         _lib = L
     return _lib
@@ -128,6 +130,13 @@ class Shim:
         if rc != 0:
             raise RuntimeError(self.L.shim_last_error().decode())
         return dig, st, ms.value
+
+    def phases(self) -> dict:
+        """The last sync's wall ms split: build (the fill), lib
+        (bv_verify_events), out (the copy-out)."""
+        v = (ctypes.c_double * 3)()
+        self.L.shim_last_phases(v)
+        return {"build": v[0], "lib": v[1], "out": v[2]}
 
     def verify_event(self, body: bytes, key: bytes, sig: bytes):
         """VerifyEvents([ev]): (digest, status, wall ms)."""

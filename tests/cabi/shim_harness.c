@@ -12,11 +12,12 @@
  *                     (bv_arena_reserve replaces cbuf.grow's per-call
  *                     bv_host_alloc / bv_host_free)
  *   VerifySync        core.sync (core.go:210-245) after ReadWireBatch: the
- *                     resolved WireEvents appended field by field into the
- *                     arena (keys deduplicated by a map, each Signature's
+ *                     resolved WireEvents written into the arena in two
+ *                     passes over chunks of events (sizes, then the fill at
+ *                     exact offsets; creators keyed by id; each Signature's
  *                     text bytes copied: the library decodes them on the
  *                     device), ONE bv_verify_events, digests and statuses
- *                     copied out (C.GoBytes)
+ *                     copied out (C.GoBytes) by chunk
  *   VerifyEvents      Event.Verify (event.go:219-247) for one event through
  *                     bv_verify_batch (addSelfEvent, core.go:291)
  *
@@ -24,6 +25,7 @@
  * `shim_path` leg times it.  Built by tests/cabi/Makefile (gcc, linked
  * against babble_amd/libbabbleverify.so).
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -45,6 +47,7 @@ typedef struct {
   size_t n[S_NSLOTS], cap[S_NSLOTS];
   uint32_t *kmap;       /* open addressing: key index + 1, 0 = empty */
   uint32_t kmap_cap, n_keys;
+  uint32_t *cid, cid_cap, n_cid; /* creator id -> key index + 1 (Go: map[uint32]uint32) */
 } builder;
 
 static int put(builder *b, int slot, const void *src, size_t len) {
@@ -61,7 +64,6 @@ static int put(builder *b, int slot, const void *src, size_t len) {
 static int put_u8(builder *b, int s, uint8_t v) { return put(b, s, &v, 1); }
 static int put_u32(builder *b, int s, uint32_t v) { return put(b, s, &v, 4); }
 static int put_u64(builder *b, int s, uint64_t v) { return put(b, s, &v, 8); }
-static int put_i64(builder *b, int s, int64_t v) { return put(b, s, &v, 8); }
 
 static uint64_t fnv(const uint8_t *p, size_t n) {
   uint64_t h = 1469598103934665603ull;
@@ -98,6 +100,8 @@ static int64_t key_index(builder *b, const uint8_t *pub, size_t len) {
 static void reset(builder *b) {
   for (int s = 0; s < S_NSLOTS; s++) b->n[s] = 0;
   if (b->kmap) memset(b->kmap, 0, (size_t)b->kmap_cap * 4);
+  if (b->cid) memset(b->cid, 0, (size_t)b->cid_cap * 8);
+  b->n_cid = 0;
   b->n_keys = 0;
 }
 
@@ -120,6 +124,7 @@ static void pool_put(builder *b) {
   }
   bv_arena_destroy(b->arena);
   free(b->kmap);
+  free(b->cid);
   free(b);
 }
 
@@ -133,6 +138,7 @@ void shim_close(void) {
     builder *b = g_free[--g_nfree];
     bv_arena_destroy(b->arena);
     free(b->kmap);
+    free(b->cid);
     free(b);
   }
   if (g_ctx) bv_destroy(g_ctx);
@@ -175,6 +181,172 @@ static double now_ms(void) {
   return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
 }
 
+/* ---- VerifySync's fill: two passes over chunks of events ----
+ * Pass 1 sizes every slot per chunk (and collects the chunk's creator ids
+ * in first-seen order), the creators get their batch key indices in event
+ * order, every slot is reserved ONCE at its exact size, and pass 2 writes
+ * each chunk at its prefix offsets: no per-field capacity check, chunks on
+ * their own threads for large batches (Go: goroutines).
+ * Pass 3 copies the digests and statuses out the same way. */
+typedef struct { uint64_t tx, txb, itx, bs, sig, nh; } fill_at;
+
+typedef struct fill_job {
+  void (*fn)(struct fill_job *);
+  const shim_wire *w;
+  builder *b;
+  uint64_t e0, e1;
+  fill_at at;           /* pass 1: the chunk's sizes; pass 2: its start offsets */
+  uint32_t *ids, n_ids; /* pass 1: the chunk's distinct creator ids, first-seen order */
+  uint32_t *set, set_cap;
+  uint8_t *dig, *st;    /* pass 3 */
+  const bv_result *res;
+} fill_job;
+
+#define MAX_JOBS 8
+
+static void *job_main(void *p) {
+  fill_job *j = (fill_job *)p;
+  j->fn(j);
+  return NULL;
+}
+
+static void run_jobs(fill_job *jobs, int nj, void (*fn)(fill_job *)) {
+  pthread_t th[MAX_JOBS];
+  int started[MAX_JOBS] = {0};
+  for (int i = 0; i < nj; i++) jobs[i].fn = fn;
+  for (int i = 1; i < nj; i++) started[i] = pthread_create(&th[i], NULL, job_main, &jobs[i]) == 0;
+  fn(&jobs[0]);
+  for (int i = 1; i < nj; i++) {
+    if (started[i]) pthread_join(th[i], NULL);
+    else fn(&jobs[i]);
+  }
+}
+
+/* id -> value + 1 in an open-addressed table of 2 * cap words (id, value+1) */
+static uint32_t *idmap_slot(uint32_t *m, uint32_t cap, uint32_t id) {
+  uint32_t h = (id * 2654435761u) & (cap - 1);
+  while (m[2 * h + 1] && m[2 * h] != id) h = (h + 1) & (cap - 1);
+  return m + 2 * h;
+}
+
+static int local_id(fill_job *j, uint32_t id) {
+  if (2 * (j->n_ids + 1) > j->set_cap) {
+    const uint32_t nc = j->set_cap ? 2 * j->set_cap : 64;
+    uint32_t *ns = (uint32_t *)calloc(2 * (size_t)nc, 4), *nl = (uint32_t *)realloc(j->ids, 4 * (size_t)nc);
+    if (!ns || !nl) return free(ns), j->ids = nl ? nl : j->ids, -1;
+    j->ids = nl;
+    for (uint32_t i = 0; i < j->n_ids; i++) {
+      uint32_t *s = idmap_slot(ns, nc, j->ids[i]);
+      s[0] = j->ids[i], s[1] = 1;
+    }
+    free(j->set);
+    j->set = ns, j->set_cap = nc;
+  }
+  uint32_t *s = idmap_slot(j->set, j->set_cap, id);
+  if (!s[1]) s[0] = id, s[1] = 1, j->ids[j->n_ids++] = id;
+  return 0;
+}
+
+static void size_chunk(fill_job *j) {
+  const shim_wire *w = j->w;
+  fill_at z = {0, 0, 0, 0, 0, 0};
+  uint32_t last = 0;
+  int have_last = 0;
+  for (uint64_t e = j->e0; e < j->e1; e++) {
+    const uint32_t c = w->creator_id[e];
+    if (!have_last || c != last) {
+      if (local_id(j, c)) j->n_ids = UINT32_MAX; /* (out of memory: the caller fails) */
+      if (j->n_ids == UINT32_MAX) return;
+      last = c, have_last = 1;
+    }
+    z.nh += (w->parent_kind[2 * e] == BV_PARENT_HASH) + (w->parent_kind[2 * e + 1] == BV_PARENT_HASH);
+    for (uint64_t t = w->tx_start[e]; t < w->tx_start[e + 1]; t++) z.txb += w->tx_off[t + 1] - w->tx_off[t];
+    z.tx += w->tx_start[e + 1] - w->tx_start[e];
+    if (w->itx_off) z.itx += w->itx_off[e + 1] - w->itx_off[e];
+    if (w->bsig_off) z.bs += w->bsig_off[e + 1] - w->bsig_off[e];
+    z.sig += w->sig_off[e + 1] - w->sig_off[e];
+  }
+  j->at = z;
+}
+
+static void fill_chunk(fill_job *j) {
+  const shim_wire *w = j->w;
+  builder *b = j->b;
+  fill_at a = j->at;
+  uint32_t *cr = (uint32_t *)b->p[S_CREATOR];
+  int64_t *idx = (int64_t *)b->p[S_INDEX], *ts = (int64_t *)b->p[S_TS];
+  uint8_t *pk = b->p[S_PKIND], *ph = b->p[S_PHASH];
+  uint64_t *pref = (uint64_t *)b->p[S_PREF], *txs = (uint64_t *)b->p[S_TXSTART], *txo = (uint64_t *)b->p[S_TXOFF];
+  uint8_t *txb = b->p[S_TXB], *txn = b->p[S_TXNIL], *tln = b->p[S_TXLNIL];
+  uint64_t *io = (uint64_t *)b->p[S_ITXOFF], *bo = (uint64_t *)b->p[S_BSOFF], *so = (uint64_t *)b->p[S_SIGOFF];
+  uint8_t *ij = b->p[S_ITX], *bj = b->p[S_BS], *sg = b->p[S_SIGTXT];
+  uint32_t last = 0, lastk = 0;
+  int have_last = 0;
+  for (uint64_t e = j->e0; e < j->e1; e++) {
+    const uint32_t c = w->creator_id[e];
+    if (!have_last || c != last) lastk = idmap_slot(b->cid, b->cid_cap, c)[1] - 1, last = c, have_last = 1;
+    cr[e] = lastk;
+    idx[e] = w->index[e];
+    ts[e] = w->timestamp[e];
+    for (int k = 0; k < 2; k++) {
+      const uint8_t kind = w->parent_kind[2 * e + k];
+      uint64_t ref = 0;
+      if (kind == BV_PARENT_HASH) {
+        memcpy(ph + 32 * a.nh, w->parent_hash + 64 * e + 32 * k, 32);
+        ref = a.nh++;
+      } else if (kind == BV_PARENT_EVENT) {
+        ref = w->parent_event[2 * e + k];
+      }
+      pk[2 * e + k] = kind;
+      pref[2 * e + k] = ref;
+    }
+    for (uint64_t t = w->tx_start[e]; t < w->tx_start[e + 1]; t++) {
+      const uint64_t len = w->tx_off[t + 1] - w->tx_off[t];
+      if (len) memcpy(txb + a.txb, w->tx_bytes + w->tx_off[t], len);
+      a.txb += len;
+      txo[a.tx + 1] = a.txb;
+      txn[a.tx++] = w->tx_nil ? w->tx_nil[t] : 0;
+    }
+    txs[e + 1] = a.tx;
+    tln[e] = w->tx_list_nil ? w->tx_list_nil[e] : 0;
+    if (w->itx_off) {
+      const uint64_t len = w->itx_off[e + 1] - w->itx_off[e];
+      if (len) memcpy(ij + a.itx, w->itx_json + w->itx_off[e], len);
+      a.itx += len;
+    }
+    io[e + 1] = a.itx;
+    if (w->bsig_off) {
+      const uint64_t len = w->bsig_off[e + 1] - w->bsig_off[e];
+      if (len) memcpy(bj + a.bs, w->bsig_json + w->bsig_off[e], len);
+      a.bs += len;
+    }
+    bo[e + 1] = a.bs;
+    const uint64_t len = w->sig_off[e + 1] - w->sig_off[e];
+    if (len) memcpy(sg + a.sig, w->sig_text + w->sig_off[e], len);
+    a.sig += len;
+    so[e + 1] = a.sig;
+  }
+}
+
+static void copy_chunk(fill_job *j) { /* C.GoBytes, per chunk */
+  const uint64_t n = j->e1 - j->e0;
+  if (j->dig) memcpy(j->dig + 32 * j->e0, j->res->msg_hash + 32 * j->e0, 32 * n);
+  if (j->st) memcpy(j->st + j->e0, j->res->status + j->e0, n);
+}
+
+/* slot s reserved at exactly `bytes` (at least 64: a non-null block) */
+static int size_slot(builder *b, int s, size_t bytes) {
+  void *np;
+  if (bv_arena_reserve(b->arena, (uint32_t)s, bytes < 64 ? 64 : bytes, 0, &np, &b->cap[s]) != BV_OK) return -1;
+  b->p[s] = (uint8_t *)np;
+  b->n[s] = bytes;
+  return 0;
+}
+
+static double g_phase[3]; /* the last shim_sync: build, library call, copy-out (ms) */
+
+void shim_last_phases(double out[3]) { memcpy(out, g_phase, sizeof g_phase); }
+
 /* VerifySync: the batch built in the arena, one bv_verify_events, results
  * copied out.  digests: 32 * n, status: n.  *ms: wall time of the whole
  * call (build + verify + copy-out). */
@@ -186,42 +358,54 @@ int shim_sync(const shim_wire *w, uint8_t *digests, uint8_t *status, double *ms)
   reset(b);
   int rc = BV_E_OOM;
   const uint64_t n = w->n_events;
-  uint64_t n_hashes = 0;
-  if (put_u64(b, S_KOFF, 0) || put_u64(b, S_TXSTART, 0) || put_u64(b, S_TXOFF, 0) || put_u64(b, S_ITXOFF, 0) ||
-      put_u64(b, S_BSOFF, 0) || put_u64(b, S_SIGOFF, 0))
-    goto out;
-  for (uint64_t e = 0; e < n; e++) {
-    const uint32_t c = w->creator_id[e];
-    const int64_t k = key_index(b, w->rep_bytes + w->rep_off[c], w->rep_off[c + 1] - w->rep_off[c]);
-    if (k < 0 || put_u32(b, S_CREATOR, (uint32_t)k) || put_i64(b, S_INDEX, w->index[e]) ||
-        put_i64(b, S_TS, w->timestamp[e]))
-      goto out;
-    for (int j = 0; j < 2; j++) {
-      const uint8_t kind = w->parent_kind[2 * e + j];
-      uint64_t ref = 0;
-      if (kind == BV_PARENT_HASH) {
-        ref = n_hashes++;
-        if (put(b, S_PHASH, w->parent_hash + 64 * e + 32 * j, 32)) goto out;
-      } else if (kind == BV_PARENT_EVENT) {
-        ref = w->parent_event[2 * e + j];
-      }
-      if (put_u8(b, S_PKIND, kind) || put_u64(b, S_PREF, ref)) goto out;
-    }
-    for (uint64_t t = w->tx_start[e]; t < w->tx_start[e + 1]; t++) {
-      if (put(b, S_TXB, w->tx_bytes + w->tx_off[t], w->tx_off[t + 1] - w->tx_off[t]) ||
-          put_u64(b, S_TXOFF, b->n[S_TXB]) || put_u8(b, S_TXNIL, w->tx_nil ? w->tx_nil[t] : 0))
-        goto out;
-    }
-    if (put_u64(b, S_TXSTART, b->n[S_TXOFF] / 8 - 1) || put_u8(b, S_TXLNIL, w->tx_list_nil ? w->tx_list_nil[e] : 0))
-      goto out;
-    if (w->itx_off && put(b, S_ITX, w->itx_json + w->itx_off[e], w->itx_off[e + 1] - w->itx_off[e])) goto out;
-    if (w->bsig_off && put(b, S_BS, w->bsig_json + w->bsig_off[e], w->bsig_off[e + 1] - w->bsig_off[e])) goto out;
-    if (put_u64(b, S_ITXOFF, b->n[S_ITX]) || put_u64(b, S_BSOFF, b->n[S_BS])) goto out;
-    if (put(b, S_SIGTXT, w->sig_text + w->sig_off[e], w->sig_off[e + 1] - w->sig_off[e]) ||
-        put_u64(b, S_SIGOFF, b->n[S_SIGTXT]))
-      goto out;
+  int nj = n >= 8192 ? (int)(n / 4096) : 1;
+  if (nj > MAX_JOBS) nj = MAX_JOBS;
+  fill_job jobs[MAX_JOBS];
+  memset(jobs, 0, sizeof jobs);
+  for (int i = 0; i < nj; i++) {
+    jobs[i].w = w, jobs[i].b = b;
+    jobs[i].e0 = n * i / nj, jobs[i].e1 = n * (i + 1) / nj;
   }
-  if (put(b, S_SIGTXT, "", 1)) goto out;  /* (a non-null text pointer even when every signature is empty) */
+  double t1 = t0, t2 = t0;
+  run_jobs(jobs, nj, size_chunk);
+  fill_at tot = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < nj; i++) { /* the creators' key indices, in event order; chunk sizes -> offsets */
+    if (jobs[i].n_ids == UINT32_MAX) goto out;
+    for (uint32_t q = 0; q < jobs[i].n_ids; q++) {
+      const uint32_t c = jobs[i].ids[q];
+      if (2 * (b->n_cid + 1) > b->cid_cap) { /* (a repertoire larger than the map: grow it) */
+        const uint32_t nc = b->cid_cap ? 2 * b->cid_cap : 256;
+        uint32_t *nm = (uint32_t *)calloc(2 * (size_t)nc, 4);
+        if (!nm) goto out;
+        for (uint32_t h = 0; h < b->cid_cap; h++)
+          if (b->cid[2 * h + 1]) memcpy(idmap_slot(nm, nc, b->cid[2 * h]), b->cid + 2 * h, 8);
+        free(b->cid);
+        b->cid = nm, b->cid_cap = nc;
+      }
+      uint32_t *s = idmap_slot(b->cid, b->cid_cap, c);
+      if (s[1]) continue;
+      const int64_t k = key_index(b, w->rep_bytes + w->rep_off[c], w->rep_off[c + 1] - w->rep_off[c]);
+      if (k < 0) goto out;
+      s[0] = c, s[1] = (uint32_t)k + 1;
+      b->n_cid++;
+    }
+    const fill_at z = jobs[i].at;
+    jobs[i].at = tot;
+    tot.tx += z.tx, tot.txb += z.txb, tot.itx += z.itx, tot.bs += z.bs, tot.sig += z.sig, tot.nh += z.nh;
+  }
+  if (!b->n_keys && put_u64(b, S_KOFF, 0)) goto out;
+  if (size_slot(b, S_CREATOR, 4 * n) || size_slot(b, S_INDEX, 8 * n) || size_slot(b, S_TS, 8 * n) ||
+      size_slot(b, S_PKIND, 2 * n) || size_slot(b, S_PREF, 16 * n) || size_slot(b, S_PHASH, 32 * tot.nh) ||
+      size_slot(b, S_TXSTART, 8 * (n + 1)) || size_slot(b, S_TXOFF, 8 * (tot.tx + 1)) ||
+      size_slot(b, S_TXB, tot.txb) || size_slot(b, S_TXLNIL, n) || size_slot(b, S_TXNIL, tot.tx) ||
+      size_slot(b, S_ITXOFF, 8 * (n + 1)) || size_slot(b, S_ITX, tot.itx) || size_slot(b, S_BSOFF, 8 * (n + 1)) ||
+      size_slot(b, S_BS, tot.bs) || size_slot(b, S_SIGOFF, 8 * (n + 1)) || size_slot(b, S_SIGTXT, tot.sig + 1))
+    goto out;
+  ((uint64_t *)b->p[S_TXSTART])[0] = ((uint64_t *)b->p[S_TXOFF])[0] = 0;
+  ((uint64_t *)b->p[S_ITXOFF])[0] = ((uint64_t *)b->p[S_BSOFF])[0] = ((uint64_t *)b->p[S_SIGOFF])[0] = 0;
+  b->p[S_SIGTXT][tot.sig] = 0; /* (a non-null text pointer even when every signature is empty) */
+  run_jobs(jobs, nj, fill_chunk);
+  t1 = now_ms();
   {
     const size_t words = (n + 63) / 64, out_bytes = 32 * n + n + 8 * words + 8;
     void *op;
@@ -238,7 +422,7 @@ int shim_sync(const shim_wire *w, uint8_t *digests, uint8_t *status, double *ms)
     in.timestamp = (const int64_t *)b->p[S_TS];
     in.parent_kind = b->p[S_PKIND];
     in.parent_ref = (const uint64_t *)b->p[S_PREF];
-    in.n_parent_hashes = n_hashes;
+    in.n_parent_hashes = tot.nh;
     in.parent_hashes = b->p[S_PHASH];
     in.tx_start = (const uint64_t *)b->p[S_TXSTART];
     in.tx_off = (const uint64_t *)b->p[S_TXOFF];
@@ -256,14 +440,18 @@ int shim_sync(const shim_wire *w, uint8_t *digests, uint8_t *status, double *ms)
     res.status = b->p[S_OUT] + 32 * n;
     res.accept_bits = (uint64_t *)(b->p[S_OUT] + ((32 * n + n + 7) & ~(size_t)7));
     rc = bv_verify_events(g_ctx, &in, &res);
-    if (rc == BV_OK) { /* C.GoBytes */
-      if (digests) memcpy(digests, res.msg_hash, 32 * n);
-      if (status) memcpy(status, res.status, n);
+    t2 = now_ms();
+    if (rc == BV_OK) {
+      for (int i = 0; i < nj; i++) jobs[i].dig = digests, jobs[i].st = status, jobs[i].res = &res;
+      run_jobs(jobs, nj, copy_chunk);
     }
   }
 out:
+  for (int i = 0; i < nj; i++) free(jobs[i].ids), free(jobs[i].set);
   pool_put(b);
-  if (ms) *ms = now_ms() - t0;
+  const double t3 = now_ms();
+  g_phase[0] = t1 - t0, g_phase[1] = t2 - t1, g_phase[2] = t3 - t2;
+  if (ms) *ms = t3 - t0;
   return rc;
 }
 

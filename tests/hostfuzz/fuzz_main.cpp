@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/babbleverify.h"
+#include "../../babble_amd/csrc/hostscalar.h"
 
 static std::vector<uint8_t> unhex(const std::string &h) {
   std::vector<uint8_t> out(h.size() / 2);
@@ -123,6 +124,23 @@ int main() {
           std::cout << t;
         }
         if (!W) std::cout << "-";
+      }
+      std::cout << "\n";
+    } else if (op == "R") {  // R <digest> <r> <s> <pre> <key|->: bv_host_item_record's 64 words
+      std::string dh, rh, sh, kh;
+      int pre;
+      in >> dh >> rh >> sh >> pre >> kh;
+      if (kh == "-") kh.clear();
+      const std::vector<uint8_t> d = unhex(dh), r = unhex(rh), s = unhex(sh), key = unhex(kh);
+      std::unique_ptr<uint8_t[]> kb(new uint8_t[key.size() ? key.size() : 1]);  // exact size
+      if (!key.empty()) memcpy(kb.get(), key.data(), key.size());
+      uint32_t rec[hrec::kWords];
+      bv_host_item_record(rec, d.data(), r.data(), s.data(), (uint8_t)pre, kb.get(), key.size(), 0x1122334455667788ull);
+      std::cout << "R";
+      for (uint32_t w = 0; w < hrec::kWords; w++) {
+        char t[12];
+        snprintf(t, sizeof t, " %08x", rec[w]);
+        std::cout << t;
       }
       std::cout << "\n";
     } else {

@@ -327,6 +327,54 @@ def test_small_batch_kernel_equals_oracle(monkeypatch):
         verifier.close()
 
 
+def test_small_batch_host_records_equal_device_scalars(monkeypatch):
+    """Latency batches (<= BV_HOST_SCALARS items, default 4) carry host item
+    records (hostscalar.h: s^-1, u1, u2 and u2's GLV split computed on the
+    host with field.h's own functions, one 256-byte read per workgroup): the
+    824 golden items (every decision-table class) in batches of 1-4 items,
+    single events and 4-item adversarial batches, cold and with part of the
+    valid keys registered (cached and uncached keys), equal to the oracle
+    and, item for item, to the device-inversion path (BV_HOST_SCALARS=0)."""
+    from babble_amd import shard
+    from babble_amd.verifier import Verifier
+
+    golden, expected, _ = golden_items_batch()
+    rng = np.random.default_rng(77)
+    cuts, lo = [], 0
+    while lo < golden.n_items:
+        hi = min(golden.n_items, lo + int(rng.integers(1, 5)))
+        cuts.append((lo, hi))
+        lo = hi
+    batches = [shard.slice_batch(golden, a, c) for a, c in cuts]
+    n_golden = len(batches)
+    batches += [synth.events(1, n_creators=1, seed=960 + i) for i in range(4)]
+    batches += [synth.adversarial(4, seed=970 + i, n_creators=2, scale_per_million=MIX) for i in range(8)]
+    good = []
+    for b in batches[n_golden:] + batches[:40]:
+        for k in range(b.n_keys):
+            if gs.Unmarshal(b.key(k)) is not None and b.key(k) not in good:
+                good.append(b.key(k))
+    for flags in (0, native.F_KEY_CACHE):
+        rec = Verifier(device=0, flags=flags)
+        monkeypatch.setenv("BV_HOST_SCALARS", "0")  # read at bv_create
+        dev = Verifier(device=0, flags=flags)
+        monkeypatch.delenv("BV_HOST_SCALARS")
+        try:
+            if flags:
+                rec.register_keys(good[:8])
+                dev.register_keys(good[:8])
+            got = []
+            for b in batches:
+                r = check_against_oracle(rec, b)
+                d = dev.verify(b)
+                assert np.array_equal(d.status, r.status) and np.array_equal(d.msg_hash, r.msg_hash)
+                got.append(r.status)
+            assert np.array_equal(np.concatenate(got[:n_golden]), expected)
+        finally:
+            rec.close()
+            dev.close()
+
+
 def test_small_batch_kernel_warm_up_to_1024(monkeypatch):
     """A 1000-event batch whose keys all have key-cache tables takes k_small
     (no per-item NAF chain: BV_SMALL_WARM_MAX, 1024, above the cold limit

@@ -157,3 +157,49 @@ def test_merge_shard_bits_fuzz_sanitized(run):
         got = [] if f[2] == "-" else [int(x, 16) for x in f[2].split(",")]
         assert got == [int(x) for x in want]
     assert run(["M 1 2 0,70,80 0,0"])[0] == "M -1"  # a shard wider than words_per_shard
+
+
+LAMBDA = 0x5363AD4CC05C30E0A5261C028812645A122E22EA20816678DF02967C1B23BD72  # phi's eigenvalue mod N
+
+
+def test_host_item_record_sanitized(run):
+    """hostscalar.cpp bv_host_item_record (the latency batch's item record):
+    u1 = e s^-1 mod N and u2 = r s^-1 = k1 + k2 lambda (mod N) with
+    |k1|, |k2| < 2^129, the key / r / s / pre / table fields in place, and
+    all-zero scalars whenever s is unusable (pre != 0, s = 0, s >= N) — on
+    random and edge values, under ASan + UBSan."""
+    rng = random.Random(11)
+    N = gs.N
+    cases = []
+    for i in range(400):
+        e = rng.getrandbits(256)
+        r = rng.getrandbits(256) if i % 7 else rng.choice([0, 1, N - 1, N, 2 ** 256 - 1])
+        s = rng.randrange(1, N) if i % 5 else rng.choice([0, 1, 2, N - 1, N, N + 1, 2 ** 256 - 1])
+        pre = 0 if i % 11 else rng.choice([1, 4, 5, 0x40])
+        klen = 65 if i % 13 else rng.choice([0, 33, 64, 66, 100])
+        key = bytes([4] + [rng.getrandbits(8) for _ in range(klen - 1)]) if klen else b""
+        cases.append((e, r, s, pre, key))
+    out = run([f"R {e:064x} {r:064x} {s:064x} {pre} {key.hex() or '-'}" for e, r, s, pre, key in cases])
+
+    def limbs(w, a, n):
+        return sum(int(w[a + i], 16) << (32 * i) for i in range(n))
+
+    for (e, r, s, pre, key), line in zip(cases, out):
+        w = line.split()[1:]
+        assert len(w) == 64
+        raw = b"".join(int(x, 16).to_bytes(4, "little") for x in w)
+        kl = min(len(key), 66)
+        assert int(w[18], 16) == kl and int(w[19], 16) == pre
+        assert raw[:65] == (key if kl == 65 else bytes(65))
+        assert raw[80:112] == r.to_bytes(32, "big") and raw[112:144] == s.to_bytes(32, "big")
+        assert limbs(w, 54, 2) == 0x1122334455667788
+        u1, k1, k2, signs = limbs(w, 36, 8), limbs(w, 44, 4), limbs(w, 48, 4), int(w[52], 16)
+        if pre or s == 0 or s >= N:
+            assert u1 == k1 == k2 == signs == 0
+            continue
+        si = pow(s, -1, N)
+        assert u1 == e * si % N
+        k1s = -k1 if signs & 1 else k1
+        k2s = -k2 if signs & 2 else k2
+        assert (k1s + k2s * LAMBDA - r * si) % N == 0
+        assert k1 < 2 ** 129 and k2 < 2 ** 129 and signs < 4
