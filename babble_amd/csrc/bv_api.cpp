@@ -32,6 +32,10 @@
 #include <new>
 #include <thread>
 
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 namespace {
 
 constexpr uint64_t kGTableBytes = BV_GTABLE_U32 * 4;                       // 21.5 GB (geometry.h)
@@ -221,6 +225,20 @@ extern "C" void bv_arena_destroy(bv_arena *a) {
   if (!a) return;
   for (void *p : a->p) bv_host_free(p);
   delete a;
+}
+
+// (diagnostics) the NUMA node of the page holding p (get_mempolicy
+// MPOL_F_NODE | MPOL_F_ADDR), or of the calling thread's CPU when p is null;
+// -1 when unknown
+static int numa_node_of(const void *p) {
+  int node = -1;
+  if (!p) {
+    unsigned cpu = 0, n = 0;
+    return syscall(SYS_getcpu, &cpu, &n, nullptr) == 0 ? (int)n : -1;
+  }
+  const long MPOL_F_NODE_ = 1, MPOL_F_ADDR_ = 2;
+  if (syscall(SYS_get_mempolicy, &node, nullptr, 0, p, MPOL_F_NODE_ | MPOL_F_ADDR_) != 0) return -1;
+  return node;
 }
 
 extern "C" int bv_arena_reserve(bv_arena *a, uint32_t slot, size_t bytes, size_t keep, void **out, size_t *cap) {
@@ -848,9 +866,13 @@ int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
   return bv_run_verify(ctx, b, d_msg_hash, d_status, d_bits, st, hashed, kc);
 }
 
+// (an event this call did not record gives -1; the failed query's error is
+// cleared, so the next launch check does not report it)
 static float elapsed(hipEvent_t a, hipEvent_t b) {
   float t;
-  return hipEventElapsedTime(&t, a, b) == hipSuccess ? t : -1.f;
+  if (hipEventElapsedTime(&t, a, b) == hipSuccess) return t;
+  (void)hipGetLastError();
+  return -1.f;
 }
 
 void bv_read_timing(bv_ctx *ctx) {
@@ -1185,6 +1207,11 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
     HIPCHK(hipEventRecord(e, cs), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, e, 0), BV_E_LAUNCH, "join chunk");
     if (m0 == 0 && ctx->host_stamps) st_first = stamp_ms();
+    if (ctx->host_stamps && call->h_call < 0) {  // (diagnostics) has the device reached the call yet?
+      const hipError_t q = hipEventQuery(ctx->S().ev[E_CALL]);
+      if (q == hipSuccess) call->h_call = stamp_ms();
+      else if (q != hipErrorNotReady) (void)hipGetLastError();
+    }
     if (m0 == 0) HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_SMALL], 0), BV_E_LAUNCH, "join offsets");
     HIPCHK(bvk::sha256(st, m1 - m0, d.msg_bytes, d.msg_off + m0, pipe.o.dig + 8 * m0, kHostHashLen), BV_E_LAUNCH,
            "k_sha256");
@@ -1231,8 +1258,9 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   if (ctx->host_stamps)
     fprintf(stderr,
             "bv_host_launch ms: validated %.3f items_staged %.3f first_msg_chunk %.3f staged %.3f (msgs %.1f MB, "
-            "%d copy threads)\n",
-            st_validated, st_items, st_first, (double)call->ms_prep, msg_len / 1e6, (int)ctx->pool->th.size());
+            "%d copy threads; staging on NUMA node %d..%d, caller on node %d)\n",
+            st_validated, st_items, st_first, (double)call->ms_prep, msg_len / 1e6, (int)ctx->pool->th.size(),
+            numa_node_of(pin), numa_node_of(pin + total - 1), numa_node_of(nullptr));
   HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_STAGED], 0), BV_E_LAUNCH, "join staging");
   HIPCHK(hipEventRecord(ctx->S().ev[E_SHA], st), BV_E_LAUNCH, "event");
   if (n_msgs == 0) HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");
@@ -1261,6 +1289,21 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
 }
 
 int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call *call, bool bits_out) {
+  double h_in = -1, h_staged = -1, h_done = -1;
+  if (ctx->host_stamps) {  // (diagnostics) host ms at which the staging end and the call's end are seen
+    auto ms = [call]() {
+      return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - call->t0).count();
+    };
+    h_in = ms();
+    if (call->h_call < 0 && hipEventQuery(ctx->S().ev[E_CALL]) == hipSuccess) call->h_call = h_in;
+    while (h_done < 0) {
+      if (h_staged < 0 && hipEventQuery(ctx->S().ev[E_STAGED]) == hipSuccess) h_staged = ms();
+      const hipError_t q = hipEventQuery(ctx->ev_done);
+      if (q == hipSuccess) h_done = ms();
+      else if (q != hipErrorNotReady) break;
+    }
+    (void)hipGetLastError();
+  }
   HIPCHK(hipEventSynchronize(ctx->ev_done), BV_E_LAUNCH, "verify sync");
   const auto t_out = std::chrono::steady_clock::now();
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
@@ -1272,6 +1315,17 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
   ctx->timing.ms_h2d = elapsed(ctx->S().ev[E_CALL], ctx->S().ev[E_STAGED]);
   ctx->timing.ms_d2h = elapsed(ctx->S().ev[E_END], ctx->S().ev[E_OUT]);
   const auto t_end = std::chrono::steady_clock::now();
+  if (ctx->host_stamps) {  // the device timeline from E_CALL (the first copy-stream command of the call)
+    hipEvent_t *ev = ctx->S().ev;
+    fprintf(stderr,
+            "bv_host_finish ms: synced %.3f (host, from the call; seen: call %.3f finish_in %.3f staged %.3f "
+            "done %.3f) | device from E_CALL: hash0 %.3f staged %.3f hashed %.3f verify_start %.3f verify_end %.3f "
+            "out %.3f\n",
+            std::chrono::duration<double, std::milli>(t_out - call->t0).count(), call->h_call, h_in, h_staged, h_done,
+            elapsed(ev[E_CALL], ev[E_HASH0]),
+            elapsed(ev[E_CALL], ev[E_STAGED]), elapsed(ev[E_CALL], ev[E_HASHED]), elapsed(ev[E_CALL], ev[E_START]),
+            elapsed(ev[E_CALL], ev[E_END]), elapsed(ev[E_CALL], ev[E_OUT]));
+  }
   ctx->timing.ms_host = std::chrono::duration<float, std::milli>(t_end - call->t0).count();
   ctx->timing.ms_host_prep = call->ms_prep;
   ctx->timing.ms_host_out = std::chrono::duration<float, std::milli>(t_end - t_out).count();

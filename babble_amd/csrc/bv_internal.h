@@ -335,6 +335,7 @@ struct bv_host_call {
   size_t o_st = 0, o_bits = 0;
   bool direct_in = false;                          // message bytes DMA'd from the caller's pinned buffer
   bool direct_hash = false, direct_status = false;  // results DMA'd into the caller's pinned buffers
+  double h_call = -1;                               // (BV_HOST_STAMPS) host ms when E_CALL was first seen done
 };
 bool bv_is_pinned(const void *p, size_t n);  // [p, p+n) inside one bv_host_alloc block
 void bv_read_small_span(bv_ctx *ctx);        // a small batch's device span into ctx->timing (bv_api.cpp)

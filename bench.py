@@ -413,6 +413,11 @@ def run(args, world: int, rank: int, local: int, worker) -> None:
                          ts0=synth.TS0 + rank * args.events * 8)
     clean_r = batch.r_be.copy()
     v = Verifier(device=local)
+    # BENCH_HOST_ENTRY_PROBE=1: the pageable host entry's rate at three
+    # points of this process, printed to stderr
+    probe = os.environ.get("BENCH_HOST_ENTRY_PROBE") == "1" and rank == 0 and world == 1
+    if probe:
+        host_entry_rate(v, batch, "before the headline steps")
     # Consecutive steps alternate two result buffers and the library's two
     # work slots, each slot on its own library lane (stream), so one batch's
     # key tables and hashing overlap the previous batch's k_verify_q tail — a
@@ -551,8 +556,12 @@ def run(args, world: int, rank: int, local: int, worker) -> None:
                              f"in-flight buffer, a different set per buffer, rejected)",
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
         }
+    if probe:
+        host_entry_rate(v, batch, "after the headline steps")
     if rank == 0 and world == 1 and not args.no_extras:
         line["warm"] = warm_leg(args, devs, world, dist, local, step_with)
+        if probe:
+            host_entry_rate(v, batch, "after the warm leg")
         line["host_entry"] = host_entry_leg(args, v, batch)
         line["host_entry_pinned"] = host_entry_pinned_leg(args, v, batch)
         line["latency_ms"] = latency_leg(args)
@@ -798,6 +807,14 @@ def host_diag(batch) -> dict:
         out["cgroup_cpu_max"] = open("/sys/fs/cgroup/cpu.max").read().strip()
     except OSError:
         out["cgroup_cpu_max"] = None
+    try:  # the GPU's NUMA node (its PCI device's), and the main thread's now
+        import torch
+
+        pr = torch.cuda.get_device_properties(int(os.environ.get("LOCAL_RANK", "0")))
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        out["gpu_numa_node"] = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+    except (OSError, AttributeError, ValueError):
+        out["gpu_numa_node"] = None
     arena = PinnedArena()
     try:
         src = batch.msg_bytes
@@ -822,6 +839,18 @@ def host_diag(batch) -> dict:
     finally:
         arena.close()
     return out
+
+
+def host_entry_rate(v, batch, tag, reps=5):
+    """(diagnostic) bv_verify_batch from pageable buffers: verifies/s of
+    `reps` calls after one untimed call, to stderr."""
+    v.verify(batch)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        v.verify(batch)
+    rate = batch.n_items * reps / (time.perf_counter() - t0)
+    print(f"host_entry_probe {tag}: {rate / 1e6:.1f} M verifies/s", file=sys.stderr, flush=True)
+    return rate
 
 
 def host_entry_leg(args, v, batch):

@@ -369,6 +369,7 @@ int shim_sync(const shim_wire *w, uint8_t *digests, uint8_t *status, double *ms)
   double t1 = t0, t2 = t0;
   run_jobs(jobs, nj, size_chunk);
   fill_at tot = {0, 0, 0, 0, 0, 0};
+  if (put_u64(b, S_KOFF, 0)) goto out;
   for (int i = 0; i < nj; i++) { /* the creators' key indices, in event order; chunk sizes -> offsets */
     if (jobs[i].n_ids == UINT32_MAX) goto out;
     for (uint32_t q = 0; q < jobs[i].n_ids; q++) {
@@ -393,7 +394,6 @@ int shim_sync(const shim_wire *w, uint8_t *digests, uint8_t *status, double *ms)
     jobs[i].at = tot;
     tot.tx += z.tx, tot.txb += z.txb, tot.itx += z.itx, tot.bs += z.bs, tot.sig += z.sig, tot.nh += z.nh;
   }
-  if (!b->n_keys && put_u64(b, S_KOFF, 0)) goto out;
   if (size_slot(b, S_CREATOR, 4 * n) || size_slot(b, S_INDEX, 8 * n) || size_slot(b, S_TS, 8 * n) ||
       size_slot(b, S_PKIND, 2 * n) || size_slot(b, S_PREF, 16 * n) || size_slot(b, S_PHASH, 32 * tot.nh) ||
       size_slot(b, S_TXSTART, 8 * (n + 1)) || size_slot(b, S_TXOFF, 8 * (tot.tx + 1)) ||

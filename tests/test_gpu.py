@@ -332,7 +332,7 @@ def test_small_batch_host_records_equal_device_scalars(monkeypatch):
     records (hostscalar.h: s^-1, u1, u2 and u2's GLV split computed on the
     host with field.h's own functions, one 256-byte read per workgroup): the
     824 golden items (every decision-table class) in batches of 1-4 items,
-    single events and 4-item adversarial batches, cold and with part of the
+    single events and a 40-item adversarial batch in 4-item slices, cold and with part of the
     valid keys registered (cached and uncached keys), equal to the oracle
     and, item for item, to the device-inversion path (BV_HOST_SCALARS=0)."""
     from babble_amd import shard
@@ -348,7 +348,8 @@ def test_small_batch_host_records_equal_device_scalars(monkeypatch):
     batches = [shard.slice_batch(golden, a, c) for a, c in cuts]
     n_golden = len(batches)
     batches += [synth.events(1, n_creators=1, seed=960 + i) for i in range(4)]
-    batches += [synth.adversarial(4, seed=970 + i, n_creators=2, scale_per_million=MIX) for i in range(8)]
+    adv = synth.adversarial(40, seed=970, n_creators=3, scale_per_million=MIX)
+    batches += [shard.slice_batch(adv, lo, lo + 4) for lo in range(0, 40, 4)]
     good = []
     for b in batches[n_golden:] + batches[:40]:
         for k in range(b.n_keys):
