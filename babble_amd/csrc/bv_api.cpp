@@ -998,7 +998,8 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   if (rc != BV_OK) return rc;
   // BV_HOST_STAMPS (diagnostics): the host phases of this call on stderr
   auto stamp_ms = [t0]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
-  double st_validated = ctx->host_stamps ? stamp_ms() : 0, st_items = 0, st_first = 0;
+  double st_validated = ctx->host_stamps ? stamp_ms() : 0, st_items = 0, st_first = 0, st_copy = 0;
+  int n_chunks = 0;
   hipStream_t st = ctx->stream, cs = bv_copy_stream(ctx);
   if (!cs) return bv_fail(ctx, BV_E_NODEVICE, "copy stream");
   ctx->last = st;
@@ -1199,7 +1200,9 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
              BV_E_LAUNCH, "h2d msgs (pinned caller buffer)");
     } else {
       const size_t len = end - base + (m1 == n_msgs ? 64 : 0);
+      const double c0 = ctx->host_stamps ? stamp_ms() : 0;
       ctx->pool->copy(pin + segs[8].off + base, b->msg_bytes + base, end - base);
+      if (ctx->host_stamps) st_copy += stamp_ms() - c0;
       HIPCHK(hipMemcpyAsync(dev + segs[8].off + base, pin + segs[8].off + base, len, hipMemcpyHostToDevice, cs),
              BV_E_LAUNCH, "h2d msgs");
     }
@@ -1207,6 +1210,7 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
     HIPCHK(hipEventRecord(e, cs), BV_E_LAUNCH, "event");
     HIPCHK(hipStreamWaitEvent(st, e, 0), BV_E_LAUNCH, "join chunk");
     if (m0 == 0 && ctx->host_stamps) st_first = stamp_ms();
+    n_chunks++;
     if (ctx->host_stamps && call->h_call < 0) {  // (diagnostics) has the device reached the call yet?
       const hipError_t q = hipEventQuery(ctx->S().ev[E_CALL]);
       if (q == hipSuccess) call->h_call = stamp_ms();
@@ -1257,10 +1261,10 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   call->ms_prep = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (ctx->host_stamps)
     fprintf(stderr,
-            "bv_host_launch ms: validated %.3f items_staged %.3f first_msg_chunk %.3f staged %.3f (msgs %.1f MB, "
-            "%d copy threads; staging on NUMA node %d..%d, caller on node %d)\n",
-            st_validated, st_items, st_first, (double)call->ms_prep, msg_len / 1e6, (int)ctx->pool->th.size(),
-            numa_node_of(pin), numa_node_of(pin + total - 1), numa_node_of(nullptr));
+            "bv_host_launch ms: validated %.3f items_staged %.3f first_msg_chunk %.3f staged %.3f (message copies "
+            "%.3f in %d chunks; msgs %.1f MB, %d copy threads; staging on NUMA node %d..%d, caller on node %d)\n",
+            st_validated, st_items, st_first, (double)call->ms_prep, st_copy, n_chunks, msg_len / 1e6,
+            (int)ctx->pool->th.size(), numa_node_of(pin), numa_node_of(pin + total - 1), numa_node_of(nullptr));
   HIPCHK(hipStreamWaitEvent(st, ctx->S().ev[E_STAGED], 0), BV_E_LAUNCH, "join staging");
   HIPCHK(hipEventRecord(ctx->S().ev[E_SHA], st), BV_E_LAUNCH, "event");
   if (n_msgs == 0) HIPCHK(hipEventRecord(ctx->S().ev[E_HASHED], st), BV_E_LAUNCH, "event");

@@ -815,6 +815,11 @@ def host_diag(batch) -> dict:
         out["gpu_numa_node"] = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
     except (OSError, AttributeError, ValueError):
         out["gpu_numa_node"] = None
+    out["msg_bytes_mapping"] = smaps_of(batch.msg_bytes.ctypes.data + batch.msg_bytes.nbytes // 2)
+    try:
+        out["thp"] = open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip()
+    except OSError:
+        out["thp"] = None
     arena = PinnedArena()
     try:
         src = batch.msg_bytes
@@ -841,6 +846,53 @@ def host_diag(batch) -> dict:
     return out
 
 
+def smaps_of(addr: int) -> dict:
+    """The /proc/self/smaps entry of the mapping holding `addr`: its size and
+    how much of it is backed by transparent huge pages (kB)."""
+    cur = None
+    try:
+        for line in open("/proc/self/smaps"):
+            f = line.split()
+            if "-" in f[0] and len(f) >= 5:
+                lo, hi = (int(x, 16) for x in f[0].split("-"))
+                cur = {} if lo <= addr < hi else None
+            elif cur is not None and f[0] in ("Size:", "Rss:", "AnonHugePages:"):
+                cur[f[0][:-1]] = int(f[1])
+                if len(cur) == 3:
+                    return cur
+    except (OSError, ValueError):
+        pass
+    return cur or {}
+
+
+def numa_counters() -> dict:
+    """Automatic NUMA balancing's activity: the sysctl, the host's hinting
+    faults and page migrations (/proc/vmstat) and this process's
+    (/proc/self/sched)."""
+    out = {}
+    try:
+        out["numa_balancing"] = int(open("/proc/sys/kernel/numa_balancing").read())
+    except (OSError, ValueError):
+        pass
+    try:
+        for line in open("/proc/vmstat"):
+            k, v = line.split()
+            if k in ("numa_hint_faults", "numa_pages_migrated", "pgmigrate_success", "numa_pte_updates"):
+                out["host_" + k] = int(v)
+    except OSError:
+        pass
+    try:
+        for line in open("/proc/self/sched"):
+            if ":" in line:
+                k, v = line.split(":", 1)
+                k = k.strip()
+                if k in ("numa_pages_migrated", "total_numa_faults"):
+                    out["self_" + k] = int(float(v))
+    except (OSError, ValueError):
+        pass
+    return out
+
+
 def host_entry_rate(v, batch, tag, reps=5):
     """(diagnostic) bv_verify_batch from pageable buffers: verifies/s of
     `reps` calls after one untimed call, to stderr."""
@@ -859,23 +911,32 @@ def host_entry_leg(args, v, batch):
 
     msgs = batch.msg_bytes.nbytes
     staged = msgs + batch.msg_off.nbytes + batch.r_be.nbytes + batch.s_be.nbytes + batch.item_msg.nbytes * 2
+    # two untimed calls: the first allocates the context's staging buffers,
+    # and the call after it waits 20-30 ms for the device to start its first
+    # copy (BV_HOST_STAMPS device timeline)
     v.verify(batch)
-    ts = []
-    ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    v.verify(batch)
+    ts, per = [], []
+    ru0, nb0 = resource.getrusage(resource.RUSAGE_SELF), numa_counters()
     t0 = time.perf_counter()
-    reps = max(2, min(5, args.steps))
+    reps = max(2, min(10, args.steps))
     for _ in range(reps):
+        t1 = time.perf_counter()
         v.verify(batch)
+        per.append(round((time.perf_counter() - t1) * 1e3, 2))
         ts.append(v.timing())
     elapsed = time.perf_counter() - t0
-    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    ru1, nb1 = resource.getrusage(resource.RUSAGE_SELF), numa_counters()
     h2d = mean(ts, "ms_h2d")
     diag = host_diag(batch)
     diag.update({"minor_faults_per_call": (ru1.ru_minflt - ru0.ru_minflt) / reps,
                  "invol_ctx_switches_per_call": (ru1.ru_nivcsw - ru0.ru_nivcsw) / reps,
                  "host_cpu_s_per_call": ((ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)) / reps,
-                 "staging_gb_s": staged / (mean(ts, "ms_host_prep") * 1e-3) / 1e9})
+                 "staging_gb_s": staged / (mean(ts, "ms_host_prep") * 1e-3) / 1e9,
+                 "numa_per_call": {k: (nb1[k] - nb0.get(k, 0)) / reps for k in nb1 if k != "numa_balancing"},
+                 "numa_balancing": nb1.get("numa_balancing")})
     return {"value": args.events * reps / elapsed, "unit": "verifies/s", "ms_per_call": elapsed / reps * 1e3,
+            "per_call_ms": per,
             "ms_h2d": h2d, "ms_d2h_tail": mean(ts, "ms_d2h"), "host_breakdown_ms": host_breakdown(ts),
             "bytes_staged": staged,
             "pcie_gb_s": staged / (h2d * 1e-3) / 1e9 if h2d > 0 else None, "host_diag": diag,
@@ -900,17 +961,21 @@ def host_entry_pinned_leg(args, v, batch):
         res = VerifyResult(arena.array((batch.n_msgs, 32), np.uint8), arena.array(batch.n_items, np.uint8),
                            arena.array((batch.n_items + 63) // 64, np.uint64))
         v.verify_into(pb, res)
-        ts = []
-        reps = max(2, min(5, args.steps))
+        v.verify_into(pb, res)  # (two untimed calls, as host_entry)
+        ts, per = [], []
+        reps = max(2, min(10, args.steps))
         t0 = time.perf_counter()
         for _ in range(reps):
+            t1 = time.perf_counter()
             v.verify_into(pb, res)
+            per.append(round((time.perf_counter() - t1) * 1e3, 2))
             ts.append(v.timing())
         elapsed = time.perf_counter() - t0
         assert np.array_equal(res.accept_bits, expected_words(0, args.events, 0))
         h2d = mean(ts, "ms_h2d")
         staged = sum(a.nbytes for a in (pb.msg_bytes, pb.msg_off, pb.r_be, pb.s_be, pb.item_msg, pb.item_key))
         return {"value": args.events * reps / elapsed, "unit": "verifies/s", "ms_per_call": elapsed / reps * 1e3,
+                "per_call_ms": per,
                 "ms_h2d": h2d, "host_breakdown_ms": host_breakdown(ts), "bytes_staged": staged,
                 "pcie_gb_s": staged / (h2d * 1e-3) / 1e9 if h2d > 0 else None,
                 "note": "inputs and results in bv_host_alloc (pinned) memory: DMA'd in place, no staging copy"}

@@ -62,12 +62,15 @@ def gpu_numa():
     return out
 
 
-def measure(v, batch, tag, reps=5):
+def measure(v, batch, tag, reps=5, pause=0.0):
     v.verify(batch)
+    time.sleep(pause)
     c0, t0, ru0 = cpu_stat(), time.perf_counter(), os.times()
-    tms = []
+    tms, per = [], []
     for _ in range(reps):
+        t1 = time.perf_counter()
         v.verify(batch)
+        per.append(round((time.perf_counter() - t1) * 1e3, 2))
         tms.append(v.timing())
     el = (time.perf_counter() - t0) / reps
     c1, ru1 = cpu_stat(), os.times()
@@ -75,7 +78,7 @@ def measure(v, batch, tag, reps=5):
     nodes = {}
     for c in cpus:
         nodes[numa_of_cpu(c)] = nodes.get(numa_of_cpu(c), 0) + 1
-    out = {"state": tag, "verifies_per_s": batch.n_items / el, "ms_per_call": el * 1e3,
+    out = {"state": tag, "verifies_per_s": batch.n_items / el, "ms_per_call": el * 1e3, "per_call_ms": per,
            "ms_h2d": float(np.mean([t["ms_h2d"] for t in tms])),
            "ms_host": float(np.mean([t["ms_host"] for t in tms])),
            "cpu_s_per_call": ((ru1.user + ru1.system) - (ru0.user + ru0.system)) / reps,
@@ -91,6 +94,13 @@ print(json.dumps({"gpu_numa": gpu_numa(), "main_cpu_numa": numa_of_cpu(thread_cp
 batch = synth.events(1_000_000, n_creators=64, seed=2)
 v = Verifier(device=0)
 measure(v, batch, "A fresh")
+v.close()
+v = Verifier(device=0)
+measure(v, batch, "A2 new context, 0.5 s pause after the first call", pause=0.5)
+v.close()
+v = Verifier(device=0)
+v.verify(batch)
+measure(v, batch, "A3 new context, two untimed calls")
 others = [Verifier(device=0) for _ in range(3)]
 for o in others:
     o.verify(synth.events(1000, n_creators=4, seed=7))
