@@ -493,6 +493,7 @@ static int create_impl(bv_ctx *ctx) {
   if (const char *s = getenv("BV_EV_VERIFY_STREAM")) ctx->ev_split_verify = atoi(s) != 0;
   if (const char *s = getenv("BV_SMALL")) ctx->small_path = atoi(s) != 0;
   if (const char *s = getenv("BV_QFIRST")) ctx->qfirst = atoi(s) != 0;
+  if (const char *s = getenv("BV_GLV_SSTREAM")) ctx->glv_in_sstream = atoi(s) != 0;
   if (const char *s = getenv("BV_EV_D2H")) ctx->ev_d2h = atoi(s);
   if (const char *s = getenv("BV_EV_TAIL")) ctx->ev_tail = atoi(s);
   if (const char *s = getenv("BV_SMALL_STAMPS")) ctx->small_stamps = atoi(s) != 0;
@@ -615,7 +616,7 @@ extern "C" int bv_get_timing(const bv_ctx *ctx, bv_timing *out) {
 // `keys_ready` (the keys in HBM).  The host entry points stage the keys
 // first, then s and pre, so the key tables build while the rest of the batch
 // still crosses PCIe.
-int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_t s_ready, bool kc) {
+int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_t s_ready, bool kc, bool split_ok) {
   const uint64_t n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
   if (n_items > 0 && (!b->item_msg || !b->item_key || !b->r_be || !b->s_be))
@@ -678,6 +679,13 @@ int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_
   const uint32_t M = (uint32_t)std::min<uint64_t>(kPrepM, std::max<uint64_t>(1, (n_items + 65535) / 65536));
   HIPCHK(bvk::sinv(ctx->sstream, n_items, M, (const uint32_t *)b->s_be, b->pre, ctx->S().scratch.as<uint32_t>()),
          BV_E_LAUNCH, "k_sinv");
+  // u2 = r s^-1 and its GLV split for k_verify_q, off k_verify_g's path
+  // (per-batch tables; the fused key-cache kernel forms its own)
+  ctx->S().glv_split = split_ok && ctx->glv_in_sstream && table_mode && !(kc && kFusedKc);
+  if (ctx->S().glv_split)
+    HIPCHK(bvk::glv_split(ctx->sstream, n_items, (const uint32_t *)b->r_be, ctx->S().scratch.as<uint32_t>(),
+                          ctx->S().u12.as<uint32_t>()),
+           BV_E_LAUNCH, "k_glv_split");
   HIPCHK(hipEventRecord(ev[E_SINV], ctx->sstream), BV_E_LAUNCH, "event");
   HIPCHK(hipStreamWaitEvent(ctx->kstream, ev[E_KDEC], 0), BV_E_LAUNCH, "fork");
   if (!kc) {
@@ -729,7 +737,7 @@ int bv_launch_items(bv_ctx *ctx, const bv_batch *b, const bv_out &o, hipStream_t
   if (part == 1) {
     if (ctx->table_mode && !fused)
       HIPCHK(bvk::verify_g(st, n, lo, hi, b->item_key, r32, s32, b->pre, kst, b->item_msg, o.dig, w, u12,
-                           ctx->g_table, ctx->S().rg.as<uint32_t>()),
+                           ctx->g_table, ctx->S().rg.as<uint32_t>(), ctx->S().glv_split),
              BV_E_LAUNCH, "k_verify_g");
     return BV_OK;
   }
@@ -861,7 +869,7 @@ int bv_run_verify(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *
 int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc) {
   HIPCHK(hipEventRecord(ctx->S().ev[E_READY], st), BV_E_LAUNCH, "event");
-  int rc = bv_run_keys(ctx, b, ctx->S().ev[E_READY], ctx->S().ev[E_READY], kc);
+  int rc = bv_run_keys(ctx, b, ctx->S().ev[E_READY], ctx->S().ev[E_READY], kc, true);
   if (rc != BV_OK) return rc;
   return bv_run_verify(ctx, b, d_msg_hash, d_status, d_bits, st, hashed, kc);
 }

@@ -42,6 +42,7 @@ hipError_t build_kc(hipStream_t, uint32_t, const uint32_t *, const uint8_t *, ui
                     const uint64_t *);
 size_t kc_pscr_bytes();
 hipError_t sinv(hipStream_t, uint64_t, uint32_t, const uint32_t *, const uint8_t *, uint32_t *);
+hipError_t glv_split(hipStream_t, uint64_t n, const uint32_t *r_be, const uint32_t *w, uint32_t *u12);
 // verify kernels over items [lo, hi) of an n-item batch (lo a multiple of 64)
 hipError_t verify_gq(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
                      const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
@@ -58,7 +59,7 @@ hipError_t verify_gf(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *
                      const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
 hipError_t verify_g(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
                     const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *, uint32_t *,
-                    const uint32_t *, uint32_t *);
+                    const uint32_t *, uint32_t *, bool split);
 hipError_t verify_q(hipStream_t, int, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
                     const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
                     const uint64_t *, const uint32_t *, uint8_t *, uint64_t *);
@@ -266,6 +267,7 @@ struct bv_ctx {
     // key cache, partial batch: a few valid keys have no table; their items
     // are left BV_DEFERRED by the KC kernels and finished by bv_run_deferred
     bool kc_partial = false;
+    bool glv_split = false;  // this call's u12 was filled by k_glv_split (k_verify_g forms only u1)
     DevBuf defer;  // the deferred items' indices, then their count
     // caller result ranges [lo, hi) of this slot's device calls that the
     // other slots' calls have not yet been ordered after (deduplicated)
@@ -319,6 +321,7 @@ struct bv_ctx {
   uint64_t k12_min_items = 8192;  // per-batch K12 (not K8) tables from this many items per key
   bool small_stamps = false;      // BV_SMALL_STAMPS=1: print k_small's phase clocks to stderr
   bool host_stamps = false;       // BV_HOST_STAMPS=1: print the host entry's phases to stderr
+  bool glv_in_sstream = true;     // BV_GLV_SSTREAM (A/B): device entry's GLV split in k_glv_split
   uint32_t host_scalar_max = 4;   // BV_HOST_SCALARS: k_small batches up to this many items get host
                                   // item records (hostscalar.h; 0: the device inverts every item)
   uint32_t small_span = 0;        // 1 + the slot of a small batch whose device span is not read yet
@@ -357,7 +360,10 @@ int bv_slot_begin(bv_ctx *ctx, hipStream_t st, const bv_batch *b, const bv_resul
 int bv_validate_host_batch(bv_ctx *ctx, const bv_batch *b);
 int bv_run_device(bv_ctx *ctx, const bv_batch *b, uint8_t *d_msg_hash, uint8_t *d_status, uint64_t *d_bits,
                   hipStream_t st, bool hashed, bool kc);
-int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_t s_ready, bool kc);
+// split_ok: r is in HBM by s_ready too, so u2's GLV split may run on the
+// s^-1 stream (k_glv_split) instead of in k_verify_g (the device entry)
+int bv_run_keys(bv_ctx *ctx, const bv_batch *b, hipEvent_t keys_ready, hipEvent_t s_ready, bool kc,
+                bool split_ok = false);
 struct bv_out {  // device outputs of one verify
   uint32_t *dig = nullptr;
   uint8_t *status = nullptr;

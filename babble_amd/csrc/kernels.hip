@@ -497,7 +497,13 @@ __device__ __forceinline__ void write_status(uint64_t i, uint64_t hi, uint8_t st
 #ifndef BV_LWAVES  // latency variants (zipped point ops, small batches)
 #define BV_LWAVES 1
 #endif
-template <bool LAT>
+__global__ void __launch_bounds__(256) k_glv_split(uint64_t n_items, const uint32_t *__restrict__ r_be,
+                                                   const uint32_t *__restrict__ w_in, uint32_t *__restrict__ u12) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_items) glv_split_item(i, r_be, w_in, u12);
+}
+
+template <bool LAT, bool SPLIT>
 __global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_GWAVES) k_verify_g(uint64_t n_items, uint64_t lo, uint64_t hi,
                                                   const uint32_t *__restrict__ item_key,
                                                   const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
@@ -508,7 +514,8 @@ __global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_GWAVES) k_verify_g(u
                                                   const uint32_t *__restrict__ g_table, uint32_t *__restrict__ rg) {
   const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < hi)
-    verify_item_g<LAT>(i, n_items, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, u12, g_table, rg);
+    verify_item_g<LAT, SPLIT>(i, n_items, item_key, r_be, s_be, pre, kstatus, item_msg, digest_words, w_in, u12,
+                              g_table, rg);
 }
 
 // Throughput variants: BV_QWAVES waves per SIMD (4: 128 VGPRs, the XYZZ
@@ -1447,17 +1454,23 @@ hipError_t sinv(hipStream_t st, uint64_t n, uint32_t M, const uint32_t *s_be, co
 }
 
 // Items [lo, hi) of an n-item batch (R_G is stored SoA with stride n).
+hipError_t glv_split(hipStream_t st, uint64_t n, const uint32_t *r_be, const uint32_t *w, uint32_t *u12) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_glv_split, grid1(n, 256), dim3(256), 0, st, n, r_be, w, u12);
+  return hipGetLastError();
+}
+
+// split: u12 holds the GLV split already (k_glv_split on the s^-1 stream)
 hipError_t verify_g(hipStream_t st, uint64_t n, uint64_t lo, uint64_t hi, const uint32_t *item_key,
                     const uint32_t *r_be, const uint32_t *s_be, const uint8_t *pre, const uint8_t *kst,
                     const uint32_t *item_msg, const uint32_t *dig, const uint32_t *w, uint32_t *u12,
-                    const uint32_t *g_table, uint32_t *rg) {
+                    const uint32_t *g_table, uint32_t *rg, bool split) {
   if (hi <= lo) return hipSuccess;
-  if (lat_variant(n))
-    hipLaunchKernelGGL(k_verify_g<true>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be, pre,
-                       kst, item_msg, dig, w, u12, g_table, rg);
-  else
-    hipLaunchKernelGGL(k_verify_g<false>, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be, pre,
-                       kst, item_msg, dig, w, u12, g_table, rg);
+  const bool lat = lat_variant(n);
+  auto k = lat ? (split ? k_verify_g<true, true> : k_verify_g<true, false>)
+               : (split ? k_verify_g<false, true> : k_verify_g<false, false>);
+  hipLaunchKernelGGL(k, grid1(hi - lo, 256), dim3(256), 0, st, n, lo, hi, item_key, r_be, s_be, pre, kst, item_msg,
+                     dig, w, u12, g_table, rg);
   return hipGetLastError();
 }
 

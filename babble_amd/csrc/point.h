@@ -489,6 +489,56 @@ DEV void pt_add_ge(gexz &r, bool &inf, const fe &x2, const fe &y2) {
   else gexz_add_ge(r, inf, x2, y2);
 }
 
+// r += (x2, y2) for r AFFINE (ZZ = ZZZ = 1, not the identity: the first
+// table entry of a sum), mmadd-2008-s: 4M + 2S — the products by ZZ1 and
+// ZZZ1 of the general step drop out (U2 = x2, S2 = y2, ZZ3 = PP, ZZZ3 =
+// PPP).  Same exceptional cases as gexz_add_ge.
+template <bool LAT>
+DEV void gexz_add_ge_aff(gexz &r, bool &inf, const fe &x2, const fe &y2) {
+  fe P, R, PP, RR, PPP, Q, t, u, v;
+  fe_sub(P, x2, r.X);
+  fe_sub(R, y2, r.Y);
+  if (fe_is_zero(P)) {
+    if (fe_is_zero(R)) {
+      gexz d;
+      gexz_double(d, r);
+      r = d;
+    } else {
+      inf = true;
+    }
+    return;
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (LAT) {
+    fe_sqr_sqr_zip_asm(PP, P, RR, R);
+    fe_mul_mul_zip_asm(PPP, P, PP, Q, r.X, PP);
+  } else
+#endif
+  {
+    fe_sqr(PP, P);
+    fe_sqr(RR, R);
+    fe_mul(PPP, P, PP);
+    fe_mul(Q, r.X, PP);
+  }
+  fe_sub(t, RR, PPP);
+  fe_sub(t, t, Q);
+  fe_sub(t, t, Q);  // X3
+  fe_sub(u, Q, t);
+  r.X = t;
+  r.ZZ = PP;
+  r.ZZZ = PPP;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (LAT) {
+    fe_mul_mul_zip_asm(t, R, u, v, r.Y, PPP);
+  } else
+#endif
+  {
+    fe_mul(t, R, u);
+    fe_mul(v, r.Y, PPP);
+  }
+  fe_sub(r.Y, t, v);
+}
+
 // One table lookup step of the verify kernels: r += (x2, y2) in lanes with
 // `take` (a nonzero digit).  Measured alternatives (profiles/r03_ab_step.log,
 // same-box PMC A/B): a straight-line common path under wave-uniform

@@ -502,7 +502,10 @@ DEV bool final_check(const gexz &R, bool inf, const fe &r) {
 // SIGNED digits in (-2^(W-1), 2^(W-1)] by carry recoding: T[j][|d|], y
 // negated for d < 0 (geometry.h).  u < N < 2^256 and W NWIN >= 257, so no
 // carry is left after the top window.
-template <int W, int NWIN, bool LAT = false, class PT = gej>
+// FROM_INF (XYZZ only): R enters as the identity, so after window 0 it is
+// that window's affine entry and window 1 adds with the 4M + 2S affine step
+// (gexz_add_ge_aff) — 4 multiplies fewer per item.
+template <int W, int NWIN, bool LAT = false, class PT = gej, bool FROM_INF = false>
 DEV void g_table_add(PT &R, bool &inf, const uint32_t *tab, uint32_t u[8]) {
   constexpr uint32_t ENT = 1u << (W - 1);
   static_assert(W * NWIN >= 257 && W < 32, "signed G windows must absorb the last carry");
@@ -522,6 +525,12 @@ DEV void g_table_add(PT &R, bool &inf, const uint32_t *tab, uint32_t u[8]) {
     fe_load4(x, e);
     fe_load4(y, e + 8);
     fe_cneg_canon(y, dneg);
+    if constexpr (FROM_INF) {
+      if (j == 1 && !inf) {  // R = window 0's entry (affine)
+        if (d != 0) gexz_add_ge_aff<LAT>(R, inf, x, y);
+        continue;
+      }
+    }
     pt_add_ge_step<LAT>(R, inf, x, y, d != 0);
   }
 }
@@ -562,26 +571,62 @@ DEV void rg_load(const uint32_t *rg, uint64_t n, uint64_t i, gexz &R, bool &inf)
 
 // Phase 1 (overlaps the key-table build): R_G = u1 G for items that reach
 // the math.
-template <bool LAT = false>
+// k_glv_split, item i (per-batch key tables, device entry): u2 = r s^-1 and
+// its GLV split into u12 as soon as s^-1 is known — on the s^-1 stream,
+// beside SHA-256 and the key tables — so k_verify_g forms only u1 = e s^-1
+// (the digest's product).  Items whose s is unusable get a split of a
+// dummy w that k_verify_q never reads (it classifies first).
+DEV void glv_split_item(uint64_t i, const uint32_t *r_be, const uint32_t *w_in, uint32_t *u12) {
+  sc w, r, b;
+  const uint4 *q = (const uint4 *)(w_in + 8 * i);
+  const uint4 x = q[0], y = q[1];
+  w.v[0] = x.x; w.v[1] = x.y; w.v[2] = x.z; w.v[3] = x.w;
+  w.v[4] = y.x; w.v[5] = y.y; w.v[6] = y.z; w.v[7] = y.w;
+  sc_load_be_words(r, r_be + 8 * i);
+  sc_mont(b, r, w);  // r * s^-1 mod N
+  uint32_t k1[4], k2[4], signs;
+  glv_split(k1, k2, signs, b);
+  uint4 *o = (uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i);
+  o[0] = make_uint4(k1[0], k1[1], k1[2], k1[3]);
+  o[1] = make_uint4(k2[0], k2[1], k2[2], k2[3]);
+  o[2] = make_uint4(signs, 0u, 0u, 0u);
+}
+
+// SPLIT: u12 already holds the GLV split (k_glv_split); else it is formed
+// here with u1.
+template <bool LAT = false, bool SPLIT = false>
 DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const uint32_t *r_be, const uint32_t *s_be,
                        const uint8_t *pre, const uint8_t *kstatus, const uint32_t *item_msg,
                        const uint32_t *digest_words, const uint32_t *w_in, uint32_t *u12, const uint32_t *g_table,
                        uint32_t *rg) {
   fe r;
   if (classify_item(i, item_key, r_be, s_be, pre, kstatus, r) != 0xFF) return;
-  uint32_t u[8], k1[4], k2[4], signs;
-  item_scalars(i, r_be, item_msg, digest_words, w_in, u, k1, k2, signs);
-  uint4 *q = (uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i);
-  q[0] = make_uint4(k1[0], k1[1], k1[2], k1[3]);
-  q[1] = make_uint4(k2[0], k2[1], k2[2], k2[3]);
-  q[2] = make_uint4(signs, 0u, 0u, 0u);
+  uint32_t u[8];
+  if (SPLIT) {
+    sc w, e, a;
+    const uint4 *q = (const uint4 *)(w_in + 8 * i);
+    const uint4 x = q[0], y = q[1];
+    w.v[0] = x.x; w.v[1] = x.y; w.v[2] = x.z; w.v[3] = x.w;
+    w.v[4] = y.x; w.v[5] = y.y; w.v[6] = y.z; w.v[7] = y.w;
+    sc_load_be_words(e, digest_words + 8 * (uint64_t)item_msg[i]);
+    sc_mont(a, e, w);  // e * s^-1 mod N
+#pragma unroll
+    for (int k = 0; k < 8; k++) u[k] = a.v[k];
+  } else {
+    uint32_t k1[4], k2[4], signs;
+    item_scalars(i, r_be, item_msg, digest_words, w_in, u, k1, k2, signs);
+    uint4 *q = (uint4 *)(u12 + (uint64_t)BV_U_STRIDE * i);
+    q[0] = make_uint4(k1[0], k1[1], k1[2], k1[3]);
+    q[1] = make_uint4(k2[0], k2[1], k2[2], k2[3]);
+    q[2] = make_uint4(signs, 0u, 0u, 0u);
+  }
   gexz R;
   bool inf = true;
   fe_set(R.X, 0);
   fe_set(R.Y, 0);
   fe_set(R.ZZ, 0);
   fe_set(R.ZZZ, 0);
-  g_table_add<BV_GW, BV_GNWIN, LAT>(R, inf, g_table, u);
+  g_table_add<BV_GW, BV_GNWIN, LAT, gexz, true>(R, inf, g_table, u);
   rg_store(rg, n, i, R, inf);
 }
 
@@ -765,7 +810,7 @@ DEV uint8_t verify_item_gq_kc(uint64_t i, const uint32_t *item_key, const uint32
   fe_set(R.Y, 0);
   fe_set(R.ZZ, 0);
   fe_set(R.ZZZ, 0);
-  g_table_add<BV_GW, BV_GNWIN, LAT>(R, inf, g_table, u);
+  g_table_add<BV_GW, BV_GNWIN, LAT, gexz, true>(R, inf, g_table, u);
 #pragma unroll 1
   for (int h = 0; h < 2; h++) {
     uint32_t kk[4];

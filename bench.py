@@ -66,25 +66,25 @@ sys.path.insert(0, ROOT)
 # accumulators are XYZZ (point.h gexz): a mixed addition is madd-2008-s,
 # 8M + 2S = 10 modmuls:
 #   u1 G:  10 signed windows of the 26-bit G table, the first lands on the
-#          identity (a copy), 9 mixed additions x 10             =  90
-#   u2 Q:  22 windows of the K12 GLV key tables, 22 x 10         = 220
-#   u1, u2 = e w, r w (2 Montgomery products), GLV split (2 wide products
-#          + 2 products) and the check X == r ZZ (1M)            ~   7
-#   = 317 modmuls = 25,360 IMUL32 per item.
-# `achieved` = items x 25,360 / (k_verify_g + k_verify_q time); `peak` = the
+#          identity (a copy), the second adds to that affine entry with
+#          mmadd-2008-s (4M + 2S = 6), 8 mixed additions x 10       =  86
+#   u2 Q:  22 windows of the K12 GLV key tables, 22 x 10            = 220
+#   u1 = e w (a Montgomery product) and the check X == r ZZ (1M)    ~   3
+#   = 309 modmuls = 24,720 IMUL32 per item in k_verify_g + k_verify_q.
+# u2 = r w and its GLV split (~2.8 modmuls) run in k_glv_split on the s^-1
+# stream, beside SHA-256 and the key tables, outside these two spans.
+# `achieved` = items x 24,720 / (k_verify_g + k_verify_q time); `peak` = the
 # v_mad_u64_u32 rate measured on MI355X (tools/ubench_int.hip,
 # profiles/r01_ubench_int.txt).  SURVEY §8d's canonical Strauss schedule
 # (4,050 modmuls per verify) is reported only as `speedup_vs_canonical`.
-MODMUL_PER_ITEM_EXEC = 317
+MODMUL_PER_ITEM_EXEC = 309
 IMUL32_PER_MODMUL = 80
 # The same executed work per kernel (k_verify_g counted on
-# its own).  k_verify_g: 9 G additions x 10 = 90, plus u1 = e w and u2 = r w
-# (two 8-limb Montgomery products mod N, 128 IMUL32 each = 1.6 modmuls) and
-# the GLV split of u2 (two 256x128-bit products + two 128x128, 96 IMUL32 =
-# 1.2) -> 94.4.  k_verify_q: 22 key-table additions x 10 + the final X == r ZZ
-# check (1) -> 221.  (Rounded into the 317 above: 94.4 + 221 + ~1.6 for the
-# digit recoding and sign handling that the modmul count does not see.)
-MODMUL_G, MODMUL_Q = 94.4, 221
+# its own).  k_verify_g: 86 (the G additions) + 1.6 (u1 = e w, an 8-limb
+# Montgomery product mod N, 128 IMUL32) -> 87.6.  k_verify_q: 22 key-table
+# additions x 10 + the final X == r ZZ check (1) -> 221.  (Rounded into the
+# 309 above with the digit recoding and sign handling.)
+MODMUL_G, MODMUL_Q = 87.6, 221
 CANONICAL_MODMUL_PER_VERIFY = 4050
 PEAK_IMUL32_PER_S = 31.76e12
 # Measured gfx950 issue costs (profiles/r01_ubench_ops.txt): a wave64
@@ -481,7 +481,8 @@ def run(args, world: int, rank: int, local: int, worker) -> None:
             "kernel": "k_verify_g<false> + k_verify_q<12, 11, false>",
             "achieved": achieved / 1e12,
             "peak": PEAK_IMUL32_PER_S / 1e12,
-            "unit": "T IMUL32/s (executed schedule: 317 modmuls x 80 IMUL32 per item; bench.py ROOFLINE)",
+            "unit": f"T IMUL32/s (executed schedule: {MODMUL_PER_ITEM_EXEC} modmuls x 80 IMUL32 per item; "
+                    "bench.py ROOFLINE)",
             "frac": achieved / PEAK_IMUL32_PER_S,
             "traffic": None,
             "speedup_vs_canonical": CANONICAL_MODMUL_PER_VERIFY / MODMUL_PER_ITEM_EXEC,
