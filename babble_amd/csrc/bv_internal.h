@@ -293,6 +293,7 @@ struct bv_ctx {
   std::unordered_map<std::string, uint32_t> kc_seen;  // valid keys without a table: batches seen (bounded)
   std::unordered_set<std::string> kc_bad;  // 65-byte 0x04 keys off the curve (bounded)
   uint32_t kc_admit = 2;                   // batches before an unregistered valid key gets a table
+  bool kc_partial_on = false;              // BV_KC_PARTIAL=1: partial mode (bv_kc_prepare; off: measured slower)
   int kc_fail_alloc = 0, kc_fail_build = 0;  // fault injection (BV_KC_FAIL), tests only
   uint64_t kc_allocs = 0, kc_build_calls = 0;
   uint64_t kc_clock = 0, kc_bytes = 0, kc_budget = 0;

@@ -60,6 +60,7 @@ void bv_kc_init(bv_ctx *ctx) {
   if (const char *s = getenv("BV_KEY_CACHE_GB")) gb = atof(s);
   ctx->kc_budget = (uint64_t)(std::max(gb, 0.0) * 1e9);
   if (const char *s = getenv("BV_KC_ADMIT")) ctx->kc_admit = (uint32_t)std::max(1, atoi(s));
+  if (const char *s = getenv("BV_KC_PARTIAL")) ctx->kc_partial_on = atoi(s) != 0;
   if (const char *s = getenv("BV_KC_FAIL")) {
     int n = 0;
     if (sscanf(s, "alloc:%d", &n) == 1) ctx->kc_fail_alloc = n;
@@ -183,6 +184,12 @@ int bv_kc_prepare(bv_ctx *ctx, uint32_t n_keys, const uint8_t *hkb, const uint64
   // chain of 128 doublings per lane), so they are bounded by ITEM count too
   // (ADVICE r5): when the table-less keys carry more than 1 item in
   // kKcPartialRatio, the per-batch tables take the batch.
+  // Partial mode is OFF by default (BV_KC_PARTIAL=1 turns it on): measured
+  // with 1 fresh key of 20 (profiles/r06_ab_partial.log), its deferred tail
+  // costs +2.4 ms (20k-400k events) to +3 ms (1M) over the full key cache,
+  // while the per-batch tables cost +0.2-0.3 ms, so a fresh key now sends
+  // the batch to the per-batch tables.
+  if (blocked && !force_build && !ctx->kc_partial_on) return bail();
   if (blocked && !force_build) {
     const uint64_t tabled = hits + admit.size();
     if (tabled == 0 || (uint64_t)n_blocked * kKcPartialRatio > tabled + n_blocked) return bail();

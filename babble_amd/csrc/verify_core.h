@@ -4,6 +4,7 @@
 // the CPU (with sanitizers) before a GPU run.  Nothing here is a CPU path of
 // the product: libbabbleverify.so only ever runs these on gfx950.
 #pragma once
+#include <type_traits>
 #include <stdint.h>
 
 #include "../../include/babbleverify.h"
@@ -637,8 +638,11 @@ DEV void verify_item_g(uint64_t i, uint64_t n, const uint32_t *item_key, const u
 // and W NWIN >= 129 bits, so no carry is left after the top window.
 // `phi`: the table holds T (the k1 half) and this half needs phi(T) =
 // (beta x, y): one multiply per lookup instead of a stored phi half (KC).
+// `from_inf` (uniform; XYZZ only): R enters as the identity, so window 1
+// adds to window 0's affine entry with the 4M + 2S step (as g_table_add).
 template <int W, int NWIN, bool SIGNED, bool LAT = false, class PT = gexz>
-DEV void key_table_add(PT &R, bool &inf, const uint32_t *tab, uint32_t k[4], bool neg, bool phi = false) {
+DEV void key_table_add(PT &R, bool &inf, const uint32_t *tab, uint32_t k[4], bool neg, bool phi = false,
+                       bool from_inf = false) {
   constexpr uint32_t ENT = SIGNED ? (1u << (W - 1)) : (1u << W);
   static_assert(!SIGNED || W * NWIN >= 129, "signed windows must absorb the last carry");
   if (neg) fe_neg(R.Y, R.Y);
@@ -667,6 +671,12 @@ DEV void key_table_add(PT &R, bool &inf, const uint32_t *tab, uint32_t k[4], boo
       fe_mul(x, x, beta);
     }
     fe_cneg_canon(y, dneg);
+    if constexpr (std::is_same<PT, gexz>::value) {
+      if (from_inf && j == 1 && !inf) {  // R = window 0's entry (affine)
+        if (d != 0) gexz_add_ge_aff<LAT>(R, inf, x, y);
+        continue;
+      }
+    }
     pt_add_ge_step<LAT>(R, inf, x, y, d != 0);
   }
   if (neg) fe_neg(R.Y, R.Y);
@@ -754,7 +764,8 @@ DEV void verify_item_qfirst(uint64_t i, uint64_t n, const uint32_t *item_key, co
     uint32_t kk[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) kk[c] = h ? k2[c] : k1[c];
-    key_table_add<W, NWIN, SIGNED, LAT>(R, inf, tab + (h && !KC ? half : 0), kk, (signs >> h) & 1u, KC && h);
+    key_table_add<W, NWIN, SIGNED, LAT>(R, inf, tab + (h && !KC ? half : 0), kk, (signs >> h) & 1u, KC && h,
+                                        h == 0);
   }
   rg_store(rq, n, i, R, inf);
 }

@@ -489,6 +489,7 @@ def test_key_cache_partial_batch(monkeypatch, device_api):
     from babble_amd.verifier import Verifier
 
     monkeypatch.setenv("BV_KC_ADMIT", "1000")  # no fresh key gets a table during the test (read at bv_create)
+    monkeypatch.setenv("BV_KC_PARTIAL", "1")  # partial mode is off by default (profiles/r06_ab_partial.log)
     b = synth.events(30_000, n_creators=20, seed=62)
     rng = np.random.default_rng(62)
     for i in rng.choice(b.n_items, 300, replace=False):
@@ -530,6 +531,16 @@ def test_key_cache_partial_batch(monkeypatch, device_api):
         assert v.timing()["key_path"] != 22
     finally:
         v.close()
+    # the default (partial mode off): one fresh key of 20 sends the batch to
+    # the per-batch tables, oracle-exact
+    monkeypatch.delenv("BV_KC_PARTIAL")
+    v = Verifier(device=0, flags=native.F_KEY_CACHE)
+    try:
+        v.register_keys(keys[1:])
+        oracle_check(run(v, b), b)
+        assert v.timing()["key_path"] != 22
+    finally:
+        v.close()
 
 
 def test_key_cache_partial_batch_events_entry(monkeypatch):
@@ -541,6 +552,7 @@ def test_key_cache_partial_batch_events_entry(monkeypatch):
     from oracle import coracle
 
     monkeypatch.setenv("BV_KC_ADMIT", "1000")
+    monkeypatch.setenv("BV_KC_PARTIAL", "1")
     packed, wire = synth.event_fields(30_000, n_creators=20, seed=64, parents="hash")
     rng = np.random.default_rng(64)
     bad = rng.choice(packed.n_items, 200, replace=False)
