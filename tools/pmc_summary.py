@@ -132,9 +132,10 @@ def kverify(summary: dict, items: int, source: str) -> dict:
     cnt = lambda c: sum(summary[k]["counters"].get(c, 0.0) for k in ks)  # noqa: E731
     # algorithmic bytes per item: 32 table entries of 64 B (10 G windows +
     # 22 K12 windows) plus the SoA streams the two kernels read and write
-    # (r, w, digest, pre, item_key, item_msg, key status ~110 B; R_G 132 B +
-    # u12 48 B written by k_verify_g and read back by k_verify_q; status 1 B)
-    table, stream = 32 * 64, 110 + 2 * (132 + 48) + 1
+    # (r, w, digest, pre, item_key, item_msg, key status ~110 B; R_G 132 B
+    # written by k_verify_g and read back by k_verify_q; u12 48 B read by
+    # k_verify_q — k_glv_split writes it since round 6; status 1 B)
+    table, stream = 32 * 64, 110 + 2 * 132 + 48 + 1
     return {"source": source, "kernels": ks, "items_per_launch": items,
             "hbm_bytes_per_launch": tot("hbm_bytes"), "hbm_read_bytes_uncorrected": cnt("FETCH_SIZE") * 1024,
             "fetch_factor": "1.00 (64-B gathers, profiles/r05_gather_calib.json)",
