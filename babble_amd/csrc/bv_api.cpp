@@ -577,26 +577,11 @@ extern "C" void *bv_last_stream(const bv_ctx *ctx) { return ctx ? (void *)ctx->l
 
 static float elapsed(hipEvent_t a, hipEvent_t b);
 
-// A small batch returns once its statuses have landed, possibly before the
-// kernel's completion signal: its device span is read when asked for.
-void bv_read_small_span(bv_ctx *ctx) {
-  if (!ctx->small_span) return;
-  const auto &sl = ctx->slot[ctx->small_span - 1];
-  if (hipEventSynchronize(sl.ev[E_END]) == hipSuccess)
-    ctx->timing.ms_total = ctx->timing.ms_verify = elapsed(sl.ev[E_START], sl.ev[E_END]);
-  ctx->small_span = 0;
-}
-
 extern "C" int bv_get_timing(const bv_ctx *ctx, bv_timing *out) {
   if (!ctx || !out) return BV_E_ARGS;
-  // under the ctx's lock: a call on another thread writes small_span and
-  // the timing; the span is the ctx's own call bookkeeping
+  // under the ctx's lock: a call on another thread writes the timing
   bv_ctx *c = const_cast<bv_ctx *>(ctx);
   std::lock_guard<std::mutex> lk(c->mu);
-  if (c->small_span) {
-    (void)hipSetDevice(c->device);
-    bv_read_small_span(c);
-  }
   *out = c->timing;
   return BV_OK;
 }
@@ -908,7 +893,6 @@ extern "C" int bv_verify_batch_device(bv_ctx *ctx, const bv_batch *dbatch, bv_re
   hipStream_t st = stream ? (hipStream_t)stream : ctx->lane[(ctx->cur + 1) % bv_ctx::kSlots];
   ctx->last = st;
   ctx->timing = bv_timing{};
-  ctx->small_span = 0;
   int rc = verify_device_impl(ctx, dbatch, dresult, st);
   if (rc != BV_OK) return bv_drain(ctx, st, rc);
   if (!async) {
@@ -1012,7 +996,6 @@ int bv_host_launch(bv_ctx *ctx, const bv_batch *b, bv_host_call *call, const bv_
   if (!cs) return bv_fail(ctx, BV_E_NODEVICE, "copy stream");
   ctx->last = st;
   ctx->timing = bv_timing{};
-  ctx->small_span = 0;
   const uint64_t n_msgs = b->n_msgs, n_items = b->n_items;
   const uint32_t n_keys = b->n_keys;
   const uint64_t msg_len = n_msgs ? b->msg_off[n_msgs] : 0;
@@ -1391,7 +1374,6 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   hipStream_t st = ctx->stream;
   ctx->last = st;
   ctx->timing = bv_timing{};
-  ctx->small_span = 0;
   size_t total = 0;
   auto at = [&](size_t bytes) {
     const size_t o = total;
@@ -1406,7 +1388,7 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
                o_pre = at(n_items), o_tab = at(n_keys * 8ull), o_st = at(n_items);
   // a latency batch: one host record per item (hostscalar.h) instead
   const bool recs = n_items <= ctx->host_scalar_max;
-  const size_t o_rec = at(recs ? n_items * hrec::kWords * 4 : 0);
+  const size_t o_rec = at(recs ? n_items * hrec::kWords * 4 : 0), o_clk = at((n_items + 1) * 8);
   if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // the previous call may still read the buffer
   const auto t_waited = std::chrono::steady_clock::now();
   ctx->small_io.flags = hipHostMallocMapped | hipHostMallocCoherent;
@@ -1439,6 +1421,7 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   // kernel's completion signal
   volatile uint8_t *stv = pin + o_st;
   memset(pin + o_st, kSmallPending, n_items);
+  memset(pin + o_clk, 0, (n_items + 1) * 8);
   const bool kc = (ctx->flags & BV_F_KEY_CACHE) && n_keys;
   uint32_t hits = 0;
   if (kc) hits = bv_kc_lookup(ctx, n_keys, b->key_bytes, b->key_off, (uint64_t *)(pin + o_tab));
@@ -1452,7 +1435,6 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
     }
   }
   const auto t_staged = std::chrono::steady_clock::now();
-  hipEvent_t *ev = ctx->S().ev;
   uint64_t *stamps = nullptr;
   if (ctx->small_stamps) {
     HIPCHK(ctx->d_stamps.ensure(16 * 8), BV_E_OOM, "alloc stamps");
@@ -1462,8 +1444,8 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   HIPCHK(bvk::verify_small(st, (uint32_t)n_items, dev + o_dig, dev + o_key, (const uint64_t *)(dev + o_koff),
                            (const uint32_t *)(dev + o_im), (const uint32_t *)(dev + o_ik), dev + o_r, dev + o_s,
                            b->pre ? dev + o_pre : nullptr, kc ? (const uint64_t *)(dev + o_tab) : nullptr,
-                           ctx->g_table, dev + o_st, stamps, ev[E_START], ev[E_END],
-                           recs ? (const uint32_t *)(dev + o_rec) : nullptr),
+                           ctx->g_table, dev + o_st, stamps, recs ? (const uint32_t *)(dev + o_rec) : nullptr,
+                           (uint64_t *)(dev + o_clk)),
          BV_E_LAUNCH, "k_small");
   int rc = bv_mark_done(ctx, st);
   if (rc != BV_OK) return rc;
@@ -1497,17 +1479,18 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
       if (stv[i] == BV_ACCEPT) res->accept_bits[i / 64] |= 1ull << (i % 64);
   }
   bv_timing &t = ctx->timing;
-  // (the device span is read from the events once the kernel has ended:
-  // here when it already has, else when bv_get_timing asks; the next call
-  // on this ctx starts a new timing and drops an unread span)
-  ctx->small_span = ctx->cur + 1;  // read lazily (bv_get_timing / bv_read_small_span)
-  if (hipEventQuery(ctx->ev_done) == hipSuccess) bv_read_small_span(ctx);
+  {  // the kernel's span from its own clock writes (100 MHz; each end lands before its status)
+    const volatile uint64_t *clk = (const volatile uint64_t *)(pin + o_clk);
+    uint64_t end = 0;
+    for (uint64_t i = 0; i < n_items; i++) end = std::max<uint64_t>(end, (uint64_t)clk[1 + i]);
+    const uint64_t start = clk[0];
+    t.ms_total = t.ms_verify = start && end >= start ? (float)((end - start) * 1e-5) : 0.f;
+  }
   t.key_path = kc && hits ? BV_KCW : 0;
   t.kc_hits = hits;
   t.kc_keys = (uint32_t)ctx->kc_index.size();
   t.ms_host = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (stamps) {  // diagnostics: workgroup 0's phase clocks, relative to its start
-    bv_read_small_span(ctx);
     uint64_t h[16];
     HIPCHK(hipMemcpy(h, stamps, sizeof h, hipMemcpyDeviceToHost), BV_E_LAUNCH, "d2h stamps");
     auto us = [&](std::chrono::steady_clock::time_point a) {

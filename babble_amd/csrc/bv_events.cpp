@@ -265,7 +265,6 @@ static int verify_events_impl(bv_ctx *ctx, const bv_event_batch *eb, bv_result *
   int rc = validate(ctx, eb);
   if (rc != BV_OK) return rc;
   ctx->timing = bv_timing{};
-  ctx->small_span = 0;
   const uint64_t n = eb->n_events;
   hipStream_t st = ctx->stream;
   ctx->last = st;

@@ -66,8 +66,8 @@ hipError_t verify_q(hipStream_t, int, uint64_t, uint64_t, uint64_t, const uint32
 hipError_t verify_small(hipStream_t, uint32_t n_items, const uint8_t *dig, const uint8_t *key_bytes,
                         const uint64_t *key_off, const uint32_t *item_msg, const uint32_t *item_key,
                         const uint8_t *r_be, const uint8_t *s_be, const uint8_t *pre, const uint64_t *kc_tabs,
-                        const uint32_t *g_table, uint8_t *status, uint64_t *stamps, hipEvent_t ev_start,
-                        hipEvent_t ev_end, const uint32_t *rec);
+                        const uint32_t *g_table, uint8_t *status, uint64_t *stamps, const uint32_t *rec,
+                        uint64_t *clk);
 hipError_t verify_generic(hipStream_t, uint64_t, uint64_t, uint64_t, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint8_t *, const uint8_t *, const uint32_t *, const uint32_t *,
                           const uint32_t *, const uint32_t *, const uint32_t *, uint8_t *, uint64_t *);
@@ -325,7 +325,6 @@ struct bv_ctx {
   bool glv_in_sstream = true;     // BV_GLV_SSTREAM (A/B): device entry's GLV split in k_glv_split
   uint32_t host_scalar_max = 4;   // BV_HOST_SCALARS: k_small batches up to this many items get host
                                   // item records (hostscalar.h; 0: the device inverts every item)
-  uint32_t small_span = 0;        // 1 + the slot of a small batch whose device span is not read yet
   uint64_t small_max = 256;       // k_small for batches of at most this many items and messages (BV_SMALL_MAX)
   uint64_t small_warm_max = 1024;  // k_small for batches whose keys are all cached (BV_SMALL_WARM_MAX)
   uint32_t lat_table_keys = 256;  // latency rule: K8 tables for batches of <= 4096 items from up to this many keys (BV_LAT_TABLE_KEYS)
@@ -342,7 +341,6 @@ struct bv_host_call {
   double h_call = -1;                               // (BV_HOST_STAMPS) host ms when E_CALL was first seen done
 };
 bool bv_is_pinned(const void *p, size_t n);  // [p, p+n) inside one bv_host_alloc block
-void bv_read_small_span(bv_ctx *ctx);        // a small batch's device span into ctx->timing (bv_api.cpp)
 
 int bv_fail(bv_ctx *c, int code, const char *what, hipError_t e = hipSuccess);
 hipStream_t bv_copy_stream(bv_ctx *ctx);   // the device's copy stream (created on first use; nullptr on failure)

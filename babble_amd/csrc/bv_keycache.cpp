@@ -406,7 +406,6 @@ extern "C" int bv_kc_register(bv_ctx *ctx, uint32_t n_keys, const uint8_t *key_b
     if (key_form_ok(key_bytes + key_off[k], key_off[k + 1] - key_off[k]))
       ctx->kc_registered.emplace((const char *)key_bytes + key_off[k], (size_t)(key_off[k + 1] - key_off[k]));
   ctx->timing = bv_timing{};
-  ctx->small_span = 0;
   if (ctx->kc_registered.empty()) return BV_OK;
   // the keys on the device (k_key_decode reads 64 bytes past the last one)
   if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;

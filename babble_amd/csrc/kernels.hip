@@ -21,7 +21,6 @@
 // workgroup per item, one launch).  bv_verify_events' bulk batches hash each
 // body as it is serialised from wire fields (k_ev_body_hash: no body stored).
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -957,8 +956,20 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
                                                const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                const uint8_t *__restrict__ pre, const uint64_t *__restrict__ kc_tabs,
                                                const uint32_t *__restrict__ g_table, uint8_t *__restrict__ status,
-                                               uint64_t *__restrict__ stamps, const uint32_t *__restrict__ rec) {
+                                               uint64_t *__restrict__ stamps, const uint32_t *__restrict__ rec,
+                                               uint64_t *__restrict__ clk) {
   const uint32_t b = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  // the launch's span on the 100 MHz constant clock, in host memory:
+  // clk[0] = workgroup 0's start, clk[1 + b] = workgroup b's end, written
+  // before its status byte (no timing events around the launch)
+  if (b == 0 && t == 0) clk[0] = __builtin_amdgcn_s_memrealtime();
+#define SMALL_DONE(value)                                \
+  do {                                                   \
+    const uint8_t st_ = (value);                         \
+    clk[1 + b] = __builtin_amdgcn_s_memrealtime();       \
+    __threadfence_system();                              \
+    status[b] = st_;                                     \
+  } while (0)
 #define SMALL_STAMP(k)                                                     \
   do {                                                                     \
     if (stamps && b == 0) stamps[k] = __builtin_amdgcn_s_memtime();        \
@@ -1078,7 +1089,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
     const uint8_t cls = classify((uint8_t)sh_pre, (uint8_t)sh_ks, r, sv);
     sh_go = cls == 0xFF;
     if (cls != 0xFF) {
-      status[b] = cls;
+      SMALL_DONE(cls);
     } else if (!rec) {  // (a host record holds u1)
       sc inv, eR, a;
 #pragma unroll
@@ -1187,7 +1198,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
       part_load(sh_b[0].w, A, ia);
       fe r;
       fe_load_be_words(r, sh_r);
-      status[b] = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
+      SMALL_DONE(final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT);
       SMALL_STAMP(13);
     }
     __syncthreads();  // no wave leaves before the last cooperative step of the workgroup
@@ -1252,12 +1263,13 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
       part_load(sh_b[0].w, A, ia);
       fe r;
       fe_load_be_words(r, sh_r);
-      status[b] = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
+      SMALL_DONE(final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT);
       SMALL_STAMP(13);
     }
   }
   __syncthreads();  // no wave leaves before the last cooperative step of the workgroup
 #undef SMALL_STAMP
+#undef SMALL_DONE
 }
 
 // ---------------------------------------------------------------------------
@@ -1580,17 +1592,17 @@ hipError_t build_kc(hipStream_t st, uint32_t n, const uint32_t *kxy, const uint8
   return hipGetLastError();
 }
 
-// (the span's events ride on the kernel's own dispatch: no separate marker
-// packets or host calls around a latency-bound launch)
+// (no timing events around a latency-bound launch: the kernel writes its
+// own span on the constant clock into `clk`, host memory)
 hipError_t verify_small(hipStream_t st, uint32_t n_items, const uint8_t *dig, const uint8_t *key_bytes,
                         const uint64_t *key_off, const uint32_t *item_msg, const uint32_t *item_key,
                         const uint8_t *r_be, const uint8_t *s_be, const uint8_t *pre, const uint64_t *kc_tabs,
-                        const uint32_t *g_table, uint8_t *status, uint64_t *stamps, hipEvent_t ev_start,
-                        hipEvent_t ev_end, const uint32_t *rec) {
+                        const uint32_t *g_table, uint8_t *status, uint64_t *stamps, const uint32_t *rec,
+                        uint64_t *clk) {
   if (n_items == 0) return hipSuccess;
-  hipExtLaunchKernelGGL(k_small, dim3(n_items), dim3(256), 0, st, ev_start, ev_end, 0, n_items,
-                        (const uint32_t *)dig, key_bytes, key_off, item_msg, item_key, (const uint32_t *)r_be,
-                        (const uint32_t *)s_be, pre, kc_tabs, g_table, status, stamps, rec);
+  hipLaunchKernelGGL(k_small, dim3(n_items), dim3(256), 0, st, n_items, (const uint32_t *)dig, key_bytes, key_off,
+                     item_msg, item_key, (const uint32_t *)r_be, (const uint32_t *)s_be, pre, kc_tabs, g_table,
+                     status, stamps, rec, clk);
   return hipGetLastError();
 }
 
