@@ -477,6 +477,12 @@ static int create_impl(bv_ctx *ctx) {
     HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming), BV_E_NODEVICE, "hipEventCreate");
   ctx->chunk_ev.resize(64);
   for (auto &e : ctx->chunk_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming), BV_E_NODEVICE, "event");
+  {  // s_memrealtime's rate (k_small's own span; 100 MHz on gfx950)
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) == hipSuccess && khz > 0)
+      ctx->wall_khz = khz;
+    (void)hipGetLastError();
+  }
   ctx->g_table = gtable_acquire(ctx->device, ctx->stream);
   if (!ctx->g_table) return bv_fail(ctx, BV_E_OOM, "generator table (geometry.h, ~21.5 GB of HBM) build failed");
   const unsigned hw = std::thread::hardware_concurrency();
@@ -1393,8 +1399,13 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   const auto t_waited = std::chrono::steady_clock::now();
   ctx->small_io.flags = hipHostMallocMapped | hipHostMallocCoherent;
   HIPCHK(ctx->small_io.ensure(total), BV_E_OOM, "alloc small-batch buffer");
-  uint8_t *pin = (uint8_t *)ctx->small_io.p, *dev = nullptr;
-  HIPCHK(hipHostGetDevicePointer((void **)&dev, pin, 0), BV_E_LAUNCH, "device pointer (small batch)");
+  uint8_t *pin = (uint8_t *)ctx->small_io.p;
+  if (ctx->small_io_host != pin || ctx->small_io_cap != ctx->small_io.cap) {  // the alias, once per allocation
+    HIPCHK(hipHostGetDevicePointer((void **)&ctx->small_io_dev, pin, 0), BV_E_LAUNCH, "device pointer (small batch)");
+    ctx->small_io_host = pin;
+    ctx->small_io_cap = ctx->small_io.cap;
+  }
+  uint8_t *dev = ctx->small_io_dev;
   auto put = [&](size_t o, const void *src, size_t n) {
     if (n) memcpy(pin + o, src, n);
   };
@@ -1479,12 +1490,12 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
       if (stv[i] == BV_ACCEPT) res->accept_bits[i / 64] |= 1ull << (i % 64);
   }
   bv_timing &t = ctx->timing;
-  {  // the kernel's span from its own clock writes (100 MHz; each end lands before its status)
+  {  // the kernel's span from its own clock writes (wall_khz; each end lands before its status)
     const volatile uint64_t *clk = (const volatile uint64_t *)(pin + o_clk);
     uint64_t end = 0;
     for (uint64_t i = 0; i < n_items; i++) end = std::max<uint64_t>(end, (uint64_t)clk[1 + i]);
     const uint64_t start = clk[0];
-    t.ms_total = t.ms_verify = start && end >= start ? (float)((end - start) * 1e-5) : 0.f;
+    t.ms_total = t.ms_verify = start && end >= start ? (float)((double)(end - start) / ctx->wall_khz) : 0.f;
   }
   t.key_path = kc && hits ? BV_KCW : 0;
   t.kc_hits = hits;

@@ -246,6 +246,9 @@ struct bv_ctx {
   // host-entry staging: one layout in pinned memory and in HBM
   PinnedBuf pin_in, pin_out;
   PinnedBuf small_io;  // k_small's inputs and statuses, read / written by the kernel in place (mapped, coherent)
+  uint8_t *small_io_host = nullptr, *small_io_dev = nullptr;  // small_io.p (of capacity small_io_cap) and its
+  size_t small_io_cap = 0;                                      // device alias
+  double wall_khz = 1e5;  // the device's constant clock (hipDeviceAttributeWallClockRate)
   DevBuf d_in;
   DevBuf d_stamps;  // BV_SMALL_STAMPS: k_small phase clocks (diagnostics)
   DevBuf d_sig;     // bv_verify_events with signature text: the decoded r, s, pre
