@@ -629,11 +629,12 @@ def warm_leg(args, devs, world, dist, local, step_with):
     return out
 
 
-# C5 roofline (key-cache path, k_verify_gq): 9 XYZZ adds from the G table +
-# 12 from the validator's KC table (6 per GLV half) at 10 modmuls each, the
-# 6 beta x products of the phi half, ~7 for u1 / u2, the GLV split and the
-# check: 223 modmuls x 80 IMUL32 per signature.
-C5_MODMUL_PER_ITEM = 223
+# C5 roofline (key-cache path, k_verify_gq): 9 XYZZ adds from the G table
+# (the first on window 0's affine entry: mmadd, 6 modmuls; 8 x 10) + 12 from
+# the validator's KC table (6 per GLV half) at 10 modmuls each, the 6 beta x
+# products of the phi half, ~7 for u1 / u2, the GLV split and the check:
+# 219 modmuls x 80 IMUL32 per signature.
+C5_MODMUL_PER_ITEM = 219
 
 
 def c5_leg(args, local, reps=5):
