@@ -1344,6 +1344,7 @@ int bv_host_finish(bv_ctx *ctx, const bv_batch *b, bv_result *res, bv_host_call 
 // profiles/r04_small_lat.log).
 // ---------------------------------------------------------------------------
 constexpr uint64_t kSmallMsgLen = 16 << 10;  // longest message (hashed on the host, inside the call)
+constexpr uint64_t kHostRecGrain = 16;       // host item records per pool task
 constexpr uint8_t kSmallPending = 0xFF;      // status sentinel (statuses are 0..3)
 
 // Small batches: <= ctx->small_max (256) items, or up to ctx->small_warm_max
@@ -1436,14 +1437,20 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   const bool kc = (ctx->flags & BV_F_KEY_CACHE) && n_keys;
   uint32_t hits = 0;
   if (kc) hits = bv_kc_lookup(ctx, n_keys, b->key_bytes, b->key_off, (uint64_t *)(pin + o_tab));
-  if (recs) {
+  if (recs) {  // the items' scalar halves, kHostRecGrain items per pool task (one inversion each)
     const uint64_t *tabs = (const uint64_t *)(pin + o_tab);
+    std::vector<HostRecItem> &it = ctx->rec_items;
+    it.resize(n_items);
     for (uint64_t i = 0; i < n_items; i++) {
       const uint32_t k = b->item_key[i];
-      bv_host_item_record((uint32_t *)(pin + o_rec) + hrec::kWords * i, dig + 32ull * b->item_msg[i],
-                          b->r_be + 32 * i, b->s_be + 32 * i, b->pre ? b->pre[i] : 0, b->key_bytes + b->key_off[k],
-                          b->key_off[k + 1] - b->key_off[k], kc ? tabs[k] : 0);
+      it[i] = {dig + 32ull * b->item_msg[i], b->r_be + 32 * i, b->s_be + 32 * i, b->key_bytes + b->key_off[k],
+               b->key_off[k + 1] - b->key_off[k], kc ? tabs[k] : 0, (uint8_t)(b->pre ? b->pre[i] : 0)};
     }
+    uint32_t *rp = (uint32_t *)(pin + o_rec);
+    ctx->pool->parallel_for(n_items, kHostRecGrain, [&](uint64_t lo, uint64_t hi) {
+      bv_host_item_records(rp + hrec::kWords * lo, it.data() + lo, hi - lo);
+      return true;
+    });
   }
   const auto t_staged = std::chrono::steady_clock::now();
   uint64_t *stamps = nullptr;

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/babbleverify.h"
+#include "hostscalar.h"
 #include "geometry.h"
 #include "hostdag.h"
 
@@ -326,8 +327,9 @@ struct bv_ctx {
   bool small_stamps = false;      // BV_SMALL_STAMPS=1: print k_small's phase clocks to stderr
   bool host_stamps = false;       // BV_HOST_STAMPS=1: print the host entry's phases to stderr
   bool glv_in_sstream = true;     // BV_GLV_SSTREAM (A/B): device entry's GLV split in k_glv_split
-  uint32_t host_scalar_max = 4;   // BV_HOST_SCALARS: k_small batches up to this many items get host
+  uint32_t host_scalar_max = 128; // BV_HOST_SCALARS: k_small batches up to this many items get host
                                   // item records (hostscalar.h; 0: the device inverts every item)
+  std::vector<HostRecItem> rec_items;  // (their inputs, reused across calls)
   uint64_t small_max = 256;       // k_small for batches of at most this many items and messages (BV_SMALL_MAX)
   uint64_t small_warm_max = 1024;  // k_small for batches whose keys are all cached (BV_SMALL_WARM_MAX)
   uint32_t lat_table_keys = 256;  // latency rule: K8 tables for batches of <= 4096 items from up to this many keys (BV_LAT_TABLE_KEYS)

@@ -13,6 +13,7 @@
 //
 // Inputs are copied into exactly-sized heap buffers so any over-read is an
 // ASan report (the process aborts and the test fails).
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -56,12 +57,50 @@ static std::string join(const T *p, size_t n) {
   return o.empty() ? "-" : o;
 }
 
+// bv_host_item_records over the queued R lines, in batches of cycling sizes
+// (1, 2, 7, 64, 65, 100: one inversion per 64 items inside), one output
+// line per item in order: "R" and the record's 64 words
+struct RItem {
+  std::vector<uint8_t> d, r, s, key;
+  uint8_t pre;
+};
+static std::vector<RItem> pending;
+static void flush_records() {
+  static const size_t sizes[] = {1, 2, 7, 64, 65, 100};
+  size_t at = 0, c = 0;
+  while (at < pending.size()) {
+    const size_t n = std::min(sizes[c++ % 6], pending.size() - at);
+    std::vector<std::unique_ptr<uint8_t[]>> keys;  // exact-size copies: an over-read aborts
+    std::vector<HostRecItem> items(n);
+    for (size_t k = 0; k < n; k++) {
+      const RItem &p = pending[at + k];
+      keys.emplace_back(new uint8_t[p.key.size() ? p.key.size() : 1]);
+      if (!p.key.empty()) memcpy(keys.back().get(), p.key.data(), p.key.size());
+      items[k] = {p.d.data(), p.r.data(), p.s.data(), keys.back().get(), p.key.size(), 0x1122334455667788ull, p.pre};
+    }
+    std::vector<uint32_t> recs(n * hrec::kWords);
+    bv_host_item_records(recs.data(), items.data(), n);
+    for (size_t k = 0; k < n; k++) {
+      std::cout << "R";
+      for (uint32_t w = 0; w < hrec::kWords; w++) {
+        char t[12];
+        snprintf(t, sizeof t, " %08x", recs[k * hrec::kWords + w]);
+        std::cout << t;
+      }
+      std::cout << "\n";
+    }
+    at += n;
+  }
+  pending.clear();
+}
+
 int main() {
   std::string line;
   while (std::getline(std::cin, line)) {
     std::stringstream in(line);
     std::string op;
     in >> op;
+    if (op != "R") flush_records();
     if (op == "S" || op == "H") {
       std::string h;
       in >> h;
@@ -126,26 +165,17 @@ int main() {
         if (!W) std::cout << "-";
       }
       std::cout << "\n";
-    } else if (op == "R") {  // R <digest> <r> <s> <pre> <key|->: bv_host_item_record's 64 words
+    } else if (op == "R") {  // R <digest> <r> <s> <pre> <key|->: queued; run by the next flush
       std::string dh, rh, sh, kh;
       int pre;
       in >> dh >> rh >> sh >> pre >> kh;
       if (kh == "-") kh.clear();
-      const std::vector<uint8_t> d = unhex(dh), r = unhex(rh), s = unhex(sh), key = unhex(kh);
-      std::unique_ptr<uint8_t[]> kb(new uint8_t[key.size() ? key.size() : 1]);  // exact size
-      if (!key.empty()) memcpy(kb.get(), key.data(), key.size());
-      uint32_t rec[hrec::kWords];
-      bv_host_item_record(rec, d.data(), r.data(), s.data(), (uint8_t)pre, kb.get(), key.size(), 0x1122334455667788ull);
-      std::cout << "R";
-      for (uint32_t w = 0; w < hrec::kWords; w++) {
-        char t[12];
-        snprintf(t, sizeof t, " %08x", rec[w]);
-        std::cout << t;
-      }
-      std::cout << "\n";
+      pending.push_back({unhex(dh), unhex(rh), unhex(sh), unhex(kh), (uint8_t)pre});
+      continue;
     } else {
       return 2;
     }
   }
+  flush_records();
   return 0;
 }

@@ -328,13 +328,15 @@ def test_small_batch_kernel_equals_oracle(monkeypatch):
 
 
 def test_small_batch_host_records_equal_device_scalars(monkeypatch):
-    """Latency batches (<= BV_HOST_SCALARS items, default 4) carry host item
-    records (hostscalar.h: s^-1, u1, u2 and u2's GLV split computed on the
-    host with field.h's own functions, one 256-byte read per workgroup): the
-    824 golden items (every decision-table class) in batches of 1-4 items,
-    single events and a 40-item adversarial batch in 4-item slices, cold and with part of the
-    valid keys registered (cached and uncached keys), equal to the oracle
-    and, item for item, to the device-inversion path (BV_HOST_SCALARS=0)."""
+    """Latency batches (<= BV_HOST_SCALARS items, default 128) carry host
+    item records (hostscalar.h: s^-1 by one batch inversion per 64 items,
+    u1, u2 and u2's GLV split computed on the host with field.h's own
+    functions, one 256-byte read per workgroup): the 824 golden items (every
+    decision-table class) in batches of 1-4 items and again in batches of
+    128 / 100 / 65 / 33, single events and a 40-item adversarial batch in
+    4-item slices, cold and with part of the valid keys registered (cached
+    and uncached keys), equal to the oracle and, item for item, to the
+    device-inversion path (BV_HOST_SCALARS=0)."""
     from babble_amd import shard
     from babble_amd.verifier import Verifier
 
@@ -347,6 +349,11 @@ def test_small_batch_host_records_equal_device_scalars(monkeypatch):
         lo = hi
     batches = [shard.slice_batch(golden, a, c) for a, c in cuts]
     n_golden = len(batches)
+    lo, k = 0, 0
+    while lo < golden.n_items:  # larger batches: more than one pool task and more than 64 items per inversion
+        hi = min(golden.n_items, lo + (128, 100, 65, 33)[k % 4])
+        batches.append(shard.slice_batch(golden, lo, hi))
+        lo, k = hi, k + 1
     batches += [synth.events(1, n_creators=1, seed=960 + i) for i in range(4)]
     adv = synth.adversarial(40, seed=970, n_creators=3, scale_per_million=MIX)
     batches += [shard.slice_batch(adv, lo, lo + 4) for lo in range(0, 40, 4)]
