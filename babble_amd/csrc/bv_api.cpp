@@ -1394,8 +1394,8 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
                o_im = at(n_items * 4), o_ik = at(n_items * 4), o_r = at(n_items * 32), o_s = at(n_items * 32),
                o_pre = at(n_items), o_tab = at(n_keys * 8ull), o_st = at(n_items);
   // a latency batch: one host record per item (hostscalar.h) instead
-  const bool recs = n_items <= ctx->host_scalar_max;
-  const size_t o_rec = at(recs ? n_items * hrec::kWords * 4 : 0), o_clk = at((n_items + 1) * 8);
+  const bool rec_room = n_items <= ctx->host_scalar_max;
+  const size_t o_rec = at(rec_room ? n_items * hrec::kWords * 4 : 0), o_clk = at((n_items + 1) * 8);
   if (bv_wait_all(ctx) != BV_OK) return BV_E_LAUNCH;  // the previous call may still read the buffer
   const auto t_waited = std::chrono::steady_clock::now();
   ctx->small_io.flags = hipHostMallocMapped | hipHostMallocCoherent;
@@ -1437,6 +1437,15 @@ static int small_verify(bv_ctx *ctx, const bv_batch *b, bv_result *res) {
   const bool kc = (ctx->flags & BV_F_KEY_CACHE) && n_keys;
   uint32_t hits = 0;
   if (kc) hits = bv_kc_lookup(ctx, n_keys, b->key_bytes, b->key_off, (uint64_t *)(pin + o_tab));
+  // Records when the scalar chain is the kernel's critical path: up to 4
+  // items always, up to host_scalar_max when every item's key has a
+  // key-cache table.  A table-less key's Q chain (~0.25 ms) hides the device's s^-1,
+  // and there the host's records only add host time; past ~16 items the
+  // host batch costs more than the device's parallel inversions (measured:
+  // profiles/r06_small_lat_hs128.log / r06_small_lat_hs4.log).
+  bool recs = rec_room && (n_items <= 4 || kc);
+  if (recs && n_items > 4)
+    for (uint64_t i = 0; i < n_items && recs; i++) recs = ((const uint64_t *)(pin + o_tab))[b->item_key[i]] != 0;
   if (recs) {  // the items' scalar halves, kHostRecGrain items per pool task (one inversion each)
     const uint64_t *tabs = (const uint64_t *)(pin + o_tab);
     std::vector<HostRecItem> &it = ctx->rec_items;

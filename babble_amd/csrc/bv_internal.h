@@ -327,7 +327,7 @@ struct bv_ctx {
   bool small_stamps = false;      // BV_SMALL_STAMPS=1: print k_small's phase clocks to stderr
   bool host_stamps = false;       // BV_HOST_STAMPS=1: print the host entry's phases to stderr
   bool glv_in_sstream = true;     // BV_GLV_SSTREAM (A/B): device entry's GLV split in k_glv_split
-  uint32_t host_scalar_max = 128; // BV_HOST_SCALARS: k_small batches up to this many items get host
+  uint32_t host_scalar_max = 16;  // BV_HOST_SCALARS: k_small batches up to this many items may get host
                                   // item records (hostscalar.h; 0: the device inverts every item)
   std::vector<HostRecItem> rec_items;  // (their inputs, reused across calls)
   uint64_t small_max = 256;       // k_small for batches of at most this many items and messages (BV_SMALL_MAX)

@@ -328,15 +328,16 @@ def test_small_batch_kernel_equals_oracle(monkeypatch):
 
 
 def test_small_batch_host_records_equal_device_scalars(monkeypatch):
-    """Latency batches (<= BV_HOST_SCALARS items, default 128) carry host
-    item records (hostscalar.h: s^-1 by one batch inversion per 64 items,
-    u1, u2 and u2's GLV split computed on the host with field.h's own
-    functions, one 256-byte read per workgroup): the 824 golden items (every
+    """Latency batches (<= 4 items, or <= BV_HOST_SCALARS (16) items whose
+    keys all have key-cache tables) carry host item records (hostscalar.h:
+    s^-1 by one batch inversion, u1, u2 and u2's GLV split computed on the
+    host with field.h's own functions, one 256-byte read per workgroup): the
+    824 golden items (every
     decision-table class) in batches of 1-4 items and again in batches of
-    128 / 100 / 65 / 33, single events and a 40-item adversarial batch in
-    4-item slices, cold and with part of the valid keys registered (cached
-    and uncached keys), equal to the oracle and, item for item, to the
-    device-inversion path (BV_HOST_SCALARS=0)."""
+    16 / 9 / 5 / 13, single events and a 40-item adversarial batch in
+    4-item slices, cold and with every valid key registered, equal to the
+    oracle and, item for item, to the device-inversion path
+    (BV_HOST_SCALARS=0)."""
     from babble_amd import shard
     from babble_amd.verifier import Verifier
 
@@ -350,15 +351,15 @@ def test_small_batch_host_records_equal_device_scalars(monkeypatch):
     batches = [shard.slice_batch(golden, a, c) for a, c in cuts]
     n_golden = len(batches)
     lo, k = 0, 0
-    while lo < golden.n_items:  # larger batches: more than one pool task and more than 64 items per inversion
-        hi = min(golden.n_items, lo + (128, 100, 65, 33)[k % 4])
+    while lo < golden.n_items:  # larger batches: records when warm (every key cached), else the device
+        hi = min(golden.n_items, lo + (16, 9, 5, 13)[k % 4])
         batches.append(shard.slice_batch(golden, lo, hi))
         lo, k = hi, k + 1
     batches += [synth.events(1, n_creators=1, seed=960 + i) for i in range(4)]
     adv = synth.adversarial(40, seed=970, n_creators=3, scale_per_million=MIX)
     batches += [shard.slice_batch(adv, lo, lo + 4) for lo in range(0, 40, 4)]
     good = []
-    for b in batches[n_golden:] + batches[:40]:
+    for b in batches:
         for k in range(b.n_keys):
             if gs.Unmarshal(b.key(k)) is not None and b.key(k) not in good:
                 good.append(b.key(k))
@@ -369,8 +370,8 @@ def test_small_batch_host_records_equal_device_scalars(monkeypatch):
         monkeypatch.delenv("BV_HOST_SCALARS")
         try:
             if flags:
-                rec.register_keys(good[:8])
-                dev.register_keys(good[:8])
+                rec.register_keys(good)  # every valid key: the 5-16-item batches take records too
+                dev.register_keys(good)
             got = []
             for b in batches:
                 r = check_against_oracle(rec, b)
