@@ -1189,7 +1189,8 @@ def shim_path_leg(args, line):
     SyncLimit SyncResponse of `events_entry.sync_dag_1000` (1000 events, 4
     creators, in-batch parents) and the C2 replay (1M events, store-hash
     parents) through bv_verify_events.  Each beside the library-only number
-    of the same shape measured in this line."""
+    of the same shape: for the SyncResponse measured in this leg, call for
+    call alternating with the shim's."""
     import numpy as np
 
     from babble_amd import synth
@@ -1213,18 +1214,36 @@ def shim_path_leg(args, line):
         out["event_1"] = {"ms_median": float(np.median(ts)), "library_ms": lib1,
                           "over_library": float(np.median(ts)) / lib1 if lib1 else None}
         dag_packed, dag = synth.event_fields(1000, n_creators=4, seed=31, parents="event")
-        sh.set_peers([dag_packed.key(k) for k in range(dag_packed.n_keys)])
+        dag_keys = [dag_packed.key(k) for k in range(dag_packed.n_keys)]
+        sh.set_peers(dag_keys)
         sw, keep = sh.wire(dag)
+        # the library's own call (Python ctypes, the same key-cache context
+        # and Signature text) alternated with the shim's on this box: the
+        # DAG path's host hashing makes separate legs' numbers drift
+        from babble_amd import native
+        from babble_amd.verifier import Verifier
+
+        vc = Verifier(device=local, flags=native.F_KEY_CACHE)
+        vc.register_keys(dag_keys)
+        dag_t = dag.with_signature_text(*harness.encode_signatures(dag.r_be, dag.s_be))
         sh.sync(sw)
-        ts, ph = [], []
-        for _ in range(15):
+        vc.verify_events(dag_t)
+        ts, tl, ph = [], [], []
+        for _ in range(21):
             _, st, ms = sh.sync(sw)
             assert np.all(st == 1)
             ts.append(ms)
             ph.append(sh.phases())
-        libd = ((line.get("events_entry") or {}).get("sync_dag_1000") or {}).get("ms_median")
+            t0 = time.perf_counter()
+            res = vc.verify_events(dag_t)
+            tl.append((time.perf_counter() - t0) * 1e3)
+            assert np.all(res.status == 1)
+        vc.close()
+        libd = float(np.median(tl))
         out["sync_dag_1000"] = {"ms_median": float(np.median(ts)), "library_ms": libd,
-                                "over_library": float(np.median(ts)) / libd if libd else None,
+                                "over_library": float(np.median(ts)) / libd,
+                                "library_ms_events_entry_leg": ((line.get("events_entry") or {}).get("sync_dag_1000")
+                                                                or {}).get("ms_median"),
                                 "phases_ms": {k: float(np.median([p[k] for p in ph])) for k in ph[0]}}
         del sw, keep
         packed, wire = synth.event_fields(args.events, n_creators=args.creators, seed=2, parents="hash")
