@@ -1183,7 +1183,7 @@ def shim_path_leg(args, line):
     """The Go shim's path through the C harness
     (tests/cabi/shim_harness.c): the key-cache context, the creators
     registered as the PeerSet (bv_kc_register), batches built field by field
-    in pooled pinned arenas, signature text decoded per event, results
+    in pooled pinned arenas, signature text copied (decoded on the device), results
     copied out — all inside the clock (the harness's own wall time).  Shapes:
     one event through bv_verify_batch (addSelfEvent, core.go:291), the
     SyncLimit SyncResponse of `events_entry.sync_dag_1000` (1000 events, 4

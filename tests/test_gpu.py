@@ -188,6 +188,28 @@ def test_host_entry_item_order(monkeypatch):
     verifier.close()
 
 
+def test_host_entry_stamps_diagnostics(monkeypatch, capfd):
+    """BV_HOST_STAMPS=1 (the host entry's phase stamps, the staging buffer's
+    NUMA node and the per-call device timeline) prints
+    its lines and changes no result: a 20k-event pageable host-entry call,
+    twice, equal to the oracle."""
+    from babble_amd.verifier import Verifier
+
+    monkeypatch.setenv("BV_HOST_STAMPS", "1")  # read at bv_create
+    b = synth.events(20_000, n_creators=8, seed=981)
+    b.r_be[5, 31] ^= 1
+    v = Verifier(device=0)
+    try:
+        for _ in range(2):
+            res = check_against_oracle(v, b)
+            assert int((res.status == 1).sum()) == b.n_items - 1
+    finally:
+        v.close()
+    err = capfd.readouterr().err
+    assert "bv_host_launch ms:" in err and "staging on NUMA node" in err
+    assert "bv_host_finish ms:" in err and "device from E_CALL" in err
+
+
 @pytest.mark.parametrize("qfirst", ["1", "0"])
 def test_host_entry_key_part_order(monkeypatch, qfirst):
     """Host entries sum every item's k1 Q + k2 phi(Q) before its message is
