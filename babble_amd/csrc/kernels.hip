@@ -576,8 +576,11 @@ __global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_QWAVES) k_verify_gf(
 }
 
 // Key-cache path, G and Q parts fused (verify_core.h: verify_item_gq_kc).
+#ifndef BV_GQWAVES
+#define BV_GQWAVES BV_QWAVES
+#endif
 template <bool LAT>
-__global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_QWAVES) k_verify_gq(uint64_t n_items, uint64_t lo, uint64_t hi,
+__global__ void __launch_bounds__(256, LAT ? BV_LWAVES : BV_GQWAVES) k_verify_gq(uint64_t n_items, uint64_t lo, uint64_t hi,
                                                    const uint32_t *__restrict__ item_key,
                                                    const uint32_t *__restrict__ r_be, const uint32_t *__restrict__ s_be,
                                                    const uint8_t *__restrict__ pre, const uint8_t *__restrict__ kstatus,
