@@ -1010,13 +1010,20 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
       sh_tab = (uint64_t)sh_rec[hrec::kTab] | (uint64_t)sh_rec[hrec::kTab + 1] << 32;
       SMALL_STAMP(2);
     } else if (lane == 0 && wave == 2) {
-      uint8_t st;
-      fe x, y;
-      key_decode_point((const uint8_t *)(sh_rec + hrec::kKey), 0, sh_rec[hrec::kKeyLen], st, x, y);
+      if (sh_rec[hrec::kTab] | sh_rec[hrec::kTab + 1]) {
+        // a key-cache table exists only for these exact bytes decoded
+        // KS_OK: phase 2 decides with that, and wave 2 decodes the key
+        // again in phase 3, beside the leaf loads, for the final decision
+        sh_ks = KS_OK;
+      } else {
+        uint8_t st;
+        fe x, y;
+        key_decode_point((const uint8_t *)(sh_rec + hrec::kKey), 0, sh_rec[hrec::kKeyLen], st, x, y);
 #pragma unroll
-      for (int c = 0; c < 8; c++) sh_q[c] = x.v[c], sh_q[8 + c] = y.v[c];
-      sh_ks = st;
-      chain = st == KS_OK && !(sh_rec[hrec::kTab] | sh_rec[hrec::kTab + 1]);
+        for (int c = 0; c < 8; c++) sh_q[c] = x.v[c], sh_q[8 + c] = y.v[c];
+        sh_ks = st;
+        chain = st == KS_OK;
+      }
       SMALL_STAMP(3);
     }
   } else if (lane == 0 && wave == 0) {
@@ -1179,6 +1186,11 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
       if (lane == 0) SMALL_STAMP(7);
       small_leaf_pairs(x, y, zero, sh_b, sh_a, kSmallLeaves, lane);  // 22 leaves -> 11 nodes (per lane)
       if (lane == 0) SMALL_STAMP(8);
+    } else if (rec && wave == 2 && lane == 0) {  // the record's key, decoded off the critical path
+      uint8_t st;
+      fe x, y;
+      key_decode_point((const uint8_t *)(sh_rec + hrec::kKey), 0, sh_rec[hrec::kKeyLen], st, x, y);
+      sh_ks = st;
     }
     __syncthreads();
     // the XYZZ tree on DPP rows (coop.h add_xyzz, ~6k clocks an addition
@@ -1201,7 +1213,14 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
       part_load(sh_b[0].w, A, ia);
       fe r;
       fe_load_be_words(r, sh_r);
-      SMALL_DONE(final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT);
+      uint8_t st = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
+      if (rec) {  // the decision table again with the key's own decode
+        fe sv;
+        fe_load_be_words(sv, sh_s);
+        const uint8_t cls = classify((uint8_t)sh_pre, (uint8_t)sh_ks, r, sv);
+        if (cls != 0xFF) st = cls;
+      }
+      SMALL_DONE(st);
       SMALL_STAMP(13);
     }
     __syncthreads();  // no wave leaves before the last cooperative step of the workgroup
