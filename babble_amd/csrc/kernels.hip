@@ -982,7 +982,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
   __shared__ uint32_t sh_ks, sh_go, sh_signs, sh_pre, sh_nb, sh_nphase;
   __shared__ uint64_t sh_tab;
   __shared__ SinvMail sh_mail;
-  __shared__ uint32_t sh_sok;
+  __shared__ uint32_t sh_sok, sh_cls;
   __shared__ SmallNode sh_a[kSmallLeaves], sh_b[kSmallLeaves / 2 + 1], sh_c[kSmallLeaves / 4 + 2];
   __shared__ SmallCold cs;
   __shared__ uint32_t sh_rec[hrec::kWords];
@@ -1198,7 +1198,14 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
     // kWarmSplit[w] .. kWarmSplit[w + 1] - 1), 4 -> 2 (waves 0, 1), 2 -> 1
     coop_sum_nodes(sh_b, kWarmSplit[wave], kWarmSplit[wave + 1], sh_c[wave]);
     __syncthreads();
-    if (wave < 2) coop_sum_nodes(sh_c, 2 * wave, 2 * wave + 2, sh_a[wave]);
+    if (wave < 2) {
+      coop_sum_nodes(sh_c, 2 * wave, 2 * wave + 2, sh_a[wave]);
+    } else if (rec && wave == 2 && lane == 0) {  // the decision table with the key's own decode, meanwhile
+      fe r, sv;
+      fe_load_be_words(r, sh_r);
+      fe_load_be_words(sv, sh_s);
+      sh_cls = classify((uint8_t)sh_pre, (uint8_t)sh_ks, r, sv);
+    }
     __syncthreads();
     if (wave == 0) {
       coop_sum_nodes(sh_a, 0, 2, sh_b[0]);
@@ -1214,12 +1221,7 @@ __global__ void __launch_bounds__(256) k_small(uint32_t n_items, const uint32_t 
       fe r;
       fe_load_be_words(r, sh_r);
       uint8_t st = final_check(A, ia, r) ? BV_ACCEPT : BV_REJECT;
-      if (rec) {  // the decision table again with the key's own decode
-        fe sv;
-        fe_load_be_words(sv, sh_s);
-        const uint8_t cls = classify((uint8_t)sh_pre, (uint8_t)sh_ks, r, sv);
-        if (cls != 0xFF) st = cls;
-      }
+      if (rec && sh_cls != 0xFF) st = (uint8_t)sh_cls;  // (the key's own decode says otherwise)
       SMALL_DONE(st);
       SMALL_STAMP(13);
     }
