@@ -478,7 +478,7 @@ def run(args, world: int, rank: int, local: int, worker) -> None:
         achieved = args.events * MODMUL_PER_ITEM_EXEC * IMUL32_PER_MODMUL / kv_s
         roof = {
             "bound": "valu-int",
-            "kernel": "k_verify_g<false> + k_verify_q<12, 11, false>",
+            "kernel": "k_verify_g<false, true> + k_verify_q<12, 11, false>",
             "achieved": achieved / 1e12,
             "peak": PEAK_IMUL32_PER_S / 1e12,
             "unit": f"T IMUL32/s (executed schedule: {MODMUL_PER_ITEM_EXEC} modmuls x 80 IMUL32 per item; "
