@@ -446,16 +446,9 @@ hipStream_t bv_copy_stream(bv_ctx *ctx) {
   if (ctx->cstream) return ctx->cstream;
   std::lock_guard<std::mutex> lk(g_streams_mu);
   DevStreams &d = g_streams[ctx->device];
-  if (!d.cstream) {
-    int least = 0, greatest = 0;
-    const char *e = getenv("BV_COPY_PRIO");  // (A/B knob: the copy stream at the highest priority)
-    hipError_t rc = (e && atoi(e) && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-                        ? hipStreamCreateWithPriority(&d.cstream, hipStreamNonBlocking, greatest)
-                        : hipStreamCreateWithFlags(&d.cstream, hipStreamNonBlocking);
-    if (rc != hipSuccess) {
-      (void)hipGetLastError();
-      d.cstream = nullptr;
-    }
+  if (!d.cstream && hipStreamCreateWithFlags(&d.cstream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    d.cstream = nullptr;
   }
   ctx->cstream = d.cstream;
   return ctx->cstream;
