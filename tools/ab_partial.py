@@ -5,7 +5,9 @@ finishes the fresh key's items on the generic per-lane path
 (k_verify_deferred); the alternative is the per-batch K12 tables for all 20
 keys (a context without the key cache).  Device entry (batch resident) and
 host entry (pinned), 5 timed calls each after one untimed; BV_KC_ADMIT is
-raised so the fresh key stays fresh.  Every result is checked."""
+raised so the fresh key stays fresh.  Every result is checked.
+Partial mode is off by default now (the result of this A/B): the first
+variant turns it on with BV_KC_PARTIAL=1, the second shows the default."""
 import os
 import sys
 import time
@@ -53,10 +55,16 @@ for n in [int(x) for x in os.environ.get("AB_SIZES", "1000000").split(",")]:
     fresh_items = int((np.asarray(b.item_key) == 0).sum())
     keys = [b.key(k) for k in range(b.n_keys)]
     print(f"{n} events, 20 creators, fresh key 0 signs {fresh_items} items", flush=True)
+    os.environ["BV_KC_PARTIAL"] = "1"  # (read at context creation; off by default since this A/B)
     vc = Verifier(device=0, flags=native.F_KEY_CACHE)
+    os.environ.pop("BV_KC_PARTIAL")
     vc.register_keys(keys[1:])
     run(vc, b, "key cache, partial (1 fresh of 20)")
     vc.close()
+    vd = Verifier(device=0, flags=native.F_KEY_CACHE)
+    vd.register_keys(keys[1:])
+    run(vd, b, "key cache, 1 fresh, default (no partial)")
+    vd.close()
     v0 = Verifier(device=0)
     run(v0, b, "per-batch tables (no cache)")
     v0.close()
