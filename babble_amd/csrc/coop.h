@@ -12,7 +12,12 @@
 //
 // Carries between limbs are resolved with a carry-lookahead over wave-wide
 // lane masks: G = lanes whose digit carries out, P = lanes whose digit is
-// 0xFFFFFFFF; the carries INTO the lanes are ((G << 1) + P) ^ P.
+// 0xFFFFFFFF; the carries INTO the lanes are ((G << 1) + P) ^ P.  A product
+// or a norm() runs ONE such resolve (two ballots and the scalar adds on its
+// dependent chain): the 2^256 folds work on unresolved 33-bit digits, with
+// one DPP carry-save step each (round 6; three resolves before).  The bounds
+// are checked digit by digit by a Python model of these functions
+// (tests/test_coop_model.py).
 //
 // Forms:  NORMAL  lanes 0..7 hold the limbs of a value < 2^256 (weakly
 //                 reduced mod p), lanes 8..15 hold 0 — what mul() takes and
@@ -57,28 +62,66 @@ __device__ __forceinline__ uint32_t resolve(uint32_t v, bool gen) {
   return v + (uint32_t)((C >> __lane_id()) & 1u);
 }
 
-// lanes 0..8 digits d (d_8 = a multiple of 2^256, small): fold d_8 (2^256 =
-// 2^32 + 977) into lanes 0 and 1 and resolve; a carry out of lane 7 (the
-// value was within ~2^45 of 2^256) folds once more.  Returns NORMAL.
-__device__ __forceinline__ uint32_t fold(uint32_t d) {
+// lanes 0..8 hold w_k < 2^32 + 2^20 (lanes 9..15: 0), the value
+// sum w_k 2^(32 k): fold w_8 (2^256 = 2^32 + 977) into lanes 0 and 1
+// unresolved, then resolve the carries ONCE.  The lanes 0..7 part is below
+// 2^256 + 2^245 and w_8 (2^32 + 977) below 2^53, so the resolved lane 8 is 0
+// or 1, and when it is 1 the rest is below 2^245: the rare second fold
+// cannot carry out of limb 7.  Whether lane 8 ends nonzero is read off the
+// scalar carry word (its input digit, or a carry into it), so the branch
+// needs no vector compare after the resolve.  N values at once (N = 1, 2):
+// their steps interleave in one basic block, one branch for all.
+constexpr uint64_t kLane8 = 0x0100010001000100ull;  // lane 8 of each row
+template <int N>
+__device__ __forceinline__ void tail_n(const uint64_t (&w)[N], uint32_t (&d)[N]) {
   const uint32_t m = lo8(), f = f977();
-  uint32_t o = dpp<0x158>(d);
-  uint64_t z = (uint64_t)(d & m) + (uint64_t)o * f;  // lane 0: + 977 o, lane 1: + o
-  uint64_t y = (uint64_t)(uint32_t)z + dpp<0x111>((uint32_t)(z >> 32));
-  d = resolve((uint32_t)y, (y >> 32) != 0);  // lane 8: the carry out of limb 7
-  if (__ballot(pos() == 8 && d != 0)) {    // rare, wave-uniform
-    o = dpp<0x158>(d);
-    z = (uint64_t)(d & m) + (uint64_t)o * f;
-    y = (uint64_t)(uint32_t)z + dpp<0x111>((uint32_t)(z >> 32));
-    d = resolve((uint32_t)y, (y >> 32) != 0);  // the value is now < 2^46: no carry out
+  uint64_t y[N], C[N], rare = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const uint64_t w8 = ((uint64_t)dpp<0x158>((uint32_t)(w[i] >> 32)) << 32) | dpp<0x158>((uint32_t)w[i]);
+    const uint64_t z = (pos() < 8 ? w[i] : 0ull) + w8 * f;  // lane 0: + 977 w_8, lane 1: + w_8 (< 2^43)
+    y[i] = (uint64_t)(uint32_t)z + dpp<0x111>((uint32_t)(z >> 32));  // < 2^33; lane 8: <= 1
   }
-  return d & m;
+#pragma unroll
+  for (int i = 0; i < N; i++) {  // resolve(), with lane 8's outcome kept in `rare`
+    const uint64_t G = __ballot((y[i] >> 32) != 0), P = __ballot((uint32_t)y[i] == 0xFFFFFFFFu);
+    C[i] = ((G << 1) + P) ^ P;
+    rare |= (__ballot((uint32_t)y[i] != 0) | C[i]) & kLane8;
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) d[i] = (uint32_t)y[i] + (uint32_t)((C[i] >> __lane_id()) & 1u);
+  if (rare) {  // rare (a value within ~2^235 of 2^256), wave-uniform
+#pragma unroll
+    for (int i = 0; i < N; i++) {  // (a no-op for a value whose lane 8 is 0)
+      const uint32_t o = dpp<0x158>(d[i]);
+      const uint64_t z2 = (uint64_t)(d[i] & m) + (uint64_t)o * f;
+      const uint64_t y2 = (uint64_t)(uint32_t)z2 + dpp<0x111>((uint32_t)(z2 >> 32));
+      d[i] = resolve((uint32_t)y2, (y2 >> 32) != 0);  // the rest is < 2^245: no carry out
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) d[i] &= m;
+}
+__device__ __forceinline__ uint32_t tail(uint64_t w) {
+  const uint64_t in[1] = {w};
+  uint32_t out[1];
+  tail_n<1>(in, out);
+  return out[0];
 }
 
-// WIDE -> NORMAL
-__device__ __forceinline__ uint32_t norm(uint64_t w) {
-  const uint64_t v = (uint64_t)(uint32_t)w + dpp<0x111>((uint32_t)(w >> 32));
-  return fold(resolve((uint32_t)v, (v >> 32) != 0));
+// WIDE -> NORMAL: one carry-save step (lane 9 stays 0: a WIDE lane 8 is
+// small), then tail()
+__device__ __forceinline__ uint64_t carry_save(uint64_t w) {
+  return (uint64_t)(uint32_t)w + dpp<0x111>((uint32_t)(w >> 32));  // < 2^32 + 2^8
+}
+__device__ __forceinline__ uint32_t norm(uint64_t w) { return tail(carry_save(w)); }
+// two independent WIDE values side by side
+__device__ __forceinline__ void norm2(uint32_t &a, uint64_t wa, uint32_t &b, uint64_t wb) {
+  const uint64_t in[2] = {carry_save(wa), carry_save(wb)};
+  uint32_t out[2];
+  tail_n<2>(in, out);
+  a = out[0];
+  b = out[1];
 }
 
 // a b mod p; a, b NORMAL (row-local), result NORMAL
@@ -101,31 +144,22 @@ __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) {
   }
   COOP_STEP(0) COOP_STEP(1) COOP_STEP(2) COOP_STEP(3) COOP_STEP(4) COOP_STEP(5) COOP_STEP(6) COOP_STEP(7)
 #undef COOP_STEP
-  // column k = lo_k + 2^32 hi_k + 2^64 cnt_k -> digit k of the 512-bit product
+  // column k = lo_k + 2^32 hi_k + 2^64 cnt_k (columns 14, 15 carry nothing
+  // out of the row) -> u_k < 2^34 with sum u_k 2^(32 k) = a b, then the
+  // product's digit E_k = (u_k mod 2^32) + (u_(k-1) div 2^32) < 2^32 + 3
+  // (E_15 < 2^32, as a b < 2^512) — left unresolved
   const uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
-  const uint64_t u = (uint64_t)lo + dpp<0x111>(hi) + dpp<0x112>(cnt);  // < 2^34
+  const uint64_t u = (uint64_t)lo + dpp<0x111>(hi) + dpp<0x112>(cnt);
   const uint64_t v = (uint64_t)(uint32_t)u + dpp<0x111>((uint32_t)(u >> 32));
-  uint32_t d = resolve((uint32_t)v, (v >> 32) != 0);  // d_0 .. d_15
-  // 2^256 = 2^32 + 977: lane k < 8 gets d_k + 977 d_(k+8) + d_(k+7) (k >= 1),
-  // lane 8 gets d_15 (row_shl:8 / :7 read zeros past the row's end)
-  const uint32_t m = lo8();
-  const uint32_t x8 = dpp<0x108>(d) & m, x7 = dpp<0x107>(d) & (k == 0 ? 0u : (k <= 8 ? 0xFFFFFFFFu : 0u));
-  const uint64_t t = (uint64_t)x8 * 977u + (d & m) + x7;
-  const uint64_t w = (uint64_t)(uint32_t)t + dpp<0x111>((uint32_t)(t >> 32));  // < 2^32 + 2^10
-  d = resolve((uint32_t)w, (w >> 32) != 0);  // lanes 0..8, lane 9 in {0, 1}
-  // second fold: r_8 + 2^32 r_9 at 2^256 -> limbs 0..2 (977 r_8 | r_8 + 977 r_9 | r_9)
-  const uint32_t r8 = dpp<0x158>(d), r9 = dpp<0x159>(d);
-  const uint32_t a8 = k == 0 ? 977u : (k == 1 ? 1u : 0u), a9 = k == 1 ? 977u : (k == 2 ? 1u : 0u);
-  const uint64_t z = (uint64_t)(d & m) + (uint64_t)r8 * a8 + (uint64_t)r9 * a9;
-  const uint64_t y = (uint64_t)(uint32_t)z + dpp<0x111>((uint32_t)(z >> 32));
-  d = resolve((uint32_t)y, (y >> 32) != 0);  // lane 8: the carry out of limb 7
-  if (__ballot(k == 8 && d != 0)) {        // rare, wave-uniform
-    const uint32_t o = dpp<0x158>(d);
-    const uint64_t z2 = (uint64_t)(d & m) + (uint64_t)o * f977();
-    const uint64_t y2 = (uint64_t)(uint32_t)z2 + dpp<0x111>((uint32_t)(z2 >> 32));
-    d = resolve((uint32_t)y2, (y2 >> 32) != 0);
-  }
-  return d & m;
+  const uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32);  // vh <= 1
+  // 2^256 = 2^32 + 977: lane k < 8 gets E_k + 977 E_(k+8) + [k >= 1] E_(k+7),
+  // lane 8 gets E_15 (row_shl:8 / :7 read zeros past the row's end); < 2^42
+  const uint64_t e8 = ((uint64_t)dpp<0x108>(vh) << 32) | dpp<0x108>(vl);
+  const uint32_t m7 = (k == 0 || k > 8) ? 0u : 0xFFFFFFFFu;
+  const uint64_t e7 = ((uint64_t)(dpp<0x107>(vh) & m7) << 32) | (dpp<0x107>(vl) & m7);
+  const uint64_t t = (k < 8 ? v : 0ull) + e8 * 977u + e7;
+  // one carry-save step: lanes 0..8, each < 2^32 + 2^10 (lane 9: E_15 div 2^32 = 0)
+  return tail((uint64_t)(uint32_t)t + dpp<0x111>((uint32_t)(t >> 32)));
 }
 
 // 4p in redundant limbs all >= 2^32 (lane k's limb; lane 8: 2): a + M4 - b
@@ -153,19 +187,18 @@ __device__ __forceinline__ void dbl(uint32_t &X, uint32_t &Y, uint32_t &Z) {
   // level 1: A = X^2 (row 0), B = Y^2 (row 1), YZ (row 2)
   uint32_t m = mul(r == 0 || r == 3 ? X : Y, r == 1 ? Y : r == 2 ? Z : X);
   const uint32_t A = from_row(m, 0), B = from_row(m, 1), YZ = from_row(m, 2);
-  const uint32_t E = norm(3ull * A);
-  const uint32_t XB = norm((uint64_t)X + B);
+  uint32_t E, XB;
+  norm2(E, 3ull * A, XB, (uint64_t)X + B);
   // level 2: C = B^2 (row 0), F = E^2 (row 1), W = (X + B)^2 (row 2)
   const uint32_t s = r == 1 ? E : r == 2 ? XB : B;
   m = mul(s, s);
   const uint32_t C = from_row(m, 0), F = from_row(m, 1), W = from_row(m, 2);
   const uint32_t D = norm(2ull * ((uint64_t)W + negw(A) + negw(C)));  // 2 ((X + B)^2 - A - C)
-  X = norm((uint64_t)F + 2ull * negw(D));                             // F - 2 D
-  const uint32_t t = norm((uint64_t)D + negw(X));                     // D - X3
+  uint32_t t;  // X3 = F - 2 D, D - X3 = 3 D - F
+  norm2(X, (uint64_t)F + 2ull * negw(D), t, 3ull * D + negw(F));
   // level 3: E (D - X3), every row
   m = mul(E, t);
-  Y = norm((uint64_t)m + 8ull * negw(C));  // E (D - X3) - 8 C
-  Z = norm(2ull * YZ);
+  norm2(Y, (uint64_t)m + 8ull * negw(C), Z, 2ull * YZ);  // E (D - X3) - 8 C, 2 Y Z
 }
 
 // a NORMAL value (replicated in every row) is 0 mod p: 0 or p itself
@@ -216,30 +249,32 @@ __device__ __forceinline__ void madd(uint32_t &X, uint32_t &Y, uint32_t &Z, bool
 // beta's limb for this lane (phi(x, y) = (beta x, y))
 __device__ __forceinline__ uint32_t beta_limb() { return pos() < 8 ? FE_BETA[pos()] : 0u; }
 
-// XYZZ doubling dbl-2008-s-1 (a = 0; x = X / ZZ, y = Y / ZZZ, the same
-// formulas as point.h gexz_double), state replicated in every row; the nine
-// products form three levels {U^2, X^2} -> {U V, X V, V ZZ, M^2} ->
-// {M (S - X3), W Y, W ZZZ, beta X3} with U = 2Y, M = 3X^2; the fourth product
-// of the last level is beta X3 of the result (phi's x for free).  The input
-// is not the identity; Y == 0 cannot occur on secp256k1.
+// XYZZ doubling dbl-2008-s-1 (a = 0; x = X / ZZ, y = Y / ZZZ; the values
+// of point.h gexz_double mod p), state replicated in every row; the nine
+// products form three levels {Y^2, X^2} -> {Y V, X V, V ZZ, M^2} ->
+// {M (S - X3), H Y, H ZZZ, beta X3} with V = U^2 = 4 Y^2 (U = 2Y),
+// H = Y V (so W = U V = 2H), M = 3X^2; the fourth product of the last level
+// is beta X3 of the result (phi's x for free).  Every reduction between two
+// levels runs beside another (V | M, X3 | S - X3 = 3S - M^2, Y3 | ZZZ3):
+// three norm() latencies on the chain.  The input is not the identity;
+// Y == 0 cannot occur on secp256k1.
 __device__ __forceinline__ void dbl_xyzz(uint32_t &X, uint32_t &Y, uint32_t &ZZ, uint32_t &ZZZ, uint32_t &BX) {
   const uint32_t r = row();
-  const uint32_t U = norm(2ull * Y);
-  uint32_t m = mul(r == 0 ? U : X, r == 0 ? U : X);  // row 0: V = U^2, row 1: X^2
-  const uint32_t V = from_row(m, 0), XX = from_row(m, 1);
-  const uint32_t M = norm(3ull * XX);
-  // row 0: W = U V, row 1: S = X V, row 2: ZZ3 = V ZZ, row 3: M^2
-  m = mul(r == 0 ? U : r == 1 ? X : r == 2 ? ZZ : M, r == 3 ? M : V);
-  const uint32_t W = from_row(m, 0), S = from_row(m, 1), ZZ3 = from_row(m, 2), MM = from_row(m, 3);
-  const uint32_t X3 = norm((uint64_t)MM + 2ull * negw(S));  // M^2 - 2 S
-  const uint32_t t = norm((uint64_t)S + negw(X3));          // S - X3
-  // row 0: M (S - X3), row 1: W Y, row 2: ZZZ3 = W ZZZ, row 3: beta X3
-  m = mul(r == 0 ? M : r == 3 ? X3 : W, r == 0 ? t : r == 1 ? Y : r == 2 ? ZZZ : beta_limb());
-  const uint32_t Mt = from_row(m, 0), WY = from_row(m, 1), ZZZ3 = from_row(m, 2), B3 = from_row(m, 3);
-  Y = norm((uint64_t)Mt + negw(WY));
+  uint32_t m = mul(r == 0 ? Y : X, r == 0 ? Y : X);  // row 0: Y^2, row 1: X^2
+  const uint32_t YY = from_row(m, 0), XX = from_row(m, 1);
+  uint32_t V, M;
+  norm2(V, 4ull * YY, M, 3ull * XX);
+  // row 0: H = Y V, row 1: S = X V, row 2: ZZ3 = V ZZ, row 3: M^2
+  m = mul(r == 0 ? Y : r == 1 ? X : r == 2 ? ZZ : M, r == 3 ? M : V);
+  const uint32_t H = from_row(m, 0), S = from_row(m, 1), ZZ3 = from_row(m, 2), MM = from_row(m, 3);
+  uint32_t X3, t;  // M^2 - 2 S, S - X3 = 3 S - M^2
+  norm2(X3, (uint64_t)MM + 2ull * negw(S), t, 3ull * S + negw(MM));
+  // row 0: M (S - X3), row 1: H Y, row 2: H ZZZ, row 3: beta X3
+  m = mul(r == 0 ? M : r == 3 ? X3 : H, r == 0 ? t : r == 1 ? Y : r == 2 ? ZZZ : beta_limb());
+  const uint32_t Mt = from_row(m, 0), HY = from_row(m, 1), HZ = from_row(m, 2), B3 = from_row(m, 3);
+  norm2(Y, (uint64_t)Mt + 2ull * negw(HY), ZZZ, 2ull * HZ);  // M (S - X3) - W Y, W ZZZ
   X = X3;
   ZZ = ZZ3;
-  ZZZ = ZZZ3;
   BX = B3;
 }
 
@@ -262,7 +297,8 @@ __device__ __forceinline__ void add_xyzz(uint32_t &X1, uint32_t &Y1, uint32_t &Z
   // row 0: U1 = X1 ZZ2, row 1: U2 = X2 ZZ1, row 2: S1 = Y1 ZZZ2, row 3: S2 = Y2 ZZZ1
   uint32_t m = mul(r == 0 ? X1 : r == 1 ? X2 : r == 2 ? Y1 : Y2, r == 0 ? ZZ2 : r == 1 ? ZZ1 : r == 2 ? ZZZ2 : ZZZ1);
   const uint32_t U1 = from_row(m, 0), U2 = from_row(m, 1), S1 = from_row(m, 2), S2 = from_row(m, 3);
-  const uint32_t P = norm((uint64_t)U2 + negw(U1)), R = norm((uint64_t)S2 + negw(S1));
+  uint32_t P, R;
+  norm2(P, (uint64_t)U2 + negw(U1), R, (uint64_t)S2 + negw(S1));
   if (is_zero(P)) {  // wave-uniform: the same x
     if (is_zero(R)) {
       uint32_t bx;
@@ -278,8 +314,8 @@ __device__ __forceinline__ void add_xyzz(uint32_t &X1, uint32_t &Y1, uint32_t &Z
   // row 0: PPP = P PP, row 1: Q = U1 PP, rows 2-3: ZZ3 = ZZ1 ZZ2 PP
   m = mul(r == 0 ? P : r == 1 ? U1 : Z12, PP);
   const uint32_t PPP = from_row(m, 0), Q = from_row(m, 1), ZZ3 = from_row(m, 2);
-  const uint32_t X3 = norm((uint64_t)RR + negw(PPP) + 2ull * negw(Q));  // R^2 - PPP - 2 Q
-  const uint32_t t = norm((uint64_t)Q + negw(X3));                       // Q - X3
+  uint32_t X3, t;  // R^2 - PPP - 2 Q, Q - X3 = 3 Q + PPP - R^2
+  norm2(X3, (uint64_t)RR + negw(PPP) + 2ull * negw(Q), t, 3ull * Q + PPP + negw(RR));
   // row 0: R (Q - X3), row 1: S1 PPP, rows 2-3: ZZZ3 = ZZZ1 ZZZ2 PPP
   m = mul(r == 0 ? R : r == 1 ? S1 : ZZZ12, r == 0 ? t : PPP);
   const uint32_t Rt = from_row(m, 0), SP = from_row(m, 1), ZZZ3 = from_row(m, 2);

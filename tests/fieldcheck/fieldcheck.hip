@@ -178,6 +178,44 @@ extern "C" int fc_coop_xyzz(uint32_t n, const uint32_t *acc, const uint32_t *pts
   return e == hipSuccess ? 0 : -(int)e;
 }
 
+// coop.h's products and reductions on hardware, four cases a wave (one a
+// DPP row): op 0 mul(a, b), 1 norm(a + (M4 - b)), 2 norm(a + 8 (M4 - b)),
+// 3 norm(3 a); a, b: n x 8 words, out: n x 8 words (NORMAL, < 2^256).
+__global__ void __launch_bounds__(64) k_coop_ops(int op, uint32_t n, const uint32_t *a, const uint32_t *b,
+                                                 uint32_t *out) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t c = coop::pos(), i = 4 * blockIdx.x + coop::row();
+  const bool live = i < n;  // (every lane runs the row code: the DPP reads and ballots are wave-wide)
+  const uint32_t x = live && c < 8 ? a[8 * (uint64_t)i + c] : 0u, y = live && c < 8 ? b[8 * (uint64_t)i + c] : 0u;
+  uint32_t r;
+  if (op == 0) r = coop::mul(x, y);
+  else if (op == 1) r = coop::norm((uint64_t)x + coop::negw(y));
+  else if (op == 2) r = coop::norm((uint64_t)x + 8ull * coop::negw(y));
+  else r = coop::norm(3ull * x);
+  if (live && c < 8) out[8 * (uint64_t)i + c] = r;
+#endif
+}
+
+extern "C" int fc_coop_ops(int op, uint32_t n, const uint32_t *a, const uint32_t *b, uint32_t *out) {
+  uint32_t *da = nullptr, *db = nullptr, *dr = nullptr;
+  const size_t bytes = (size_t)(n ? n : 1) * 32;
+  hipError_t e = hipMalloc(&da, bytes);
+  if (e == hipSuccess) e = hipMalloc(&db, bytes);
+  if (e == hipSuccess) e = hipMalloc(&dr, bytes);
+  if (e == hipSuccess && n) e = hipMemcpy(da, a, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) e = hipMemcpy(db, b, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) {
+    hipLaunchKernelGGL(k_coop_ops, dim3((n + 3) / 4), dim3(64), 0, 0, op, n, da, db, dr);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess && n) e = hipMemcpy(out, dr, bytes, hipMemcpyDeviceToHost);
+  (void)hipFree(da);
+  (void)hipFree(db);
+  (void)hipFree(dr);
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
 // Key-table base chains B_j = 2^(w j) Q (j < nwin) of n affine points
 // (16 words each: x, y limbs), per lane (verify_core.h table_bases_one, the
 // zipped doubling) or wave-cooperative (coop.h: one wave per point, the

@@ -256,6 +256,33 @@ def test_xyzz_mixed_add_exceptional_cases(lat):
         assert (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P) == w, (i, i % 4)
 
 
+def test_coop_mul_norm_match_python_ints():
+    """coop.h's cooperative product and WIDE reduction (one field element
+    per 16-lane DPP row, ONE carry resolve each since round 6) on hardware
+    against Python integers, over the edge-heavy operands of the per-lane
+    tests plus values whose top limbs are all ones (the unresolved folds'
+    largest digits and tail()'s rare second fold).  The digit bounds behind
+    the single resolve are asserted by tests/test_coop_model.py."""
+    rng = random.Random(31)
+    a, b = _pairs(n=6000, seed=41)
+    tops = [2**256 - 1 - rng.getrandbits(rng.choice([1, 4, 12, 33, 70])) for _ in range(4000)]
+    a += tops
+    b += [rng.choice(tops) for _ in tops]
+    a = [x % 2**256 for x in a]
+    b = [x % 2**256 for x in b]
+    A, B = _pack(a), _pack(b)
+    L = _lib()
+    L.fc_coop_ops.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.fc_coop_ops.restype = ctypes.c_int
+    want = {0: lambda x, y: x * y, 1: lambda x, y: x - y, 2: lambda x, y: x - 8 * y, 3: lambda x, y: 3 * x}
+    for op, f in want.items():
+        R = np.zeros_like(A)
+        assert L.fc_coop_ops(op, len(a), A.ctypes.data, B.ctypes.data, R.ctypes.data) == 0
+        r = _unpack(R)
+        bad = [(op, hex(x), hex(y), hex(z)) for x, y, z in zip(a, b, r) if z >= 2**256 or (z - f(x, y)) % P]
+        assert not bad, bad[:5]
+
+
 def test_coop_xyzz_add_and_double():
     """The wave-cooperative XYZZ addition and doubling of k_small's cold
     path (coop.h add_xyzz / dbl_xyzz: one point per wave, the products of a
