@@ -88,8 +88,13 @@ __device__ __forceinline__ void tail_n(const uint64_t (&w)[N], uint32_t (&d)[N])
     C[i] = ((G << 1) + P) ^ P;
     rare |= (__ballot((uint32_t)y[i] != 0) | C[i]) & kLane8;
   }
+  // v + (bit `lane` of C): ONE v_addc with the scalar carry word as its
+  // carry-in mask (instead of a 64-bit shift, an and and an add)
 #pragma unroll
-  for (int i = 0; i < N; i++) d[i] = (uint32_t)y[i] + (uint32_t)((C[i] >> __lane_id()) & 1u);
+  for (int i = 0; i < N; i++) {
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(d[i]), "=s"(co) : "v"((uint32_t)y[i]), "s"(C[i]));
+  }
   if (rare) {  // rare (a value within ~2^235 of 2^256), wave-uniform
 #pragma unroll
     for (int i = 0; i < N; i++) {  // (a no-op for a value whose lane 8 is 0)
@@ -99,8 +104,8 @@ __device__ __forceinline__ void tail_n(const uint64_t (&w)[N], uint32_t (&d)[N])
       d[i] = resolve((uint32_t)y2, (y2 >> 32) != 0);  // the rest is < 2^245: no carry out
     }
   }
-#pragma unroll
-  for (int i = 0; i < N; i++) d[i] &= m;
+  // (lane 8 is 0 here: without the rare fold y_8 = 0 and no carry reached
+  // it; after it, the rest had no carry out; lanes 9..15 stayed 0)
 }
 __device__ __forceinline__ uint32_t tail(uint64_t w) {
   const uint64_t in[1] = {w};

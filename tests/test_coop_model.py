@@ -59,7 +59,8 @@ def tail(w, stats):
         y2 = [(z2[k] & M32) + shr([x >> 32 for x in z2])[k] for k in range(16)]
         d = resolve([x & M32 for x in y2], [x >> 32 != 0 for x in y2], stats)
         assert d[8] == 0, "carry out of limb 7 after the second fold"
-    return [d[k] if k < 8 else 0 for k in range(16)]
+    assert not any(d[8:]), "tail() returns without masking: lanes 8..15 must be 0"
+    return d
 
 
 def norm(w, stats):
