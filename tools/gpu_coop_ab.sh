@@ -1,6 +1,11 @@
 # coop.h A/B: one-wave chain latencies (HEAD's / the tree's header, same
 # box), the coop field tests, the whole GPU suite, then small-batch latency
-# of HEAD's library (gpurun_var/old.so) against the tree's.
+# of HEAD's library (gpurun_var/old.so) against the tree's.  Build first, here:
+#   git show HEAD:babble_amd/csrc/coop.h > /tmp/coop_old.h
+#   H="hipcc --offload-arch=gfx950 -O3 -std=c++17 -Ibabble_amd/csrc"
+#   $H -DCOOP_HEADER='"/tmp/coop_old.h"' -o gpurun_var/ubench_coop_old tools/ubench_coop_chain.hip
+#   $H -o gpurun_var/ubench_coop_new tools/ubench_coop_chain.hip
+#   BV_REV=HEAD bash tools/build_variant.sh gpurun_var/old.so
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
